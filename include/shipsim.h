@@ -1,0 +1,271 @@
+/*
+ * shipsim.h — C ABI of the MI355X-native batched ship-in-transit simulator.
+ *
+ * The reference (AndreasKing-Goks/ast-sac) has no FFI: its boundary is the Python object API of
+ * MultiShipRLEnv (rl_env/ship_in_transit/env.py:41) — reset() (:238) / step(action) (:624) —
+ * plus run_colav/env.py:MultiShipNonIWEnv._step (:613) for the C1 loop and the
+ * SimpleShipModel/controller loop of run_colav/run_simplified_model.py:245-249 for single ships.
+ * These entry points are what that object API lowers to when N environments are batched on one
+ * device; the Python facade in ast_sac_amd/ re-exposes the reference's reset/step signatures on
+ * top of them (INTEGRATION.md shows the ctypes binding).
+ *
+ * Conventions
+ *   - every function returns 0 on success or a negative SHIPSIM_E* code; never aborts or throws;
+ *     shipsim_last_error(h) gives the message of the last failure on that handle.
+ *   - one handle <-> one device <-> one HIP stream; calls are asynchronous on that stream.
+ *     A handle is not thread-safe; handles on different devices are independent.
+ *   - the library owns all device state (SoA ship state, per-env route tables, map);
+ *     every I/O buffer below is a caller-owned DEVICE pointer (e.g. a torch tensor's data_ptr()).
+ *   - no host allocation or synchronisation inside reset/step/tick.
+ */
+#ifndef SHIPSIM_H
+#define SHIPSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHIPSIM_ABI_VERSION 1
+
+#define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
+#define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
+#define SHIPSIM_MAX_VERTS 128  /* total polygon vertices */
+
+/* status codes */
+#define SHIPSIM_OK 0
+#define SHIPSIM_EINVAL -1   /* bad argument / config */
+#define SHIPSIM_EHIP -2     /* HIP runtime failure */
+#define SHIPSIM_ESTATE -3   /* call not valid in the current state (e.g. step before reset) */
+#define SHIPSIM_ENOMEM -4
+
+/* environment kinds */
+#define SHIPSIM_KIND_SINGLE 0  /* one ship per env, no termination (config C2; run_simplified_model loop) */
+#define SHIPSIM_KIND_NONIW 1   /* two ships, fixed routes, env_info flags only (C1; run_colav/env.py:37) */
+#define SHIPSIM_KIND_AST 2     /* two-ship AST env with IW sampling + reward (C3/C4/C5; rl_env/.../env.py:41) */
+
+/* collision avoidance of the ship under test (env.py:53, args.collav_mode) */
+#define SHIPSIM_COLLAV_NONE 0
+#define SHIPSIM_COLLAV_SIMPLE 1
+#define SHIPSIM_COLLAV_SBMPC 2
+
+/* propulsion model */
+#define SHIPSIM_MACH_SIMPLIFIED 0 /* SimpleShipModel + ThrustFromSpeedSetPoint (run_colav) */
+#define SHIPSIM_MACH_DETAILED 1   /* ShipModelAST + ShipMachineryModel + EngineThrottleFromSpeedSetPoint */
+
+/* MachineryMode.shaft_generator_state (ship_engine.py:32-76) */
+#define SHIPSIM_SG_GEN 0   /* PTO */
+#define SHIPSIM_SG_MOTOR 1 /* PTI */
+#define SHIPSIM_SG_OFF 2   /* MEC */
+
+/* event bits, in the order get_reward_and_env_info appends its strings (reward_function.py:204-262) */
+#define SHIPSIM_EV_COLLISION (1u << 0)
+#define SHIPSIM_EV_TEST_GROUNDING (1u << 1)
+#define SHIPSIM_EV_TEST_NAV_FAILURE (1u << 2)
+#define SHIPSIM_EV_OBS_GROUNDING (1u << 3)
+#define SHIPSIM_EV_OBS_NAV_FAILURE (1u << 4)
+#define SHIPSIM_EV_TEST_REACHES_END (1u << 5)
+#define SHIPSIM_EV_TEST_OUTSIDE_MAP (1u << 6)
+#define SHIPSIM_EV_OBS_REACHES_END (1u << 7)
+#define SHIPSIM_EV_OBS_OUTSIDE_MAP (1u << 8)
+#define SHIPSIM_EV_TIME_LIMIT (1u << 9)
+#define SHIPSIM_EV_SAMPLING_FAILURE (1u << 10) /* env.py:684 */
+#define SHIPSIM_EV_TERMINAL (1u << 16)          /* env_info['terminal'] */
+#define SHIPSIM_EV_TEST_STOP (1u << 17)         /* env_info['test_ship_stop'] */
+#define SHIPSIM_EV_OBS_STOP (1u << 18)          /* env_info['obs_ship_stop'] */
+#define SHIPSIM_EV_NONFINITE (1u << 24)         /* build-only: a state went NaN/Inf */
+
+/* One ship: ShipConfiguration (ship_model.py:20), SimulationConfiguration (:45), rudder / machinery
+ * (ship_engine.py:121,160), controller gains (controllers.py:16-38), LOS (LOS_guidance.py:15) and
+ * the route file contents. Field names follow the reference's NamedTuple fields. */
+typedef struct shipsim_ship_config {
+  double dead_weight_tonnage;
+  double coefficient_of_deadweight_to_displacement;
+  double bunkers;
+  double ballast;
+  double length_of_ship;
+  double width_of_ship;
+  double added_mass_coefficient_in_surge;
+  double added_mass_coefficient_in_sway;
+  double added_mass_coefficient_in_yaw;
+  double mass_over_linear_friction_coefficient_in_surge;
+  double mass_over_linear_friction_coefficient_in_sway;
+  double mass_over_linear_friction_coefficient_in_yaw;
+  double nonlinear_friction_coefficient_in_surge;
+  double nonlinear_friction_coefficient_in_sway;
+  double nonlinear_friction_coefficient_in_yaw;
+  /* initial state (SimulationConfiguration) */
+  double initial_north_position_m;
+  double initial_east_position_m;
+  double initial_yaw_angle_rad;
+  double initial_forward_speed_m_per_s;
+  double initial_sideways_speed_m_per_s;
+  double initial_yaw_rate_rad_per_s;
+  /* rudder */
+  double rudder_angle_to_sway_force_coefficient;
+  double rudder_angle_to_yaw_force_coefficient;
+  double max_rudder_angle_degrees;
+  /* detailed machinery (MachinerySystemConfiguration, one active MachineryMode) */
+  double hotel_load;
+  double main_engine_capacity;
+  double electrical_capacity;
+  double rated_speed_main_engine_rpm;
+  double linear_friction_main_engine;
+  double linear_friction_hybrid_shaft_generator;
+  double gear_ratio_between_main_engine_and_propeller;
+  double gear_ratio_between_hybrid_shaft_generator_and_propeller;
+  double propeller_inertia;
+  double propeller_speed_to_torque_coefficient;
+  double propeller_diameter;
+  double propeller_speed_to_thrust_force_coefficient;
+  double initial_propeller_shaft_speed_rad_per_s;
+  /* EngineThrottleFromSpeedSetPoint gains (detailed) */
+  double kp_ship_speed;
+  double ki_ship_speed;
+  double kp_shaft_speed;
+  double ki_shaft_speed;
+  double initial_shaft_speed_integral_error;
+  /* ThrustFromSpeedSetPoint PID (simplified); max_thrust may be +inf */
+  double speed_kp;
+  double speed_ki;
+  double speed_kd;
+  double max_thrust;
+  /* heading autopilot PID */
+  double heading_kp;
+  double heading_kd;
+  double heading_ki;
+  /* LOS guidance */
+  double radius_of_acceptance;
+  double lookahead_distance;
+  double los_integral_gain;
+  double los_integrator_windup_limit;
+  double desired_forward_speed;
+  int32_t shaft_generator_state; /* SHIPSIM_SG_* */
+  int32_t n_route;               /* waypoints in route_north/route_east */
+  double route_north[SHIPSIM_MAX_ROUTE];
+  double route_east[SHIPSIM_MAX_ROUTE];
+} shipsim_ship_config;
+
+typedef struct shipsim_config {
+  int32_t abi_version;            /* = SHIPSIM_ABI_VERSION */
+  int32_t kind;                   /* SHIPSIM_KIND_* */
+  int32_t machinery;              /* SHIPSIM_MACH_* */
+  int32_t collav;                 /* SHIPSIM_COLLAV_* */
+  int32_t max_sampling_frequency; /* args.max_sampling_frequency (9) */
+  int32_t machinery_dt_quirk;     /* 1: machinery integrates with dt 0.01 after reset */
+  int32_t normalize_action;       /* args.normalize_action: env denormalizes [-1,1] itself */
+  int32_t n_ships;                /* 1 (SINGLE) or 2 */
+  double time_step;               /* args.time_step */
+  double simulation_time;         /* SimulationConfiguration.simulation_time */
+  double env_radius_of_acceptance;/* args.radius_of_acceptance used by is_reach_radius_of_acceptance */
+  /* EnvironmentConfiguration */
+  double current_velocity_component_from_north;
+  double current_velocity_component_from_east;
+  double wind_speed;
+  double wind_direction;
+  /* SBMPC(tf, dt) (env.py:123) */
+  double sbmpc_tf;
+  double sbmpc_dt;
+  /* action box of the wrapped env (env.py:93-104), float32 as in the reference */
+  float action_low;
+  float action_high;
+  shipsim_ship_config ship[2]; /* [0] ship under test, [1] obstacle ship */
+  /* PolygonObstacle map: polygon p owns vertices [poly_start[p], poly_start[p+1]), (east, north) */
+  int32_t n_polys;
+  int32_t poly_start[SHIPSIM_MAX_POLYS + 1];
+  double poly_east[SHIPSIM_MAX_VERTS];
+  double poly_north[SHIPSIM_MAX_VERTS];
+} shipsim_config;
+
+/* Per-ship state fields for get/set_state (SoA, double unless noted) */
+#define SHIPSIM_F_NORTH 0
+#define SHIPSIM_F_EAST 1
+#define SHIPSIM_F_YAW 2
+#define SHIPSIM_F_U 3
+#define SHIPSIM_F_V 4
+#define SHIPSIM_F_R 5
+#define SHIPSIM_F_OMEGA 6        /* propeller shaft speed (detailed) */
+#define SHIPSIM_F_TIME 7         /* ship_model.int.time */
+#define SHIPSIM_F_E_CT 8         /* navigate.e_ct */
+#define SHIPSIM_F_E_CT_INT 9     /* navigate.e_ct_int */
+#define SHIPSIM_F_HDG_EI 10      /* heading PID error_i */
+#define SHIPSIM_F_HDG_PREV 11    /* heading PID prev_error */
+#define SHIPSIM_F_SPD_A 12       /* ship-speed PI error_i (detailed) | thrust PID error_i (simplified) */
+#define SHIPSIM_F_SPD_B 13       /* shaft-speed PI error_i (detailed) | thrust PID prev_error (simplified) */
+#define SHIPSIM_F_RUDDER 14      /* last commanded rudder angle (logged) */
+#define SHIPSIM_F_THRUST 15      /* last thrust force [N] (logged) */
+#define SHIPSIM_F_LOG_ECT 16     /* last logged cross-track error */
+#define SHIPSIM_F_NEXT_WPT 17    /* int32: auto_pilot.next_wpt */
+#define SHIPSIM_F_STOP 18        /* int32: ShipAssets.stop_flag */
+#define SHIPSIM_N_SHIP_FIELDS 19
+
+/* Per-env fields (AST / NONIW) */
+#define SHIPSIM_E_SAMPLING_COUNT 100 /* int32 */
+#define SHIPSIM_E_TRAVEL_DIST 101
+#define SHIPSIM_E_TRAVEL_TIME 102
+#define SHIPSIM_E_ACC_REWARD 103
+#define SHIPSIM_E_N_BASE 104
+#define SHIPSIM_E_E_BASE 105
+#define SHIPSIM_E_SBMPC_P_LAST 106
+#define SHIPSIM_E_SBMPC_CHI_LAST 107
+#define SHIPSIM_E_ROUTE_LEN 108      /* int32: obstacle-ship route length */
+#define SHIPSIM_E_ROUTE_NORTH 109    /* double[SHIPSIM_MAX_ROUTE] per env, env-major */
+#define SHIPSIM_E_ROUTE_EAST 110
+
+typedef struct shipsim_handle shipsim_handle;
+
+/* Build info / ABI version of the loaded library. */
+int32_t shipsim_abi_version(void);
+const char* shipsim_build_info(void);
+
+/* Fill *cfg with the reference scenario of record:
+ *   kind SHIPSIM_KIND_AST : run/env_setup.py:17-254 (two ShipModelAST, PTI machinery, time_step 4,
+ *                           runner defaults run/ast-sac_runner.py:27-43), collav as given;
+ *   kind SHIPSIM_KIND_NONIW / SINGLE : run_colav/run_simplified_model.py:55-233 (SimpleShipModel,
+ *                           ThrustFromSpeedSetPoint, time_step 30).
+ * Routes and the 6-polygon map are the reference data files' contents. */
+int shipsim_default_config(int32_t kind, int32_t machinery, int32_t collav, double time_step,
+                           shipsim_config* cfg);
+
+/* Allocate device state for n_envs environments on `device`, bound to `stream` (hipStream_t;
+ * NULL = default stream). The handle starts un-reset. */
+int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, void* stream,
+                   shipsim_handle** out);
+int shipsim_destroy(shipsim_handle* h);
+const char* shipsim_last_error(const shipsim_handle* h);
+int32_t shipsim_num_envs(const shipsim_handle* h);
+
+/* MultiShipRLEnv.reset(): every env with env_mask[i] != 0 (NULL = all) is reset and placed with
+ * init_step (one control + integrate tick, env.py:297); obs_out (N x 8 float32, device, may be NULL)
+ * receives the reference's constant initial_states row for reset envs (Q11). */
+int shipsim_reset(shipsim_handle* h, const uint8_t* env_mask, float* obs_out);
+
+/* MultiShipRLEnv.step(action) for all N envs at once (AST kind only).
+ *   action     N float32 scoping angles in radians (already denormalized, i.e. what
+ *              NormalizedBoxEnv passes to the wrapped env), device.
+ *   active     optional N uint8 mask (NULL = all): envs with 0 are left untouched.
+ *   max_ticks  safety bound on ticks per env in this call (<=0: derived from simulation_time).
+ * Outputs (device, each may be NULL): obs N x 8 float32, reward N double (un-scaled),
+ * done N uint8 (combined_done), events N uint32 (SHIPSIM_EV_* bits), ticks N int32 (_step calls). */
+int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks,
+                 float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
+                 int32_t* ticks_out);
+
+/* Raw ticks for the SINGLE and NONIW kinds (and debugging AST): advance every env by k ticks of
+ * the reference loop body (run_simplified_model.py:248-249 / env._step). events_out (N uint32,
+ * may be NULL) receives the OR of the per-tick env_info bits of the last tick. */
+int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out);
+
+/* Read / write one state field for all envs (device pointer dst/src; ship fields are laid out
+ * [ship][env], env fields [env] or [env][SHIPSIM_MAX_ROUTE] for routes). */
+int shipsim_get_state(shipsim_handle* h, int32_t field, void* dst);
+int shipsim_set_state(shipsim_handle* h, int32_t field, const void* src);
+
+/* Block until all work queued on the handle's stream is done. */
+int shipsim_synchronize(shipsim_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHIPSIM_H */

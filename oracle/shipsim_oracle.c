@@ -1,0 +1,1274 @@
+/*
+ * shipsim_oracle.c — CPU restatement of the reference ship-in-transit simulator.
+ *
+ * TEST INFRASTRUCTURE ONLY: the checker for the HIP product path (tests/, __graft_entry__.smoke,
+ * bench.py's cpu_baseline leg). Nothing in ast_sac_amd/ links, loads or calls this file.
+ *
+ * A scalar, one-env-at-a-time, object-by-object transcription of AndreasKing-Goks/ast-sac
+ * (snapshot 2025-09-05); every function cites the reference file:line it restates. It is
+ * deliberately written independently of the HIP kernels (AoS structs mirroring the reference's
+ * Python objects) so that parity between the two is a real check. Parity of this oracle itself
+ * is pinned by the tests/golden fixtures, produced by running the reference in the build container
+ * (tests/golden/gen_golden.py). Compile with -ffp-contract=off (no FMA contraction, like NumPy).
+ *
+ * Paths below are relative to the reference root.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/shipsim.h"
+
+#define PI 3.141592653589793
+#define DEG2RAD(x) ((x) * (PI / 180.0)) /* numpy deg2rad: x * (NPY_PI/180) */
+
+/* ------------------------------------------------------------------------------------------ */
+/* small helpers                                                                              */
+/* ------------------------------------------------------------------------------------------ */
+static double py_min(double a, double b) { return (b < a) ? b : a; } /* Python min(a, b) */
+static double py_max(double a, double b) { return (b > a) ? b : a; } /* Python max(a, b) */
+static double sat(double v, double lo, double hi) { return py_max(lo, py_min(v, hi)); } /* controllers.py:68 */
+
+/* Python / numpy floored modulo (np.remainder) */
+static double floor_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0) != (m < 0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+
+/* sbmpc_misc.py:3-32 wrap_angle_to_pmpi: x_min + (x - x_min) % (x_max - x_min) */
+static double wrap_pmpi(double x) { return -PI + floor_mod(x - (-PI), PI - (-PI)); }
+
+/* ------------------------------------------------------------------------------------------ */
+/* ship model (rl_env/ship_in_transit/sub_systems/ship_model.py BaseShipModel :401-658,        */
+/* ShipModelAST :803-967; run_colav/.../ship_model.py SimpleShipModel :322-449)                */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  /* BaseShipModel.__init__ :412-474 */
+  double mass, i_z, x_du, y_dv, n_dr, t_surge, t_sway, t_yaw, ku, kv, kr, l_ship, w_ship;
+  double rho_a, proj_area_f, proj_area_l, cx, cy, cn;
+  double vel_c[3], wind_dir, wind_speed;
+  double north, east, yaw, u, v, r;
+  double d_north, d_east, d_yaw, d_u, d_v, d_r;
+  double init_north, init_east, init_yaw, init_u, init_v, init_r;
+  double time, dt, sim_time; /* EulerInt (utils.py:7-53) */
+  /* rudder */
+  double c_rudder_v, c_rudder_r;
+  /* detailed machinery: ShipMachineryModel ship_engine.py:341-481 */
+  int detailed;
+  int sg_state;
+  double me_cap, el_cap, hotel_load, avail, avail_me, avail_el; /* MachineryMode :23-76 */
+  double w_rated_me, d_me, d_hsg, r_me, r_hsg, jp, kp, dp, kt, shaft_speed_max;
+  double omega, d_omega, init_omega, mach_dt, mach_dt_init;
+  double fuel_cons_me, fuel_cons_el, fuel_cons;
+  double fa_me, fb_me, fc_me, fa_dg, fb_dg, fc_dg;
+} o_ship;
+
+static void ship_init(o_ship* s, const shipsim_config* cfg, const shipsim_ship_config* c, int detailed) {
+  memset(s, 0, sizeof(*s));
+  double payload = 0.9 * (c->dead_weight_tonnage - c->bunkers);
+  double lsw = c->dead_weight_tonnage / c->coefficient_of_deadweight_to_displacement - c->dead_weight_tonnage;
+  s->mass = lsw + payload + c->bunkers + c->ballast;
+  s->l_ship = c->length_of_ship;
+  s->w_ship = c->width_of_ship;
+  s->i_z = s->mass * (s->l_ship * s->l_ship + s->w_ship * s->w_ship) / 12;
+  s->x_du = s->mass * c->added_mass_coefficient_in_surge;
+  s->y_dv = s->mass * c->added_mass_coefficient_in_sway;
+  s->n_dr = s->i_z * c->added_mass_coefficient_in_yaw;
+  s->t_surge = c->mass_over_linear_friction_coefficient_in_surge;
+  s->t_sway = c->mass_over_linear_friction_coefficient_in_sway;
+  s->t_yaw = c->mass_over_linear_friction_coefficient_in_yaw;
+  s->ku = c->nonlinear_friction_coefficient_in_surge;
+  s->kv = c->nonlinear_friction_coefficient_in_sway;
+  s->kr = c->nonlinear_friction_coefficient_in_yaw;
+  s->vel_c[0] = cfg->current_velocity_component_from_north;
+  s->vel_c[1] = cfg->current_velocity_component_from_east;
+  s->vel_c[2] = 0.0;
+  s->wind_dir = cfg->wind_direction;
+  s->wind_speed = cfg->wind_speed;
+  s->init_north = s->north = c->initial_north_position_m;
+  s->init_east = s->east = c->initial_east_position_m;
+  s->init_yaw = s->yaw = c->initial_yaw_angle_rad;
+  s->init_u = s->u = c->initial_forward_speed_m_per_s;
+  s->init_v = s->v = c->initial_sideways_speed_m_per_s;
+  s->init_r = s->r = c->initial_yaw_rate_rad_per_s;
+  s->time = 0.0;
+  s->dt = cfg->time_step;
+  s->sim_time = cfg->simulation_time;
+  s->rho_a = 1.2;
+  s->proj_area_f = s->w_ship * 8.0;
+  s->proj_area_l = s->l_ship * 8.0;
+  s->cx = 0.5;
+  s->cy = 0.7;
+  s->cn = 0.08;
+  s->c_rudder_v = c->rudder_angle_to_sway_force_coefficient;
+  s->c_rudder_r = c->rudder_angle_to_yaw_force_coefficient;
+  s->detailed = detailed;
+  if (detailed) {
+    s->sg_state = c->shaft_generator_state;
+    s->me_cap = c->main_engine_capacity;
+    s->el_cap = c->electrical_capacity;
+    s->hotel_load = c->hotel_load;
+    /* MachineryMode.update_available_propulsion_power :32-44 */
+    if (s->sg_state == SHIPSIM_SG_MOTOR) {
+      s->avail = s->me_cap + s->el_cap - s->hotel_load;
+      s->avail_me = s->me_cap;
+      s->avail_el = s->el_cap - s->hotel_load;
+    } else if (s->sg_state == SHIPSIM_SG_GEN) {
+      s->avail = s->me_cap - s->hotel_load;
+      s->avail_me = s->me_cap - s->hotel_load;
+      s->avail_el = 0;
+    } else {
+      s->avail = s->me_cap;
+      s->avail_me = s->me_cap;
+      s->avail_el = 0;
+    }
+    s->w_rated_me = c->rated_speed_main_engine_rpm * PI / 30;
+    s->d_me = c->linear_friction_main_engine;
+    s->d_hsg = c->linear_friction_hybrid_shaft_generator;
+    s->r_me = c->gear_ratio_between_main_engine_and_propeller;
+    s->r_hsg = c->gear_ratio_between_hybrid_shaft_generator_and_propeller;
+    s->jp = c->propeller_inertia;
+    s->kp = c->propeller_speed_to_torque_coefficient;
+    s->dp = c->propeller_diameter;
+    s->kt = c->propeller_speed_to_thrust_force_coefficient;
+    s->shaft_speed_max = 1.1 * s->w_rated_me * s->r_me;
+    s->init_omega = s->omega = c->initial_propeller_shaft_speed_rad_per_s;
+    s->mach_dt = s->mach_dt_init = cfg->time_step;
+    /* env_setup.py:85-86: Wartila6L26 (ME), Baudouin6M26Dot3 (DG) */
+    s->fa_me = 128.9; s->fb_me = -168.9; s->fc_me = 246.8;
+    s->fa_dg = 108.7; s->fb_dg = -289.9; s->fc_dg = 324.9;
+  }
+}
+
+/* BaseShipModel.reset :645-658 + ShipMachineryModel.reset :468-481 (-> BaseMachineryModel.reset
+ * :324-333, whose `EulerInt(); set_dt(self.int.dt)` leaves dt = 0.01: SURVEY Q1) */
+static void ship_reset(o_ship* s, int machinery_dt_quirk) {
+  s->north = s->init_north; s->east = s->init_east; s->yaw = s->init_yaw;
+  s->u = s->init_u; s->v = s->init_v; s->r = s->init_r;
+  s->d_north = s->d_east = s->d_yaw = s->d_u = s->d_v = s->d_r = 0;
+  s->time = 0.0;
+  if (s->detailed) {
+    s->omega = s->init_omega;
+    s->d_omega = 0;
+    s->mach_dt = machinery_dt_quirk ? 0.01 : s->mach_dt_init;
+    s->fuel_cons_me = s->fuel_cons_el = s->fuel_cons = 0;
+  }
+}
+
+/* get_wind_force :497-517 */
+static void wind_force(const o_ship* s, double tau[3]) {
+  double uw = s->wind_speed * cos(s->wind_dir - s->yaw);
+  double vw = s->wind_speed * sin(s->wind_dir - s->yaw);
+  double u_rw = uw - s->u;
+  double v_rw = vw - s->v;
+  double gamma_rw = -atan2(v_rw, u_rw);
+  double wind_rw2 = u_rw * u_rw + v_rw * v_rw;
+  double c_x = -s->cx * cos(gamma_rw);
+  double c_y = s->cy * sin(gamma_rw);
+  double c_n = s->cn * sin(2 * gamma_rw);
+  double tau_coeff = 0.5 * s->rho_a * wind_rw2;
+  tau[0] = tau_coeff * c_x * s->proj_area_f;
+  tau[1] = tau_coeff * c_y * s->proj_area_l;
+  tau[2] = tau_coeff * c_n * s->proj_area_l * s->l_ship;
+}
+
+/* three_dof_kinematics :519-528 with rotation() :530-536 */
+static void kinematics(o_ship* s) {
+  double c = cos(s->yaw), sn = sin(s->yaw);
+  s->d_north = c * s->u + (-sn) * s->v + 0 * s->r;
+  s->d_east = sn * s->u + c * s->v + 0 * s->r;
+  s->d_yaw = 0 * s->u + 0 * s->v + 1 * s->r;
+}
+
+/* inv(rotation()) @ vel_c — the inverse of a z-rotation is its transpose */
+static void current_in_body(const o_ship* s, double vc[3]) {
+  double c = cos(s->yaw), sn = sin(s->yaw);
+  vc[0] = c * s->vel_c[0] + sn * s->vel_c[1];
+  vc[1] = -sn * s->vel_c[0] + c * s->vel_c[1];
+  vc[2] = s->vel_c[2];
+}
+
+/* rudder :866-880 */
+static void rudder_force(const o_ship* s, double delta, double* fv, double* fr) {
+  double vc[3];
+  current_in_body(s, vc);
+  *fv = -s->c_rudder_v * delta * (s->u - vc[0]);
+  *fr = -s->c_rudder_r * delta * (s->u - vc[0]);
+}
+
+/* ShipModelAST.three_dof_kinetics :834-864 (mass_matrix .. non_linear_damping_matrix :538-562);
+ * x_g = 0 so M is diagonal and inv(M) = diag(1/M_ii). */
+static void kinetics(o_ship* s, double thrust, double delta) {
+  double fv, fr, tau[3], vc[3];
+  rudder_force(s, delta, &fv, &fr);
+  wind_force(s, tau);
+  current_in_body(s, vc);
+  double u_r = s->u - vc[0];
+  double v_r = s->v - vc[1];
+  double x_g = 0.0;
+  double vel[3] = {s->u, s->v, s->r};
+  double vrel[3] = {s->u - vc[0], s->v - vc[1], s->r - vc[2]};
+  double crb_v[3];
+  crb_v[0] = 0 * vel[0] + 0 * vel[1] + (-s->mass * (x_g * s->r + s->v)) * vel[2];
+  crb_v[1] = 0 * vel[0] + 0 * vel[1] + (s->mass * s->u) * vel[2];
+  crb_v[2] = (s->mass * (x_g * s->r + s->v)) * vel[0] + (-s->mass * s->u) * vel[1] + 0 * vel[2];
+  double ca_v[3];
+  ca_v[0] = 0 * vrel[0] + 0 * vrel[1] + (s->y_dv * v_r) * vrel[2];
+  ca_v[1] = 0 * vrel[0] + 0 * vrel[1] + (-s->x_du * u_r) * vrel[2];
+  ca_v[2] = (-s->y_dv * v_r) * vrel[0] + (s->x_du * u_r) * vrel[1] + 0 * vrel[2];
+  double d0 = s->mass / s->t_surge + s->ku * s->u;
+  double d1 = s->mass / s->t_sway + s->kv * s->v;
+  double d2 = s->i_z / s->t_yaw + s->kr * s->r;
+  double dmp[3] = {d0 * vrel[0], d1 * vrel[1], d2 * vrel[2]};
+  double f[3];
+  f[0] = -crb_v[0] - ca_v[0] - dmp[0] + tau[0] + 0 + thrust;
+  f[1] = -crb_v[1] - ca_v[1] - dmp[1] + tau[1] + 0 + fv;
+  f[2] = -crb_v[2] - ca_v[2] - dmp[2] + tau[2] + 0 + fr;
+  double m0 = 1.0 / (s->mass + s->x_du);
+  double m1 = 1.0 / (s->mass + s->y_dv);
+  double m2 = 1.0 / (s->i_z + s->n_dr);
+  s->d_u = m0 * f[0];
+  s->d_v = m1 * f[1];
+  s->d_r = m2 * f[2];
+}
+
+/* ShipMachineryModel :403-443 */
+static double mach_thrust(const o_ship* s) { return pow(s->dp, 4) * s->kt * s->omega * fabs(s->omega); }
+static double me_torque(const o_ship* s, double load) {
+  return py_min(load * s->avail_me / (s->omega + 0.1), s->avail_me / 5 * PI / 30);
+}
+static double hsg_torque(const o_ship* s, double load) {
+  return py_min(load * s->avail_el / (s->omega + 0.1), s->avail_el / 5 * PI / 30);
+}
+static void shaft_eq(o_ship* s, double t_me, double t_hsg) {
+  double eq_me = (t_me - s->d_me * s->omega) / s->r_me;
+  double eq_hsg = (t_hsg - s->d_hsg * s->omega) / s->r_hsg;
+  s->d_omega = (eq_me + eq_hsg - s->kp * (s->omega * s->omega)) / s->jp;
+}
+
+/* MachineryMode.distribute_load :46-76 */
+static void distribute_load(const o_ship* s, double load, double* l_me, double* l_el, double* p_me, double* p_el) {
+  double total = load * s->avail;
+  if (s->sg_state == SHIPSIM_SG_MOTOR) {
+    *l_me = py_min(total, s->me_cap);
+    *l_el = total + s->hotel_load - *l_me;
+    *p_el = *l_el / s->el_cap;
+    *p_me = (s->me_cap == 0) ? 0 : *l_me / s->me_cap;
+  } else if (s->sg_state == SHIPSIM_SG_GEN) {
+    *l_el = py_min(s->hotel_load, s->el_cap);
+    *l_me = total + s->hotel_load - *l_el;
+    *p_me = *l_me / s->me_cap;
+    *p_el = (s->el_cap == 0) ? 0 : *l_el / s->el_cap;
+  } else {
+    *l_me = total;
+    *l_el = s->hotel_load;
+    *p_me = *l_me / s->me_cap;
+    *p_el = *l_el / s->el_cap;
+  }
+}
+
+/* BaseMachineryModel.fuel_consumption :266-295 (logging only) */
+static void fuel_consumption(o_ship* s, double load) {
+  double l_me, l_el, p_me, p_el;
+  distribute_load(s, load, &l_me, &l_el, &p_me, &p_el);
+  double rate_me = (l_me == 0) ? 0 : l_me * ((s->fa_me * p_me * p_me + s->fb_me * p_me + s->fc_me) / 3.6e9);
+  double rate_el = (p_el == 0) ? 0 : l_el * ((s->fa_dg * p_el * p_el + s->fb_dg * p_el + s->fc_dg) / 3.6e9);
+  s->fuel_cons_me = s->fuel_cons_me + rate_me * s->mach_dt;
+  s->fuel_cons_el = s->fuel_cons_el + rate_el * s->mach_dt;
+  s->fuel_cons = s->fuel_cons + (rate_me + rate_el) * s->mach_dt;
+}
+
+/* update_differentials: ShipModelAST :882-888 (ctrl = engine throttle) or SimpleShipModel
+ * run_colav :399-404 (ctrl = thrust force) */
+static void update_differentials(o_ship* s, double ctrl, double rudder) {
+  kinematics(s);
+  double thrust = ctrl;
+  if (s->detailed) {
+    shaft_eq(s, me_torque(s, ctrl), hsg_torque(s, ctrl));
+    thrust = mach_thrust(s);
+  }
+  kinetics(s, thrust, rudder);
+}
+
+/* integrate_differentials :890-901 (EulerInt.integrate utils.py:50) */
+static void integrate_differentials(o_ship* s) {
+  s->north = s->north + s->d_north * s->dt;
+  s->east = s->east + s->d_east * s->dt;
+  s->yaw = s->yaw + s->d_yaw * s->dt;
+  s->u = s->u + s->d_u * s->dt;
+  s->v = s->v + s->d_v * s->dt;
+  s->r = s->r + s->d_r * s->dt;
+  if (s->detailed) s->omega = s->omega + s->d_omega * s->mach_dt;
+}
+static void next_time(o_ship* s) { s->time = s->time + s->dt; } /* utils.py:42-48 */
+
+/* ------------------------------------------------------------------------------------------ */
+/* controllers (rl_env/.../controllers.py; run_colav/.../controllers.py) and LOS guidance      */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { double kp, ki, error_i, init_error_i, dt; } o_pi;            /* :45-92 */
+typedef struct { double kp, kd, ki, error_i, prev_error, dt; } o_pid;          /* :94-149 */
+
+static double pi_ctrl(o_pi* c, double setpoint, double meas) { /* :55-65 */
+  double error = setpoint - meas;
+  double error_i = c->error_i + error * c->dt;
+  c->error_i = error_i;
+  return error * c->kp + error_i * c->ki;
+}
+static double pid_ctrl(o_pid* c, double setpoint, double meas) { /* :106-118 */
+  double error = setpoint - meas;
+  double d_error = (error - c->prev_error) / c->dt;
+  double error_i = c->error_i + error * c->dt;
+  c->prev_error = error;
+  c->error_i = error_i;
+  return error * c->kp + d_error * c->kd + error_i * c->ki;
+}
+
+typedef struct {
+  int n, n0;
+  double north[SHIPSIM_MAX_ROUTE], east[SHIPSIM_MAX_ROUTE];
+  double north0[SHIPSIM_MAX_ROUTE], east0[SHIPSIM_MAX_ROUTE];
+  double ra, r, ki, e_ct, e_ct_int, limit;
+} o_nav; /* LOS_guidance.py NavigationSystem :26-136 */
+
+static void nav_next_wpt(const o_nav* nv, int k, double N, double E, int* nk, int* pk) { /* :83-98 */
+  double dn = nv->north[k] - N, de = nv->east[k] - E;
+  if (dn * dn + de * de <= nv->ra * nv->ra) {
+    if (nv->n > k + 1) { *nk = k + 1; *pk = k; }
+    else { *nk = k; *pk = k; }
+  } else {
+    *nk = k; *pk = k - 1;
+  }
+}
+static double nav_los(o_nav* nv, int k, double x, double y) { /* :100-117 */
+  double dx = nv->north[k] - nv->north[k - 1];
+  double dy = nv->east[k] - nv->east[k - 1];
+  double alpha_k = atan2(dy, dx);
+  double e_ct = -(x - nv->north[k - 1]) * sin(alpha_k) + (y - nv->east[k - 1]) * cos(alpha_k);
+  nv->e_ct = e_ct;
+  if (e_ct * e_ct >= nv->r * nv->r) {
+    e_ct = 0.99 * nv->r;
+    nv->e_ct = e_ct;
+  }
+  double delta = py_max(1e-6, sqrt(nv->r * nv->r - e_ct * e_ct));
+  if (fabs(nv->e_ct_int + e_ct / delta) <= nv->limit) nv->e_ct_int += e_ct / delta;
+  double chi_r = atan(-e_ct / delta - nv->e_ct_int * nv->ki);
+  return alpha_k + chi_r;
+}
+static void nav_reset(o_nav* nv) { /* :129-136 */
+  nv->e_ct = 0.0;
+  nv->e_ct_int = 0.0;
+  nv->n = nv->n0;
+  for (int i = 0; i < nv->n0; ++i) { nv->north[i] = nv->north0[i]; nv->east[i] = nv->east0[i]; }
+}
+
+typedef struct {
+  o_pid hdg;
+  double max_rudder;
+  o_nav nav;
+  int next_wpt, prev_wpt;
+  double heading_ref, heading_mea;
+} o_autopilot; /* HeadingBySampledRouteController :344-429 / HeadingByRouteController :276-342 */
+
+/* rudder_angle_from_sampled_route :385-393 (HeadingByReferenceController :246-255) */
+static double ap_rudder(o_autopilot* ap, double n, double e, double heading, double offset) {
+  nav_next_wpt(&ap->nav, ap->next_wpt, n, e, &ap->next_wpt, &ap->prev_wpt);
+  ap->heading_ref = nav_los(&ap->nav, ap->next_wpt, n, e);
+  ap->heading_mea = heading;
+  double rudder = -pid_ctrl(&ap->hdg, ap->heading_ref + offset, heading);
+  return sat(rudder, -ap->max_rudder, ap->max_rudder);
+}
+static void ap_reset(o_autopilot* ap) { /* :413-428 */
+  ap->next_wpt = 1; ap->prev_wpt = 0; ap->heading_ref = 0; ap->heading_mea = 0;
+  ap->hdg.error_i = 0; ap->hdg.prev_error = 0;
+  nav_reset(&ap->nav);
+}
+static void ap_update_route(o_autopilot* ap, double iw_n, double iw_e) { /* :377-382 list.insert(-1) */
+  o_nav* nv = &ap->nav;
+  nv->north[nv->n] = nv->north[nv->n - 1];
+  nv->east[nv->n] = nv->east[nv->n - 1];
+  nv->north[nv->n - 1] = iw_n;
+  nv->east[nv->n - 1] = iw_e;
+  nv->n += 1;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* one ship asset (env.py ShipAssets :29-39)                                                  */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  o_ship m;
+  o_autopilot ap;
+  o_pi ship_speed, shaft_speed; double max_shaft_speed; /* EngineThrottleFromSpeedSetPoint :157-209 */
+  o_pid thrust_pid; double max_thrust;                  /* ThrustFromSpeedSetPoint run_colav :156-195 */
+  double desired_speed;
+  int stop_flag;
+  double length_cfg, width_cfg;
+  /* last simulation_results row (what [-1] lookups see) */
+  double log_n, log_e, log_ect, log_rudder, log_thrust;
+  int has_log;
+  /* optional per-tick log sink */
+  double* log_buf;
+  int log_cap, log_len;
+  double last_row[13];
+} o_asset;
+
+static void asset_init(o_asset* a, const shipsim_config* cfg, int which) {
+  const shipsim_ship_config* c = &cfg->ship[which];
+  memset(a, 0, sizeof(*a));
+  int detailed = cfg->machinery == SHIPSIM_MACH_DETAILED;
+  ship_init(&a->m, cfg, c, detailed);
+  a->ap.hdg.kp = c->heading_kp; a->ap.hdg.kd = c->heading_kd; a->ap.hdg.ki = c->heading_ki;
+  a->ap.hdg.dt = cfg->time_step;
+  a->ap.max_rudder = c->max_rudder_angle_degrees * PI / 180;
+  a->ap.nav.ra = c->radius_of_acceptance;
+  a->ap.nav.r = c->lookahead_distance;
+  a->ap.nav.ki = c->los_integral_gain;
+  a->ap.nav.limit = c->los_integrator_windup_limit;
+  a->ap.nav.n0 = c->n_route;
+  for (int i = 0; i < c->n_route; ++i) { a->ap.nav.north0[i] = c->route_north[i]; a->ap.nav.east0[i] = c->route_east[i]; }
+  ap_reset(&a->ap);
+  a->ship_speed.kp = c->kp_ship_speed; a->ship_speed.ki = c->ki_ship_speed; a->ship_speed.dt = cfg->time_step;
+  a->ship_speed.init_error_i = a->ship_speed.error_i = 0;
+  a->shaft_speed.kp = c->kp_shaft_speed; a->shaft_speed.ki = c->ki_shaft_speed; a->shaft_speed.dt = cfg->time_step;
+  a->shaft_speed.init_error_i = a->shaft_speed.error_i = c->initial_shaft_speed_integral_error;
+  a->max_shaft_speed = a->m.shaft_speed_max;
+  a->thrust_pid.kp = c->speed_kp; a->thrust_pid.ki = c->speed_ki; a->thrust_pid.kd = c->speed_kd;
+  a->thrust_pid.dt = cfg->time_step;
+  a->max_thrust = c->max_thrust;
+  a->desired_speed = c->desired_forward_speed;
+  a->length_cfg = c->length_of_ship;
+  a->width_cfg = c->width_of_ship;
+}
+
+static void asset_reset(o_asset* a, int quirk) { /* env.py:252-271 */
+  ship_reset(&a->m, quirk);
+  a->ship_speed.error_i = a->ship_speed.init_error_i;
+  a->shaft_speed.error_i = a->shaft_speed.init_error_i;
+  a->thrust_pid.error_i = 0; a->thrust_pid.prev_error = 0;
+  ap_reset(&a->ap);
+  a->stop_flag = 0;
+  a->has_log = 0;
+  a->log_len = 0;
+}
+
+/* throttle (detailed, controllers.py:185-189, Q2: measured_shaft_speed = forward speed) or thrust
+ * (simplified, run_colav controllers.py:183-185) */
+static double speed_ctrl(o_asset* a, double setpoint, double u) {
+  if (a->m.detailed) {
+    double desired_shaft = pi_ctrl(&a->ship_speed, setpoint, u);
+    desired_shaft = sat(desired_shaft, 0, a->max_shaft_speed);
+    double thr = pi_ctrl(&a->shaft_speed, desired_shaft, u);
+    return sat(thr, 0, 1.1);
+  }
+  double t = pid_ctrl(&a->thrust_pid, setpoint, u);
+  return sat(t, -a->max_thrust, a->max_thrust);
+}
+
+/* store_simulation_data (ship_model.py:903-942 / run_colav :418-429): keep the last row */
+static void asset_store(o_asset* a, double ctrl, double rudder) {
+  o_ship* m = &a->m;
+  double thrust_logged;
+  if (m->detailed) {
+    fuel_consumption(m, ctrl);
+    thrust_logged = mach_thrust(m) / 1000;
+  } else {
+    thrust_logged = ctrl;
+  }
+  double row[13] = {m->time, m->north, m->east, m->yaw * 180 / PI, rudder * 180 / PI, m->u, m->v,
+                    m->r * 180 / PI, m->detailed ? m->omega * 30 / PI : 0.0, thrust_logged, a->ap.nav.e_ct,
+                    fabs(a->ap.heading_mea - a->ap.heading_ref), m->detailed ? m->fuel_cons : 0.0};
+  memcpy(a->last_row, row, sizeof(row));
+  a->log_n = m->north; a->log_e = m->east; a->log_ect = a->ap.nav.e_ct;
+  a->log_rudder = rudder; a->log_thrust = thrust_logged;
+  a->has_log = 1;
+  if (a->log_buf && a->log_len < a->log_cap) memcpy(a->log_buf + 13 * a->log_len++, row, sizeof(row));
+}
+/* store_last_simulation_data (ship_model.py:946-957): repeat the last row with the current time */
+static void asset_store_last(o_asset* a) {
+  a->last_row[0] = a->m.time;
+  if (a->log_buf && a->log_len < a->log_cap) memcpy(a->log_buf + 13 * a->log_len++, a->last_row, sizeof(a->last_row));
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* map (obstacle.py PolygonObstacle :92-141) — shapely/GEOS semantics restated                 */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int n_polys;
+  int start[SHIPSIM_MAX_POLYS + 1];
+  double x[SHIPSIM_MAX_VERTS], y[SHIPSIM_MAX_VERTS]; /* x = east, y = north */
+  double min_north, max_north, min_east, max_east;
+} o_map;
+
+static void map_init(o_map* mp, const shipsim_config* cfg) {
+  mp->n_polys = cfg->n_polys;
+  for (int p = 0; p <= cfg->n_polys; ++p) mp->start[p] = cfg->poly_start[p];
+  int nv = cfg->poly_start[cfg->n_polys];
+  mp->min_east = mp->max_east = cfg->poly_east[0];
+  mp->min_north = mp->max_north = cfg->poly_north[0];
+  for (int i = 0; i < nv; ++i) {
+    mp->x[i] = cfg->poly_east[i];
+    mp->y[i] = cfg->poly_north[i];
+    mp->min_east = py_min(mp->min_east, mp->x[i]); mp->max_east = py_max(mp->max_east, mp->x[i]);
+    mp->min_north = py_min(mp->min_north, mp->y[i]); mp->max_north = py_max(mp->max_north, mp->y[i]);
+  }
+}
+
+/* GEOS RayCrossingCounter over a closed ring; boundary points are not contained */
+static int poly_contains(const o_map* mp, int p, double px, double py) {
+  int s = mp->start[p], e = mp->start[p + 1], n = e - s;
+  int crossings = 0;
+  for (int i = 0; i < n; ++i) {
+    double x1 = mp->x[s + i], y1 = mp->y[s + i];
+    int j = (i + 1 == n) ? 0 : i + 1;
+    double x2 = mp->x[s + j], y2 = mp->y[s + j];
+    if (x1 < px && x2 < px) continue;
+    if (px == x2 && py == y2) return 0;
+    if (y1 == py && y2 == py) {
+      double mn = py_min(x1, x2), mx = py_max(x1, x2);
+      if (mn <= px && px <= mx) return 0;
+      continue;
+    }
+    if ((y1 > py && y2 <= py) || (y2 > py && y1 <= py)) {
+      double det = (x2 - x1) * (py - y1) - (y2 - y1) * (px - x1);
+      int sign = (det > 0) - (det < 0);
+      if (sign == 0) return 0;
+      if (y2 < y1) sign = -sign;
+      if (sign > 0) crossings++;
+    }
+  }
+  return crossings & 1;
+}
+static int map_inside(const o_map* mp, double n, double e) { /* if_pos_inside_obstacles :126-129 */
+  for (int p = 0; p < mp->n_polys; ++p)
+    if (poly_contains(mp, p, e, n)) return 1;
+  return 0;
+}
+static double pt_seg(double px, double py, double ax, double ay, double bx, double by) { /* GEOS pointToSegment */
+  if (ax == bx && ay == by) return hypot(px - ax, py - ay);
+  double dx = bx - ax, dy = by - ay;
+  double len2 = dx * dx + dy * dy;
+  double r = ((px - ax) * dx + (py - ay) * dy) / len2;
+  if (r <= 0.0) return hypot(px - ax, py - ay);
+  if (r >= 1.0) return hypot(px - bx, py - by);
+  double s = ((ay - py) * dx - (ax - px) * dy) / len2;
+  return fabs(s) * sqrt(len2);
+}
+static double map_distance(const o_map* mp, double n, double e) { /* obstacles_distance :138-141 */
+  double best = INFINITY;
+  for (int p = 0; p < mp->n_polys; ++p) {
+    int s = mp->start[p], en = mp->start[p + 1], cnt = en - s;
+    double d = INFINITY;
+    for (int i = 0; i < cnt; ++i) {
+      int j = (i + 1 == cnt) ? 0 : i + 1;
+      d = py_min(d, pt_seg(e, n, mp->x[s + i], mp->y[s + i], mp->x[s + j], mp->y[s + j]));
+    }
+    best = py_min(best, d);
+  }
+  return best;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* check_condition.py                                                                         */
+/* ------------------------------------------------------------------------------------------ */
+static int is_reaches_endpoint(double ne, double ee, double n, double e) { /* :5-16 */
+  return sqrt((n - ne) * (n - ne) + (e - ee) * (e - ee)) <= 200;
+}
+static int is_pos_outside_horizon(const o_map* mp, double n, double e, double L) { /* :18-48 */
+  double margin = L / 2;
+  int on = n < mp->min_north + margin || n > mp->max_north - margin;
+  int oe = e < mp->min_east + margin || e > mp->max_east - margin;
+  return on || oe;
+}
+static int is_pos_inside_obstacles(const o_map* mp, double n, double e, double L) { /* :50-78 */
+  double margin = L / 2;
+  double mnn = n - margin, mne = e - margin, mxn = n + margin, mxe = e + margin;
+  int inside = 0;
+  if (map_inside(mp, mnn, mne)) inside = 1;
+  if (map_inside(mp, mnn, mxe)) inside = 1;
+  if (map_inside(mp, mxn, mne)) inside = 1;
+  if (map_inside(mp, mxn, mxe)) inside = 1;
+  return inside;
+}
+static int is_route_outside_horizon(const o_map* mp, double n, double e) { /* :80-107 */
+  return (n < mp->min_north || n > mp->max_north) || (e < mp->min_east || e > mp->max_east);
+}
+
+/* compute_distance.py:16-40 ; returns 0 head-on, 1 crossing, 2 overtaking */
+static int encounter(double n1, double e1, double h1, double n2, double e2, double* dist) {
+  double dx = n2 - n1, dy = e2 - e1;
+  *dist = sqrt(dx * dx + dy * dy);
+  double phi = atan2(dy, dx);
+  double beta = phi - h1;
+  beta = floor_mod(beta + PI, 2 * PI) - PI;
+  if (fabs(beta) < DEG2RAD(15.0)) return 0;
+  if (fabs(beta) > DEG2RAD(165.0)) return 2;
+  return 1;
+}
+
+/* reward_designs.py:33-55 */
+static double rd3(double target, double off, double val) { return (val < target) ? exp(-((val - target) * (val - target)) / off) : 1; }
+static double rd4(double target, double off, double val) { return (val < target) ? 1 : exp(-((val - target) * (val - target)) / off); }
+
+/* numpy sum of a 5-vector: a0 + ((((0 + a1) + a2) + a3) + a4) (pairwise_sum n<8 after the first) */
+static double np_sum5(const double* a) {
+  double r = 0.0;
+  for (int i = 1; i < 5; ++i) r += a[i];
+  return a[0] + r;
+}
+
+/* reward_function.py:272-314 */
+static double termination_reward(double r_total, double acc, const int cond[5]) {
+  static const double mult[5] = {10.0, 5.0, 5.0, -2.5, -2.5};
+  int any = 0;
+  for (int i = 0; i < 5; ++i) any |= cond[i];
+  if (!any) return r_total;
+  double reward = r_total + acc;
+  double out = 0;
+  for (int i = 0; i < 5; ++i) {
+    if (acc > 0 && cond[i]) out += reward * mult[i];
+    else if (acc < 0 && cond[i]) out += reward * -mult[i];
+  }
+  return out;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SBMPC (sbmpc.py :90-314, sbmpc_misc.py :34-123)                                            */
+/* ------------------------------------------------------------------------------------------ */
+#define SB_MAXN 256
+typedef struct { double P_last, Chi_last; int active; } o_sbmpc;
+
+static double sb_cost(const o_sbmpc* sb, int n_samp, double DT, double P_ca, double Chi_ca,
+                      const double* ox, const double* oy, double opsi, double ou0, double ov0, double obs_l,
+                      double obs_w, const double* sx, const double* sy, const double* spsi, const double* su,
+                      const double* sv) {
+  const double os_l = 25, os_w = 80; /* ShipLinearModel defaults (sbmpc_misc.py:86, Q7) */
+  (void)os_w;
+  const double d_safe = 1000.0, d_close = 2000.0;
+  const double PHI_AH = DEG2RAD(68.5), PHI_OT = DEG2RAD(68.5);
+  double H0, H1 = 0, t = 0, t0 = 0;
+  for (int i = 0; i < n_samp; ++i) {
+    t += DT;
+    double d0 = ox[i] - sx[i], d1 = oy[i] - sy[i];
+    double dist = sqrt(d0 * d0 + d1 * d1);
+    double R = 0, C = 0;
+    if (dist < d_close) {
+      /* rot2d :312-314 */
+      double vo0 = -sin(opsi) * ou0 + cos(opsi) * ov0;
+      double vo1 = cos(opsi) * ou0 + sin(opsi) * ov0;
+      double vs0 = -sin(spsi[i]) * su[i] + cos(spsi[i]) * sv[i];
+      double vs1 = cos(spsi[i]) * su[i] + sin(spsi[i]) * sv[i];
+      double phi_o = wrap_pmpi(atan2(-d1, -d0) - opsi + PI / 2);
+      double d_safe_i;
+      if (phi_o < PHI_AH) d_safe_i = d_safe + obs_l / 2;
+      else if (phi_o > PHI_OT) d_safe_i = 0.5 * d_safe + obs_l / 2;
+      else d_safe_i = d_safe + obs_w / 2;
+      double dot = vs0 * vo0 + vs1 * vo1;
+      double ns = sqrt(vs0 * vs0 + vs1 * vs1), no = sqrt(vo0 * vo0 + vo1 * vo1);
+      if (dot > cos(DEG2RAD(PHI_OT)) * ns * no && ns > no) d_safe_i = d_safe + os_l / 2 + obs_l / 2;
+      if (dist < d_safe_i) {
+        R = (1 / pow(fabs(t - t0), 1.0)) * pow(d_safe / dist, 4.0);
+        double k_coll = 1e-6 * os_l * obs_l;
+        double w0 = vs0 - vo0, w1 = vs1 - vo1;
+        double nrm = sqrt(w0 * w0 + w1 * w1);
+        C = k_coll * (nrm * nrm);
+      }
+    }
+    H0 = C * R + 0.0 * 0;
+    if (H0 > H1) H1 = H0;
+  }
+  double dchi = Chi_ca - sb->Chi_last;
+  double dChi = (dchi > 0) ? 20 * dchi * dchi : (dchi < 0 ? 30 * dchi * dchi : 0);
+  double H2 = 25 * (1 - P_ca) + 30 * (Chi_ca * Chi_ca) + 20 * fabs(sb->P_last - P_ca) + dChi;
+  return H1 + H2;
+}
+
+/* get_optimal_ctrl_offset :113-185 for one dynamic obstacle */
+static void sbmpc_offset(o_sbmpc* sb, double T, double DT, double u_d, double chi_d, const double os[6],
+                         const double ob[5], double obs_l, double obs_w, double* P_best, double* Chi_best) {
+  int n = (int)(T / DT);
+  if (n > SB_MAXN) n = SB_MAXN;
+  double ox[SB_MAXN], oy[SB_MAXN], ou[SB_MAXN], ov[SB_MAXN];
+  /* Obstacle.__init__ / calculate_trajectory sbmpc_misc.py:35-83 */
+  double opsi = ob[2];
+  double r11 = -sin(opsi), r12 = cos(opsi), r21 = cos(opsi), r22 = sin(opsi);
+  ox[0] = ob[0]; oy[0] = ob[1]; ou[0] = ob[3]; ov[0] = ob[4];
+  for (int i = 1; i < n; ++i) {
+    ox[i] = ox[i - 1] + (r11 * ou[i - 1] + r12 * ov[i - 1]) * DT;
+    oy[i] = oy[i - 1] + (r21 * ou[i - 1] + r22 * ov[i - 1]) * DT;
+    ou[i] = ou[i - 1];
+    ov[i] = ov[i - 1];
+  }
+  sb->active = 0;
+  double d0 = ox[0] - os[0], d1 = oy[0] - os[1];
+  if (sqrt(d0 * d0 + d1 * d1) < 2000.0) sb->active = 1;
+  if (!sb->active) {
+    *P_best = 1; *Chi_best = 0;
+    sb->P_last = 1; sb->Chi_last = 0;
+    return;
+  }
+  static const double CHI_DEG[7] = {-30.0, -20.0, -10.0, 0.0, 10.0, 20.0, 30.0};
+  static const double P_CA[4] = {0.4, 0.6, 0.8, 1.0};
+  double cost = INFINITY, pb = 1, cb = 0;
+  double sx[SB_MAXN], sy[SB_MAXN], spsi[SB_MAXN], su[SB_MAXN], sv[SB_MAXN];
+  for (int i = 0; i < 7; ++i) {
+    double chi_ca = DEG2RAD(CHI_DEG[i]);
+    for (int j = 0; j < 4; ++j) {
+      /* ShipLinearModel.linear_pred sbmpc_misc.py:103-123 */
+      double ud = u_d * P_CA[j], psi_d = chi_d + chi_ca;
+      spsi[0] = wrap_pmpi(psi_d);
+      sx[0] = os[0]; sy[0] = os[1]; su[0] = ud; sv[0] = os[4];
+      double q11 = -sin(psi_d), q12 = cos(psi_d), q21 = cos(psi_d), q22 = sin(psi_d);
+      for (int k = 1; k < n; ++k) {
+        sx[k] = sx[k - 1] + DT * (q11 * su[k - 1] + q12 * sv[k - 1]);
+        sy[k] = sy[k - 1] + DT * (q21 * su[k - 1] + q22 * sv[k - 1]);
+        spsi[k] = psi_d;
+        su[k] = ud;
+        sv[k] = 0;
+      }
+      double cost_i = -1;
+      double ck = sb_cost(sb, n, DT, P_CA[j], chi_ca, ox, oy, opsi, ou[0], ov[0], obs_l, obs_w, sx, sy, spsi, su, sv);
+      if (ck > cost_i) cost_i = ck;
+      if (cost_i < cost) { cost = cost_i; pb = P_CA[j]; cb = chi_ca; }
+    }
+  }
+  sb->P_last = pb; sb->Chi_last = cb;
+  *P_best = pb; *Chi_best = cb;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* environments                                                                               */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  shipsim_config cfg;
+  o_asset a[2]; /* [test, obs] */
+  o_map map;
+  o_sbmpc sb;
+  /* intermediate waypoint sampler env.py:143-169 */
+  double AB_length, AB_seg, AB_seg_n, AB_seg_e, omega, n_base, e_base;
+  int sampling_count, tracker_active;
+  double travel_dist, travel_time;
+  double accumulated_rewards;
+  float initial_states[8], states[8], next_observations[8];
+  uint32_t snap_bits; /* self.env_info snapshot */
+  double last_reward_tick;
+  int ticks_total;
+  double* rtick_buf; int rtick_cap, rtick_len;
+} o_env;
+
+static void env_init_iw(o_env* env) { /* init_get_intermediate_waypoints env.py:143-169 */
+  o_nav* nv = &env->a[1].ap.nav;
+  double ABn = nv->north[nv->n - 1] - nv->north[0];
+  double ABe = nv->east[nv->n - 1] - nv->east[0];
+  int msf = env->cfg.max_sampling_frequency;
+  env->AB_length = sqrt(ABn * ABn + ABe * ABe);
+  env->AB_seg = env->AB_length / (msf + 1);
+  env->AB_seg_n = ABn / (msf + 1);
+  env->AB_seg_e = ABe / (msf + 1);
+  double AB_alpha = atan2(ABe, ABn);
+  double AB_beta = PI / 2 - AB_alpha;
+  env->omega = PI / 2 - AB_beta;
+  env->n_base = env->AB_seg_n + nv->north[0];
+  env->e_base = env->AB_seg_e + nv->east[0];
+  env->sampling_count = 0;
+  env->tracker_active = 0;
+  env->travel_dist = 0;
+  env->travel_time = 0;
+}
+
+o_env* oracle_env_create(const shipsim_config* cfg) {
+  o_env* env = (o_env*)calloc(1, sizeof(o_env));
+  env->cfg = *cfg;
+  int ns = cfg->kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
+  for (int i = 0; i < ns; ++i) asset_init(&env->a[i], cfg, i);
+  map_init(&env->map, cfg);
+  env->sb.P_last = 1.0;
+  env->sb.Chi_last = 0.0;
+  if (ns == 2) {
+    env_init_iw(env);
+    /* env.py:107-113 initial_states */
+    float* s = env->initial_states;
+    s[0] = (float)env->a[0].m.north; s[1] = (float)env->a[0].m.east; s[2] = 0.0f;
+    s[3] = (float)env->a[1].m.north; s[4] = (float)env->a[1].m.east; s[5] = (float)env->a[1].m.yaw;
+    s[6] = 0.0f; s[7] = (float)env->a[1].m.u;
+    memcpy(env->states, s, sizeof(env->states));
+    memcpy(env->next_observations, s, sizeof(env->states));
+  }
+  return env;
+}
+void oracle_env_destroy(o_env* env) { free(env); }
+
+void oracle_env_set_log(o_env* env, int ship, double* buf, int cap) {
+  env->a[ship].log_buf = buf; env->a[ship].log_cap = cap; env->a[ship].log_len = 0;
+}
+int oracle_env_log_len(const o_env* env, int ship) { return env->a[ship].log_len; }
+void oracle_env_set_rtick(o_env* env, double* buf, int cap) { env->rtick_buf = buf; env->rtick_cap = cap; env->rtick_len = 0; }
+int oracle_env_rtick_len(const o_env* env) { return env->rtick_len; }
+
+/* one non-frozen ship tick body shared by init_step / test_step / obs_step */
+static void ship_tick(o_asset* a, double rudder, double ctrl) {
+  asset_store(a, ctrl, rudder);
+  update_differentials(&a->m, ctrl, rudder);
+  integrate_differentials(&a->m);
+  next_time(&a->m);
+}
+
+static void env_init_step(o_env* env) { /* init_step env.py:297-342 (run_colav/env.py:279-323) */
+  int ns = env->cfg.kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
+  for (int i = 0; i < ns; ++i) {
+    o_asset* a = &env->a[i];
+    double n = a->m.north, e = a->m.east, h = a->m.yaw, u = a->m.u;
+    double rudder = ap_rudder(&a->ap, n, e, h, 0.0);
+    double ctrl = speed_ctrl(a, a->desired_speed, u);
+    ship_tick(a, rudder, ctrl);
+  }
+  env->tracker_active = 1;
+}
+
+/* SBMPC block of test_step env.py:360-385 (and run_colav/env.py:371-396 / :502-527) */
+static void sbmpc_block(o_env* env, o_asset* self, double n, double e, double* sf, double* off) {
+  int nk, pk;
+  nav_next_wpt(&self->ap.nav, self->ap.next_wpt, n, e, &nk, &pk); /* result discarded (self.next_wpt) */
+  double chi_d = nav_los(&self->ap.nav, self->ap.next_wpt, n, e); /* Q3: integrates e_ct_int */
+  double u_d = self->desired_speed;
+  const o_ship* o = &env->a[0].m;
+  double os[6] = {o->east, o->north, -o->yaw, o->u, o->v, o->r};
+  const o_ship* b = &env->a[1].m;
+  double ob[5] = {b->east, b->north, -b->yaw, b->u, b->v};
+  sbmpc_offset(&env->sb, env->cfg.sbmpc_tf, env->cfg.sbmpc_dt, u_d, -chi_d, os, ob, env->a[1].length_cfg,
+               env->a[1].width_cfg, sf, off);
+}
+
+/* float32 is_collision_imminent on self.states (check_condition.py:130-140) */
+static int imminent_f32(const float* st) {
+  float dn = st[0] - st[3], de = st[1] - st[4];
+  float d2 = dn * dn + de * de;
+  return d2 < 9000000.0f;
+}
+
+/* RL env test_step env.py:345-445 */
+static void ast_test_step(o_env* env, float out3[3]) {
+  o_asset* a = &env->a[0];
+  double n = a->m.north, e = a->m.east, h = a->m.yaw, u = a->m.u;
+  double sf = 1.0, off = 0.0;
+  if (env->cfg.collav == SHIPSIM_COLLAV_SBMPC) sbmpc_block(env, a, n, e, &sf, &off);
+  double rudder = ap_rudder(&a->ap, n, e, h, -off);
+  double thr = speed_ctrl(a, a->desired_speed * sf, u);
+  if (env->cfg.collav == SHIPSIM_COLLAV_SIMPLE) {
+    if (imminent_f32(env->states)) {
+      thr *= 0.5;
+      thr = py_min(py_max(thr, 0.0), 1.1); /* np.clip */
+      rudder += DEG2RAD(-15.0);
+      rudder = py_min(py_max(rudder, -a->ap.max_rudder), a->ap.max_rudder);
+    }
+  }
+  ship_tick(a, rudder, thr);
+  out3[0] = (float)a->m.north; out3[1] = (float)a->m.east; out3[2] = (float)a->log_ect;
+}
+
+/* RL env obs_step env.py:447-536 */
+static void ast_obs_step(o_env* env, float out5[5]) {
+  o_asset* a = &env->a[1];
+  if (a->stop_flag) {
+    asset_store_last(a);
+    next_time(&a->m);
+    next_time(&a->m); /* Q9 */
+    out5[0] = (float)a->m.north; out5[1] = (float)a->m.east; out5[2] = (float)a->m.yaw; out5[3] = 0.0f;
+    out5[4] = (float)a->log_ect;
+    return;
+  }
+  double n = a->m.north, e = a->m.east, h = a->m.yaw, u = a->m.u;
+  double prev_log_n = a->log_n, prev_log_e = a->log_e;
+  double rudder = ap_rudder(&a->ap, n, e, h, 0.0);
+  double thr = speed_ctrl(a, a->desired_speed, u);
+  ship_tick(a, rudder, thr);
+  out5[0] = (float)a->m.north; out5[1] = (float)a->m.east; out5[2] = (float)a->m.yaw; out5[3] = (float)u;
+  out5[4] = (float)a->log_ect;
+  if (env->tracker_active) { /* Q6 */
+    double tn = a->log_n - prev_log_n, te = a->log_e - prev_log_e;
+    env->travel_dist += sqrt(tn * tn + te * te);
+    env->travel_time += a->m.dt;
+  }
+}
+
+/* get_reward_and_env_info reward_function.py:59-270 (+ get_env_info run_colav :53-225 when
+ * with_reward == 0). Returns r_total, fills event bits. */
+static double reward_and_info(o_env* env, uint32_t* bits_out, int with_reward) {
+  o_asset* T = &env->a[0];
+  o_asset* O = &env->a[1];
+  const o_map* mp = &env->map;
+  double tn = T->m.north, te = T->m.east, th = T->m.yaw, tect = T->log_ect, tL = T->m.l_ship;
+  double on = O->m.north, oe = O->m.east, oect = O->log_ect, oL = O->m.l_ship;
+  double dist;
+  int enc = encounter(tn, te, th, on, oe, &dist);
+  double cd = (tn - on) * (tn - on) + (te - oe) * (te - oe);
+  int is_collision = cd < 50.0 * 50.0;
+  double t_ground = map_distance(mp, tn, te);
+  int is_tg = is_pos_inside_obstacles(mp, tn, te, tL);
+  double o_ground = map_distance(mp, on, oe);
+  int is_og = is_pos_inside_obstacles(mp, on, oe, oL);
+  int is_tnav = fabs(tect) > 3000;
+  int is_onav = (env->travel_dist > env->AB_seg * 2) || (env->travel_time > INFINITY) || (fabs(oect) > 500);
+  double r_total = 0;
+  if (with_reward) {
+    double r[5] = {0, 0, 0, 0, 0};
+    if (dist < 10000 && (enc == 0 || enc == 1)) r[0] = rd4(0, 200000000, dist); /* :316-357 */
+    if (t_ground <= 1000) r[1] = rd4(0, 175000, t_ground);                     /* :359-396 */
+    r[2] = rd3(3000, 1250000, fabs(tect));                                     /* :398-427 */
+    if (o_ground <= 1000) r[3] = -rd4(0, 50000, o_ground);                     /* :429-466 */
+    r[4] = -rd3(500, 12500, fabs(oect));                                       /* :468-497 */
+    r_total = np_sum5(r) / 5;
+    int cond[5] = {is_collision, is_tg, is_tnav, is_og, is_onav};
+    r_total = termination_reward(r_total, env->accumulated_rewards, cond);
+  }
+  int t6 = is_reaches_endpoint(T->ap.nav.north[T->ap.nav.n - 1], T->ap.nav.east[T->ap.nav.n - 1], tn, te);
+  int t7 = is_pos_outside_horizon(mp, tn, te, tL);
+  int t8 = is_reaches_endpoint(O->ap.nav.north[O->ap.nav.n - 1], O->ap.nav.east[O->ap.nav.n - 1], on, oe);
+  int t9 = is_pos_outside_horizon(mp, on, oe, oL);
+  int t10 = T->m.time > T->m.sim_time;
+  int flags[10] = {is_collision, is_tg, is_tnav, is_og, is_onav, t6, t7, t8, t9, t10};
+  static const int term[10] = {1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+  static const int tstop[10] = {1, 1, 1, 0, 0, 1, 1, 0, 0, 1};
+  static const int ostop[10] = {1, 0, 0, 1, 1, 0, 0, 1, 1, 1};
+  uint32_t bits = 0;
+  for (int i = 0; i < 10; ++i) {
+    if (!flags[i]) continue;
+    bits |= 1u << i;
+    if (term[i]) bits |= SHIPSIM_EV_TERMINAL;
+    if (tstop[i]) bits |= SHIPSIM_EV_TEST_STOP;
+    if (ostop[i]) bits |= SHIPSIM_EV_OBS_STOP;
+  }
+  *bits_out = bits;
+  return r_total;
+}
+
+/* MultiShipRLEnv._step env.py:563-622 */
+static double ast_underscore_step(o_env* env, float obs8[8], int* combined_done, uint32_t* bits) {
+  float t3[3], o5[5];
+  ast_test_step(env, t3);
+  ast_obs_step(env, o5);
+  float ns[8] = {t3[0], t3[1], t3[2], o5[0], o5[1], o5[2], o5[3], o5[4]};
+  memcpy(env->states, ns, sizeof(ns));
+  memcpy(obs8, ns, sizeof(ns));
+  double r = reward_and_info(env, bits, 1);
+  int terminal = (*bits & SHIPSIM_EV_TERMINAL) != 0;
+  int done = ((*bits & SHIPSIM_EV_TEST_STOP) != 0) && !terminal;
+  int obs_stop = ((*bits & SHIPSIM_EV_OBS_STOP) != 0) && !terminal;
+  if (obs_stop) env->a[1].stop_flag = 1;
+  *combined_done = terminal || done;
+  env->ticks_total++;
+  if (env->rtick_buf && env->rtick_len < env->rtick_cap) env->rtick_buf[env->rtick_len++] = r;
+  return r;
+}
+
+/* MultiShipRLEnv.reset env.py:238-295 */
+void oracle_env_reset(o_env* env, float obs8[8]) {
+  if (env->cfg.kind == SHIPSIM_KIND_SINGLE) { /* ship_model/throttle/auto_pilot .reset() only */
+    asset_reset(&env->a[0], env->cfg.machinery_dt_quirk);
+    return;
+  }
+  for (int i = 0; i < 2; ++i) asset_reset(&env->a[i], env->cfg.machinery_dt_quirk);
+  env_init_iw(env);
+  memcpy(env->next_observations, env->initial_states, sizeof(env->initial_states));
+  env->accumulated_rewards = 0;
+  env->snap_bits = 0;
+  env->rtick_len = 0;
+  env_init_step(env);
+  if (obs8) memcpy(obs8, env->initial_states, sizeof(env->initial_states));
+}
+
+/* is_reach_radius_of_acceptance check_condition.py:181-205 */
+static int reach_roa(const o_env* env) {
+  const o_asset* O = &env->a[1];
+  int k = O->ap.next_wpt;
+  double dn = O->m.north - O->ap.nav.north[k], de = O->m.east - O->ap.nav.east[k];
+  double d2 = dn * dn + de * de;
+  double roa = env->cfg.env_radius_of_acceptance;
+  return d2 < roa * roa;
+}
+
+/* MultiShipRLEnv.step env.py:624-773. `a` is the (denormalized) float32 scoping angle. */
+int oracle_env_step(o_env* env, float a, int max_ticks, float obs8[8], double* reward, int* done_out,
+                    uint32_t* bits_out) {
+  int is_reach_roa = 0, combined_done = 0, have_iw = 0, ticks = 0;
+  float next_obs[8];
+  double acc_out = 0;
+  uint32_t bits = 0;
+  float sa = a;
+  if (env->cfg.normalize_action) /* do_denormalize_action :192-196 */
+    sa = (sa + 1.0f) / 2.0f * (env->cfg.action_high - env->cfg.action_low) + env->cfg.action_low;
+  if (env->sampling_count < env->cfg.max_sampling_frequency) {
+    /* obs_ship_uses_scoping_angle :538-561 -> get_intermediate_waypoints :198-236 */
+    env->sampling_count += 1;
+    float tn = (float)tan((double)sa);
+    double l_s = fabs(env->AB_seg * (double)tn);
+    double e_s = l_s * cos(env->omega);
+    double n_s = l_s * sin(env->omega);
+    if (sa > 0) e_s *= -1;
+    else n_s *= -1;
+    double iw_n = env->n_base + n_s, iw_e = env->e_base + e_s;
+    env->n_base = iw_n + env->AB_seg_n;
+    env->e_base = iw_e + env->AB_seg_e;
+    ap_update_route(&env->a[1].ap, iw_n, iw_e);
+    env->travel_dist = 0;
+    env->travel_time = 0;
+    have_iw = 1;
+    int fail = map_inside(&env->map, iw_n, iw_e) || is_route_outside_horizon(&env->map, iw_n, iw_e);
+    if (fail) {
+      double acc = env->accumulated_rewards;
+      double r = (acc >= 0) ? -acc * 2.0 : acc * 2.0; /* reward_function.py:499-527 */
+      env->snap_bits |= SHIPSIM_EV_SAMPLING_FAILURE | SHIPSIM_EV_TERMINAL;
+      env->snap_bits &= ~(SHIPSIM_EV_TEST_STOP | SHIPSIM_EV_OBS_STOP);
+      memcpy(obs8, env->next_observations, sizeof(next_obs));
+      *reward = r;
+      *done_out = 1;
+      *bits_out = env->snap_bits;
+      return 0;
+    }
+    env->accumulated_rewards = 0;
+  }
+  while (!is_reach_roa && !combined_done) {
+    if (max_ticks > 0 && ticks >= max_ticks) break;
+    double r = ast_underscore_step(env, next_obs, &combined_done, &bits);
+    ticks++;
+    env->accumulated_rewards += r;
+    is_reach_roa = reach_roa(env);
+    if (combined_done) {
+      acc_out = env->accumulated_rewards;
+      memcpy(env->next_observations, next_obs, sizeof(next_obs));
+      env->snap_bits = bits;
+      break;
+    }
+    if (is_reach_roa && have_iw) {
+      r = ast_underscore_step(env, next_obs, &combined_done, &bits);
+      ticks++;
+      env->accumulated_rewards += r;
+      acc_out = env->accumulated_rewards;
+      if (env->sampling_count == env->cfg.max_sampling_frequency) {
+        env->travel_dist = 0;
+        env->travel_time = 0;
+        while (!combined_done) {
+          if (max_ticks > 0 && ticks >= max_ticks) break;
+          r = ast_underscore_step(env, next_obs, &combined_done, &bits);
+          ticks++;
+          env->accumulated_rewards += r;
+          acc_out = env->accumulated_rewards;
+        }
+      }
+      memcpy(env->next_observations, next_obs, sizeof(next_obs));
+      env->snap_bits = bits;
+      break;
+    }
+  }
+  memcpy(obs8, next_obs, sizeof(next_obs));
+  *reward = acc_out;
+  *done_out = combined_done;
+  *bits_out = bits;
+  return ticks;
+}
+
+/* ---------------- C1: MultiShipNonIWEnv (run_colav/env.py:37-677) ---------------- */
+static void noniw_ship_step(o_env* env, int which, float out[5]) { /* test_step :326-455 / obs_step :457-586 */
+  o_asset* a = &env->a[which];
+  if (a->stop_flag) {
+    asset_store_last(a);
+    next_time(&a->m);
+    next_time(&a->m);
+    out[0] = (float)a->m.north; out[1] = (float)a->m.east; out[2] = (float)a->m.yaw; out[3] = 0.0f;
+    out[4] = (float)a->log_ect;
+    return;
+  }
+  double n = a->m.north, e = a->m.east, h = a->m.yaw, u = a->m.u;
+  double sf = 1.0, off = 0.0;
+  if (env->cfg.collav == SHIPSIM_COLLAV_SBMPC) sbmpc_block(env, a, n, e, &sf, &off);
+  double rudder = ap_rudder(&a->ap, n, e, h, -off);
+  double thr = speed_ctrl(a, a->desired_speed * sf, u);
+  if (env->cfg.collav == SHIPSIM_COLLAV_SIMPLE) {
+    /* self.states here is the 6-vector [t_n, t_e, t_ect, o_n, o_e, o_ect] (:632-639) */
+    if (imminent_f32(env->states)) {
+      thr *= 0.5;
+      thr = py_min(py_max(thr, 0.0), 1.1);
+      rudder += DEG2RAD(15.0);
+      rudder = py_min(py_max(rudder, -a->ap.max_rudder), a->ap.max_rudder);
+    }
+  }
+  ship_tick(a, rudder, thr);
+  out[0] = (float)a->m.north; out[1] = (float)a->m.east; out[2] = (float)a->log_ect;
+}
+
+/* _step :613-676; returns event bits */
+static uint32_t noniw_underscore_step(o_env* env) {
+  float t[5], o[5];
+  noniw_ship_step(env, 0, t);
+  noniw_ship_step(env, 1, o);
+  /* next_states (6): stopped ships report (n, e, yaw) in their first three slots */
+  float s6[6] = {t[0], t[1], t[2], o[0], o[1], o[2]};
+  memset(env->states, 0, sizeof(env->states));
+  memcpy(env->states, s6, sizeof(s6));
+  uint32_t bits;
+  reward_and_info(env, &bits, 0);
+  int terminal = (bits & SHIPSIM_EV_TERMINAL) != 0;
+  if ((bits & SHIPSIM_EV_TEST_STOP) && !terminal) env->a[0].stop_flag = 1;
+  if ((bits & SHIPSIM_EV_OBS_STOP) && !terminal) env->a[1].stop_flag = 1;
+  env->ticks_total++;
+  return bits;
+}
+
+/* C1 loop run_colav/run_simplified_model.py:245-249; returns ticks run */
+int oracle_c1_run(o_env* env, int max_ticks, uint32_t* bits_out, int32_t* stops_out) {
+  env_init_step(env);
+  int k = 0;
+  while (env->a[0].m.time < env->a[0].m.sim_time && k < max_ticks) {
+    uint32_t b = noniw_underscore_step(env);
+    if (bits_out) bits_out[k] = b;
+    if (stops_out) { stops_out[2 * k] = env->a[0].stop_flag; stops_out[2 * k + 1] = env->a[1].stop_flag; }
+    ++k;
+  }
+  return k;
+}
+
+/* k ticks of the single-ship loop body (SINGLE kind), logging into the ship's sink */
+int oracle_single_run(o_env* env, int k) {
+  o_asset* a = &env->a[0];
+  for (int i = 0; i < k; ++i) {
+    double rudder = ap_rudder(&a->ap, a->m.north, a->m.east, a->m.yaw, 0.0);
+    double thr = speed_ctrl(a, a->desired_speed, a->m.u);
+    ship_tick(a, rudder, thr);
+  }
+  return k;
+}
+
+/* ---------------- C2: single ship loop (run_simplified_model.py loop shape, HeadingByRoute) ---- */
+/* init: n x 4 (north, east, yaw, u); final: n x 7 (time, n, e, yaw, u, v, r); trace: n x T x 12 */
+int oracle_c2_run(const shipsim_config* cfg, int n_ships, const double* init, int max_ticks, double* trace,
+                  double* final_out, int n_threads) {
+  int T = 0;
+#pragma omp parallel for schedule(dynamic, 16) num_threads(n_threads > 0 ? n_threads : 1) reduction(max : T)
+  for (int s = 0; s < n_ships; ++s) {
+    shipsim_config c = *cfg;
+    c.ship[0].initial_north_position_m = init[4 * s + 0];
+    c.ship[0].initial_east_position_m = init[4 * s + 1];
+    c.ship[0].initial_yaw_angle_rad = init[4 * s + 2];
+    c.ship[0].initial_forward_speed_m_per_s = init[4 * s + 3];
+    o_asset a;
+    asset_init(&a, &c, 0);
+    int k = 0;
+    while (a.m.time < a.m.sim_time && k < max_ticks) {
+      double rudder = ap_rudder(&a.ap, a.m.north, a.m.east, a.m.yaw, 0.0);
+      double thr = speed_ctrl(&a, a.desired_speed, a.m.u);
+      if (trace) {
+        double* row = trace + ((size_t)s * max_ticks + k) * 12;
+        double v[12] = {a.m.time, a.m.north, a.m.east, a.m.yaw, a.m.u, a.m.v, a.m.r, rudder, thr,
+                        a.ap.nav.e_ct, a.ap.nav.e_ct_int, (double)a.ap.next_wpt};
+        memcpy(row, v, sizeof(v));
+      }
+      ship_tick(&a, rudder, thr);
+      ++k;
+    }
+    double f[7] = {a.m.time, a.m.north, a.m.east, a.m.yaw, a.m.u, a.m.v, a.m.r};
+    memcpy(final_out + 7 * s, f, sizeof(f));
+    if (k > T) T = k;
+  }
+  return T;
+}
+
+/* ---------------- batched AST rollouts (CPU baseline; SURVEY §8(d) C3 input) ----------------- */
+/* Each env: reset, then up to n_dec decisions with actions[env][d] (scoping angles, float32),
+ * stopping at done. Outputs per env: total ticks, decisions taken, sum of rewards. */
+long long oracle_ast_rollouts(const shipsim_config* cfg, int n_envs, int n_dec, const float* actions,
+                              int32_t* ticks_out, int32_t* dec_out, double* ret_out, uint32_t* bits_out,
+                              int n_threads) {
+  long long total = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : 1) reduction(+ : total)
+  for (int i = 0; i < n_envs; ++i) {
+    o_env* env = oracle_env_create(cfg);
+    float obs[8];
+    oracle_env_reset(env, obs);
+    int ticks = 1, d = 0, done = 0;
+    double ret = 0;
+    uint32_t bits = 0;
+    for (d = 0; d < n_dec && !done; ++d) {
+      double r;
+      ticks += oracle_env_step(env, actions[(size_t)i * n_dec + d], 0, obs, &r, &done, &bits);
+      ret += r;
+    }
+    if (ticks_out) ticks_out[i] = ticks;
+    if (dec_out) dec_out[i] = d;
+    if (ret_out) ret_out[i] = ret;
+    if (bits_out) bits_out[i] = bits;
+    total += ticks;
+    oracle_env_destroy(env);
+  }
+  return total;
+}
+
+/* ---------------- state access + pure-function probes for the tests ------------------------- */
+void oracle_env_get_ship(const o_env* env, int which, double out[20]) {
+  const o_asset* a = &env->a[which];
+  double v[20] = {a->m.north, a->m.east, a->m.yaw, a->m.u, a->m.v, a->m.r, a->m.omega, a->m.time,
+                  a->ap.nav.e_ct, a->ap.nav.e_ct_int, a->ap.hdg.error_i, a->ap.hdg.prev_error,
+                  a->m.detailed ? a->ship_speed.error_i : a->thrust_pid.error_i,
+                  a->m.detailed ? a->shaft_speed.error_i : a->thrust_pid.prev_error,
+                  a->log_rudder, a->log_thrust, a->log_ect, (double)a->ap.next_wpt, (double)a->stop_flag,
+                  a->m.mach_dt};
+  memcpy(out, v, sizeof(v));
+}
+void oracle_env_get_env(const o_env* env, double out[12]) {
+  double v[12] = {(double)env->sampling_count, env->travel_dist, env->travel_time, env->accumulated_rewards,
+                  env->n_base, env->e_base, env->sb.P_last, env->sb.Chi_last, (double)env->a[1].ap.nav.n,
+                  env->AB_seg, (double)env->ticks_total, 0};
+  memcpy(out, v, sizeof(v));
+}
+void oracle_env_get_route(const o_env* env, double* north, double* east) {
+  const o_nav* nv = &env->a[1].ap.nav;
+  for (int i = 0; i < nv->n; ++i) { north[i] = nv->north[i]; east[i] = nv->east[i]; }
+}
+
+void oracle_sbmpc(double tf, double dt, double* p_last, double* chi_last, double u_d, double chi_d,
+                  const double os[6], const double ob[5], double obs_l, double obs_w, double out[3]) {
+  o_sbmpc sb = {*p_last, *chi_last, 0};
+  double p, c;
+  sbmpc_offset(&sb, tf, dt, u_d, chi_d, os, ob, obs_l, obs_w, &p, &c);
+  *p_last = sb.P_last; *chi_last = sb.Chi_last;
+  out[0] = p; out[1] = c; out[2] = sb.active;
+}
+
+void oracle_map_query(const shipsim_config* cfg, int n, const double* ne, int32_t* inside, double* dist) {
+  o_map mp;
+  map_init(&mp, cfg);
+  for (int i = 0; i < n; ++i) {
+    inside[i] = map_inside(&mp, ne[2 * i], ne[2 * i + 1]);
+    dist[i] = map_distance(&mp, ne[2 * i], ne[2 * i + 1]);
+  }
+}
+
+void oracle_encounter(int n, const double* rows /* n x 6 */, double* out /* n x 3: dist, enc, r_coll */) {
+  for (int i = 0; i < n; ++i) {
+    const double* q = rows + 6 * i;
+    double dist;
+    int enc = encounter(q[0], q[1], q[2], q[3], q[4], &dist);
+    out[3 * i] = dist;
+    out[3 * i + 1] = enc;
+    out[3 * i + 2] = (dist < 10000 && (enc == 0 || enc == 1)) ? rd4(0, 200000000, dist) : 0;
+  }
+}
+
+void oracle_reward_terms(int n, const double* rows /* n x 3 */, double* out /* n x 4 */) {
+  for (int i = 0; i < n; ++i) {
+    double dg = rows[3 * i], ect = rows[3 * i + 1], ecto = rows[3 * i + 2];
+    out[4 * i] = dg <= 1000 ? rd4(0, 175000, dg) : 0;
+    out[4 * i + 1] = rd3(3000, 1250000, fabs(ect));
+    out[4 * i + 2] = dg <= 1000 ? -rd4(0, 50000, dg) : 0;
+    out[4 * i + 3] = -rd3(500, 12500, fabs(ecto));
+  }
+}
+
+double oracle_termination_reward(double r, double acc, const int32_t cond[5]) {
+  int c[5];
+  for (int i = 0; i < 5; ++i) c[i] = cond[i];
+  return termination_reward(r, acc, c);
+}

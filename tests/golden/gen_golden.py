@@ -1,0 +1,720 @@
+"""Generate golden fixtures by running the reference (AndreasKing-Goks/ast-sac) in THIS container.
+
+TEST INFRASTRUCTURE ONLY.  Never imported by the product, by bench.py or by the GPU tests;
+it needs /root/reference, which does not exist on the GPU box.  The fixtures it writes
+(tests/golden/*.npz, data only) are what travel.
+
+Run:   python3 -B tests/golden/gen_golden.py          (from the repo root)
+
+What runs is the reference's own code: ship_model / ship_engine / controllers / LOS_guidance /
+sbmpc / check_condition / reward_function / env.py / run_colav/env.py / ast_sac SACTrainer.
+Three third-party imports are absent from the image and are replaced here, in-process, by
+stand-ins:
+
+* gymnasium (pinned 1.1.1 in ast-sac.yml): only `Env`, `spaces.Box`, `utils.seeding` are used
+  and none of them does arithmetic on the env path -> trivial containers.
+* gtimer (1.0.0b5): timing stamps only -> no-ops.
+* shapely (2.0.6 / GEOS 3.10.6): `Polygon.contains(Point)` and `Polygon.exterior.distance(Point)`
+  ARE arithmetic.  The stand-in restates GEOS' published algorithms (RayCrossingCounter for
+  point-in-ring with "boundary is not interior", Distance::pointToSegment for the ring
+  distance).  The fixtures are therefore pinned to the reference everywhere except at exact
+  polygon-boundary points, which the reference's own tests never pin either ("parity unpinned"
+  there).
+"""
+import argparse
+import copy
+import math
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# ----------------------------------------------------------------------------------------------
+# stand-ins for the missing third-party packages
+# ----------------------------------------------------------------------------------------------
+def _install_stubs():
+    gym = types.ModuleType("gymnasium")
+
+    class Env:
+        def __init__(self, *a, **k):
+            pass
+
+    gym.Env = Env
+    spaces = types.ModuleType("gymnasium.spaces")
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            low = np.asarray(low)
+            high = np.asarray(high)
+            if shape is not None:
+                low = np.full(shape, low)
+                high = np.full(shape, high)
+            self.low = low.astype(dtype)
+            self.high = high.astype(dtype)
+            self.shape = self.low.shape
+            self.dtype = np.dtype(dtype)
+
+    class Discrete:
+        def __init__(self, n):
+            self.n = n
+
+    class Tuple:
+        def __init__(self, spaces_):
+            self.spaces = spaces_
+
+    spaces.Box, spaces.Discrete, spaces.Tuple = Box, Discrete, Tuple
+    gym.spaces = spaces
+    utils = types.ModuleType("gymnasium.utils")
+    seeding = types.ModuleType("gymnasium.utils.seeding")
+    seeding.np_random = lambda seed=None: (np.random.default_rng(seed), seed)
+    utils.seeding = seeding
+    gym.utils = utils
+    sys.modules.update({"gymnasium": gym, "gymnasium.spaces": spaces,
+                        "gymnasium.utils": utils, "gymnasium.utils.seeding": seeding})
+
+    gt = types.ModuleType("gtimer")
+    gt.stamp = lambda *a, **k: None
+    gt.blank_stamp = lambda *a, **k: None
+    gt.timed_for = lambda it, **k: it
+    gt.reset_root = lambda *a, **k: None
+    gt.get_times = lambda *a, **k: None
+    sys.modules["gtimer"] = gt
+
+    shp = types.ModuleType("shapely")
+    geom = types.ModuleType("shapely.geometry")
+
+    class Point:
+        def __init__(self, x, y):
+            self.x = float(x)
+            self.y = float(y)
+
+    def _pt_seg(px, py, ax, ay, bx, by):
+        # GEOS Distance::pointToSegment
+        if ax == bx and ay == by:
+            return math.hypot(px - ax, py - ay)
+        dx, dy = bx - ax, by - ay
+        len2 = dx * dx + dy * dy
+        r = ((px - ax) * dx + (py - ay) * dy) / len2
+        if r <= 0.0:
+            return math.hypot(px - ax, py - ay)
+        if r >= 1.0:
+            return math.hypot(px - bx, py - by)
+        s = ((ay - py) * dx - (ax - px) * dy) / len2
+        return abs(s) * math.sqrt(len2)
+
+    class _Ring:
+        def __init__(self, verts):
+            self.coords = list(verts) + [verts[0]]
+
+        def distance(self, p):
+            c = self.coords
+            return min(_pt_seg(p.x, p.y, c[i][0], c[i][1], c[i + 1][0], c[i + 1][1])
+                       for i in range(len(c) - 1))
+
+    class Polygon:
+        def __init__(self, verts):
+            self.exterior = _Ring([(float(a), float(b)) for a, b in verts])
+
+        def contains(self, p):
+            # GEOS RayCrossingCounter; a point on the boundary is not contained
+            c = self.exterior.coords
+            crossings = 0
+            for i in range(len(c) - 1):
+                x1, y1 = c[i]
+                x2, y2 = c[i + 1]
+                if x1 < p.x and x2 < p.x:
+                    continue
+                if p.x == x2 and p.y == y2:
+                    return False
+                if y1 == p.y and y2 == p.y:
+                    minx, maxx = min(x1, x2), max(x1, x2)
+                    if minx <= p.x <= maxx:
+                        return False
+                    continue
+                if (y1 > p.y and y2 <= p.y) or (y2 > p.y and y1 <= p.y):
+                    det = (x2 - x1) * (p.y - y1) - (y2 - y1) * (p.x - x1)
+                    sign = (det > 0) - (det < 0)
+                    if sign == 0:
+                        return False
+                    if y2 < y1:
+                        sign = -sign
+                    if sign > 0:
+                        crossings += 1
+            return (crossings & 1) == 1
+
+    geom.Point, geom.Polygon = Point, Polygon
+    shp.geometry = geom
+    sys.modules.update({"shapely": shp, "shapely.geometry": geom})
+
+    import matplotlib
+    matplotlib.use("Agg")
+
+
+_install_stubs()
+sys.path.insert(0, REF)
+sys.dont_write_bytecode = True
+
+MAP_DATA = [
+    [(0, 10000), (10000, 10000), (9200, 9000), (7600, 8500), (6700, 7300), (4900, 6500), (4300, 5400),
+     (4700, 4500), (6000, 4000), (5800, 3600), (4200, 3200), (3200, 4100), (2000, 4500), (1000, 4000),
+     (900, 3500), (500, 2600), (0, 2350)],
+    [(10000, 0), (11500, 750), (12000, 2000), (11700, 3000), (11000, 3600), (11250, 4250), (12300, 4000),
+     (13000, 3800), (14000, 3000), (14500, 2300), (15000, 1700), (16000, 800), (17500, 0)],
+    [(15500, 10000), (16000, 9000), (18000, 8000), (19000, 7500), (20000, 6000), (20000, 10000)],
+    [(5500, 5300), (6000, 5000), (6800, 4500), (8000, 5000), (8700, 5500), (9200, 6700), (8000, 7000),
+     (6700, 6300), (6000, 6000)],
+    [(15000, 5000), (14000, 5500), (12500, 5000), (14000, 4100), (16000, 2000), (15700, 3700)],
+    [(11000, 2000), (10300, 3200), (9000, 1500), (10000, 1000)],
+]
+
+# Termination-flag bit order used by every fixture and by the build (reward_function.py:204-262)
+EVENT_STRINGS = [
+    "Ships collision!",
+    "|Ship under test experiences grounding!|",
+    "|Ship under test suffers navigational failure!|",
+    "|Obstacle ship experiences grounding!|",
+    "|Obstacle ship suffers navigational failure!|",
+    "|Ship under test reaches its final destination!|",
+    "|Ship under test goes outside the map horizon!|",
+    "|Obstacle ship reaches its final destination!|",
+    "|Obstacle ship goes outside the map horizon!|",
+    "|Simulation reaches its time limit|",
+    "|Learning agent samples false intermediate waypoints!|",
+]
+
+
+def events_to_bits(s):
+    bits = 0
+    rest = s
+    for i, e in enumerate(EVENT_STRINGS):
+        if e in rest:
+            bits |= 1 << i
+            rest = rest.replace(e, "", 1)
+    assert rest == "", (s, rest)
+    return bits
+
+
+def ns(**kw):
+    return argparse.Namespace(**kw)
+
+
+# ----------------------------------------------------------------------------------------------
+# F2: C2 unit — single SimpleShipModel + ThrustFromSpeedSetPoint + HeadingByRouteController
+# ----------------------------------------------------------------------------------------------
+def c1_configs(time_step):
+    from run_colav.ship_in_transit.sub_systems.ship_model import (ShipConfiguration, EnvironmentConfiguration,
+                                                                 SimulationConfiguration)
+    from run_colav.ship_in_transit.sub_systems.ship_engine import RudderConfiguration
+    ship_config = ShipConfiguration(
+        coefficient_of_deadweight_to_displacement=0.7, bunkers=200000, ballast=200000, length_of_ship=80,
+        width_of_ship=16, added_mass_coefficient_in_surge=0.4, added_mass_coefficient_in_sway=0.4,
+        added_mass_coefficient_in_yaw=0.4, dead_weight_tonnage=3850000,
+        mass_over_linear_friction_coefficient_in_surge=130, mass_over_linear_friction_coefficient_in_sway=18,
+        mass_over_linear_friction_coefficient_in_yaw=90, nonlinear_friction_coefficient__in_surge=2400,
+        nonlinear_friction_coefficient__in_sway=4000, nonlinear_friction_coefficient__in_yaw=400)
+    env_config = EnvironmentConfiguration(current_velocity_component_from_north=-1,
+                                          current_velocity_component_from_east=-1, wind_speed=2,
+                                          wind_direction=-np.pi / 4)
+    rudder_config = RudderConfiguration(rudder_angle_to_sway_force_coefficient=50e3,
+                                        rudder_angle_to_yaw_force_coefficient=500e3, max_rudder_angle_degrees=30)
+
+    def sim(n, e, psi, u):
+        return SimulationConfiguration(initial_north_position_m=n, initial_east_position_m=e,
+                                       initial_yaw_angle_rad=psi, initial_forward_speed_m_per_s=u,
+                                       initial_sideways_speed_m_per_s=0, initial_yaw_rate_rad_per_s=0,
+                                       integration_step=time_step, simulation_time=10000)
+    return ship_config, env_config, rudder_config, sim
+
+
+def gen_c2():
+    from run_colav.ship_in_transit.sub_systems.ship_model import SimpleShipModel
+    from run_colav.ship_in_transit.sub_systems.LOS_guidance import LosParameters
+    from run_colav.ship_in_transit.sub_systems.controllers import (SpeedControllerGains, HeadingControllerGains,
+                                                                  ThrustFromSpeedSetPoint, HeadingByRouteController)
+    route = os.path.join(REF, "run_colav/ship_in_transit/data/own_ship_route.txt")
+    out = {}
+    rng = np.random.Generator(np.random.PCG64(20251015))
+    for dt, m in ((30, 4), (4, 2)):
+        ship_config, env_config, rudder_config, sim = c1_configs(dt)
+        inits = []
+        traces = []
+        finals = []
+        for k in range(m):
+            n0 = 100 + rng.uniform(-200, 200)
+            e0 = 100 + rng.uniform(-200, 200)
+            p0 = 60 * np.pi / 180 + rng.uniform(-np.deg2rad(10), np.deg2rad(10))
+            u0 = rng.uniform(3.5, 5.0)
+            inits.append([n0, e0, p0, u0])
+            ship = SimpleShipModel(ship_config=ship_config, rudder_config=rudder_config,
+                                   environment_config=env_config, simulation_config=sim(n0, e0, p0, u0))
+            ctrl = ThrustFromSpeedSetPoint(gains=SpeedControllerGains(kp=150, ki=150, kd=75), max_thrust=np.inf,
+                                           time_step=dt)
+            ap = HeadingByRouteController(route, heading_controller_gains=HeadingControllerGains(kp=.5, ki=0.01,
+                                                                                                 kd=84),
+                                          los_parameters=LosParameters(radius_of_acceptance=300,
+                                                                       lookahead_distance=1000,
+                                                                       integral_gain=0.002,
+                                                                       integrator_windup_limit=4000),
+                                          time_step=dt, max_rudder_angle=np.deg2rad(30))
+            rows = []
+            while ship.int.time < ship.int.sim_time:
+                rudder = ap.rudder_angle_from_route(north_position=ship.north, east_position=ship.east,
+                                                    heading=ship.yaw_angle)
+                thrust = ctrl.thrust(speed_set_point=4.5, measured_speed=ship.forward_speed)
+                rows.append([ship.int.time, ship.north, ship.east, ship.yaw_angle, ship.forward_speed,
+                             ship.sideways_speed, ship.yaw_rate, rudder, thrust, ap.navigate.e_ct,
+                             ap.navigate.e_ct_int, ap.next_wpt])
+                ship.store_simulation_data(thrust, rudder, ap.navigate.e_ct, 0.0)
+                ship.update_differentials(thrust_force=thrust, rudder_angle=rudder)
+                ship.integrate_differentials()
+                ship.int.next_time()
+            traces.append(rows)
+            finals.append([ship.int.time, ship.north, ship.east, ship.yaw_angle, ship.forward_speed,
+                           ship.sideways_speed, ship.yaw_rate])
+        out[f"dt{dt}_init"] = np.array(inits)
+        out[f"dt{dt}_trace"] = np.array(traces)
+        out[f"dt{dt}_final"] = np.array(finals)
+    out["trace_cols"] = np.array(["time", "north", "east", "yaw", "u", "v", "r", "rudder", "thrust", "e_ct",
+                                  "e_ct_int", "next_wpt"])
+    np.savez_compressed(os.path.join(OUT, "c2_single_ship.npz"), **out)
+    print("c2:", {k: v.shape for k, v in out.items()})
+
+
+# ----------------------------------------------------------------------------------------------
+# F1: C1 two-ship NonIW loop (run_colav/run_simplified_model.py:55-249)
+# ----------------------------------------------------------------------------------------------
+def build_c1_env(collav, time_step=30):
+    from run_colav.env import MultiShipNonIWEnv, ShipAssets
+    from run_colav.ship_in_transit.sub_systems.ship_model import SimpleShipModel
+    from run_colav.ship_in_transit.sub_systems.LOS_guidance import LosParameters
+    from run_colav.ship_in_transit.sub_systems.obstacle import PolygonObstacle
+    from run_colav.ship_in_transit.sub_systems.controllers import (SpeedControllerGains, HeadingControllerGains,
+                                                                  ThrustFromSpeedSetPoint,
+                                                                  HeadingBySampledRouteController)
+    ship_config, env_config, rudder_config, sim = c1_configs(time_step)
+    test_ship = SimpleShipModel(ship_config=ship_config, rudder_config=rudder_config, environment_config=env_config,
+                                simulation_config=sim(100, 100, 60 * np.pi / 180, 4.25))
+    obs_ship = SimpleShipModel(ship_config=ship_config, rudder_config=rudder_config, environment_config=env_config,
+                               simulation_config=sim(9900, 14900, -135 * np.pi / 180, 3.5))
+    los = LosParameters(radius_of_acceptance=300, lookahead_distance=1000, integral_gain=0.002,
+                        integrator_windup_limit=4000)
+    d = os.path.join(REF, "run_colav/ship_in_transit/data")
+    test = ShipAssets(ship_model=test_ship,
+                      speed_controller=ThrustFromSpeedSetPoint(gains=SpeedControllerGains(kp=150, ki=150, kd=75),
+                                                               max_thrust=np.inf, time_step=time_step),
+                      auto_pilot=HeadingBySampledRouteController(
+                          os.path.join(d, "own_ship_route.txt"),
+                          heading_controller_gains=HeadingControllerGains(kp=.5, ki=0.01, kd=84),
+                          los_parameters=los, time_step=time_step, max_rudder_angle=np.deg2rad(30),
+                          num_of_samplings=2),
+                      desired_forward_speed=4.5, integrator_term=[], time_list=[], stop_flag=False,
+                      type_tag="test_ship")
+    obs = ShipAssets(ship_model=obs_ship,
+                     speed_controller=ThrustFromSpeedSetPoint(gains=SpeedControllerGains(kp=.025, ki=700.5,
+                                                                                         kd=550.5),
+                                                              max_thrust=np.inf, time_step=time_step),
+                     auto_pilot=HeadingBySampledRouteController(
+                         os.path.join(d, "obs_ship_route_nonIW.txt"),
+                         heading_controller_gains=HeadingControllerGains(kp=.65, ki=0.001, kd=50),
+                         los_parameters=los, time_step=time_step, max_rudder_angle=np.deg2rad(30),
+                         num_of_samplings=2),
+                     desired_forward_speed=4.0, integrator_term=[], time_list=[], stop_flag=False,
+                     type_tag="obs_ship")
+    args = ns(max_sampling_frequency=9, time_step=time_step, radius_of_acceptance=300, lookahead_distance=1000,
+              collav_mode=collav, ship_draw=False, time_since_last_ship_drawing=30, normalize_action=False)
+    env = MultiShipNonIWEnv(assets=[test, obs], map=PolygonObstacle(MAP_DATA), args=args)
+    return env, test, obs
+
+
+SR_KEYS = ["time [s]", "north position [m]", "east position [m]", "yaw angle [deg]", "rudder angle [deg]",
+           "forward speed [m/s]", "sideways speed [m/s]", "yaw rate [deg/sec]", "thrust force [kN]",
+           "cross track error [m]", "heading error [deg]"]
+
+
+def sr_array(ship, keys=SR_KEYS):
+    r = ship.simulation_results
+    return np.array([r[k] for k in keys], dtype=np.float64).T
+
+
+def gen_c1():
+    out = {}
+    for collav in ("none", "sbmpc", "simple"):
+        env, test, obs = build_c1_env(collav)
+        env.init_step()
+        bits = []
+        stops = []
+        while test.ship_model.int.time < test.ship_model.int.sim_time:
+            _, done, info = env._step()
+            bits.append(events_to_bits(info["events"]))
+            stops.append([test.stop_flag, obs.stop_flag, bool(done)])
+        out[f"{collav}_test_log"] = sr_array(test.ship_model)
+        out[f"{collav}_obs_log"] = sr_array(obs.ship_model)
+        out[f"{collav}_event_bits"] = np.array(bits, dtype=np.int64)
+        out[f"{collav}_stops"] = np.array(stops, dtype=np.int64)
+        out[f"{collav}_final"] = np.array([[s.ship_model.int.time, s.ship_model.north, s.ship_model.east,
+                                            s.ship_model.yaw_angle, s.ship_model.forward_speed,
+                                            s.ship_model.sideways_speed, s.ship_model.yaw_rate]
+                                           for s in (test, obs)])
+        print("c1", collav, "ticks", len(bits), "final time", test.ship_model.int.time)
+    out["log_cols"] = np.array(SR_KEYS)
+    np.savez_compressed(os.path.join(OUT, "c1_noniw.npz"), **out)
+
+
+# ----------------------------------------------------------------------------------------------
+# F3 + F4: the RL env (run/env_setup.py) with ShipModelAST detailed PTI machinery
+# ----------------------------------------------------------------------------------------------
+AST_KEYS = ["time [s]", "north position [m]", "east position [m]", "yaw angle [deg]", "rudder angle [deg]",
+            "forward speed [m/s]", "sideways speed [m/s]", "yaw rate [deg/sec]", "propeller shaft speed [rpm]",
+            "thrust force [kN]", "cross track error [m]", "heading error [deg]", "fuel consumption [kg]"]
+
+
+def rl_args(collav, time_step=4):
+    return ns(max_sampling_frequency=9, time_step=time_step, radius_of_acceptance=300, lookahead_distance=1000,
+              collav_mode=collav, ship_draw=False, time_since_last_ship_drawing=30, normalize_action=False)
+
+
+def gen_ast_single():
+    """ShipModelAST + EngineThrottleFromSpeedSetPoint + sampled-route autopilot; before/after reset (Q1)."""
+    from run.env_setup import prepare_multiship_rl_env
+    env, assets = prepare_multiship_rl_env(rl_args("none"))
+    test = assets[0]
+    out = {}
+    for phase in ("fresh", "after_reset"):
+        if phase == "after_reset":
+            test.ship_model.reset()
+            test.throttle_controller.reset()
+            test.auto_pilot.reset()
+        m = test.ship_model
+        out[f"{phase}_mach_dt"] = np.array(m.ship_machinery_model.int.dt)
+        for _ in range(500):
+            rudder = test.auto_pilot.rudder_angle_from_sampled_route(north_position=m.north, east_position=m.east,
+                                                                     heading=m.yaw_angle)
+            thr = test.throttle_controller.throttle(speed_set_point=4.5, measured_speed=m.forward_speed,
+                                                    measured_shaft_speed=m.forward_speed)
+            m.store_simulation_data(thr, rudder, test.auto_pilot.get_cross_track_error(),
+                                    test.auto_pilot.get_heading_error())
+            m.update_differentials(engine_throttle=thr, rudder_angle=rudder)
+            m.integrate_differentials()
+            m.int.next_time()
+        out[f"{phase}_log"] = np.array([m.simulation_results[k] for k in AST_KEYS], dtype=np.float64).T
+        out[f"{phase}_final"] = np.array([m.north, m.east, m.yaw_angle, m.forward_speed, m.sideways_speed,
+                                          m.yaw_rate, m.ship_machinery_model.omega])
+    out["log_cols"] = np.array(AST_KEYS)
+    np.savez_compressed(os.path.join(OUT, "ast_single_ship.npz"), **out)
+    print("ast single: mach dt fresh", out["fresh_mach_dt"], "after reset", out["after_reset_mach_dt"])
+
+
+def scaled_action(a_norm):
+    """NormalizedBoxEnv.step's float32 mapping onto the wrapped env's +-30 deg box
+    (ast_sac/env_wrapper/normalized_box_env.py:48-51)."""
+    lb = np.array([-np.deg2rad(30)], dtype=np.float32)
+    ub = np.array([np.deg2rad(30)], dtype=np.float32)
+    a = np.asarray(a_norm, dtype=np.float32).reshape(1)
+    s = lb + (a + 1.) * 0.5 * (ub - lb)
+    return np.clip(s, lb, ub)
+
+
+class SimplifiedThrustAdapter:
+    """Throttle-controller shaped adapter so the rl_env reward env can drive run_colav's
+    SimpleShipModel (no reference script composes them; SURVEY.md §8(d) C3 input)."""
+
+    def __init__(self, ctrl):
+        self.ctrl = ctrl
+
+    def throttle(self, speed_set_point, measured_speed, measured_shaft_speed):
+        return self.ctrl.thrust(speed_set_point=speed_set_point, measured_speed=measured_speed)
+
+    def reset(self):
+        self.ctrl.reset()
+
+
+def make_simplified_rl_env(collav):
+    from run.env_setup import prepare_multiship_rl_env
+    from rl_env.ship_in_transit.env import MultiShipRLEnv, ShipAssets
+    from run_colav.ship_in_transit.sub_systems.ship_model import SimpleShipModel
+    from run_colav.ship_in_transit.sub_systems.controllers import SpeedControllerGains, ThrustFromSpeedSetPoint
+
+    class SimpleShipModelRL(SimpleShipModel):
+        def update_differentials(self, engine_throttle=None, rudder_angle=None, *a, **k):
+            return super().update_differentials(thrust_force=engine_throttle, rudder_angle=rudder_angle)
+
+    args = rl_args(collav)
+    ref_env, assets = prepare_multiship_rl_env(args)
+    ship_config, env_config, rudder_config, sim = c1_configs(args.time_step)
+    test_ship = SimpleShipModelRL(ship_config=ship_config, rudder_config=rudder_config,
+                                  environment_config=env_config,
+                                  simulation_config=sim(100, 100, 60 * np.pi / 180, 4.25))
+    obs_ship = SimpleShipModelRL(ship_config=ship_config, rudder_config=rudder_config,
+                                 environment_config=env_config,
+                                 simulation_config=sim(9900, 14900, -135 * np.pi / 180, 3.5))
+    new_assets = []
+    for old, ship, gains in ((assets[0], test_ship, (150, 150, 75)), (assets[1], obs_ship, (150, 150, 75))):
+        ctrl = ThrustFromSpeedSetPoint(gains=SpeedControllerGains(kp=gains[0], ki=gains[1], kd=gains[2]),
+                                       max_thrust=np.inf, time_step=args.time_step)
+        ap = copy.deepcopy(old.init_copy.auto_pilot)
+        new_assets.append(ShipAssets(ship_model=ship, throttle_controller=SimplifiedThrustAdapter(ctrl),
+                                     auto_pilot=ap, desired_forward_speed=old.desired_forward_speed,
+                                     integrator_term=[], time_list=[], stop_flag=False, type_tag=old.type_tag))
+    return MultiShipRLEnv(assets=new_assets, map=ref_env.map, args=args)
+
+
+def run_rl_episodes(env, action_tables):
+    """Drive env.reset()/env.step() exactly as ast_sac_rollout does (max_path_length 9)."""
+    test, obs = env.test, env.obs
+    ep = []
+    for table in action_tables:
+        o0 = env.reset()
+        n_log0 = 0
+        dec = []
+        ticks = []
+        for a_norm in table:
+            a = scaled_action(a_norm)
+            before = len(test.ship_model.simulation_results["time [s]"])
+            o, r, d, info = env.step(a.copy())
+            after = len(test.ship_model.simulation_results["time [s]"])
+            dec.append(dict(a_norm=np.float32(a_norm), a=a[0], obs=np.asarray(o, np.float32), r=float(r),
+                            done=bool(d), bits=events_to_bits(info["events"]), terminal=bool(info["terminal"]),
+                            test_stop=bool(info["test_ship_stop"]), obs_stop=bool(info["obs_ship_stop"]),
+                            nticks=after - before, sampling_count=env.sampling_count,
+                            state=[test.ship_model.north, test.ship_model.east, test.ship_model.yaw_angle,
+                                   test.ship_model.forward_speed, test.ship_model.sideways_speed,
+                                   test.ship_model.yaw_rate, obs.ship_model.north, obs.ship_model.east,
+                                   obs.ship_model.yaw_angle, obs.ship_model.forward_speed,
+                                   obs.ship_model.sideways_speed, obs.ship_model.yaw_rate]))
+            if d:
+                break
+        keys = AST_KEYS if hasattr(test.ship_model, "ship_machinery_model") else SR_KEYS
+        ep.append(dict(o0=np.asarray(o0, np.float32), dec=dec,
+                       test_log=np.array([test.ship_model.simulation_results[k] for k in keys], np.float64).T,
+                       obs_log=np.array([obs.ship_model.simulation_results[k] for k in keys], np.float64).T,
+                       r_tick=np.array(env.reward_tracker.total, np.float64),
+                       obs_route=np.array([obs.auto_pilot.navigate.north, obs.auto_pilot.navigate.east]).T,
+                       n_log0=n_log0))
+    return ep
+
+
+def pack_episodes(prefix, eps, out):
+    out[f"{prefix}_n_episodes"] = np.array(len(eps))
+    for i, e in enumerate(eps):
+        p = f"{prefix}_ep{i}"
+        out[p + "_o0"] = e["o0"]
+        out[p + "_a_norm"] = np.array([d["a_norm"] for d in e["dec"]], np.float32)
+        out[p + "_a"] = np.array([d["a"] for d in e["dec"]], np.float32)
+        out[p + "_obs"] = np.array([d["obs"] for d in e["dec"]], np.float32)
+        out[p + "_reward"] = np.array([d["r"] for d in e["dec"]], np.float64)
+        out[p + "_done"] = np.array([d["done"] for d in e["dec"]], np.int64)
+        out[p + "_bits"] = np.array([d["bits"] for d in e["dec"]], np.int64)
+        out[p + "_terminal"] = np.array([d["terminal"] for d in e["dec"]], np.int64)
+        out[p + "_test_stop"] = np.array([d["test_stop"] for d in e["dec"]], np.int64)
+        out[p + "_obs_stop"] = np.array([d["obs_stop"] for d in e["dec"]], np.int64)
+        out[p + "_nticks"] = np.array([d["nticks"] for d in e["dec"]], np.int64)
+        out[p + "_state"] = np.array([d["state"] for d in e["dec"]], np.float64)
+        out[p + "_test_log"] = e["test_log"]
+        out[p + "_obs_log"] = e["obs_log"]
+        out[p + "_r_tick"] = e["r_tick"]
+        out[p + "_obs_route"] = e["obs_route"]
+
+
+def action_tables():
+    tabs = [np.zeros(9, np.float32)]
+    for k in range(2):
+        rng = np.random.Generator(np.random.PCG64(20251015 + k))
+        tabs.append(rng.uniform(-1, 1, 9).astype(np.float32))
+    tabs.append(np.ones(9, np.float32))       # IW drift -> sampling failure
+    tabs.append(-np.ones(9, np.float32))
+    return tabs
+
+
+def gen_rl():
+    from run.env_setup import prepare_multiship_rl_env
+    tabs = action_tables()
+    out = {}
+    for collav in ("none", "sbmpc", "simple"):
+        env, _ = prepare_multiship_rl_env(rl_args(collav))
+        eps = run_rl_episodes(env, tabs)
+        pack_episodes(collav, eps, out)
+        for i, e in enumerate(eps):
+            print("rl", collav, "ep", i, "decisions", len(e["dec"]), "ticks", [d["nticks"] for d in e["dec"]],
+                  "bits", [hex(d["bits"]) for d in e["dec"]][-1], "rewards",
+                  np.round([d["r"] for d in e["dec"]], 4))
+    out["log_cols"] = np.array(AST_KEYS)
+    np.savez_compressed(os.path.join(OUT, "rl_env_detailed.npz"), **out)
+
+    out = {}
+    for collav in ("none", "sbmpc"):
+        env = make_simplified_rl_env(collav)
+        eps = run_rl_episodes(env, tabs[:3])
+        pack_episodes(collav, eps, out)
+        for i, e in enumerate(eps):
+            print("rl-simplified", collav, "ep", i, "ticks", [d["nticks"] for d in e["dec"]],
+                  "bits", hex(e["dec"][-1]["bits"]))
+    out["log_cols"] = np.array(SR_KEYS)
+    np.savez_compressed(os.path.join(OUT, "rl_env_simplified.npz"), **out)
+
+
+# ----------------------------------------------------------------------------------------------
+# F5 SBMPC known answers, F6 geometry / reward pure functions
+# ----------------------------------------------------------------------------------------------
+def gen_sbmpc_geometry():
+    from rl_env.ship_in_transit.sub_systems.sbmpc import SBMPC
+    from rl_env.ship_in_transit.sub_systems.obstacle import PolygonObstacle
+    from rl_env.ship_in_transit.utils.compute_distance import get_distance_and_encounter_type
+    from rl_env.ship_in_transit.evaluation.reward_function import (get_reward_due_to_ships_termination,
+                                                                   ships_collision_reward,
+                                                                   test_ship_grounding_reward,
+                                                                   test_ship_nav_failure_reward,
+                                                                   obs_ship_grounding_reward,
+                                                                   obs_ship_nav_failure_reward)
+    rng = np.random.Generator(np.random.PCG64(7))
+    out = {}
+    # SBMPC: one persistent controller, a sequence of calls (last-offset state carries over, Q7)
+    sb = SBMPC(tf=1000, dt=20)
+    ins, outs = [], []
+    for k in range(64):
+        os_state = np.array([rng.uniform(0, 20000), rng.uniform(0, 10000), rng.uniform(-np.pi, np.pi),
+                             rng.uniform(0, 6), rng.uniform(-0.5, 0.5), rng.uniform(-0.01, 0.01)])
+        ang = rng.uniform(-np.pi, np.pi)
+        rad = rng.uniform(50, 2600) if k % 8 else 5000.0
+        ob = np.array([os_state[0] + rad * np.cos(ang), os_state[1] + rad * np.sin(ang),
+                       rng.uniform(-np.pi, np.pi), rng.uniform(0, 6), rng.uniform(-0.5, 0.5)])
+        u_d = rng.uniform(3, 5)
+        chi_d = rng.uniform(-4, 4)
+        p, c = sb.get_optimal_ctrl_offset(u_d=u_d, chi_d=chi_d, os_state=os_state,
+                                          do_list=[(0, ob, None, 80, 16)])
+        ins.append(np.concatenate([[u_d, chi_d], os_state, ob]))
+        outs.append([p, c, float(sb.is_stephen_useful()), sb._params.P_ca_last_, sb._params.Chi_ca_last_])
+    out["sbmpc_in"] = np.array(ins)
+    out["sbmpc_out"] = np.array(outs)
+    sb2 = SBMPC(tf=1000, dt=20)
+    out["sbmpc_survey_ka"] = np.array(sb2.get_optimal_ctrl_offset(
+        u_d=4.5, chi_d=-1.0, os_state=np.array([1000, 1000, -1, 4.5, 0, 0]),
+        do_list=[(0, np.array([2000, 1500, 2, 4, 0]), None, 80, 16)]), dtype=np.float64)
+
+    # polygons (stand-in == restated GEOS) on random and near-coastline points
+    pm = PolygonObstacle(MAP_DATA)
+    pts = np.concatenate([np.stack([rng.uniform(-500, 10500, 3000), rng.uniform(-500, 20500, 3000)], 1),
+                          np.stack([rng.uniform(3000, 7000, 1000), rng.uniform(3000, 9000, 1000)], 1)])
+    out["poly_pts_ne"] = pts
+    out["poly_inside"] = np.array([pm.if_pos_inside_obstacles(n, e) for n, e in pts], np.int64)
+    out["poly_dist"] = np.array([pm.obstacles_distance(n, e) for n, e in pts])
+    out["map_bounds"] = np.array([pm.min_north, pm.max_north, pm.min_east, pm.max_east])
+
+    # encounter classification + reward shaping terms
+    enc_codes = {"head-on": 0, "crossing": 1, "overtaking": 2}
+    rows = []
+    for k in range(2000):
+        a = [rng.uniform(0, 10000), rng.uniform(0, 20000)]
+        b = [a[0] + rng.uniform(-12000, 12000), a[1] + rng.uniform(-12000, 12000)]
+        h1 = rng.uniform(-8, 8)
+        h2 = rng.uniform(-8, 8)
+        dist, enc = get_distance_and_encounter_type(a, h1, b, h2)
+        rc, _ = ships_collision_reward(dist, enc, dist < 50)
+        rows.append([a[0], a[1], h1, b[0], b[1], h2, dist, enc_codes[enc], rc])
+    out["encounter"] = np.array(rows)
+    rows = []
+    for k in range(2000):
+        dg = rng.uniform(0, 1500)
+        ect = rng.uniform(-4000, 4000)
+        ect_o = rng.uniform(-700, 700)
+        rows.append([dg, ect, ect_o, test_ship_grounding_reward(dg, False)[0],
+                     test_ship_nav_failure_reward(ect, False)[0], obs_ship_grounding_reward(dg, False)[0],
+                     obs_ship_nav_failure_reward(ect_o, False)[0]])
+    out["reward_terms"] = np.array(rows)
+    rows = []
+    for k in range(512):
+        r = rng.normal()
+        acc = [rng.normal() * 5, 0.0, -1.0, 1.0][k % 4]
+        conds = [bool(x) for x in rng.integers(0, 2, 5)] if k % 3 else [False] * 5
+        rows.append([r, acc] + [float(c) for c in conds] + [get_reward_due_to_ships_termination(r, acc, *conds)])
+    out["terminal_reward"] = np.array(rows)
+    np.savez_compressed(os.path.join(OUT, "sbmpc_geometry_reward.npz"), **out)
+    print("sbmpc/geometry: survey KA", out["sbmpc_survey_ka"])
+
+
+# ----------------------------------------------------------------------------------------------
+# F7 SAC grad steps (sac.py:102-154) with fixed weights, batch and reparameterisation noise
+# ----------------------------------------------------------------------------------------------
+def gen_sac():
+    import torch
+    import ast_sac.torch.utils.pytorch_util as ptu
+    ptu.set_gpu_mode(False)
+    from ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac.torch.networks.mlp import ConcatMlp
+    from ast_sac.torch.sac.sac import SACTrainer
+    from ast_sac.torch.core import distributions as D
+
+    torch.manual_seed(0)
+    H, B, OBS, ACT = 32, 64, 8, 1
+    qf1, qf2, tq1, tq2 = [ConcatMlp(input_size=OBS + ACT, output_size=1, hidden_sizes=[H, H]) for _ in range(4)]
+    policy = TanhGaussianPolicy(obs_dim=OBS, action_dim=ACT, hidden_sizes=[H, H])
+
+    class E:
+        class action_space:
+            shape = (1,)
+
+    tr = SACTrainer(env=E, policy=policy, qf1=qf1, qf2=qf2, target_qf1=tq1, target_qf2=tq2, discount=0.965,
+                    soft_target_tau=1e-3, target_update_period=1, policy_lr=8e-5, qf_lr=8e-5, reward_scale=0.75,
+                    use_automatic_entropy_tuning=True, action_reg_coeff=0.01, clip_val=100)
+    nets = {"policy": policy, "qf1": qf1, "qf2": qf2, "target_qf1": tq1, "target_qf2": tq2}
+    out = {}
+    for name, net in nets.items():
+        for pn, p in net.named_parameters():
+            out[f"init/{name}/{pn}"] = p.detach().numpy().copy()
+    rng = np.random.Generator(np.random.PCG64(11))
+    n_steps = 3
+    noise = rng.standard_normal((n_steps, 2, B, ACT)).astype(np.float32)
+    queue = []
+    orig = D.MultivariateDiagonalNormal.sample
+
+    def fake_sample(self, *a, **k):
+        return queue.pop(0)
+
+    D.MultivariateDiagonalNormal.sample = fake_sample
+    try:
+        for s in range(n_steps):
+            batch = dict(observations=rng.uniform(-1, 1, (B, OBS)) * 1000.0,
+                         actions=rng.uniform(-1, 1, (B, ACT)),
+                         rewards=rng.normal(size=(B, 1)) * 3.0,
+                         terminals=(rng.uniform(size=(B, 1)) < 0.2).astype(np.uint8),
+                         next_observations=rng.uniform(-1, 1, (B, OBS)) * 1000.0)
+            for k, v in batch.items():
+                out[f"step{s}/batch/{k}"] = v
+            out[f"step{s}/noise"] = noise[s]
+            queue[:] = [torch.from_numpy(noise[s, 0]), torch.from_numpy(noise[s, 1])]
+            tb = {k: torch.from_numpy(np.asarray(v)).float() for k, v in batch.items()}
+            losses, _ = tr.compute_loss(tb, skip_statistics=True)
+            out[f"step{s}/losses"] = np.array([losses.policy_loss.item(), losses.qf1_loss.item(),
+                                              losses.qf2_loss.item(), losses.alpha_loss.item()])
+            queue[:] = [torch.from_numpy(noise[s, 0]), torch.from_numpy(noise[s, 1])]
+            tr.train_from_torch(tb)
+            out[f"step{s}/log_alpha"] = tr.log_alpha.detach().numpy().copy()
+            for name, net in nets.items():
+                for pn, p in net.named_parameters():
+                    out[f"step{s}/{name}/{pn}"] = p.detach().numpy().copy()
+    finally:
+        D.MultivariateDiagonalNormal.sample = orig
+    out["hparams"] = np.array([H, B, OBS, ACT, 0.965, 1e-3, 8e-5, 8e-5, 0.75, 0.01, 100.0])
+    np.savez_compressed(os.path.join(OUT, "sac_step.npz"), **out)
+    print("sac: losses", out["step0/losses"], out[f"step{n_steps - 1}/losses"])
+
+
+if __name__ == "__main__":
+    what = sys.argv[1:] or ["c2", "c1", "ast", "rl", "sbmpc", "sac"]
+    os.chdir(REF)
+    if "c2" in what:
+        gen_c2()
+    if "c1" in what:
+        gen_c1()
+    if "ast" in what:
+        gen_ast_single()
+    if "sbmpc" in what:
+        gen_sbmpc_geometry()
+    if "sac" in what:
+        gen_sac()
+    if "rl" in what:
+        gen_rl()

@@ -1,0 +1,150 @@
+"""Pin the CPU oracle (oracle/shipsim_oracle.c) against the golden vectors captured from the
+reference (tests/golden/gen_golden.py). CPU only."""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from ast_sac_amd import shipsim_abi as abi
+from parity import assert_close
+
+# oracle log columns -> fixture log columns
+AST_COLS = list(range(13))                          # AST_KEYS incl. shaft rpm, thrust kN, fuel
+SR_COLS = [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11]       # SR_KEYS (SimpleShipModel; no shaft / fuel)
+
+
+@pytest.mark.parametrize("dt", [30, 4])
+def test_c2_single_ship_trace(golden, dt):
+    g = golden("c2_single_ship")
+    tr, fin = O.c2_run(abi.c2_config(dt), g[f"dt{dt}_init"])
+    ref = g[f"dt{dt}_trace"]
+    assert tr.shape == ref.shape
+    np.testing.assert_array_equal(tr[..., 11], ref[..., 11])  # waypoint index: exact
+    assert_close(tr[..., :11], ref[..., :11], what=f"c2 dt{dt} trace")
+    assert_close(fin, g[f"dt{dt}_final"], what="c2 final")
+
+
+def test_c2_initial_states_match_fixture(golden):
+    g = golden("c2_single_ship")
+    init = abi.c2_initial_states(6)
+    np.testing.assert_array_equal(init[:4], g["dt30_init"])
+    np.testing.assert_array_equal(init[4:6], g["dt4_init"])
+
+
+@pytest.mark.parametrize("collav", ["none", "sbmpc", "simple"])
+def test_c1_noniw_loop(golden, collav):
+    g = golden("c1_noniw")
+    env = O.OracleEnv(abi.c1_config(collav), log_cap=2000)
+    bits, stops = env.run_c1()
+    np.testing.assert_array_equal(bits & abi.EVENT_MASK, g[f"{collav}_event_bits"])
+    np.testing.assert_array_equal(stops, g[f"{collav}_stops"][:, :2])
+    for s, name in ((0, "test"), (1, "obs")):
+        assert_close(env.log(s)[:, SR_COLS], g[f"{collav}_{name}_log"], what=f"c1 {collav} {name}")
+    fin = np.array([env.ship_state(s)[[7, 0, 1, 2, 3, 4, 5]] for s in (0, 1)])
+    assert_close(fin, g[f"{collav}_final"], what="c1 final")
+
+
+def test_ast_single_ship_and_machinery_dt_quirk(golden):
+    """ShipModelAST + PTI machinery; reset() switches the machinery integrator to dt=0.01 (Q1)."""
+    g = golden("ast_single_ship")
+    cfg = abi.ast_config("none")
+    cfg.kind = abi.KIND_SINGLE
+    cfg.n_ships = 1
+    env = O.OracleEnv(cfg, log_cap=600)
+    assert env.ship_state(0)[19] == float(g["fresh_mach_dt"])
+    env.run_single(500)
+    assert_close(env.log(0), g["fresh_log"], what="fresh")
+    assert_close(env.ship_state(0)[[0, 1, 2, 3, 4, 5, 6]], g["fresh_final"], what="fresh final")
+    env.reset()
+    assert env.ship_state(0)[19] == float(g["after_reset_mach_dt"]) == 0.01
+    env.run_single(500)
+    assert_close(env.log(0), g["after_reset_log"], what="after reset")
+    assert_close(env.ship_state(0)[[0, 1, 2, 3, 4, 5, 6]], g["after_reset_final"], what="after reset final")
+
+
+def _run_episodes(golden, fname, collav, machinery, cols):
+    g = golden(fname)
+    env = O.OracleEnv(abi.ast_config(collav, machinery=machinery), log_cap=4000)
+    for ep in range(int(g[f"{collav}_n_episodes"])):
+        p = f"{collav}_ep{ep}"
+        np.testing.assert_array_equal(env.reset(), g[p + "_o0"])
+        n_dec = len(g[p + "_a"])
+        got = {k: [] for k in ("obs", "reward", "done", "bits", "nticks")}
+        for a in g[p + "_a"]:
+            o, r, d, bits, ticks = env.step(a)
+            got["obs"].append(o)
+            got["reward"].append(r)
+            got["done"].append(d)
+            got["bits"].append(bits)
+            got["nticks"].append(ticks)
+            if d:
+                break
+        assert len(got["obs"]) == n_dec
+        np.testing.assert_array_equal(got["nticks"], g[p + "_nticks"], err_msg=p)
+        np.testing.assert_array_equal(np.array(got["bits"]) & abi.EVENT_MASK, g[p + "_bits"], err_msg=p)
+        np.testing.assert_array_equal(got["done"], g[p + "_done"].astype(bool), err_msg=p)
+        bits = np.array(got["bits"])
+        np.testing.assert_array_equal((bits & abi.EV_TERMINAL) != 0, g[p + "_terminal"].astype(bool))
+        np.testing.assert_array_equal((bits & abi.EV_TEST_STOP) != 0, g[p + "_test_stop"].astype(bool))
+        np.testing.assert_array_equal((bits & abi.EV_OBS_STOP) != 0, g[p + "_obs_stop"].astype(bool))
+        assert_close(np.array(got["obs"]), g[p + "_obs"], what=p + " obs")
+        assert_close(np.array(got["reward"]), g[p + "_reward"], what=p + " reward")
+        assert_close(env.log(0)[:, cols], g[p + "_test_log"], what=p + " test log")
+        assert_close(env.log(1)[:, cols], g[p + "_obs_log"], what=p + " obs log")
+        r_tick = env.rewards_per_tick()
+        ref_r = g[p + "_r_tick"]
+        # the reference's reward tracker also holds the sampling-failure total (update_r_total_only)
+        if bits[-1] & abi.EV_SAMPLING_FAILURE:
+            ref_r = ref_r[:-1]
+        assert_close(r_tick, ref_r, what=p + " reward per tick")
+        np.testing.assert_allclose(env.route(), g[p + "_obs_route"], rtol=0, atol=1e-3)
+
+
+@pytest.mark.parametrize("collav", ["none", "sbmpc", "simple"])
+def test_rl_env_detailed_episodes(golden, collav):
+    _run_episodes(golden, "rl_env_detailed", collav, abi.MACH_DETAILED, AST_COLS)
+
+
+@pytest.mark.parametrize("collav", ["none", "sbmpc"])
+def test_rl_env_simplified_episodes(golden, collav):
+    _run_episodes(golden, "rl_env_simplified", collav, abi.MACH_SIMPLIFIED, SR_COLS)
+
+
+def test_sbmpc_known_answers(golden):
+    g = golden("sbmpc_geometry_reward")
+    p_last, chi_last = 1.0, 0.0
+    for row, out in zip(g["sbmpc_in"], g["sbmpc_out"]):
+        res, p_last, chi_last = O.sbmpc(p_last, chi_last, row[0], row[1], row[2:8], row[8:13])
+        np.testing.assert_array_equal(res[:2], out[:2])
+        assert res[2] == out[2]
+        assert (p_last, chi_last) == (out[3], out[4])
+    res, _, _ = O.sbmpc(1.0, 0.0, 4.5, -1.0, [1000, 1000, -1, 4.5, 0, 0], [2000, 1500, 2, 4, 0])
+    np.testing.assert_array_equal(res[:2], g["sbmpc_survey_ka"])
+
+
+def test_polygon_map_queries(golden):
+    g = golden("sbmpc_geometry_reward")
+    inside, dist = O.map_query(abi.ast_config(), g["poly_pts_ne"])
+    np.testing.assert_array_equal(inside, g["poly_inside"])
+    np.testing.assert_allclose(dist, g["poly_dist"], rtol=1e-12, atol=1e-9)
+
+
+def test_encounter_and_reward_terms(golden):
+    g = golden("sbmpc_geometry_reward")
+    enc = g["encounter"]
+    out = np.zeros((len(enc), 3))
+    O.lib().oracle_encounter(len(enc), np.ascontiguousarray(enc[:, :6]), out)
+    np.testing.assert_allclose(out[:, 0], enc[:, 6], rtol=1e-14)
+    np.testing.assert_array_equal(out[:, 1], enc[:, 7])
+    np.testing.assert_allclose(out[:, 2], enc[:, 8], rtol=1e-13, atol=1e-300)
+    rt = g["reward_terms"]
+    out = np.zeros((len(rt), 4))
+    O.lib().oracle_reward_terms(len(rt), np.ascontiguousarray(rt[:, :3]), out)
+    np.testing.assert_allclose(out, rt[:, 3:], rtol=1e-13, atol=1e-300)
+    for row in g["terminal_reward"]:
+        cond = np.ascontiguousarray(row[2:7].astype(np.int32))
+        assert O.lib().oracle_termination_reward(row[0], row[1], cond) == pytest.approx(row[7], rel=1e-14, abs=0)
+
+
+def test_map_bounds(golden):
+    g = golden("sbmpc_geometry_reward")
+    np.testing.assert_array_equal(g["map_bounds"], [0, 10000, 0, 20000])
