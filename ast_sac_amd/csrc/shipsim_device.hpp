@@ -1,0 +1,381 @@
+// shipsim_device.hpp — CDNA4 (gfx950) device code of the batched ship-in-transit simulator.
+//
+// Lane mapping: one ship per lane. Two-ship envs (AST) occupy an adjacent lane pair
+// (lane 2e = ship under test, lane 2e+1 = obstacle ship), so both ships of an env advance in
+// the same VALU instructions and exchange what the reward / termination logic needs through
+// one DPP quad-permute (no LDS). Single-ship envs (C2) use one lane per env.
+// All state is fp64 (the reference is NumPy float64) and lives in registers for the whole
+// launch; HBM sees one coalesced SoA read at launch start and one write at the end.
+//
+// Every function restates the reference function cited next to it (paths relative to the
+// reference root, AndreasKing-Goks/ast-sac @ 2025-09-05). Operation order follows the
+// reference expression by expression (compiled with -ffp-contract=off) so that results differ
+// from the NumPy reference only through libm ulps.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "shipsim.h"
+
+namespace shipsim {
+
+constexpr double kPi = 3.141592653589793;
+constexpr int kMaxRoute = SHIPSIM_MAX_ROUTE;
+
+// ---------------------------------------------------------------------------------------------
+// constants (computed once on the host, identical arithmetic to the reference constructors)
+// ---------------------------------------------------------------------------------------------
+struct ShipConst {
+  // BaseShipModel.__init__ (ship_model.py:412-474)
+  double mass, i_z, x_du, y_dv, n_dr;
+  double inv_m0, inv_m1, inv_m2;    // inv(mass_matrix()) diagonal (x_g = 0)
+  double dlin0, dlin1, dlin2;       // linear_damping_matrix diagonal: mass/t_surge, mass/t_sway, i_z/t_yaw
+  double ku, kv, kr;
+  double l_ship, w_ship, obs_l_cfg, obs_w_cfg;  // ship_config.length/width (SBMPC do_list)
+  double rho_a, proj_area_f, proj_area_l, cx, cy, cn;
+  double c_rudder_v, c_rudder_r, max_rudder;
+  // ShipMachineryModel (ship_engine.py:341-443) with the active MachineryMode
+  double avail_me, avail_el, cap_me, cap_el;   // available powers; torque caps avail/5*pi/30
+  double d_me, d_hsg, r_me, r_hsg, jp, kp_prop, thrust_coeff, shaft_speed_max;
+  double init_omega;
+  // controllers (controllers.py:45-209; run_colav ThrustFromSpeedSetPoint)
+  double kp_ship_speed, ki_ship_speed, kp_shaft_speed, ki_shaft_speed, init_shaft_ei;
+  double spd_kp, spd_ki, spd_kd, max_thrust;
+  double hdg_kp, hdg_kd, hdg_ki;
+  // NavigationSystem (LOS_guidance.py:38-58)
+  double ra2, los_r, los_r2, los_ki, los_limit;
+  double desired_speed;
+  // SimulationConfiguration
+  double init_n, init_e, init_yaw, init_u, init_v, init_r;
+  int32_t n_route, pad_;
+};
+
+struct Params {
+  ShipConst sc[2];
+  int32_t kind, machinery, collav, n_ships;
+  int32_t max_sampling, n_envs, n_polys, pad_;
+  double dt, sim_time, mach_dt_reset, mach_dt_init;
+  double vc_n, vc_e, wind_dir, wind_speed;
+  double roa2;                       // args.radius_of_acceptance ** 2
+  double sbmpc_tf, sbmpc_dt;
+  // IW sampler (env.py:143-161), identical for every env of a handle
+  double AB_seg, AB_seg_n, AB_seg_e, omega_iw, n_base0, e_base0;
+  double min_north, max_north, min_east, max_east;
+  float action_low, action_high;
+  int32_t normalize_action, pad2_;
+  float initial_states[8];           // env.py:107-109
+};
+
+// Map edges (obstacle.py PolygonObstacle). Stored as a flat read-only device table; every lane
+// walks it with the same (wave-uniform) index, so loads are scalar/broadcast.
+struct Edge {
+  double ax, ay, bx, by;   // (east, north) of the edge endpoints
+};
+struct PolyBox {
+  double minx, maxx, miny, maxy;
+  int32_t first, count, pad0, pad1;
+};
+
+// ---------------------------------------------------------------------------------------------
+// register-resident ship state
+// ---------------------------------------------------------------------------------------------
+struct Ship {
+  double n, e, yaw, u, v, r, omega, time;
+  double e_ct, e_ct_int;          // navigate
+  double hdg_ei, hdg_prev;        // heading PID
+  double spd_a, spd_b;            // ship-speed PI ei | thrust PID ei ; shaft PI ei | thrust PID prev
+  double log_rudder, log_thrust, log_ect, log_n, log_e;  // simulation_results[-1]
+  double wp_prev_n, wp_prev_e, wp_n, wp_e;  // navigate.north/east[k-1], [k] (register cache)
+  double end_n, end_e;            // navigate.north/east[-1]
+  int32_t next_wpt, n_route, stop;
+};
+
+__device__ __forceinline__ double sel(bool c, double a, double b) { return c ? a : b; }
+
+// Python min/max semantics: min(a, b) returns a unless b < a
+__device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double py_max(double a, double b) { return (b > a) ? b : a; }
+__device__ __forceinline__ double sat(double v, double lo, double hi) { return py_max(lo, py_min(v, hi)); }
+
+// np.remainder / Python float % (floored)
+__device__ __forceinline__ double floor_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0) != (m < 0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+// sbmpc_misc.py:20-32
+__device__ __forceinline__ double wrap_pmpi(double x) { return -kPi + floor_mod(x - (-kPi), kPi - (-kPi)); }
+
+// swap a double with the partner lane (lane ^ 1) — DPP quad_perm [1,0,3,2]
+__device__ __forceinline__ double pair_swap(double x) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int pair_swap_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
+
+// ---------------------------------------------------------------------------------------------
+// ship model: ship_model.py BaseShipModel / ShipModelAST, run_colav SimpleShipModel
+// ---------------------------------------------------------------------------------------------
+struct Deriv {
+  double dn, de, dyaw, du, dv, dr, domega;
+};
+
+// get_wind_force :497-517
+__device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, const Ship& s, double tau[3]) {
+  double sw, cw;
+  sincos(P.wind_dir - s.yaw, &sw, &cw);
+  double uw = P.wind_speed * cw;
+  double vw = P.wind_speed * sw;
+  double u_rw = uw - s.u;
+  double v_rw = vw - s.v;
+  double gamma_rw = -atan2(v_rw, u_rw);
+  double wind_rw2 = u_rw * u_rw + v_rw * v_rw;
+  double sg, cg;
+  sincos(gamma_rw, &sg, &cg);
+  double c_x = -c.cx * cg;
+  double c_y = c.cy * sg;
+  double c_n = c.cn * sin(2 * gamma_rw);
+  double tau_coeff = 0.5 * c.rho_a * wind_rw2;
+  tau[0] = tau_coeff * c_x * c.proj_area_f;
+  tau[1] = tau_coeff * c_y * c.proj_area_l;
+  tau[2] = tau_coeff * c_n * c.proj_area_l * c.l_ship;
+}
+
+// update_differentials (ShipModelAST :882-888 / SimpleShipModel run_colav :399-404):
+// three_dof_kinematics :519-528, shaft_eq + thrust (ship_engine.py:403-443), three_dof_kinetics
+// :834-864 with rudder :866-880. `ctrl` is the engine throttle (detailed) or thrust force (simplified).
+__device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params& P, const Ship& s, double ctrl,
+                                               double delta, bool detailed) {
+  Deriv d;
+  double sy, cy;
+  sincos(s.yaw, &sy, &cy);
+  d.dn = cy * s.u + (-sy) * s.v + 0 * s.r;
+  d.de = sy * s.u + cy * s.v + 0 * s.r;
+  d.dyaw = 0 * s.u + 0 * s.v + 1 * s.r;
+  double thrust = ctrl;
+  d.domega = 0.0;
+  if (detailed) {
+    // main_engine_torque / hsg_torque :416-432
+    double t_me = py_min(ctrl * c.avail_me / (s.omega + 0.1), c.cap_me);
+    double t_hsg = py_min(ctrl * c.avail_el / (s.omega + 0.1), c.cap_el);
+    double eq_me = (t_me - c.d_me * s.omega) / c.r_me;
+    double eq_hsg = (t_hsg - c.d_hsg * s.omega) / c.r_hsg;
+    d.domega = (eq_me + eq_hsg - c.kp_prop * (s.omega * s.omega)) / c.jp;
+    thrust = c.thrust_coeff * s.omega * fabs(s.omega);
+  }
+  // inv(rotation()) @ vel_c
+  double vc0 = cy * P.vc_n + sy * P.vc_e;
+  double vc1 = -sy * P.vc_n + cy * P.vc_e;
+  double fv = -c.c_rudder_v * delta * (s.u - vc0);
+  double fr = -c.c_rudder_r * delta * (s.u - vc0);
+  double tau[3];
+  wind_force(c, P, s, tau);
+  double u_r = s.u - vc0;
+  double v_r = s.v - vc1;
+  double x_g = 0.0;
+  double vr0 = s.u - vc0, vr1 = s.v - vc1, vr2 = s.r - 0.0;
+  double crb0 = 0 * s.u + 0 * s.v + (-c.mass * (x_g * s.r + s.v)) * s.r;
+  double crb1 = 0 * s.u + 0 * s.v + (c.mass * s.u) * s.r;
+  double crb2 = (c.mass * (x_g * s.r + s.v)) * s.u + (-c.mass * s.u) * s.v + 0 * s.r;
+  double ca0 = 0 * vr0 + 0 * vr1 + (c.y_dv * v_r) * vr2;
+  double ca1 = 0 * vr0 + 0 * vr1 + (-c.x_du * u_r) * vr2;
+  double ca2 = (-c.y_dv * v_r) * vr0 + (c.x_du * u_r) * vr1 + 0 * vr2;
+  double d0 = c.dlin0 + c.ku * s.u;
+  double d1 = c.dlin1 + c.kv * s.v;
+  double d2 = c.dlin2 + c.kr * s.r;
+  double f0 = -crb0 - ca0 - d0 * vr0 + tau[0] + 0 + thrust;
+  double f1 = -crb1 - ca1 - d1 * vr1 + tau[1] + 0 + fv;
+  double f2 = -crb2 - ca2 - d2 * vr2 + tau[2] + 0 + fr;
+  d.du = c.inv_m0 * f0;
+  d.dv = c.inv_m1 * f1;
+  d.dr = c.inv_m2 * f2;
+  return d;
+}
+
+// integrate_differentials :890-901 (EulerInt.integrate utils.py:50) + int.next_time :42
+__device__ __forceinline__ void integrate(Ship& s, const Deriv& d, double dt, double mach_dt, bool detailed) {
+  s.n = s.n + d.dn * dt;
+  s.e = s.e + d.de * dt;
+  s.yaw = s.yaw + d.dyaw * dt;
+  s.u = s.u + d.du * dt;
+  s.v = s.v + d.dv * dt;
+  s.r = s.r + d.dr * dt;
+  if (detailed) s.omega = s.omega + d.domega * mach_dt;
+  s.time = s.time + dt;
+}
+
+// ---------------------------------------------------------------------------------------------
+// guidance & control
+// ---------------------------------------------------------------------------------------------
+// LOS_guidance.py:100-117 (k = next_wpt; waypoints k-1, k are register-cached)
+__device__ __forceinline__ double los_guidance(const ShipConst& c, Ship& s, double x, double y) {
+  double dx = s.wp_n - s.wp_prev_n;
+  double dy = s.wp_e - s.wp_prev_e;
+  double alpha_k = atan2(dy, dx);
+  double sa, ca;
+  sincos(alpha_k, &sa, &ca);
+  double e_ct = -(x - s.wp_prev_n) * sa + (y - s.wp_prev_e) * ca;
+  s.e_ct = e_ct;
+  if (e_ct * e_ct >= c.los_r2) {
+    e_ct = 0.99 * c.los_r;
+    s.e_ct = e_ct;
+  }
+  double delta = py_max(1e-6, sqrt(c.los_r2 - e_ct * e_ct));
+  if (fabs(s.e_ct_int + e_ct / delta) <= c.los_limit) s.e_ct_int += e_ct / delta;
+  double chi_r = atan(-e_ct / delta - s.e_ct_int * c.los_ki);
+  return alpha_k + chi_r;
+}
+
+// LOS_guidance.py:83-98: true when the index advances (caller reloads the segment cache)
+__device__ __forceinline__ bool next_wpt_advance(const ShipConst& c, const Ship& s, double N, double E) {
+  double dn = s.wp_n - N, de = s.wp_e - E;
+  return (dn * dn + de * de <= c.ra2) && (s.n_route > s.next_wpt + 1);
+}
+
+// reload the cached LOS segment (k-1, k) from the route table
+__device__ __forceinline__ void load_segment(Ship& s, const double* __restrict__ rn, const double* __restrict__ re) {
+  s.wp_prev_n = rn[s.next_wpt - 1];
+  s.wp_prev_e = re[s.next_wpt - 1];
+  s.wp_n = rn[s.next_wpt];
+  s.wp_e = re[s.next_wpt];
+  s.end_n = rn[s.n_route - 1];
+  s.end_e = re[s.n_route - 1];
+}
+
+// PidController.pid_ctrl controllers.py:106-118
+__device__ __forceinline__ double pid(double& ei, double& prev, double kp, double kd, double ki, double dt,
+                                      double setpoint, double meas) {
+  double error = setpoint - meas;
+  double d_error = (error - prev) / dt;
+  double error_i = ei + error * dt;
+  prev = error;
+  ei = error_i;
+  return error * kp + d_error * kd + error_i * ki;
+}
+// PiController.pi_ctrl controllers.py:55-65
+__device__ __forceinline__ double pi_ctrl(double& ei, double kp, double ki, double dt, double setpoint, double meas) {
+  double error = setpoint - meas;
+  double error_i = ei + error * dt;
+  ei = error_i;
+  return error * kp + error_i * ki;
+}
+
+// speed control: EngineThrottleFromSpeedSetPoint.throttle controllers.py:185-189 (Q2: shaft
+// measurement = forward speed) | ThrustFromSpeedSetPoint.thrust run_colav controllers.py:183-185
+__device__ __forceinline__ double speed_ctrl(const ShipConst& c, Ship& s, double setpoint, double u, double dt,
+                                             bool detailed) {
+  if (detailed) {
+    double desired_shaft = pi_ctrl(s.spd_a, c.kp_ship_speed, c.ki_ship_speed, dt, setpoint, u);
+    desired_shaft = sat(desired_shaft, 0, c.shaft_speed_max);
+    double thr = pi_ctrl(s.spd_b, c.kp_shaft_speed, c.ki_shaft_speed, dt, desired_shaft, u);
+    return sat(thr, 0, 1.1);
+  }
+  double t = pid(s.spd_a, s.spd_b, c.spd_kp, c.spd_kd, c.spd_ki, dt, setpoint, u);
+  return sat(t, -c.max_thrust, c.max_thrust);
+}
+
+// HeadingByReferenceController.rudder_angle_from_heading_setpoint :246-255
+__device__ __forceinline__ double heading_ctrl(const ShipConst& c, Ship& s, double heading_ref, double heading,
+                                               double dt) {
+  double rudder = -pid(s.hdg_ei, s.hdg_prev, c.hdg_kp, c.hdg_kd, c.hdg_ki, dt, heading_ref, heading);
+  return sat(rudder, -c.max_rudder, c.max_rudder);
+}
+
+// ---------------------------------------------------------------------------------------------
+// map queries (obstacle.py:126-141 over shapely/GEOS; restated GEOS semantics)
+// ---------------------------------------------------------------------------------------------
+// GEOS RayCrossingCounter for one polygon, boundary -> not contained
+__device__ __forceinline__ bool poly_contains(const Edge* __restrict__ edges, int first, int count, double px,
+                                              double py) {
+  int crossings = 0;
+  bool boundary = false;
+  for (int i = 0; i < count; ++i) {
+    const Edge ed = edges[first + i];
+    double x1 = ed.ax, y1 = ed.ay, x2 = ed.bx, y2 = ed.by;
+    if (x1 < px && x2 < px) continue;
+    if (px == x2 && py == y2) boundary = true;
+    if (y1 == py && y2 == py) {
+      double mn = py_min(x1, x2), mx = py_max(x1, x2);
+      if (mn <= px && px <= mx) boundary = true;
+      continue;
+    }
+    if ((y1 > py && y2 <= py) || (y2 > py && y1 <= py)) {
+      double det = (x2 - x1) * (py - y1) - (y2 - y1) * (px - x1);
+      int sign = (det > 0) - (det < 0);
+      if (sign == 0) boundary = true;
+      if (y2 < y1) sign = -sign;
+      if (sign > 0) crossings++;
+    }
+  }
+  return !boundary && (crossings & 1);
+}
+
+// if_pos_inside_obstacles :126-129 (bbox rejection is exact for the crossing rule)
+__device__ __forceinline__ bool map_inside(const Edge* __restrict__ edges, const PolyBox* __restrict__ boxes,
+                                           int n_polys, double n, double e) {
+  bool inside = false;
+  for (int p = 0; p < n_polys; ++p) {
+    const PolyBox b = boxes[p];
+    if (e < b.minx || e > b.maxx || n < b.miny || n > b.maxy) continue;
+    if (poly_contains(edges, b.first, b.count, e, n)) inside = true;
+  }
+  return inside;
+}
+
+// obstacles_distance :138-141, GEOS Distance::pointToSegment min over every ring edge
+__device__ __forceinline__ double map_distance(const Edge* __restrict__ edges, int n_edges, double n, double e) {
+  double best = INFINITY;
+  const double px = e, py = n;
+  for (int i = 0; i < n_edges; ++i) {
+    const Edge ed = edges[i];
+    double ax = ed.ax, ay = ed.ay, bx = ed.bx, by = ed.by;
+    double d;
+    if (ax == bx && ay == by) {
+      d = hypot(px - ax, py - ay);
+    } else {
+      double dx = bx - ax, dy = by - ay;
+      double len2 = dx * dx + dy * dy;
+      double r = ((px - ax) * dx + (py - ay) * dy) / len2;
+      if (r <= 0.0) {
+        d = hypot(px - ax, py - ay);
+      } else if (r >= 1.0) {
+        d = hypot(px - bx, py - by);
+      } else {
+        double sv = ((ay - py) * dx - (ax - px) * dy) / len2;
+        d = fabs(sv) * sqrt(len2);
+      }
+    }
+    best = py_min(best, d);
+  }
+  return best;
+}
+
+// check_condition.py:50-78 four hull hard points
+__device__ __forceinline__ bool pos_inside_obstacles(const Edge* __restrict__ edges,
+                                                     const PolyBox* __restrict__ boxes, int n_polys, double n,
+                                                     double e, double L) {
+  double margin = L / 2;
+  double mnn = n - margin, mne = e - margin, mxn = n + margin, mxe = e + margin;
+  bool inside = false;
+  if (map_inside(edges, boxes, n_polys, mnn, mne)) inside = true;
+  if (map_inside(edges, boxes, n_polys, mnn, mxe)) inside = true;
+  if (map_inside(edges, boxes, n_polys, mxn, mne)) inside = true;
+  if (map_inside(edges, boxes, n_polys, mxn, mxe)) inside = true;
+  return inside;
+}
+
+// reward_designs.py:33-55
+__device__ __forceinline__ double rd3(double target, double off, double val) {
+  return (val < target) ? exp(-((val - target) * (val - target)) / off) : 1.0;
+}
+__device__ __forceinline__ double rd4(double target, double off, double val) {
+  return (val < target) ? 1.0 : exp(-((val - target) * (val - target)) / off);
+}
+
+}  // namespace shipsim

@@ -1,0 +1,1227 @@
+// shipsim_kernels.hip — HIP kernels (gfx950) + C ABI (include/shipsim.h) of the batched
+// ship-in-transit simulator. One translation unit -> ast_sac_amd/lib/libshipsim.so.
+//
+// Kernels
+//   init_kernel    : state as constructed (ShipModelAST/SimpleShipModel.__init__, controllers,
+//                    NavigationSystem, MultiShipRLEnv.__init__ :54-141)
+//   reset_kernel   : MultiShipRLEnv.reset (env.py:238-295) incl. init_step (:297-342)
+//   ast_step_kernel: MultiShipRLEnv.step (env.py:624-773) — event-driven: each env ticks
+//                    (_step :563-622) until its decision point (RoA + 1 tick) or done
+//   single_tick_kernel: C2 single-ship loop body (run_colav/run_simplified_model.py:248-249 shape)
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+
+#include "shipsim.h"
+#include "shipsim_device.hpp"
+
+using namespace shipsim;
+
+// ---------------------------------------------------------------------------------------------
+// device state (SoA). Ship arrays are indexed q = env * n_ships + ship (lane order).
+// ---------------------------------------------------------------------------------------------
+struct DevState {
+  double* f[SHIPSIM_N_SHIP_FIELDS];  // double ship fields (int ones unused here)
+  int32_t* next_wpt;
+  int32_t* stop;
+  int32_t* n_route;
+  double* route_n;  // [q][kMaxRoute]
+  double* route_e;
+  // env
+  int32_t* sampling_count;
+  double* travel_dist;
+  double* travel_time;
+  double* acc;
+  double* n_base;
+  double* e_base;
+  double* p_last;
+  double* chi_last;
+  double* mach_dt;
+  float* states4;    // [env][4] self.states (test n, e, obs n, e) for the 'simple' collav quirk
+  float* next_obs8;  // [env][8] self.next_observations snapshot
+  uint32_t* snap_bits;
+  int32_t* was_reset;
+};
+enum { SF_N = 0, SF_E, SF_YAW, SF_U, SF_V, SF_R, SF_OMEGA, SF_TIME, SF_ECT, SF_ECT_INT, SF_HDG_EI, SF_HDG_PREV,
+       SF_SPD_A, SF_SPD_B, SF_RUDDER, SF_THRUST, SF_LOG_ECT, SF_LOG_N, SF_LOG_E };
+
+struct ConstBuf {
+  const Edge* edges;
+  const PolyBox* boxes;
+  const double* cfg_route_n;  // [2][kMaxRoute]
+  const double* cfg_route_e;
+  int32_t n_edges;
+};
+
+__device__ __forceinline__ void load_ship(const DevState& S, int q, Ship& s) {
+  s.n = S.f[SF_N][q]; s.e = S.f[SF_E][q]; s.yaw = S.f[SF_YAW][q];
+  s.u = S.f[SF_U][q]; s.v = S.f[SF_V][q]; s.r = S.f[SF_R][q];
+  s.omega = S.f[SF_OMEGA][q]; s.time = S.f[SF_TIME][q];
+  s.e_ct = S.f[SF_ECT][q]; s.e_ct_int = S.f[SF_ECT_INT][q];
+  s.hdg_ei = S.f[SF_HDG_EI][q]; s.hdg_prev = S.f[SF_HDG_PREV][q];
+  s.spd_a = S.f[SF_SPD_A][q]; s.spd_b = S.f[SF_SPD_B][q];
+  s.log_rudder = S.f[SF_RUDDER][q]; s.log_thrust = S.f[SF_THRUST][q]; s.log_ect = S.f[SF_LOG_ECT][q];
+  s.log_n = S.f[SF_LOG_N][q]; s.log_e = S.f[SF_LOG_E][q];
+  s.next_wpt = S.next_wpt[q]; s.stop = S.stop[q]; s.n_route = S.n_route[q];
+  load_segment(s, S.route_n + (size_t)q * kMaxRoute, S.route_e + (size_t)q * kMaxRoute);
+}
+__device__ __forceinline__ void store_ship(const DevState& S, int q, const Ship& s) {
+  S.f[SF_N][q] = s.n; S.f[SF_E][q] = s.e; S.f[SF_YAW][q] = s.yaw;
+  S.f[SF_U][q] = s.u; S.f[SF_V][q] = s.v; S.f[SF_R][q] = s.r;
+  S.f[SF_OMEGA][q] = s.omega; S.f[SF_TIME][q] = s.time;
+  S.f[SF_ECT][q] = s.e_ct; S.f[SF_ECT_INT][q] = s.e_ct_int;
+  S.f[SF_HDG_EI][q] = s.hdg_ei; S.f[SF_HDG_PREV][q] = s.hdg_prev;
+  S.f[SF_SPD_A][q] = s.spd_a; S.f[SF_SPD_B][q] = s.spd_b;
+  S.f[SF_RUDDER][q] = s.log_rudder; S.f[SF_THRUST][q] = s.log_thrust; S.f[SF_LOG_ECT][q] = s.log_ect;
+  S.f[SF_LOG_N][q] = s.log_n; S.f[SF_LOG_E][q] = s.log_e;
+  S.next_wpt[q] = s.next_wpt; S.stop[q] = s.stop; S.n_route[q] = s.n_route;
+}
+
+// per-block LDS copy of the two ShipConst (lanes of either parity read one of two addresses)
+__device__ __forceinline__ const ShipConst* stage_consts(const Params& P, ShipConst* lds) {
+  const int nwords = (int)(sizeof(ShipConst) * 2 / sizeof(double));
+  const double* src = reinterpret_cast<const double*>(&P.sc[0]);
+  double* dst = reinterpret_cast<double*>(lds);
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  return lds;
+}
+
+// one controlled ship tick: autopilot -> speed control -> store -> update -> integrate -> next_time
+// (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339)
+template <bool DETAILED>
+__device__ __forceinline__ void control_and_integrate(const ShipConst& c, const Params& P, Ship& s,
+                                                      const double* __restrict__ rn, const double* __restrict__ re,
+                                                      double offset, double speed_factor, double mach_dt,
+                                                      int simple_collav_flag /*0 none, 1 rl(-15deg), 2 noniw(+15)*/,
+                                                      bool imminent) {
+  const double N = s.n, E = s.e, H = s.yaw, U = s.u;
+  if (next_wpt_advance(c, s, N, E)) {
+    s.next_wpt += 1;
+    load_segment(s, rn, re);
+  }
+  double href = los_guidance(c, s, N, E);
+  double rudder = heading_ctrl(c, s, href + offset, H, P.dt);
+  double ctrl = speed_ctrl(c, s, c.desired_speed * speed_factor, U, P.dt, DETAILED);
+  if (simple_collav_flag && imminent) {
+    ctrl *= 0.5;
+    ctrl = py_min(py_max(ctrl, 0.0), 1.1);
+    rudder += (simple_collav_flag == 1 ? -15.0 : 15.0) * (kPi / 180.0);
+    rudder = py_min(py_max(rudder, -c.max_rudder), c.max_rudder);
+  }
+  // store_simulation_data (the fields later read back through simulation_results[-1])
+  s.log_rudder = rudder;
+  s.log_ect = s.e_ct;
+  s.log_n = N;
+  s.log_e = E;
+  s.log_thrust = DETAILED ? (c.thrust_coeff * s.omega * fabs(s.omega)) / 1000 : ctrl;
+  Deriv d = differentials(c, P, s, ctrl, rudder, DETAILED);
+  integrate(s, d, P.dt, mach_dt, DETAILED);
+}
+
+// ---------------------------------------------------------------------------------------------
+// SBMPC (sbmpc.py:113-298), wave-cooperative: each requesting env's 7 x 4 scenarios are spread
+// over 28 lanes of a half-wave; two envs are served per pass.
+// ---------------------------------------------------------------------------------------------
+struct SbIn {
+  double u_d, chi_d, os_x, os_y, os_v, ob_x, ob_y, ob_psi, ob_u, ob_v, obs_l, obs_w, p_last, chi_last;
+};
+
+__device__ __forceinline__ double shfl_d(double x, int src) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  lo = __shfl(lo, src, 64);
+  hi = __shfl(hi, src, 64);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
+  const double os_l = 25.0;  // ShipLinearModel default length (sbmpc_misc.py:86, Q7)
+  const double d_safe = 1000.0, d_close = 2000.0;
+  const double PHI_AH = 68.5 * (kPi / 180.0), PHI_OT = 68.5 * (kPi / 180.0);
+  const double cos_ot = cos(PHI_OT * (kPi / 180.0));  // np.cos(np.deg2rad(PHI_OT_)) — PHI_OT_ already in rad
+  const double CHI_DEG = -30.0 + 10.0 * ichi;
+  const double P_CA[4] = {0.4, 0.6, 0.8, 1.0};
+  const double P_ca = P_CA[jp];
+  const double Chi_ca = CHI_DEG * (kPi / 180.0);
+  const double ud = in.u_d * P_ca;
+  const double psi_d = in.chi_d + Chi_ca;
+  // Obstacle trajectory (sbmpc_misc.py:65-83) and linear_pred (:103-123), advanced incrementally
+  double so, co;
+  sincos(in.ob_psi, &so, &co);
+  const double r11 = -so, r12 = co, r21 = co, r22 = so;
+  const double vo0 = -so * in.ob_u + co * in.ob_v;  // rot2d(obstacle.psi_, [u, v])
+  const double vo1 = co * in.ob_u + so * in.ob_v;
+  const double no = sqrt(vo0 * vo0 + vo1 * vo1);
+  double sp, cp;
+  sincos(psi_d, &sp, &cp);
+  const double q11 = -sp, q12 = cp, q21 = cp, q22 = sp;
+  double sp0, cp0;
+  sincos(wrap_pmpi(psi_d), &sp0, &cp0);
+  double ox = in.ob_x, oy = in.ob_y, sx = in.os_x, sy = in.os_y, sv = in.os_v;
+  double H1 = 0, t = 0;
+  for (int i = 0; i < n_samp; ++i) {
+    if (i > 0) {
+      ox = ox + (r11 * in.ob_u + r12 * in.ob_v) * DT;
+      oy = oy + (r21 * in.ob_u + r22 * in.ob_v) * DT;
+      sx = sx + DT * (q11 * ud + q12 * sv);
+      sy = sy + DT * (q21 * ud + q22 * sv);
+      sv = 0.0;
+    }
+    t += DT;
+    double d0 = ox - sx, d1 = oy - sy;
+    double dist = sqrt(d0 * d0 + d1 * d1);
+    double R = 0, C = 0;
+    if (dist < d_close) {
+      double ss = (i == 0) ? sp0 : sp, cs = (i == 0) ? cp0 : cp;
+      double vs0 = -ss * ud + cs * sv;
+      double vs1 = cs * ud + ss * sv;
+      double phi_o = wrap_pmpi(atan2(-d1, -d0) - in.ob_psi + kPi / 2);
+      double d_safe_i;
+      if (phi_o < PHI_AH) d_safe_i = d_safe + in.obs_l / 2;
+      else if (phi_o > PHI_OT) d_safe_i = 0.5 * d_safe + in.obs_l / 2;
+      else d_safe_i = d_safe + in.obs_w / 2;
+      double dot = vs0 * vo0 + vs1 * vo1;
+      double ns = sqrt(vs0 * vs0 + vs1 * vs1);
+      if (dot > cos_ot * ns * no && ns > no) d_safe_i = d_safe + os_l / 2 + in.obs_l / 2;
+      if (dist < d_safe_i) {
+        R = (1 / pow(fabs(t - 0.0), 1.0)) * pow(d_safe / dist, 4.0);
+        double k_coll = 1e-6 * os_l * in.obs_l;
+        double w0 = vs0 - vo0, w1 = vs1 - vo1;
+        double nrm = sqrt(w0 * w0 + w1 * w1);
+        C = k_coll * (nrm * nrm);
+      }
+    }
+    double H0 = C * R + 0.0 * 0;
+    if (H0 > H1) H1 = H0;
+  }
+  double dchi = Chi_ca - in.chi_last;
+  double dChi = (dchi > 0) ? 20 * dchi * dchi : (dchi < 0 ? 30 * dchi * dchi : 0);
+  double H2 = 25 * (1 - P_ca) + 30 * (Chi_ca * Chi_ca) + 20 * fabs(in.p_last - P_ca) + dChi;
+  return H1 + H2;
+}
+
+// Must be called by every lane of the wave (wave-uniform control flow). `need` marks lanes that
+// request an optimisation with inputs `in`; they receive (P_best, Chi_best).
+__device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double DT, double& p_best,
+                                  double& chi_best) {
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int scen = lane & 31;
+  uint64_t req = __ballot(need);
+  while (req) {
+    int src0 = __ffsll((unsigned long long)req) - 1;
+    req &= req - 1;
+    int src1 = -1;
+    if (req) {
+      src1 = __ffsll((unsigned long long)req) - 1;
+      req &= req - 1;
+    }
+    int src = half ? src1 : src0;
+    int srcc = src < 0 ? src0 : src;
+    SbIn g;
+    g.u_d = shfl_d(in.u_d, srcc); g.chi_d = shfl_d(in.chi_d, srcc);
+    g.os_x = shfl_d(in.os_x, srcc); g.os_y = shfl_d(in.os_y, srcc); g.os_v = shfl_d(in.os_v, srcc);
+    g.ob_x = shfl_d(in.ob_x, srcc); g.ob_y = shfl_d(in.ob_y, srcc); g.ob_psi = shfl_d(in.ob_psi, srcc);
+    g.ob_u = shfl_d(in.ob_u, srcc); g.ob_v = shfl_d(in.ob_v, srcc);
+    g.obs_l = shfl_d(in.obs_l, srcc); g.obs_w = shfl_d(in.obs_w, srcc);
+    g.p_last = shfl_d(in.p_last, srcc); g.chi_last = shfl_d(in.chi_last, srcc);
+    double cost = INFINITY;
+    int idx = 64;
+    if (src >= 0 && scen < 28) {
+      cost = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3);
+      idx = scen;
+    }
+    // argmin over the half-wave; ties -> lowest scenario index (first strict improvement in the
+    // reference's i-major / j-minor loop)
+    for (int off = 16; off >= 1; off >>= 1) {
+      double oc = shfl_d(cost, lane ^ off);
+      int oi = __shfl(idx, lane ^ off, 64);
+      if (oc < cost || (oc == cost && oi < idx)) { cost = oc; idx = oi; }
+    }
+    int best0 = __shfl(idx, 0, 64);
+    int best1 = __shfl(idx, 32, 64);
+    const double P_CA[4] = {0.4, 0.6, 0.8, 1.0};
+    if (lane == src0) {
+      p_best = P_CA[best0 & 3];
+      chi_best = (-30.0 + 10.0 * (best0 >> 2)) * (kPi / 180.0);
+    }
+    if (src1 >= 0 && lane == src1) {
+      p_best = P_CA[best1 & 3];
+      chi_best = (-30.0 + 10.0 * (best1 >> 2)) * (kPi / 180.0);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------------------------
+// fresh state as constructed; for AST also env-level fields of MultiShipRLEnv.__init__
+__global__ void init_kernel(const Params P, DevState S, ConstBuf K) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nq = P.n_envs * P.n_ships;
+  if (q >= nq) return;
+  const int ship = q % P.n_ships;
+  const int env = q / P.n_ships;
+  const ShipConst& c = P.sc[ship];
+  Ship s;
+  s.n = c.init_n; s.e = c.init_e; s.yaw = c.init_yaw; s.u = c.init_u; s.v = c.init_v; s.r = c.init_r;
+  s.omega = c.init_omega; s.time = 0.0;
+  s.e_ct = 0; s.e_ct_int = 0; s.hdg_ei = 0; s.hdg_prev = 0;
+  s.spd_a = 0; s.spd_b = (P.machinery == SHIPSIM_MACH_DETAILED) ? c.init_shaft_ei : 0.0;
+  s.log_rudder = 0; s.log_thrust = 0; s.log_ect = 0; s.log_n = s.n; s.log_e = s.e;
+  s.next_wpt = 1; s.stop = 0; s.n_route = c.n_route;
+  double* rn = S.route_n + (size_t)q * kMaxRoute;
+  double* re = S.route_e + (size_t)q * kMaxRoute;
+  for (int i = 0; i < kMaxRoute; ++i) {
+    rn[i] = K.cfg_route_n[ship * kMaxRoute + i];
+    re[i] = K.cfg_route_e[ship * kMaxRoute + i];
+  }
+  store_ship(S, q, s);
+  if (ship == 0) {
+    S.sampling_count[env] = 0;
+    S.travel_dist[env] = 0; S.travel_time[env] = 0; S.acc[env] = 0;
+    S.n_base[env] = P.n_base0; S.e_base[env] = P.e_base0;
+    S.p_last[env] = 1.0; S.chi_last[env] = 0.0;  // SBMPCParams defaults (sbmpc.py:28-29)
+    S.mach_dt[env] = P.mach_dt_init;
+    for (int i = 0; i < 4; ++i) S.states4[env * 4 + i] = P.initial_states[i < 2 ? i : i + 1];
+    for (int i = 0; i < 8; ++i) S.next_obs8[env * 8 + i] = P.initial_states[i];
+    S.snap_bits[env] = 0;
+    S.was_reset[env] = 0;
+  }
+}
+
+// MultiShipRLEnv.reset (env.py:238-295): reset assets + IW sampler + snapshot, then init_step
+template <bool DETAILED>
+__global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, ConstBuf K, const uint8_t* mask,
+                                                   float* obs_out) {
+  __shared__ ShipConst lds_sc[2];
+  const ShipConst* SC = stage_consts(P, lds_sc);
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nq = P.n_envs * P.n_ships;
+  if (q >= nq) return;
+  const int ship = q % P.n_ships;
+  const int env = q / P.n_ships;
+  if (mask && !mask[env]) return;
+  const ShipConst& c = SC[ship];
+  Ship s;
+  s.n = c.init_n; s.e = c.init_e; s.yaw = c.init_yaw; s.u = c.init_u; s.v = c.init_v; s.r = c.init_r;
+  s.omega = c.init_omega; s.time = 0.0;
+  s.e_ct = 0; s.e_ct_int = 0; s.hdg_ei = 0; s.hdg_prev = 0;
+  s.spd_a = 0; s.spd_b = DETAILED ? c.init_shaft_ei : 0.0;
+  s.next_wpt = 1; s.stop = 0; s.n_route = c.n_route;
+  double* rn = S.route_n + (size_t)q * kMaxRoute;
+  double* re = S.route_e + (size_t)q * kMaxRoute;
+  for (int i = 0; i < c.n_route; ++i) {
+    rn[i] = K.cfg_route_n[ship * kMaxRoute + i];
+    re[i] = K.cfg_route_e[ship * kMaxRoute + i];
+  }
+  load_segment(s, rn, re);
+  const double mach_dt = P.mach_dt_reset;
+  // init_step (env.py:307-339): one control + integrate tick, no collision avoidance
+  control_and_integrate<DETAILED>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false);
+  store_ship(S, q, s);
+  if (ship == 0) {
+    S.sampling_count[env] = 0;
+    S.travel_dist[env] = 0; S.travel_time[env] = 0; S.acc[env] = 0;
+    S.n_base[env] = P.n_base0; S.e_base[env] = P.e_base0;
+    S.mach_dt[env] = mach_dt;
+    for (int i = 0; i < 8; ++i) S.next_obs8[env * 8 + i] = P.initial_states[i];
+    S.snap_bits[env] = 0;
+    S.was_reset[env] = 1;
+    if (obs_out)
+      for (int i = 0; i < 8; ++i) obs_out[env * 8 + i] = P.initial_states[i];
+  }
+}
+
+// MultiShipRLEnv.step (env.py:624-773) for lane pairs (2e: test ship, 2e+1: obstacle ship)
+template <bool DETAILED, int COLLAV>
+__global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K,
+                                                      const float* __restrict__ action,
+                                                      const uint8_t* __restrict__ active_mask, int max_ticks,
+                                                      float* obs_out, double* reward_out, uint8_t* done_out,
+                                                      uint32_t* events_out, int32_t* ticks_out) {
+  __shared__ ShipConst lds_sc[2];
+  const ShipConst* SC = stage_consts(P, lds_sc);
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int env = q >> 1;
+  const int ship = q & 1;
+  const bool is_test = ship == 0;
+  const bool valid = env < P.n_envs;
+  const int envc = valid ? env : 0;
+  const int qc = valid ? q : 0;
+  const ShipConst& c = SC[ship];
+  const double* rn = S.route_n + (size_t)qc * kMaxRoute;
+  const double* re = S.route_e + (size_t)qc * kMaxRoute;
+  double* rn_w = S.route_n + (size_t)qc * kMaxRoute;
+  double* re_w = S.route_e + (size_t)qc * kMaxRoute;
+
+  bool running = valid && (active_mask == nullptr || active_mask[envc]) && S.was_reset[envc];
+  const bool touched = running;
+
+  Ship s;
+  load_ship(S, qc, s);
+  int sampling_count = S.sampling_count[envc];
+  double travel_dist = S.travel_dist[envc], travel_time = S.travel_time[envc], acc = S.acc[envc];
+  double n_base = S.n_base[envc], e_base = S.e_base[envc];
+  double p_last = S.p_last[envc], chi_last = S.chi_last[envc];
+  const double mach_dt = S.mach_dt[envc];
+  float st4[4];
+  for (int i = 0; i < 4; ++i) st4[i] = S.states4[envc * 4 + i];
+  uint32_t snap_bits = S.snap_bits[envc];
+
+  float ns[8];  // next_states of the last tick
+  for (int i = 0; i < 8; ++i) ns[i] = S.next_obs8[envc * 8 + i];
+  double out_r = 0.0;
+  bool out_done = false;
+  uint32_t out_bits = 0;
+  int ticks = 0, phase = 0;
+  bool have_iw = false;
+
+  if (running) {
+    // ---- intermediate waypoint sampling (env.py:659-696) ----
+    float sa = action[envc];
+    if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
+    if (sampling_count < P.max_sampling) {
+      sampling_count += 1;
+      float tn = (float)tan((double)sa);  // np.tan on the float32 scoping angle
+      double l_s = fabs(P.AB_seg * (double)tn);
+      double e_s = l_s * cos(P.omega_iw);
+      double n_s = l_s * sin(P.omega_iw);
+      if (sa > 0) e_s *= -1;
+      else n_s *= -1;
+      double iw_n = n_base + n_s, iw_e = e_base + e_s;
+      n_base = iw_n + P.AB_seg_n;
+      e_base = iw_e + P.AB_seg_e;
+      if (!is_test) {  // auto_pilot.update_route: list.insert(-1, IW)
+        int L = s.n_route;
+        rn_w[L] = rn_w[L - 1]; re_w[L] = re_w[L - 1];
+        rn_w[L - 1] = iw_n; re_w[L - 1] = iw_e;
+        s.n_route = L + 1;
+        load_segment(s, rn, re);
+      }
+      travel_dist = 0;
+      travel_time = 0;
+      have_iw = true;
+      bool fail = map_inside(K.edges, K.boxes, P.n_polys, iw_n, iw_e) ||
+                  ((iw_n < P.min_north || iw_n > P.max_north) || (iw_e < P.min_east || iw_e > P.max_east));
+      if (fail) {  // env.py:673-693 with obs_ship_IW_sampling_failure_reward (multiplier 2)
+        out_r = (acc >= 0) ? -acc * 2.0 : acc * 2.0;
+        snap_bits = (snap_bits | SHIPSIM_EV_SAMPLING_FAILURE | SHIPSIM_EV_TERMINAL) &
+                    ~(uint32_t)(SHIPSIM_EV_TEST_STOP | SHIPSIM_EV_OBS_STOP);
+        out_bits = snap_bits;
+        out_done = true;
+        running = false;
+      } else {
+        acc = 0;
+      }
+    }
+  }
+
+  const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
+  while (__any(running)) {
+    // partner's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
+    const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
+    const double pu = pair_swap(s.u), pv = pair_swap(s.v);
+    double sf = 1.0, off = 0.0;
+    if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
+      bool need = false;
+      SbIn in;
+      if (running && is_test) {
+        // env.py:362-363: next_wpt result discarded; los_guidance integrates e_ct_int (Q3)
+        double chi_d = los_guidance(c, s, s.n, s.e);
+        in.u_d = c.desired_speed; in.chi_d = -chi_d;
+        in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
+        in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
+        in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
+        in.p_last = p_last; in.chi_last = chi_last;
+        double d0 = pe - s.e, d1 = pn - s.n;
+        need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
+        if (!need) { p_last = 1; chi_last = 0; }
+      } else {
+        in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      double pb = 1.0, cb = 0.0;
+      sbmpc_cooperative(need, in, n_samp, P.sbmpc_dt, pb, cb);
+      if (need) { p_last = pb; chi_last = cb; sf = pb; off = cb; }
+      const double p_other = pair_swap(p_last), c_other = pair_swap(chi_last);
+      if (!is_test) { p_last = p_other; chi_last = c_other; }
+    }
+
+    // ---- ship ticks (test_step :345-445 / obs_step :447-536) ----
+    double my_speed_out = 0.0, dtravel = 0.0, dtime = 0.0;
+    if (running) {
+      if (!is_test && s.stop) {
+        // frozen obstacle ship: store_last_simulation_data + two next_time (Q9)
+        s.time = s.time + P.dt;
+        s.time = s.time + P.dt;
+        my_speed_out = 0.0;
+      } else {
+        const double prev_log_n = s.log_n, prev_log_e = s.log_e;
+        const double U = s.u;
+        bool imminent = false;
+        if (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) {  // check_condition.py:130 on float32 self.states
+          float dn = st4[0] - st4[2], de = st4[1] - st4[3];
+          imminent = (dn * dn + de * de) < 9000000.0f;
+        }
+        control_and_integrate<DETAILED>(c, P, s, rn, re, -off, sf, mach_dt,
+                                        (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) ? 1 : 0, imminent);
+        my_speed_out = U;
+        if (!is_test) {  // travel tracker (env.py:527-534, Q6)
+          double tn = s.log_n - prev_log_n, te = s.log_e - prev_log_e;
+          dtravel = sqrt(tn * tn + te * te);
+          dtime = P.dt;
+        }
+      }
+    }
+    // ---- own-ship part of get_reward_and_env_info (reward_function.py:80-168) ----
+    double my_ground = 0.0;
+    bool my_grounding = false, my_end = false, my_outside = false, my_roa = false;
+    if (running) {
+      my_ground = map_distance(K.edges, K.n_edges, s.n, s.e);
+      my_grounding = pos_inside_obstacles(K.edges, K.boxes, P.n_polys, s.n, s.e, c.l_ship);
+      my_end = sqrt((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e)) <= 200;
+      double margin = c.l_ship / 2;
+      my_outside = (s.n < P.min_north + margin || s.n > P.max_north - margin) ||
+                   (s.e < P.min_east + margin || s.e > P.max_east - margin);
+      double rdn = s.n - s.wp_n, rde = s.e - s.wp_e;  // is_reach_radius_of_acceptance (obstacle lane)
+      my_roa = (rdn * rdn + rde * rde) < P.roa2;
+    }
+    const int my_flags = (my_grounding ? 1 : 0) | (my_end ? 2 : 0) | (my_outside ? 4 : 0) | (my_roa ? 8 : 0);
+    const int o_flags = pair_swap_i(my_flags);
+    const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
+    const double o_ect = pair_swap(s.log_ect), o_ground = pair_swap(my_ground);
+    const double o_speed = pair_swap(my_speed_out), o_dtravel = pair_swap(dtravel), o_dtime = pair_swap(dtime);
+    const double o_time = pair_swap(s.time);
+    if (running) {
+      // arrange as (test, obstacle)
+      const double Tn = is_test ? s.n : o_n, Te = is_test ? s.e : o_e, Th = is_test ? s.yaw : o_yaw;
+      const double On = is_test ? o_n : s.n, Oe = is_test ? o_e : s.e, Oyaw = is_test ? o_yaw : s.yaw;
+      const double Tect = is_test ? s.log_ect : o_ect, Oect = is_test ? o_ect : s.log_ect;
+      const double Tground = is_test ? my_ground : o_ground, Oground = is_test ? o_ground : my_ground;
+      const int Tf = is_test ? my_flags : o_flags, Of = is_test ? o_flags : my_flags;
+      const double Ospeed = is_test ? o_speed : my_speed_out;
+      const double Ttime = is_test ? s.time : o_time;
+      travel_dist += is_test ? o_dtravel : dtravel;
+      travel_time += is_test ? o_dtime : dtime;
+      // next_states (env.py:582-591) and self.states
+      ns[0] = (float)Tn; ns[1] = (float)Te; ns[2] = (float)Tect;
+      ns[3] = (float)On; ns[4] = (float)Oe; ns[5] = (float)Oyaw; ns[6] = (float)Ospeed; ns[7] = (float)Oect;
+      st4[0] = ns[0]; st4[1] = ns[1]; st4[2] = ns[3]; st4[3] = ns[4];
+      // encounter (compute_distance.py:16-40) and collision (check_condition.py:142-159)
+      double dx = On - Tn, dy = Oe - Te;
+      double dist = sqrt(dx * dx + dy * dy);
+      double beta = floor_mod((atan2(dy, dx) - Th) + kPi, 2 * kPi) - kPi;
+      const bool enc_ok = !(fabs(beta) > 165.0 * (kPi / 180.0));  // head-on or crossing
+      const bool is_collision = ((Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe)) < 2500.0;
+      const bool is_tg = Tf & 1, is_og = Of & 1;
+      const bool is_tnav = fabs(Tect) > 3000;
+      const bool is_onav = (travel_dist > P.AB_seg * 2) || (travel_time > INFINITY) || (fabs(Oect) > 500);
+      double r0 = (dist < 10000 && enc_ok) ? rd4(0, 200000000, dist) : 0.0;
+      double r1 = (Tground <= 1000) ? rd4(0, 175000, Tground) : 0.0;
+      double r2 = rd3(3000, 1250000, fabs(Tect));
+      double r3 = (Oground <= 1000) ? -rd4(0, 50000, Oground) : 0.0;
+      double r4 = -rd3(500, 12500, fabs(Oect));
+      double r = (r0 + ((((0.0 + r1) + r2) + r3) + r4)) / 5;  // np.sum(5 terms) / 5
+      // get_reward_due_to_ships_termination (reward_function.py:272-314)
+      if (is_collision || is_tg || is_tnav || is_og || is_onav) {
+        const double reward = r + acc;
+        double o = 0;
+        const bool cond[5] = {is_collision, is_tg, is_tnav, is_og, is_onav};
+        const double mult[5] = {10.0, 5.0, 5.0, -2.5, -2.5};
+        for (int i = 0; i < 5; ++i) {
+          if (acc > 0 && cond[i]) o += reward * mult[i];
+          else if (acc < 0 && cond[i]) o += reward * -mult[i];
+        }
+        r = o;
+      }
+      const bool t6 = Tf & 2, t7 = Tf & 4, t8 = Of & 2, t9 = Of & 4;
+      const bool t10 = Ttime > P.sim_time;
+      uint32_t bits = (is_collision ? SHIPSIM_EV_COLLISION : 0) | (is_tg ? SHIPSIM_EV_TEST_GROUNDING : 0) |
+                      (is_tnav ? SHIPSIM_EV_TEST_NAV_FAILURE : 0) | (is_og ? SHIPSIM_EV_OBS_GROUNDING : 0) |
+                      (is_onav ? SHIPSIM_EV_OBS_NAV_FAILURE : 0) | (t6 ? SHIPSIM_EV_TEST_REACHES_END : 0) |
+                      (t7 ? SHIPSIM_EV_TEST_OUTSIDE_MAP : 0) | (t8 ? SHIPSIM_EV_OBS_REACHES_END : 0) |
+                      (t9 ? SHIPSIM_EV_OBS_OUTSIDE_MAP : 0) | (t10 ? SHIPSIM_EV_TIME_LIMIT : 0);
+      const bool terminal = bits & 0x1F;
+      const bool test_stop = is_collision || is_tg || is_tnav || t6 || t7 || t10;
+      const bool obs_stop = is_collision || is_og || is_onav || t8 || t9 || t10;
+      if (terminal) bits |= SHIPSIM_EV_TERMINAL;
+      if (test_stop) bits |= SHIPSIM_EV_TEST_STOP;
+      if (obs_stop) bits |= SHIPSIM_EV_OBS_STOP;
+      if (obs_stop && !terminal && !is_test) s.stop = 1;
+      const bool combined_done = terminal || (test_stop && !terminal);
+      // ---- env.py:700-771 decision logic ----
+      acc += r;
+      ticks += 1;
+      bool finish = false;
+      if (phase == 0) {
+        const bool roa = Of & 8;
+        if (combined_done) {
+          finish = true;
+        } else if (roa) {
+          if (have_iw) phase = 1;
+          else finish = true;
+        }
+      } else if (phase == 1) {
+        if (sampling_count == P.max_sampling) {
+          travel_dist = 0;
+          travel_time = 0;
+          if (combined_done) finish = true;
+          else phase = 2;
+        } else {
+          finish = true;
+        }
+      } else {
+        if (combined_done) finish = true;
+      }
+      if (!finish && max_ticks > 0 && ticks >= max_ticks) finish = true;
+      if (finish) {
+        out_r = acc;
+        out_done = combined_done;
+        out_bits = bits;
+        snap_bits = bits;
+        running = false;
+      }
+    }
+  }
+
+  if (!valid || !touched) return;
+  store_ship(S, q, s);
+  if (is_test) {
+    S.sampling_count[env] = sampling_count;
+    S.travel_dist[env] = travel_dist; S.travel_time[env] = travel_time; S.acc[env] = acc;
+    S.n_base[env] = n_base; S.e_base[env] = e_base;
+    S.p_last[env] = p_last; S.chi_last[env] = chi_last;
+    for (int i = 0; i < 4; ++i) S.states4[env * 4 + i] = st4[i];
+    for (int i = 0; i < 8; ++i) S.next_obs8[env * 8 + i] = ns[i];
+    S.snap_bits[env] = snap_bits;
+    if (reward_out) reward_out[env] = out_r;
+    if (done_out) done_out[env] = out_done ? 1 : 0;
+    if (events_out) events_out[env] = out_bits;
+    if (ticks_out) ticks_out[env] = ticks;
+  }
+  if (obs_out) {  // test lane writes obs[0..3], obstacle lane obs[4..7]
+    for (int i = 0; i < 4; ++i) obs_out[env * 8 + ship * 4 + i] = ns[ship * 4 + i];
+  }
+}
+
+// C2 single-ship loop body, k ticks per launch (one lane per ship)
+template <bool DETAILED>
+__global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevState S, ConstBuf K, int k) {
+  __shared__ ShipConst lds_sc[2];
+  const ShipConst* SC = stage_consts(P, lds_sc);
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P.n_envs) return;
+  const ShipConst& c = SC[0];
+  const double* rn = S.route_n + (size_t)q * kMaxRoute;
+  const double* re = S.route_e + (size_t)q * kMaxRoute;
+  Ship s;
+  load_ship(S, q, s);
+  const double mach_dt = S.mach_dt[q];
+  for (int i = 0; i < k; ++i) control_and_integrate<DETAILED>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false);
+  store_ship(S, q, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+struct shipsim_handle {
+  shipsim_config cfg;
+  Params P;
+  DevState S;
+  ConstBuf K;
+  int device;
+  hipStream_t stream;
+  void* dev_block;
+  void* const_block;
+  size_t dev_bytes;
+  int ever_reset;
+  char err[512];
+};
+
+static int fail(shipsim_handle* h, int code, const char* fmt, ...) {
+  if (h) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(h->err, sizeof(h->err), fmt, ap);
+    va_end(ap);
+  }
+  return code;
+}
+
+#define HIPCHK(h, x)                                                              \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) return fail(h, SHIPSIM_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+extern "C" {
+
+int32_t shipsim_abi_version(void) { return SHIPSIM_ABI_VERSION; }
+
+const char* shipsim_build_info(void) {
+  return "shipsim gfx950 HIP (fp64, lane-pair AST kernel, wave-cooperative SBMPC) built " __DATE__ " " __TIME__;
+}
+
+static void fill_ship_common(shipsim_ship_config* s, double n, double e, double yaw, double u) {
+  memset(s, 0, sizeof(*s));
+  s->coefficient_of_deadweight_to_displacement = 0.7;
+  s->bunkers = 200000;
+  s->ballast = 200000;
+  s->length_of_ship = 80;
+  s->width_of_ship = 16;
+  s->added_mass_coefficient_in_surge = 0.4;
+  s->added_mass_coefficient_in_sway = 0.4;
+  s->added_mass_coefficient_in_yaw = 0.4;
+  s->dead_weight_tonnage = 3850000;
+  s->mass_over_linear_friction_coefficient_in_surge = 130;
+  s->mass_over_linear_friction_coefficient_in_sway = 18;
+  s->mass_over_linear_friction_coefficient_in_yaw = 90;
+  s->nonlinear_friction_coefficient_in_surge = 2400;
+  s->nonlinear_friction_coefficient_in_sway = 4000;
+  s->nonlinear_friction_coefficient_in_yaw = 400;
+  s->initial_north_position_m = n;
+  s->initial_east_position_m = e;
+  s->initial_yaw_angle_rad = yaw;
+  s->initial_forward_speed_m_per_s = u;
+  s->rudder_angle_to_sway_force_coefficient = 50e3;
+  s->rudder_angle_to_yaw_force_coefficient = 500e3;
+  s->max_rudder_angle_degrees = 30;
+  s->hotel_load = 200000;
+  s->main_engine_capacity = 0;
+  s->electrical_capacity = 2 * 510e3;
+  s->shaft_generator_state = SHIPSIM_SG_MOTOR;
+  s->rated_speed_main_engine_rpm = 1000;
+  s->linear_friction_main_engine = 68;
+  s->linear_friction_hybrid_shaft_generator = 57;
+  s->gear_ratio_between_main_engine_and_propeller = 0.6;
+  s->gear_ratio_between_hybrid_shaft_generator_and_propeller = 0.6;
+  s->propeller_inertia = 6000;
+  s->propeller_diameter = 3.1;
+  s->propeller_speed_to_torque_coefficient = 7.5;
+  s->propeller_speed_to_thrust_force_coefficient = 1.7;
+  s->kp_ship_speed = 205.25;
+  s->ki_ship_speed = 0.0525;
+  s->kp_shaft_speed = 50;
+  s->ki_shaft_speed = 0.00025;
+  s->initial_shaft_speed_integral_error = 114;
+  s->max_thrust = INFINITY;
+  s->radius_of_acceptance = 300;
+  s->lookahead_distance = 1000;
+  s->los_integral_gain = 0.002;
+  s->los_integrator_windup_limit = 4000;
+}
+
+static void set_route(shipsim_ship_config* s, const double (*r)[2], int n) {
+  s->n_route = n;
+  for (int i = 0; i < n; ++i) {
+    s->route_north[i] = r[i][0];
+    s->route_east[i] = r[i][1];
+  }
+}
+
+int shipsim_default_config(int32_t kind, int32_t machinery, int32_t collav, double time_step, shipsim_config* cfg) {
+  if (!cfg || kind < 0 || kind > 2 || machinery < 0 || machinery > 1 || collav < 0 || collav > 2) return SHIPSIM_EINVAL;
+  static const double map_e_n[][2] = {
+      {0, 10000}, {10000, 10000}, {9200, 9000}, {7600, 8500}, {6700, 7300}, {4900, 6500}, {4300, 5400},
+      {4700, 4500}, {6000, 4000}, {5800, 3600}, {4200, 3200}, {3200, 4100}, {2000, 4500}, {1000, 4000},
+      {900, 3500}, {500, 2600}, {0, 2350},
+      {10000, 0}, {11500, 750}, {12000, 2000}, {11700, 3000}, {11000, 3600}, {11250, 4250}, {12300, 4000},
+      {13000, 3800}, {14000, 3000}, {14500, 2300}, {15000, 1700}, {16000, 800}, {17500, 0},
+      {15500, 10000}, {16000, 9000}, {18000, 8000}, {19000, 7500}, {20000, 6000}, {20000, 10000},
+      {5500, 5300}, {6000, 5000}, {6800, 4500}, {8000, 5000}, {8700, 5500}, {9200, 6700}, {8000, 7000},
+      {6700, 6300}, {6000, 6000},
+      {15000, 5000}, {14000, 5500}, {12500, 5000}, {14000, 4100}, {16000, 2000}, {15700, 3700},
+      {11000, 2000}, {10300, 3200}, {9000, 1500}, {10000, 1000}};
+  static const int poly_counts[6] = {17, 13, 6, 9, 6, 4};
+  static const double test_route[7][2] = {{0, 0}, {2000, 4500}, {2500, 7500}, {7000, 12000}, {6500, 16000},
+                                          {3000, 17500}, {0, 20000}};
+  static const double obs_route[2][2] = {{10000, 15000}, {0, 5000}};
+  static const double obs_route_noniw[11][2] = {{10000, 15000}, {9500, 13500}, {8000, 13000}, {6500, 12500},
+                                                {6000, 11000}, {5500, 9500}, {4000, 9000}, {2500, 8500},
+                                                {2000, 7000}, {1500, 5500}, {0, 5000}};
+  memset(cfg, 0, sizeof(*cfg));
+  cfg->abi_version = SHIPSIM_ABI_VERSION;
+  cfg->kind = kind;
+  cfg->machinery = machinery;
+  cfg->collav = collav;
+  cfg->max_sampling_frequency = 9;
+  cfg->machinery_dt_quirk = 1;
+  cfg->normalize_action = 0;
+  cfg->n_ships = kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
+  cfg->time_step = time_step;
+  cfg->simulation_time = 10000;
+  cfg->env_radius_of_acceptance = 300;
+  cfg->current_velocity_component_from_north = -1;
+  cfg->current_velocity_component_from_east = -1;
+  cfg->wind_speed = 2;
+  cfg->wind_direction = -M_PI / 4;
+  cfg->sbmpc_tf = 1000;
+  cfg->sbmpc_dt = 20;
+  shipsim_ship_config* t = &cfg->ship[0];
+  shipsim_ship_config* o = &cfg->ship[1];
+  fill_ship_common(t, 100, 100, 60 * M_PI / 180, 4.25);
+  fill_ship_common(o, 9900, 14900, -135 * M_PI / 180, 3.5);
+  set_route(t, test_route, 7);
+  t->desired_forward_speed = 4.5;
+  o->desired_forward_speed = 4.0;
+  if (kind == SHIPSIM_KIND_AST) {  // run/env_setup.py
+    t->initial_propeller_shaft_speed_rad_per_s = 420 * M_PI / 30;
+    o->initial_propeller_shaft_speed_rad_per_s = 200 * M_PI / 30;
+    for (int i = 0; i < 2; ++i) {
+      cfg->ship[i].heading_kp = 1.65; cfg->ship[i].heading_kd = 75; cfg->ship[i].heading_ki = 0.001;
+      cfg->ship[i].speed_kp = 150; cfg->ship[i].speed_ki = 150; cfg->ship[i].speed_kd = 75;
+    }
+    set_route(o, obs_route, 2);
+    cfg->action_low = (float)(-(30 * (M_PI / 180.0)));
+    cfg->action_high = (float)(30 * (M_PI / 180.0));
+  } else {  // run_colav/run_simplified_model.py
+    t->speed_kp = 150; t->speed_ki = 150; t->speed_kd = 75;
+    o->speed_kp = .025; o->speed_ki = 700.5; o->speed_kd = 550.5;
+    t->heading_kp = .5; t->heading_ki = 0.01; t->heading_kd = 84;
+    o->heading_kp = .65; o->heading_ki = 0.001; o->heading_kd = 50;
+    set_route(o, obs_route_noniw, 11);
+    cfg->action_low = (float)(-M_PI / 6);
+    cfg->action_high = (float)(M_PI / 6);
+  }
+  int k = 0, p = 0;
+  for (p = 0; p < 6; ++p) {
+    cfg->poly_start[p] = k;
+    for (int i = 0; i < poly_counts[p]; ++i, ++k) {
+      cfg->poly_east[k] = map_e_n[k][0];
+      cfg->poly_north[k] = map_e_n[k][1];
+    }
+  }
+  cfg->poly_start[6] = k;
+  cfg->n_polys = 6;
+  return SHIPSIM_OK;
+}
+
+// host restatement of the constructors' derived constants (ship_model.py:412-474,
+// ship_engine.py:32-44, 341-401)
+static void make_ship_const(const shipsim_config* cfg, const shipsim_ship_config* c, ShipConst* k) {
+  memset(k, 0, sizeof(*k));
+  double payload = 0.9 * (c->dead_weight_tonnage - c->bunkers);
+  double lsw = c->dead_weight_tonnage / c->coefficient_of_deadweight_to_displacement - c->dead_weight_tonnage;
+  k->mass = lsw + payload + c->bunkers + c->ballast;
+  k->l_ship = c->length_of_ship;
+  k->w_ship = c->width_of_ship;
+  k->obs_l_cfg = c->length_of_ship;
+  k->obs_w_cfg = c->width_of_ship;
+  k->i_z = k->mass * (k->l_ship * k->l_ship + k->w_ship * k->w_ship) / 12;
+  k->x_du = k->mass * c->added_mass_coefficient_in_surge;
+  k->y_dv = k->mass * c->added_mass_coefficient_in_sway;
+  k->n_dr = k->i_z * c->added_mass_coefficient_in_yaw;
+  k->inv_m0 = 1.0 / (k->mass + k->x_du);
+  k->inv_m1 = 1.0 / (k->mass + k->y_dv);
+  k->inv_m2 = 1.0 / (k->i_z + k->n_dr);
+  k->dlin0 = k->mass / c->mass_over_linear_friction_coefficient_in_surge;
+  k->dlin1 = k->mass / c->mass_over_linear_friction_coefficient_in_sway;
+  k->dlin2 = k->i_z / c->mass_over_linear_friction_coefficient_in_yaw;
+  k->ku = c->nonlinear_friction_coefficient_in_surge;
+  k->kv = c->nonlinear_friction_coefficient_in_sway;
+  k->kr = c->nonlinear_friction_coefficient_in_yaw;
+  k->rho_a = 1.2;
+  k->proj_area_f = k->w_ship * 8.0;
+  k->proj_area_l = k->l_ship * 8.0;
+  k->cx = 0.5;
+  k->cy = 0.7;
+  k->cn = 0.08;
+  k->c_rudder_v = c->rudder_angle_to_sway_force_coefficient;
+  k->c_rudder_r = c->rudder_angle_to_yaw_force_coefficient;
+  k->max_rudder = c->max_rudder_angle_degrees * M_PI / 180;
+  double me = c->main_engine_capacity, el = c->electrical_capacity, hl = c->hotel_load;
+  if (c->shaft_generator_state == SHIPSIM_SG_MOTOR) {
+    k->avail_me = me;
+    k->avail_el = el - hl;
+  } else if (c->shaft_generator_state == SHIPSIM_SG_GEN) {
+    k->avail_me = me - hl;
+    k->avail_el = 0;
+  } else {
+    k->avail_me = me;
+    k->avail_el = 0;
+  }
+  k->cap_me = k->avail_me / 5 * M_PI / 30;
+  k->cap_el = k->avail_el / 5 * M_PI / 30;
+  k->d_me = c->linear_friction_main_engine;
+  k->d_hsg = c->linear_friction_hybrid_shaft_generator;
+  k->r_me = c->gear_ratio_between_main_engine_and_propeller;
+  k->r_hsg = c->gear_ratio_between_hybrid_shaft_generator_and_propeller;
+  k->jp = c->propeller_inertia;
+  k->kp_prop = c->propeller_speed_to_torque_coefficient;
+  k->thrust_coeff = pow(c->propeller_diameter, 4) * c->propeller_speed_to_thrust_force_coefficient;
+  k->shaft_speed_max = 1.1 * (c->rated_speed_main_engine_rpm * M_PI / 30) * k->r_me;
+  k->init_omega = c->initial_propeller_shaft_speed_rad_per_s;
+  k->kp_ship_speed = c->kp_ship_speed;
+  k->ki_ship_speed = c->ki_ship_speed;
+  k->kp_shaft_speed = c->kp_shaft_speed;
+  k->ki_shaft_speed = c->ki_shaft_speed;
+  k->init_shaft_ei = c->initial_shaft_speed_integral_error;
+  k->spd_kp = c->speed_kp;
+  k->spd_ki = c->speed_ki;
+  k->spd_kd = c->speed_kd;
+  k->max_thrust = c->max_thrust;
+  k->hdg_kp = c->heading_kp;
+  k->hdg_kd = c->heading_kd;
+  k->hdg_ki = c->heading_ki;
+  k->ra2 = c->radius_of_acceptance * c->radius_of_acceptance;
+  k->los_r = c->lookahead_distance;
+  k->los_r2 = c->lookahead_distance * c->lookahead_distance;
+  k->los_ki = c->los_integral_gain;
+  k->los_limit = c->los_integrator_windup_limit;
+  k->desired_speed = c->desired_forward_speed;
+  k->init_n = c->initial_north_position_m;
+  k->init_e = c->initial_east_position_m;
+  k->init_yaw = c->initial_yaw_angle_rad;
+  k->init_u = c->initial_forward_speed_m_per_s;
+  k->init_v = c->initial_sideways_speed_m_per_s;
+  k->init_r = c->initial_yaw_rate_rad_per_s;
+  k->n_route = c->n_route;
+  (void)cfg;
+}
+
+static int validate(const shipsim_config* cfg, char* err, size_t n) {
+  if (cfg->abi_version != SHIPSIM_ABI_VERSION) return snprintf(err, n, "abi_version %d != %d", cfg->abi_version, SHIPSIM_ABI_VERSION), 1;
+  if (cfg->kind < 0 || cfg->kind > 2) return snprintf(err, n, "bad kind %d", cfg->kind), 1;
+  if (cfg->kind == SHIPSIM_KIND_NONIW) return snprintf(err, n, "KIND_NONIW (C1) runs on the CPU oracle only"), 1;
+  if (cfg->machinery < 0 || cfg->machinery > 1) return snprintf(err, n, "bad machinery %d", cfg->machinery), 1;
+  if (cfg->collav < 0 || cfg->collav > 2) return snprintf(err, n, "bad collav %d", cfg->collav), 1;
+  int ns = cfg->kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
+  if (cfg->n_ships != ns) return snprintf(err, n, "n_ships %d != %d for kind %d", cfg->n_ships, ns, cfg->kind), 1;
+  if (!(cfg->time_step > 0)) return snprintf(err, n, "time_step must be > 0"), 1;
+  if (cfg->max_sampling_frequency < 0 || cfg->max_sampling_frequency + 2 > SHIPSIM_MAX_ROUTE)
+    return snprintf(err, n, "max_sampling_frequency %d out of range", cfg->max_sampling_frequency), 1;
+  for (int i = 0; i < ns; ++i) {
+    int nr = cfg->ship[i].n_route;
+    if (nr < 2 || nr > SHIPSIM_MAX_ROUTE) return snprintf(err, n, "ship %d route length %d out of range", i, nr), 1;
+    if (i == 1 && nr + cfg->max_sampling_frequency > SHIPSIM_MAX_ROUTE)
+      return snprintf(err, n, "obstacle route %d + samplings %d exceeds %d", nr, cfg->max_sampling_frequency, SHIPSIM_MAX_ROUTE), 1;
+  }
+  if (cfg->n_polys < 0 || cfg->n_polys > SHIPSIM_MAX_POLYS) return snprintf(err, n, "n_polys %d out of range", cfg->n_polys), 1;
+  if (cfg->poly_start[0] != 0 || cfg->poly_start[cfg->n_polys] > SHIPSIM_MAX_VERTS)
+    return snprintf(err, n, "bad poly_start"), 1;
+  for (int p = 0; p < cfg->n_polys; ++p)
+    if (cfg->poly_start[p + 1] - cfg->poly_start[p] < 3) return snprintf(err, n, "polygon %d has < 3 vertices", p), 1;
+  if (cfg->sbmpc_dt <= 0 || cfg->sbmpc_tf / cfg->sbmpc_dt > 4096) return snprintf(err, n, "bad sbmpc horizon"), 1;
+  return 0;
+}
+
+int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, void* stream, shipsim_handle** out) {
+  if (!cfg || !out || n_envs <= 0) return SHIPSIM_EINVAL;
+  *out = nullptr;
+  shipsim_handle* h = new (std::nothrow) shipsim_handle();
+  if (!h) return SHIPSIM_ENOMEM;
+  memset(h, 0, sizeof(*h));
+  if (validate(cfg, h->err, sizeof(h->err))) {
+    // keep the message reachable for the caller through a static buffer
+    static char last[512];
+    snprintf(last, sizeof(last), "%s", h->err);
+    delete h;
+    return SHIPSIM_EINVAL;
+  }
+  h->cfg = *cfg;
+  h->device = device;
+  h->stream = (hipStream_t)stream;
+  DeviceGuard g(device);
+  Params& P = h->P;
+  memset(&P, 0, sizeof(P));
+  const int ns = cfg->n_ships;
+  for (int i = 0; i < ns; ++i) make_ship_const(cfg, &cfg->ship[i], &P.sc[i]);
+  if (ns == 1) P.sc[1] = P.sc[0];
+  P.sc[1].obs_l_cfg = cfg->ship[ns - 1].length_of_ship;
+  P.sc[1].obs_w_cfg = cfg->ship[ns - 1].width_of_ship;
+  P.kind = cfg->kind;
+  P.machinery = cfg->machinery;
+  P.collav = cfg->collav;
+  P.n_ships = ns;
+  P.max_sampling = cfg->max_sampling_frequency;
+  P.n_envs = n_envs;
+  P.n_polys = cfg->n_polys;
+  P.dt = cfg->time_step;
+  P.sim_time = cfg->simulation_time;
+  P.mach_dt_init = cfg->time_step;
+  P.mach_dt_reset = cfg->machinery_dt_quirk ? 0.01 : cfg->time_step;
+  P.vc_n = cfg->current_velocity_component_from_north;
+  P.vc_e = cfg->current_velocity_component_from_east;
+  P.wind_dir = cfg->wind_direction;
+  P.wind_speed = cfg->wind_speed;
+  P.roa2 = cfg->env_radius_of_acceptance * cfg->env_radius_of_acceptance;
+  P.sbmpc_tf = cfg->sbmpc_tf;
+  P.sbmpc_dt = cfg->sbmpc_dt;
+  P.action_low = cfg->action_low;
+  P.action_high = cfg->action_high;
+  P.normalize_action = cfg->normalize_action;
+  if (ns == 2) {  // init_get_intermediate_waypoints env.py:143-161
+    const shipsim_ship_config* o = &cfg->ship[1];
+    double ABn = o->route_north[o->n_route - 1] - o->route_north[0];
+    double ABe = o->route_east[o->n_route - 1] - o->route_east[0];
+    int msf = cfg->max_sampling_frequency;
+    double AB_length = sqrt(ABn * ABn + ABe * ABe);
+    P.AB_seg = AB_length / (msf + 1);
+    P.AB_seg_n = ABn / (msf + 1);
+    P.AB_seg_e = ABe / (msf + 1);
+    double AB_alpha = atan2(ABe, ABn);
+    double AB_beta = M_PI / 2 - AB_alpha;
+    P.omega_iw = M_PI / 2 - AB_beta;
+    P.n_base0 = P.AB_seg_n + o->route_north[0];
+    P.e_base0 = P.AB_seg_e + o->route_east[0];
+    P.initial_states[0] = (float)cfg->ship[0].initial_north_position_m;
+    P.initial_states[1] = (float)cfg->ship[0].initial_east_position_m;
+    P.initial_states[2] = 0.0f;
+    P.initial_states[3] = (float)o->initial_north_position_m;
+    P.initial_states[4] = (float)o->initial_east_position_m;
+    P.initial_states[5] = (float)o->initial_yaw_angle_rad;
+    P.initial_states[6] = 0.0f;
+    P.initial_states[7] = (float)o->initial_forward_speed_m_per_s;
+  }
+  // map
+  int nv = cfg->poly_start[cfg->n_polys];
+  double mn_e = cfg->poly_east[0], mx_e = mn_e, mn_n = cfg->poly_north[0], mx_n = mn_n;
+  for (int i = 0; i < nv; ++i) {
+    if (cfg->poly_east[i] < mn_e) mn_e = cfg->poly_east[i];
+    if (cfg->poly_east[i] > mx_e) mx_e = cfg->poly_east[i];
+    if (cfg->poly_north[i] < mn_n) mn_n = cfg->poly_north[i];
+    if (cfg->poly_north[i] > mx_n) mx_n = cfg->poly_north[i];
+  }
+  P.min_east = mn_e; P.max_east = mx_e; P.min_north = mn_n; P.max_north = mx_n;
+
+  // constant block: edges, boxes, config routes
+  size_t c_edges = sizeof(Edge) * nv, c_boxes = sizeof(PolyBox) * SHIPSIM_MAX_POLYS;
+  size_t c_routes = sizeof(double) * 2 * kMaxRoute * 2;
+  size_t cbytes = c_edges + c_boxes + c_routes;
+  char* hostc = (char*)calloc(1, cbytes);
+  Edge* E = (Edge*)hostc;
+  PolyBox* B = (PolyBox*)(hostc + c_edges);
+  double* R = (double*)(hostc + c_edges + c_boxes);
+  for (int p = 0; p < cfg->n_polys; ++p) {
+    int s0 = cfg->poly_start[p], cnt = cfg->poly_start[p + 1] - s0;
+    B[p].first = s0;
+    B[p].count = cnt;
+    B[p].minx = B[p].maxx = cfg->poly_east[s0];
+    B[p].miny = B[p].maxy = cfg->poly_north[s0];
+    for (int i = 0; i < cnt; ++i) {
+      int j = (i + 1 == cnt) ? 0 : i + 1;
+      E[s0 + i].ax = cfg->poly_east[s0 + i];
+      E[s0 + i].ay = cfg->poly_north[s0 + i];
+      E[s0 + i].bx = cfg->poly_east[s0 + j];
+      E[s0 + i].by = cfg->poly_north[s0 + j];
+      if (E[s0 + i].ax < B[p].minx) B[p].minx = E[s0 + i].ax;
+      if (E[s0 + i].ax > B[p].maxx) B[p].maxx = E[s0 + i].ax;
+      if (E[s0 + i].ay < B[p].miny) B[p].miny = E[s0 + i].ay;
+      if (E[s0 + i].ay > B[p].maxy) B[p].maxy = E[s0 + i].ay;
+    }
+  }
+  for (int s = 0; s < ns; ++s)
+    for (int i = 0; i < cfg->ship[s].n_route; ++i) {
+      R[s * kMaxRoute + i] = cfg->ship[s].route_north[i];
+      R[2 * kMaxRoute + s * kMaxRoute + i] = cfg->ship[s].route_east[i];
+    }
+  hipError_t e = hipMalloc(&h->const_block, cbytes);
+  if (e != hipSuccess) {
+    free(hostc);
+    int rc = fail(h, SHIPSIM_EHIP, "hipMalloc(const): %s", hipGetErrorString(e));
+    *out = h;
+    return rc;
+  }
+  e = hipMemcpy(h->const_block, hostc, cbytes, hipMemcpyHostToDevice);
+  free(hostc);
+  if (e != hipSuccess) {
+    *out = h;
+    return fail(h, SHIPSIM_EHIP, "hipMemcpy(const): %s", hipGetErrorString(e));
+  }
+  h->K.edges = (const Edge*)h->const_block;
+  h->K.boxes = (const PolyBox*)((char*)h->const_block + c_edges);
+  h->K.cfg_route_n = (const double*)((char*)h->const_block + c_edges + c_boxes);
+  h->K.cfg_route_e = h->K.cfg_route_n + 2 * kMaxRoute;
+  h->K.n_edges = nv;
+
+  // state block
+  const size_t S = (size_t)n_envs * ns, N = (size_t)n_envs;
+  size_t bytes = 0;
+  auto take = [&](size_t b) { size_t o = bytes; bytes += (b + 255) & ~(size_t)255; return o; };
+  size_t off_f[SHIPSIM_N_SHIP_FIELDS];
+  for (int i = 0; i < SHIPSIM_N_SHIP_FIELDS; ++i) off_f[i] = take(S * sizeof(double));
+  size_t o_wpt = take(S * 4), o_stop = take(S * 4), o_nr = take(S * 4);
+  size_t o_rn = take(S * kMaxRoute * 8), o_re = take(S * kMaxRoute * 8);
+  size_t o_sc = take(N * 4), o_td = take(N * 8), o_tt = take(N * 8), o_acc = take(N * 8), o_nb = take(N * 8),
+         o_eb = take(N * 8), o_pl = take(N * 8), o_cl = take(N * 8), o_md = take(N * 8), o_s4 = take(N * 16),
+         o_no = take(N * 32), o_sb = take(N * 4), o_wr = take(N * 4);
+  e = hipMalloc(&h->dev_block, bytes);
+  if (e != hipSuccess) {
+    *out = h;
+    return fail(h, SHIPSIM_EHIP, "hipMalloc(state %zu B): %s", bytes, hipGetErrorString(e));
+  }
+  h->dev_bytes = bytes;
+  char* d = (char*)h->dev_block;
+  for (int i = 0; i < SHIPSIM_N_SHIP_FIELDS; ++i) h->S.f[i] = (double*)(d + off_f[i]);
+  h->S.next_wpt = (int32_t*)(d + o_wpt);
+  h->S.stop = (int32_t*)(d + o_stop);
+  h->S.n_route = (int32_t*)(d + o_nr);
+  h->S.route_n = (double*)(d + o_rn);
+  h->S.route_e = (double*)(d + o_re);
+  h->S.sampling_count = (int32_t*)(d + o_sc);
+  h->S.travel_dist = (double*)(d + o_td);
+  h->S.travel_time = (double*)(d + o_tt);
+  h->S.acc = (double*)(d + o_acc);
+  h->S.n_base = (double*)(d + o_nb);
+  h->S.e_base = (double*)(d + o_eb);
+  h->S.p_last = (double*)(d + o_pl);
+  h->S.chi_last = (double*)(d + o_cl);
+  h->S.mach_dt = (double*)(d + o_md);
+  h->S.states4 = (float*)(d + o_s4);
+  h->S.next_obs8 = (float*)(d + o_no);
+  h->S.snap_bits = (uint32_t*)(d + o_sb);
+  h->S.was_reset = (int32_t*)(d + o_wr);
+  e = hipMemsetAsync(h->dev_block, 0, bytes, h->stream);
+  if (e != hipSuccess) {
+    *out = h;
+    return fail(h, SHIPSIM_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+  }
+  int threads = 256, blocks = (int)((S + threads - 1) / threads);
+  hipLaunchKernelGGL(init_kernel, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K);
+  e = hipGetLastError();
+  *out = h;
+  if (e != hipSuccess) return fail(h, SHIPSIM_EHIP, "init_kernel: %s", hipGetErrorString(e));
+  return SHIPSIM_OK;
+}
+
+int shipsim_destroy(shipsim_handle* h) {
+  if (!h) return SHIPSIM_EINVAL;
+  {
+    DeviceGuard g(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    else (void)hipDeviceSynchronize();
+    if (h->dev_block) (void)hipFree(h->dev_block);
+    if (h->const_block) (void)hipFree(h->const_block);
+  }
+  delete h;
+  return SHIPSIM_OK;
+}
+
+const char* shipsim_last_error(const shipsim_handle* h) { return h ? h->err : "null handle"; }
+int32_t shipsim_num_envs(const shipsim_handle* h) { return h ? h->P.n_envs : -1; }
+
+int shipsim_reset(shipsim_handle* h, const uint8_t* env_mask, float* obs_out) {
+  if (!h || !h->dev_block) return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_AST && h->P.kind != SHIPSIM_KIND_SINGLE)
+    return fail(h, SHIPSIM_EINVAL, "reset: kind %d not supported on device", h->P.kind);
+  DeviceGuard g(h->device);
+  int S = h->P.n_envs * h->P.n_ships, threads = 256, blocks = (S + threads - 1) / threads;
+  if (h->P.machinery == SHIPSIM_MACH_DETAILED)
+    hipLaunchKernelGGL(reset_kernel<true>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, env_mask, obs_out);
+  else
+    hipLaunchKernelGGL(reset_kernel<false>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, env_mask, obs_out);
+  HIPCHK(h, hipGetLastError());
+  h->ever_reset = 1;
+  return SHIPSIM_OK;
+}
+
+int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks, float* obs_out,
+                 double* reward_out, uint8_t* done_out, uint32_t* events_out, int32_t* ticks_out) {
+  if (!h || !h->dev_block) return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "step: only SHIPSIM_KIND_AST has decision steps");
+  if (!action) return fail(h, SHIPSIM_EINVAL, "step: action is NULL");
+  if (!h->ever_reset) return fail(h, SHIPSIM_ESTATE, "step before reset");
+  DeviceGuard g(h->device);
+  if (max_ticks <= 0) max_ticks = (int)(2.0 * h->P.sim_time / h->P.dt) + 16;
+  const int lanes = h->P.n_envs * 2, threads = 64, blocks = (lanes + threads - 1) / threads;
+  const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
+#define LAUNCH(D, CA)                                                                                              \
+  hipLaunchKernelGGL((ast_step_kernel<D, CA>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, action, \
+                     active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out)
+  switch (h->P.collav) {
+    case SHIPSIM_COLLAV_NONE: if (det) LAUNCH(true, 0); else LAUNCH(false, 0); break;
+    case SHIPSIM_COLLAV_SIMPLE: if (det) LAUNCH(true, 1); else LAUNCH(false, 1); break;
+    default: if (det) LAUNCH(true, 2); else LAUNCH(false, 2); break;
+  }
+#undef LAUNCH
+  HIPCHK(h, hipGetLastError());
+  return SHIPSIM_OK;
+}
+
+int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
+  if (!h || !h->dev_block || k < 0) return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_SINGLE)
+    return fail(h, SHIPSIM_EINVAL, "tick: device raw ticks implemented for SHIPSIM_KIND_SINGLE");
+  (void)events_out;
+  if (k == 0) return SHIPSIM_OK;
+  DeviceGuard g(h->device);
+  const int threads = 64, blocks = (h->P.n_envs + threads - 1) / threads;
+  if (h->P.machinery == SHIPSIM_MACH_DETAILED)
+    hipLaunchKernelGGL(single_tick_kernel<true>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
+  else
+    hipLaunchKernelGGL(single_tick_kernel<false>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
+  HIPCHK(h, hipGetLastError());
+  return SHIPSIM_OK;
+}
+
+static int field_ptr(shipsim_handle* h, int32_t field, void** p, size_t* bytes) {
+  const size_t S = (size_t)h->P.n_envs * h->P.n_ships, N = (size_t)h->P.n_envs;
+  if (field >= 0 && field < SHIPSIM_N_SHIP_FIELDS) {
+    if (field == SHIPSIM_F_NEXT_WPT) { *p = h->S.next_wpt; *bytes = S * 4; return 0; }
+    if (field == SHIPSIM_F_STOP) { *p = h->S.stop; *bytes = S * 4; return 0; }
+    *p = h->S.f[field]; *bytes = S * 8;
+    return 0;
+  }
+  switch (field) {
+    case SHIPSIM_E_SAMPLING_COUNT: *p = h->S.sampling_count; *bytes = N * 4; return 0;
+    case SHIPSIM_E_TRAVEL_DIST: *p = h->S.travel_dist; *bytes = N * 8; return 0;
+    case SHIPSIM_E_TRAVEL_TIME: *p = h->S.travel_time; *bytes = N * 8; return 0;
+    case SHIPSIM_E_ACC_REWARD: *p = h->S.acc; *bytes = N * 8; return 0;
+    case SHIPSIM_E_N_BASE: *p = h->S.n_base; *bytes = N * 8; return 0;
+    case SHIPSIM_E_E_BASE: *p = h->S.e_base; *bytes = N * 8; return 0;
+    case SHIPSIM_E_SBMPC_P_LAST: *p = h->S.p_last; *bytes = N * 8; return 0;
+    case SHIPSIM_E_SBMPC_CHI_LAST: *p = h->S.chi_last; *bytes = N * 8; return 0;
+    case SHIPSIM_E_ROUTE_LEN: *p = h->S.n_route; *bytes = S * 4; return 0;
+    case SHIPSIM_E_ROUTE_NORTH: *p = h->S.route_n; *bytes = S * kMaxRoute * 8; return 0;
+    case SHIPSIM_E_ROUTE_EAST: *p = h->S.route_e; *bytes = S * kMaxRoute * 8; return 0;
+  }
+  return 1;
+}
+
+int shipsim_get_state(shipsim_handle* h, int32_t field, void* dst) {
+  if (!h || !dst) return SHIPSIM_EINVAL;
+  void* p;
+  size_t b;
+  if (field_ptr(h, field, &p, &b)) return fail(h, SHIPSIM_EINVAL, "unknown field %d", field);
+  DeviceGuard g(h->device);
+  HIPCHK(h, hipMemcpyAsync(dst, p, b, hipMemcpyDefault, h->stream));
+  return SHIPSIM_OK;
+}
+
+int shipsim_set_state(shipsim_handle* h, int32_t field, const void* src) {
+  if (!h || !src) return SHIPSIM_EINVAL;
+  void* p;
+  size_t b;
+  if (field_ptr(h, field, &p, &b)) return fail(h, SHIPSIM_EINVAL, "unknown field %d", field);
+  DeviceGuard g(h->device);
+  HIPCHK(h, hipMemcpyAsync(p, src, b, hipMemcpyDefault, h->stream));
+  return SHIPSIM_OK;
+}
+
+int shipsim_synchronize(shipsim_handle* h) {
+  if (!h) return SHIPSIM_EINVAL;
+  DeviceGuard g(h->device);
+  if (h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
+  else HIPCHK(h, hipDeviceSynchronize());
+  return SHIPSIM_OK;
+}
+
+}  // extern "C"

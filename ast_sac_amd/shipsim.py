@@ -1,0 +1,164 @@
+"""Python binding of libshipsim.so (include/shipsim.h) over torch device tensors.
+
+The library is the product path: there is no CPU fallback. If the shared library is missing or
+cannot be loaded, importing/constructing raises — build it with `python -c "import
+__graft_entry__ as g; g.build()"` (hipcc --offload-arch=gfx950).
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (loads torch's HIP runtime first; libshipsim binds to the same libamdhip64.so.7)
+
+from . import shipsim_abi as abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libshipsim.so")
+
+_lib = None
+
+
+class ShipSimError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ShipSimError(f"native library {path} not found: build it first (__graft_entry__.build())")
+    L = C.CDLL(path)
+    P = C.c_void_p
+    cfgp = C.POINTER(abi.Config)
+    L.shipsim_abi_version.restype = C.c_int32
+    L.shipsim_build_info.restype = C.c_char_p
+    L.shipsim_default_config.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_double, cfgp]
+    L.shipsim_create.argtypes = [cfgp, C.c_int32, C.c_int32, P, C.POINTER(P)]
+    L.shipsim_destroy.argtypes = [P]
+    L.shipsim_last_error.argtypes = [P]
+    L.shipsim_last_error.restype = C.c_char_p
+    L.shipsim_num_envs.argtypes = [P]
+    L.shipsim_num_envs.restype = C.c_int32
+    L.shipsim_reset.argtypes = [P, P, P]
+    L.shipsim_step.argtypes = [P, P, P, C.c_int32, P, P, P, P, P]
+    L.shipsim_tick.argtypes = [P, C.c_int32, P]
+    L.shipsim_get_state.argtypes = [P, C.c_int32, P]
+    L.shipsim_set_state.argtypes = [P, C.c_int32, P]
+    L.shipsim_synchronize.argtypes = [P]
+    if L.shipsim_abi_version() != abi.ABI_VERSION:
+        raise ShipSimError(f"ABI mismatch: library {L.shipsim_abi_version()} vs binding {abi.ABI_VERSION}")
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_default_config", "shipsim_create",
+                    "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
+                    "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize")
+
+
+def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
+    cfg = abi.Config()
+    rc = load_library().shipsim_default_config(kind, machinery, collav, time_step, C.byref(cfg))
+    if rc:
+        raise ShipSimError(f"shipsim_default_config failed ({rc})")
+    return cfg
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class ShipSim:
+    """N independent environments on one device, state resident in HBM."""
+
+    def __init__(self, cfg, n_envs, device=None):
+        if not torch.cuda.is_available():
+            raise ShipSimError("ShipSim needs a HIP device (torch.cuda.is_available() is False)")
+        self.L = load_library()
+        self.cfg = cfg
+        self.n_envs = int(n_envs)
+        self.n_ships = int(cfg.n_ships)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
+        with torch.cuda.device(self.device):
+            self.stream = torch.cuda.current_stream(self.device)
+            h = C.c_void_p()
+            rc = self.L.shipsim_create(C.byref(cfg), self.n_envs, self.device.index, C.c_void_p(self.stream.cuda_stream),
+                                       C.byref(h))
+            if rc:
+                msg = self.L.shipsim_last_error(h).decode() if h.value else "invalid config"
+                if h.value:
+                    self.L.shipsim_destroy(h)
+                raise ShipSimError(f"shipsim_create failed ({rc}): {msg}")
+        self.h = h
+
+    def _check(self, rc, what):
+        if rc:
+            raise ShipSimError(f"{what} failed ({rc}): {self.L.shipsim_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.L.shipsim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _dev(self, x, dtype):
+        if x is None:
+            return None
+        t = torch.as_tensor(x, dtype=dtype, device=self.device).contiguous()
+        return t
+
+    def reset(self, mask=None, obs_out=None):
+        m = self._dev(mask, torch.uint8) if mask is not None else None
+        obs = obs_out if obs_out is not None else torch.empty((self.n_envs, 8), dtype=torch.float32, device=self.device)
+        self._check(self.L.shipsim_reset(self.h, _ptr(m), _ptr(obs)), "shipsim_reset")
+        return obs
+
+    def step(self, action, active=None, max_ticks=0, out=None):
+        """action: (N,) or (N,1) float32 scoping angles [rad] (already denormalized)."""
+        a = self._dev(action, torch.float32).reshape(-1)
+        if a.numel() != self.n_envs:
+            raise ShipSimError(f"action has {a.numel()} entries, expected {self.n_envs}")
+        act = self._dev(active, torch.uint8) if active is not None else None
+        if out is None:
+            out = dict(obs=torch.empty((self.n_envs, 8), dtype=torch.float32, device=self.device),
+                       reward=torch.empty(self.n_envs, dtype=torch.float64, device=self.device),
+                       done=torch.empty(self.n_envs, dtype=torch.uint8, device=self.device),
+                       events=torch.empty(self.n_envs, dtype=torch.int32, device=self.device),
+                       ticks=torch.empty(self.n_envs, dtype=torch.int32, device=self.device))
+        self._check(self.L.shipsim_step(self.h, _ptr(a), _ptr(act), int(max_ticks), _ptr(out["obs"]), _ptr(out["reward"]),
+                                        _ptr(out["done"]), _ptr(out["events"]), _ptr(out["ticks"])), "shipsim_step")
+        self._keep = (a, act)
+        return out
+
+    def tick(self, k=1):
+        self._check(self.L.shipsim_tick(self.h, int(k), None), "shipsim_tick")
+
+    def _field_shape(self, field):
+        S, N = self.n_envs * self.n_ships, self.n_envs
+        if field < abi.N_SHIP_FIELDS:
+            return (S,), torch.int32 if field in abi.INT_FIELDS else torch.float64
+        if field == abi.E_ROUTE_LEN:
+            return (S,), torch.int32
+        if field in (abi.E_ROUTE_NORTH, abi.E_ROUTE_EAST):
+            return (S, abi.MAX_ROUTE), torch.float64
+        return (N,), torch.int32 if field in abi.INT_FIELDS else torch.float64
+
+    def get(self, field):
+        shape, dt = self._field_shape(field)
+        t = torch.empty(shape, dtype=dt, device=self.device)
+        self._check(self.L.shipsim_get_state(self.h, int(field), _ptr(t)), "shipsim_get_state")
+        return t
+
+    def set(self, field, value):
+        shape, dt = self._field_shape(field)
+        t = self._dev(value, dt).reshape(shape)
+        self._check(self.L.shipsim_set_state(self.h, int(field), _ptr(t)), "shipsim_set_state")
+        self._keep_set = t
+
+    def synchronize(self):
+        self._check(self.L.shipsim_synchronize(self.h), "shipsim_synchronize")

@@ -1,0 +1,204 @@
+"""Headline benchmark: batched two-ship AST env-steps/sec (BASELINE.json metric) on 1..8 MI355X.
+
+A "step" is one batched MultiShipRLEnv.step() over every env of every rank: each env consumes one
+scoping-angle decision and ticks until its next decision point (RoA + 1 tick) or done (≈156
+env-ticks per decision at dt = 4 s); envs that finished are auto-reset (masked reset kernel)
+inside the step. Actions come from a device-resident synthetic table U(-1, 1) (PCG64 seeded per
+global env id, SURVEY.md §8(d) C3 input) mapped by NormalizedBoxEnv's float32 rule.
+
+value = env-ticks (one `_step` of one env, both ships + reward/termination) summed over all ranks
+        / max-over-ranks wall time of the K timed steps.
+
+Workload (config C3, BASELINE.json configs[2]): 4096 two-ship AST envs per GPU, ShipModelAST
+with PTI machinery, HeadingBySampledRouteController, reward_designs, collav = sbmpc (the runner
+default, run/ast-sac_runner.py:35), dt = 4 s. Weak scaling: envs per GPU fixed.
+
+Launch:  python bench.py                       (N = 1)
+         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ALGO_BYTES_PER_ENV_TICK = 616  # C3/C5 detailed dynamics, one obstacle ship
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=40)
+    p.add_argument("--warmup", type=int, default=12)
+    p.add_argument("--envs-per-gpu", type=int, default=4096)
+    p.add_argument("--collav", default="sbmpc", choices=["none", "simple", "sbmpc"])
+    p.add_argument("--machinery", default="detailed", choices=["detailed", "simplified"])
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round1_pmc_traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, seconds, n_threads):
+    """The oracle (C restatement, OpenMP over envs) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle_ffi as O
+    from ast_sac_amd import shipsim_abi as abi
+    n = max(n_threads, 8)
+    while True:
+        acts = abi.normalized_to_scoping(abi.ast_action_table(n))
+        t0 = time.perf_counter()
+        total, ticks, dec, ret, bits = O.ast_rollouts(cfg, acts, n_threads=n_threads)
+        dt = time.perf_counter() - t0
+        if dt >= seconds * 0.5 or n >= 1 << 16:
+            break
+        n = int(n * min(8.0, max(2.0, seconds / max(dt, 1e-3))))
+    return dict(value=total / dt, unit="env-ticks/s", cores=n_threads, kind="port",
+                sample=f"{n} two-ship AST envs x 1 episode (<=9 decisions, auto from PCG64 table), "
+                       f"{int(total)} env-ticks in {dt:.1f} s, oracle/shipsim_oracle.c -O2 OpenMP")
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ast_sac_amd import shipsim_abi as abi
+    from ast_sac_amd.shipsim import ShipSim
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    mach = abi.MACH_DETAILED if args.machinery == "detailed" else abi.MACH_SIMPLIFIED
+    cfg = abi.ast_config(args.collav, machinery=mach)
+    N = args.envs_per_gpu
+    sim = ShipSim(cfg, N, device=dev)
+
+    # device-resident synthetic decision table: 9 decisions per episode, new table row per episode
+    n_dec = cfg.max_sampling_frequency
+    table_eps = 8
+    gen = np.random.Generator(np.random.PCG64(20251015 + rank))
+    a_norm = gen.uniform(-1, 1, (table_eps, n_dec, N)).astype(np.float32)
+    table = torch.from_numpy(abi.normalized_to_scoping(a_norm)).to(dev)  # (eps, dec, N)
+    ep_idx = torch.zeros(N, dtype=torch.long, device=dev)
+    dec_idx = torch.zeros(N, dtype=torch.long, device=dev)
+    ar = torch.arange(N, device=dev)
+    out = dict(obs=torch.empty((N, 8), dtype=torch.float32, device=dev),
+               reward=torch.empty(N, dtype=torch.float64, device=dev),
+               done=torch.empty(N, dtype=torch.uint8, device=dev),
+               events=torch.empty(N, dtype=torch.int32, device=dev),
+               ticks=torch.empty(N, dtype=torch.int32, device=dev))
+    obs_reset = torch.empty((N, 8), dtype=torch.float32, device=dev)
+    total_ticks = torch.zeros((), dtype=torch.int64, device=dev)
+    total_decisions = torch.zeros((), dtype=torch.int64, device=dev)
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def one_step(timed_i=None):
+        act = table[ep_idx % table_eps, dec_idx, ar]
+        if timed_i is not None:
+            ev0[timed_i].record()
+        sim.step(act, out=out)
+        if timed_i is not None:
+            ev1[timed_i].record()
+        done = out["done"].bool() | (dec_idx + 1 >= n_dec)
+        total_ticks.add_(out["ticks"].sum())
+        total_decisions.add_(N)
+        dec_idx.add_(1)
+        dec_idx.masked_fill_(done, 0)
+        ep_idx.add_(done.long())
+        sim.reset(mask=done.to(torch.uint8), obs_out=obs_reset)
+
+    sim.reset(obs_out=obs_reset)
+    for _ in range(args.warmup):
+        one_step()
+    total_ticks.zero_()
+    total_decisions.zero_()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    kern_ms = np.array([a.elapsed_time(b) for a, b in zip(ev0, ev1)])
+    local_ticks = int(total_ticks.item())
+    stats = torch.tensor([elapsed, float(local_ticks), float(total_decisions.item()), float(kern_ms.mean())],
+                         dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, kmean = float(mx[0]), float(mx[3])
+        all_ticks, all_dec = float(sm[1]), float(sm[2])
+    else:
+        all_ticks, all_dec, kmean = float(local_ticks), float(total_decisions.item()), float(kern_ms.mean())
+
+    if rank == 0:
+        value = all_ticks / elapsed
+        ticks_per_launch = local_ticks / args.steps
+        achieved = ALGO_BYTES_PER_ENV_TICK * ticks_per_launch / (kmean * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(args.pmc_json) as f:
+                pmc = json.load(f)
+            if pmc.get("collav") == args.collav and pmc.get("envs") == N:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        cpu = None
+        if not args.no_cpu_baseline:
+            nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            nthreads = min(nthreads, 16)
+            cpu = cpu_baseline(cfg, args.cpu_baseline_seconds, nthreads)
+        line = {
+            "metric": "batched env-steps/sec (two-ship AST)",
+            "value": value,
+            "unit": "env-ticks/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded PCG64 scoping-angle table, reference scenario of record)",
+            "config": {"workload": "C3: two-ship AST envs (ShipModelAST PTI machinery, sampled-route LOS, "
+                                   "reward_designs), dt 4 s",
+                       "envs_per_gpu": N, "global_envs": N * world, "collav": args.collav,
+                       "machinery": args.machinery, "parallelism": f"env-shard x{world}"},
+            "decisions_per_s": all_dec / elapsed,
+            "env_ticks_per_decision": all_ticks / max(all_dec, 1),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": f"ast_step_kernel (avg {kmean:.3f} ms/launch, "
+                                   f"{ticks_per_launch:.0f} env-ticks x {ALGO_BYTES_PER_ENV_TICK} B)"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    sim.close()
+
+
+if __name__ == "__main__":
+    main()
