@@ -128,6 +128,10 @@ struct Deriv {
 
 // get_wind_force :497-517
 __device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, const Ship& s, double tau[3]) {
+#ifdef SHIPSIM_ABL_NO_WIND
+  tau[0] = tau[1] = tau[2] = 0.0;
+  return;
+#endif
   double sw, cw;
   sincos(P.wind_dir - s.yaw, &sw, &cw);
   double uw = P.wind_speed * cw;

@@ -27,60 +27,81 @@ using namespace shipsim;
 // device state (SoA). Ship arrays are indexed q = env * n_ships + ship (lane order).
 // ---------------------------------------------------------------------------------------------
 struct DevState {
-  double* f[SHIPSIM_N_SHIP_FIELDS];  // double ship fields (int ones unused here)
-  int32_t* next_wpt;
-  int32_t* stop;
-  int32_t* n_route;
-  double* route_n;  // [q][kMaxRoute]
-  double* route_e;
-  // env
-  int32_t* sampling_count;
-  double* travel_dist;
-  double* travel_time;
-  double* acc;
-  double* n_base;
-  double* e_base;
-  double* p_last;
-  double* chi_last;
-  double* mach_dt;
-  float* states4;    // [env][4] self.states (test n, e, obs n, e) for the 'simple' collav quirk
-  float* next_obs8;  // [env][8] self.next_observations snapshot
-  uint32_t* snap_bits;
-  int32_t* was_reset;
+  // One device block; every array lives at base + (index * stride). Keeping the table as one base
+  // pointer + strides (instead of ~40 pointers) keeps it out of the SGPR budget of the big kernel.
+  char* base;
+  int64_t ship_stride;   // bytes of one [env][ship] array (doubles)
+  int64_t route_stride;  // bytes of one [env][ship][kMaxRoute] route array
+  int64_t env_stride;    // bytes of one per-env array (sized for the widest: 8 floats)
+  int64_t env_off;       // start of the per-env arrays
+  __host__ __device__ double* f(int k) const { return (double*)(base + k * ship_stride); }
+  __host__ __device__ int32_t* next_wpt() const { return (int32_t*)(base + 19 * ship_stride); }
+  __host__ __device__ int32_t* stop() const { return (int32_t*)(base + 20 * ship_stride); }
+  __host__ __device__ int32_t* n_route() const { return (int32_t*)(base + 21 * ship_stride); }
+  __host__ __device__ double* route_n() const { return (double*)(base + 22 * ship_stride); }
+  __host__ __device__ double* route_e() const { return (double*)(base + 22 * ship_stride + route_stride); }
+  __host__ __device__ char* ev(int k) const { return base + env_off + k * env_stride; }
+  __host__ __device__ int32_t* sampling_count() const { return (int32_t*)ev(0); }
+  __host__ __device__ double* travel_dist() const { return (double*)ev(1); }
+  __host__ __device__ double* travel_time() const { return (double*)ev(2); }
+  __host__ __device__ double* acc() const { return (double*)ev(3); }
+  __host__ __device__ double* n_base() const { return (double*)ev(4); }
+  __host__ __device__ double* e_base() const { return (double*)ev(5); }
+  __host__ __device__ double* p_last() const { return (double*)ev(6); }
+  __host__ __device__ double* chi_last() const { return (double*)ev(7); }
+  __host__ __device__ double* mach_dt() const { return (double*)ev(8); }
+  __host__ __device__ float* states4() const { return (float*)ev(9); }      // [env][4] self.states (simple collav)
+  __host__ __device__ float* next_obs8() const { return (float*)ev(10); }   // [env][8] self.next_observations
+  __host__ __device__ uint32_t* snap_bits() const { return (uint32_t*)ev(11); }
+  __host__ __device__ int32_t* was_reset() const { return (int32_t*)ev(12); }
+  __host__ __device__ int32_t* dec_flags() const { return (int32_t*)ev(13); }  // DF_* (sliced stepping)
+  static constexpr int kEnvArrays = 14;
+  static constexpr int kShipArrays = 22;
 };
+// dec_flags bits (per env, persistent across calls)
+#define DF_AWAITING 1
+#define DF_HAVE_IW 2
+#define DF_PHASE_SHIFT 2
+
 enum { SF_N = 0, SF_E, SF_YAW, SF_U, SF_V, SF_R, SF_OMEGA, SF_TIME, SF_ECT, SF_ECT_INT, SF_HDG_EI, SF_HDG_PREV,
        SF_SPD_A, SF_SPD_B, SF_RUDDER, SF_THRUST, SF_LOG_ECT, SF_LOG_N, SF_LOG_E };
 
 struct ConstBuf {
-  const Edge* edges;
-  const PolyBox* boxes;
-  const double* cfg_route_n;  // [2][kMaxRoute]
-  const double* cfg_route_e;
+  // edges [SHIPSIM_MAX_VERTS] | boxes [SHIPSIM_MAX_POLYS] | config routes n/e [2][kMaxRoute] each
+  const char* base;
   int32_t n_edges;
+  __host__ __device__ const Edge* edges() const { return (const Edge*)base; }
+  __host__ __device__ const PolyBox* boxes() const { return (const PolyBox*)(base + sizeof(Edge) * SHIPSIM_MAX_VERTS); }
+  __host__ __device__ const double* cfg_route_n() const {
+    return (const double*)(base + sizeof(Edge) * SHIPSIM_MAX_VERTS + sizeof(PolyBox) * SHIPSIM_MAX_POLYS);
+  }
+  __host__ __device__ const double* cfg_route_e() const { return cfg_route_n() + 2 * kMaxRoute; }
+  static constexpr size_t kBytes = sizeof(Edge) * SHIPSIM_MAX_VERTS + sizeof(PolyBox) * SHIPSIM_MAX_POLYS +
+                                   sizeof(double) * 4 * kMaxRoute;
 };
 
 __device__ __forceinline__ void load_ship(const DevState& S, int q, Ship& s) {
-  s.n = S.f[SF_N][q]; s.e = S.f[SF_E][q]; s.yaw = S.f[SF_YAW][q];
-  s.u = S.f[SF_U][q]; s.v = S.f[SF_V][q]; s.r = S.f[SF_R][q];
-  s.omega = S.f[SF_OMEGA][q]; s.time = S.f[SF_TIME][q];
-  s.e_ct = S.f[SF_ECT][q]; s.e_ct_int = S.f[SF_ECT_INT][q];
-  s.hdg_ei = S.f[SF_HDG_EI][q]; s.hdg_prev = S.f[SF_HDG_PREV][q];
-  s.spd_a = S.f[SF_SPD_A][q]; s.spd_b = S.f[SF_SPD_B][q];
-  s.log_rudder = S.f[SF_RUDDER][q]; s.log_thrust = S.f[SF_THRUST][q]; s.log_ect = S.f[SF_LOG_ECT][q];
-  s.log_n = S.f[SF_LOG_N][q]; s.log_e = S.f[SF_LOG_E][q];
-  s.next_wpt = S.next_wpt[q]; s.stop = S.stop[q]; s.n_route = S.n_route[q];
-  load_segment(s, S.route_n + (size_t)q * kMaxRoute, S.route_e + (size_t)q * kMaxRoute);
+  s.n = S.f(SF_N)[q]; s.e = S.f(SF_E)[q]; s.yaw = S.f(SF_YAW)[q];
+  s.u = S.f(SF_U)[q]; s.v = S.f(SF_V)[q]; s.r = S.f(SF_R)[q];
+  s.omega = S.f(SF_OMEGA)[q]; s.time = S.f(SF_TIME)[q];
+  s.e_ct = S.f(SF_ECT)[q]; s.e_ct_int = S.f(SF_ECT_INT)[q];
+  s.hdg_ei = S.f(SF_HDG_EI)[q]; s.hdg_prev = S.f(SF_HDG_PREV)[q];
+  s.spd_a = S.f(SF_SPD_A)[q]; s.spd_b = S.f(SF_SPD_B)[q];
+  s.log_rudder = S.f(SF_RUDDER)[q]; s.log_thrust = S.f(SF_THRUST)[q]; s.log_ect = S.f(SF_LOG_ECT)[q];
+  s.log_n = S.f(SF_LOG_N)[q]; s.log_e = S.f(SF_LOG_E)[q];
+  s.next_wpt = S.next_wpt()[q]; s.stop = S.stop()[q]; s.n_route = S.n_route()[q];
+  load_segment(s, S.route_n() + (size_t)q * kMaxRoute, S.route_e() + (size_t)q * kMaxRoute);
 }
 __device__ __forceinline__ void store_ship(const DevState& S, int q, const Ship& s) {
-  S.f[SF_N][q] = s.n; S.f[SF_E][q] = s.e; S.f[SF_YAW][q] = s.yaw;
-  S.f[SF_U][q] = s.u; S.f[SF_V][q] = s.v; S.f[SF_R][q] = s.r;
-  S.f[SF_OMEGA][q] = s.omega; S.f[SF_TIME][q] = s.time;
-  S.f[SF_ECT][q] = s.e_ct; S.f[SF_ECT_INT][q] = s.e_ct_int;
-  S.f[SF_HDG_EI][q] = s.hdg_ei; S.f[SF_HDG_PREV][q] = s.hdg_prev;
-  S.f[SF_SPD_A][q] = s.spd_a; S.f[SF_SPD_B][q] = s.spd_b;
-  S.f[SF_RUDDER][q] = s.log_rudder; S.f[SF_THRUST][q] = s.log_thrust; S.f[SF_LOG_ECT][q] = s.log_ect;
-  S.f[SF_LOG_N][q] = s.log_n; S.f[SF_LOG_E][q] = s.log_e;
-  S.next_wpt[q] = s.next_wpt; S.stop[q] = s.stop; S.n_route[q] = s.n_route;
+  S.f(SF_N)[q] = s.n; S.f(SF_E)[q] = s.e; S.f(SF_YAW)[q] = s.yaw;
+  S.f(SF_U)[q] = s.u; S.f(SF_V)[q] = s.v; S.f(SF_R)[q] = s.r;
+  S.f(SF_OMEGA)[q] = s.omega; S.f(SF_TIME)[q] = s.time;
+  S.f(SF_ECT)[q] = s.e_ct; S.f(SF_ECT_INT)[q] = s.e_ct_int;
+  S.f(SF_HDG_EI)[q] = s.hdg_ei; S.f(SF_HDG_PREV)[q] = s.hdg_prev;
+  S.f(SF_SPD_A)[q] = s.spd_a; S.f(SF_SPD_B)[q] = s.spd_b;
+  S.f(SF_RUDDER)[q] = s.log_rudder; S.f(SF_THRUST)[q] = s.log_thrust; S.f(SF_LOG_ECT)[q] = s.log_ect;
+  S.f(SF_LOG_N)[q] = s.log_n; S.f(SF_LOG_E)[q] = s.log_e;
+  S.next_wpt()[q] = s.next_wpt; S.stop()[q] = s.stop; S.n_route()[q] = s.n_route;
 }
 
 // per-block LDS copy of the two ShipConst (lanes of either parity read one of two addresses)
@@ -145,6 +166,8 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   const double d_safe = 1000.0, d_close = 2000.0;
   const double PHI_AH = 68.5 * (kPi / 180.0), PHI_OT = 68.5 * (kPi / 180.0);
   const double cos_ot = cos(PHI_OT * (kPi / 180.0));  // np.cos(np.deg2rad(PHI_OT_)) — PHI_OT_ already in rad
+  const double max_d_safe = py_max(py_max(d_safe + in.obs_l / 2, 0.5 * d_safe + in.obs_l / 2),
+                                   py_max(d_safe + in.obs_w / 2, d_safe + os_l / 2 + in.obs_l / 2));
   const double CHI_DEG = -30.0 + 10.0 * ichi;
   const double P_CA[4] = {0.4, 0.6, 0.8, 1.0};
   const double P_ca = P_CA[jp];
@@ -177,7 +200,9 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     double d0 = ox - sx, d1 = oy - sy;
     double dist = sqrt(d0 * d0 + d1 * d1);
     double R = 0, C = 0;
-    if (dist < d_close) {
+    // R and C stay 0 unless dist < d_safe_i <= max_d_safe, so the sector geometry (atan2, wrap,
+    // norms) is only evaluated there; identical results to the reference's `dist < d_close` block.
+    if (dist < d_close && dist < max_d_safe) {
       double ss = (i == 0) ? sp0 : sp, cs = (i == 0) ? cp0 : cp;
       double vs0 = -ss * ud + cs * sv;
       double vs1 = cs * ud + ss * sv;
@@ -276,23 +301,24 @@ __global__ void init_kernel(const Params P, DevState S, ConstBuf K) {
   s.spd_a = 0; s.spd_b = (P.machinery == SHIPSIM_MACH_DETAILED) ? c.init_shaft_ei : 0.0;
   s.log_rudder = 0; s.log_thrust = 0; s.log_ect = 0; s.log_n = s.n; s.log_e = s.e;
   s.next_wpt = 1; s.stop = 0; s.n_route = c.n_route;
-  double* rn = S.route_n + (size_t)q * kMaxRoute;
-  double* re = S.route_e + (size_t)q * kMaxRoute;
+  double* rn = S.route_n() + (size_t)q * kMaxRoute;
+  double* re = S.route_e() + (size_t)q * kMaxRoute;
   for (int i = 0; i < kMaxRoute; ++i) {
-    rn[i] = K.cfg_route_n[ship * kMaxRoute + i];
-    re[i] = K.cfg_route_e[ship * kMaxRoute + i];
+    rn[i] = K.cfg_route_n()[ship * kMaxRoute + i];
+    re[i] = K.cfg_route_e()[ship * kMaxRoute + i];
   }
   store_ship(S, q, s);
   if (ship == 0) {
-    S.sampling_count[env] = 0;
-    S.travel_dist[env] = 0; S.travel_time[env] = 0; S.acc[env] = 0;
-    S.n_base[env] = P.n_base0; S.e_base[env] = P.e_base0;
-    S.p_last[env] = 1.0; S.chi_last[env] = 0.0;  // SBMPCParams defaults (sbmpc.py:28-29)
-    S.mach_dt[env] = P.mach_dt_init;
-    for (int i = 0; i < 4; ++i) S.states4[env * 4 + i] = P.initial_states[i < 2 ? i : i + 1];
-    for (int i = 0; i < 8; ++i) S.next_obs8[env * 8 + i] = P.initial_states[i];
-    S.snap_bits[env] = 0;
-    S.was_reset[env] = 0;
+    S.sampling_count()[env] = 0;
+    S.travel_dist()[env] = 0; S.travel_time()[env] = 0; S.acc()[env] = 0;
+    S.n_base()[env] = P.n_base0; S.e_base()[env] = P.e_base0;
+    S.p_last()[env] = 1.0; S.chi_last()[env] = 0.0;  // SBMPCParams defaults (sbmpc.py:28-29)
+    S.mach_dt()[env] = P.mach_dt_init;
+    for (int i = 0; i < 4; ++i) S.states4()[env * 4 + i] = P.initial_states[i < 2 ? i : i + 1];
+    for (int i = 0; i < 8; ++i) S.next_obs8()[env * 8 + i] = P.initial_states[i];
+    S.snap_bits()[env] = 0;
+    S.was_reset()[env] = 0;
+    S.dec_flags()[env] = DF_AWAITING;
   }
 }
 
@@ -315,11 +341,11 @@ __global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, 
   s.e_ct = 0; s.e_ct_int = 0; s.hdg_ei = 0; s.hdg_prev = 0;
   s.spd_a = 0; s.spd_b = DETAILED ? c.init_shaft_ei : 0.0;
   s.next_wpt = 1; s.stop = 0; s.n_route = c.n_route;
-  double* rn = S.route_n + (size_t)q * kMaxRoute;
-  double* re = S.route_e + (size_t)q * kMaxRoute;
+  double* rn = S.route_n() + (size_t)q * kMaxRoute;
+  double* re = S.route_e() + (size_t)q * kMaxRoute;
   for (int i = 0; i < c.n_route; ++i) {
-    rn[i] = K.cfg_route_n[ship * kMaxRoute + i];
-    re[i] = K.cfg_route_e[ship * kMaxRoute + i];
+    rn[i] = K.cfg_route_n()[ship * kMaxRoute + i];
+    re[i] = K.cfg_route_e()[ship * kMaxRoute + i];
   }
   load_segment(s, rn, re);
   const double mach_dt = P.mach_dt_reset;
@@ -327,66 +353,140 @@ __global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, 
   control_and_integrate<DETAILED>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false);
   store_ship(S, q, s);
   if (ship == 0) {
-    S.sampling_count[env] = 0;
-    S.travel_dist[env] = 0; S.travel_time[env] = 0; S.acc[env] = 0;
-    S.n_base[env] = P.n_base0; S.e_base[env] = P.e_base0;
-    S.mach_dt[env] = mach_dt;
-    for (int i = 0; i < 8; ++i) S.next_obs8[env * 8 + i] = P.initial_states[i];
-    S.snap_bits[env] = 0;
-    S.was_reset[env] = 1;
+    S.sampling_count()[env] = 0;
+    S.travel_dist()[env] = 0; S.travel_time()[env] = 0; S.acc()[env] = 0;
+    S.n_base()[env] = P.n_base0; S.e_base()[env] = P.e_base0;
+    S.mach_dt()[env] = mach_dt;
+    for (int i = 0; i < 8; ++i) S.next_obs8()[env * 8 + i] = P.initial_states[i];
+    S.snap_bits()[env] = 0;
+    S.was_reset()[env] = 1;
+    S.dec_flags()[env] = DF_AWAITING;
     if (obs_out)
       for (int i = 0; i < 8; ++i) obs_out[env * 8 + i] = P.initial_states[i];
   }
 }
 
-// MultiShipRLEnv.step (env.py:624-773) for lane pairs (2e: test ship, 2e+1: obstacle ship)
-template <bool DETAILED, int COLLAV>
+// Map edge table with the per-edge constants of GEOS pointToSegment, staged in LDS.
+struct EdgeX {
+  double ax, ay, bx, by, dx, dy, len2, inv_len2;
+};
+
+// min over this lane's share of the edges (i = sub, sub + nsub, ...) of the squared point-segment
+// distance. Equivalent to GEOS Distance::pointToSegment up to rounding (sqrt taken once at the end).
+__device__ __forceinline__ double map_dist2_part(const EdgeX* __restrict__ E, int n_edges, double n, double e,
+                                                 int sub, int nsub) {
+  const double px = e, py = n;
+  double best = INFINITY;
+  for (int i = sub; i < n_edges; i += nsub) {
+    const EdgeX ed = E[i];
+    const double qx = px - ed.ax, qy = py - ed.ay;
+    const double t = qx * ed.dx + qy * ed.dy;
+    const double da = qx * qx + qy * qy;
+    const double rx = px - ed.bx, ry = py - ed.by;
+    const double db = rx * rx + ry * ry;
+    const double c = (ed.ay - py) * ed.dx - (ed.ax - px) * ed.dy;
+    const double dp = c * c * ed.inv_len2;
+    const double d2 = (t <= 0.0) ? da : ((t >= ed.len2) ? db : dp);
+    best = py_min(best, d2);
+  }
+  return best;
+}
+
+__device__ __forceinline__ bool corner_inside(const Edge* __restrict__ edges, const PolyBox* __restrict__ boxes,
+                                              int n_polys, double n, double e) {
+  return map_inside(edges, boxes, n_polys, n, e);
+}
+
+__device__ __forceinline__ double xor_shfl_d(double x, int mask) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  lo = __shfl_xor(lo, mask, 64);
+  hi = __shfl_xor(hi, mask, 64);
+  return __hiloint2double(hi, lo);
+}
+
+
+// MultiShipRLEnv.step (env.py:624-773), sliced: every env of the launch ticks (_step :563-622)
+// until its decision point (RoA + one tick, or done) or until `max_ticks` ticks have run in this
+// call; an env that paused resumes in the next call without consuming an action. Envs waiting
+// for a decision consume action[env] first (IW sampling). LPE lanes per env: lane & 1 selects the
+// ship, the LPE/2 sub-lanes of a ship hold identical state, run the control chain redundantly and
+// split the map queries (edges for the coastline distance, hull corners for grounding).
+template <bool DETAILED, int COLLAV, int LPE>
 __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K,
                                                       const float* __restrict__ action,
                                                       const uint8_t* __restrict__ active_mask, int max_ticks,
                                                       float* obs_out, double* reward_out, uint8_t* done_out,
-                                                      uint32_t* events_out, int32_t* ticks_out) {
+                                                      uint32_t* events_out, int32_t* ticks_out, uint8_t* ready_out) {
+  constexpr int NSUB = LPE / 2;
+  static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 64, "LPE must be a power of two in [2, 64]");
   __shared__ ShipConst lds_sc[2];
+  __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
+  __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
+  __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
   const ShipConst* SC = stage_consts(P, lds_sc);
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  const int env = q >> 1;
-  const int ship = q & 1;
+  for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) {
+    const Edge ed = K.edges()[i];
+    EdgeX x;
+    x.ax = ed.ax; x.ay = ed.ay; x.bx = ed.bx; x.by = ed.by;
+    x.dx = ed.bx - ed.ax; x.dy = ed.by - ed.ay;
+    x.len2 = x.dx * x.dx + x.dy * x.dy;
+    x.inv_len2 = x.len2 > 0 ? 1.0 / x.len2 : 0.0;
+    lds_edges[i] = x;
+    lds_edges_raw[i] = ed;
+  }
+  for (int i = threadIdx.x; i < P.n_polys; i += blockDim.x) lds_boxes[i] = K.boxes()[i];
+  __syncthreads();
+
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int env = gl / LPE;
+  const int lie = gl % LPE;
+  const int ship = lie & 1;
+  const int sub = lie >> 1;
   const bool is_test = ship == 0;
+  const int lane = threadIdx.x & 63;
+  const int env_lane0 = lane - lie;
   const bool valid = env < P.n_envs;
   const int envc = valid ? env : 0;
-  const int qc = valid ? q : 0;
+  const int qc = envc * 2 + ship;
   const ShipConst& c = SC[ship];
-  const double* rn = S.route_n + (size_t)qc * kMaxRoute;
-  const double* re = S.route_e + (size_t)qc * kMaxRoute;
-  double* rn_w = S.route_n + (size_t)qc * kMaxRoute;
-  double* re_w = S.route_e + (size_t)qc * kMaxRoute;
+  double* rn = S.route_n() + (size_t)qc * kMaxRoute;
+  double* re = S.route_e() + (size_t)qc * kMaxRoute;
 
-  bool running = valid && (active_mask == nullptr || active_mask[envc]) && S.was_reset[envc];
+  bool running = valid && (active_mask == nullptr || active_mask[envc]) && S.was_reset()[envc];
   const bool touched = running;
 
   Ship s;
   load_ship(S, qc, s);
-  int sampling_count = S.sampling_count[envc];
-  double travel_dist = S.travel_dist[envc], travel_time = S.travel_time[envc], acc = S.acc[envc];
-  double n_base = S.n_base[envc], e_base = S.e_base[envc];
-  double p_last = S.p_last[envc], chi_last = S.chi_last[envc];
-  const double mach_dt = S.mach_dt[envc];
+  int sampling_count = S.sampling_count()[envc];
+  double travel_dist = S.travel_dist()[envc], travel_time = S.travel_time()[envc], acc = S.acc()[envc];
+  double n_base = S.n_base()[envc], e_base = S.e_base()[envc];
+  double p_last = S.p_last()[envc], chi_last = S.chi_last()[envc];
+  const double mach_dt = S.mach_dt()[envc];
   float st4[4];
-  for (int i = 0; i < 4; ++i) st4[i] = S.states4[envc * 4 + i];
-  uint32_t snap_bits = S.snap_bits[envc];
+  for (int i = 0; i < 4; ++i) st4[i] = S.states4()[envc * 4 + i];
+  uint32_t snap_bits = S.snap_bits()[envc];
+  int dflags = S.dec_flags()[envc];
+  bool have_iw = dflags & DF_HAVE_IW;
+  int phase = (dflags >> DF_PHASE_SHIFT) & 3;
 
-  float ns[8];  // next_states of the last tick
-  for (int i = 0; i < 8; ++i) ns[i] = S.next_obs8[envc * 8 + i];
+  float ns[8];
+  for (int i = 0; i < 8; ++i) ns[i] = S.next_obs8()[envc * 8 + i];
   double out_r = 0.0;
-  bool out_done = false;
+  bool out_done = false, ready = false;
   uint32_t out_bits = 0;
-  int ticks = 0, phase = 0;
-  bool have_iw = false;
+  int ticks = 0;
 
-  if (running) {
+#ifdef SHIPSIM_DEBUG_ENV
+  if (env == SHIPSIM_DEBUG_ENV && valid)
+    printf("[dbg] env %d lie %d start: running %d dflags %d sc %d n_base %f phase %d\n", env, lie, (int)running, dflags,
+           sampling_count, n_base, phase);
+#endif
+  if (running && (dflags & DF_AWAITING)) {
     // ---- intermediate waypoint sampling (env.py:659-696) ----
     float sa = action[envc];
     if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
+    phase = 0;
+    have_iw = false;
     if (sampling_count < P.max_sampling) {
       sampling_count += 1;
       float tn = (float)tan((double)sa);  // np.tan on the float32 scoping angle
@@ -398,17 +498,17 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       double iw_n = n_base + n_s, iw_e = e_base + e_s;
       n_base = iw_n + P.AB_seg_n;
       e_base = iw_e + P.AB_seg_e;
-      if (!is_test) {  // auto_pilot.update_route: list.insert(-1, IW)
+      if (!is_test) {  // auto_pilot.update_route: list.insert(-1, IW); every sub-lane writes the same bytes
         int L = s.n_route;
-        rn_w[L] = rn_w[L - 1]; re_w[L] = re_w[L - 1];
-        rn_w[L - 1] = iw_n; re_w[L - 1] = iw_e;
+        rn[L] = s.end_n; re[L] = s.end_e;
+        rn[L - 1] = iw_n; re[L - 1] = iw_e;
+        if (s.next_wpt == L - 1) { s.wp_n = iw_n; s.wp_e = iw_e; }
         s.n_route = L + 1;
-        load_segment(s, rn, re);
       }
       travel_dist = 0;
       travel_time = 0;
       have_iw = true;
-      bool fail = map_inside(K.edges, K.boxes, P.n_polys, iw_n, iw_e) ||
+      bool fail = map_inside(lds_edges_raw, lds_boxes, P.n_polys, iw_n, iw_e) ||
                   ((iw_n < P.min_north || iw_n > P.max_north) || (iw_e < P.min_east || iw_e > P.max_east));
       if (fail) {  // env.py:673-693 with obs_ship_IW_sampling_failure_reward (multiplier 2)
         out_r = (acc >= 0) ? -acc * 2.0 : acc * 2.0;
@@ -416,7 +516,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
                     ~(uint32_t)(SHIPSIM_EV_TEST_STOP | SHIPSIM_EV_OBS_STOP);
         out_bits = snap_bits;
         out_done = true;
-        running = false;
+        ready = true;
       } else {
         acc = 0;
       }
@@ -424,15 +524,16 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   }
 
   const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
-  while (__any(running)) {
-    // partner's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
+  bool going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
+  while (__any(going)) {
+    // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
     double sf = 1.0, off = 0.0;
     if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
       bool need = false;
-      SbIn in;
-      if (running && is_test) {
+      SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      if (going && is_test) {
         // env.py:362-363: next_wpt result discarded; los_guidance integrates e_ct_int (Q3)
         double chi_d = los_guidance(c, s, s.n, s.e);
         in.u_d = c.desired_speed; in.chi_d = -chi_d;
@@ -442,25 +543,26 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         in.p_last = p_last; in.chi_last = chi_last;
         double d0 = pe - s.e, d1 = pn - s.n;
         need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
-        if (!need) { p_last = 1; chi_last = 0; }
-      } else {
-        in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       }
       double pb = 1.0, cb = 0.0;
-      sbmpc_cooperative(need, in, n_samp, P.sbmpc_dt, pb, cb);
-      if (need) { p_last = pb; chi_last = cb; sf = pb; off = cb; }
-      const double p_other = pair_swap(p_last), c_other = pair_swap(chi_last);
-      if (!is_test) { p_last = p_other; chi_last = c_other; }
+      sbmpc_cooperative(need && sub == 0, in, n_samp, P.sbmpc_dt, pb, cb);
+      pb = shfl_d(pb, env_lane0);
+      cb = shfl_d(cb, env_lane0);
+      const int need0 = __shfl((int)need, env_lane0, 64);
+      if (going) {
+        if (need0) { p_last = pb; chi_last = cb; }
+        else { p_last = 1; chi_last = 0; }
+        if (is_test && need0) { sf = pb; off = cb; }
+      }
     }
 
     // ---- ship ticks (test_step :345-445 / obs_step :447-536) ----
     double my_speed_out = 0.0, dtravel = 0.0, dtime = 0.0;
-    if (running) {
+    if (going) {
       if (!is_test && s.stop) {
         // frozen obstacle ship: store_last_simulation_data + two next_time (Q9)
         s.time = s.time + P.dt;
         s.time = s.time + P.dt;
-        my_speed_out = 0.0;
       } else {
         const double prev_log_n = s.log_n, prev_log_e = s.log_e;
         const double U = s.u;
@@ -479,27 +581,45 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         }
       }
     }
-    // ---- own-ship part of get_reward_and_env_info (reward_function.py:80-168) ----
-    double my_ground = 0.0;
-    bool my_grounding = false, my_end = false, my_outside = false, my_roa = false;
-    if (running) {
-      my_ground = map_distance(K.edges, K.n_edges, s.n, s.e);
-      my_grounding = pos_inside_obstacles(K.edges, K.boxes, P.n_polys, s.n, s.e, c.l_ship);
+    // ---- own-ship map queries, split over the ship's sub-lanes ----
+    double d2 = INFINITY;
+    bool gr = false;
+    if (going) {
+#ifndef SHIPSIM_ABL_NO_MAPDIST
+      d2 = map_dist2_part(lds_edges, K.n_edges, s.n, s.e, sub, NSUB);
+#endif
+      const double margin = c.l_ship / 2;  // check_condition.py:50-78 hull hard points
+#ifndef SHIPSIM_ABL_NO_GROUND
+      for (int k = sub; k < 4; k += NSUB) {
+        const double cn = (k < 2) ? s.n - margin : s.n + margin;
+        const double ce = (k & 1) ? s.e + margin : s.e - margin;
+        if (corner_inside(lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) gr = true;
+      }
+#endif
+    }
+    int gri = gr ? 1 : 0;
+#pragma unroll
+    for (int m = 2; m < LPE; m <<= 1) {
+      d2 = py_min(d2, xor_shfl_d(d2, m));
+      gri |= __shfl_xor(gri, m, 64);
+    }
+    const double my_ground = sqrt(d2);
+    bool my_end = false, my_outside = false, my_roa = false;
+    if (going) {
       my_end = sqrt((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e)) <= 200;
       double margin = c.l_ship / 2;
       my_outside = (s.n < P.min_north + margin || s.n > P.max_north - margin) ||
                    (s.e < P.min_east + margin || s.e > P.max_east - margin);
-      double rdn = s.n - s.wp_n, rde = s.e - s.wp_e;  // is_reach_radius_of_acceptance (obstacle lane)
+      double rdn = s.n - s.wp_n, rde = s.e - s.wp_e;  // is_reach_radius_of_acceptance (obstacle ship)
       my_roa = (rdn * rdn + rde * rde) < P.roa2;
     }
-    const int my_flags = (my_grounding ? 1 : 0) | (my_end ? 2 : 0) | (my_outside ? 4 : 0) | (my_roa ? 8 : 0);
+    const int my_flags = gri | (my_end ? 2 : 0) | (my_outside ? 4 : 0) | (my_roa ? 8 : 0);
     const int o_flags = pair_swap_i(my_flags);
     const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
     const double o_ect = pair_swap(s.log_ect), o_ground = pair_swap(my_ground);
     const double o_speed = pair_swap(my_speed_out), o_dtravel = pair_swap(dtravel), o_dtime = pair_swap(dtime);
     const double o_time = pair_swap(s.time);
-    if (running) {
-      // arrange as (test, obstacle)
+    if (going) {
       const double Tn = is_test ? s.n : o_n, Te = is_test ? s.e : o_e, Th = is_test ? s.yaw : o_yaw;
       const double On = is_test ? o_n : s.n, Oe = is_test ? o_e : s.e, Oyaw = is_test ? o_yaw : s.yaw;
       const double Tect = is_test ? s.log_ect : o_ect, Oect = is_test ? o_ect : s.log_ect;
@@ -513,11 +633,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       ns[0] = (float)Tn; ns[1] = (float)Te; ns[2] = (float)Tect;
       ns[3] = (float)On; ns[4] = (float)Oe; ns[5] = (float)Oyaw; ns[6] = (float)Ospeed; ns[7] = (float)Oect;
       st4[0] = ns[0]; st4[1] = ns[1]; st4[2] = ns[3]; st4[3] = ns[4];
-      // encounter (compute_distance.py:16-40) and collision (check_condition.py:142-159)
+      // get_reward_and_env_info (reward_function.py:59-270)
       double dx = On - Tn, dy = Oe - Te;
       double dist = sqrt(dx * dx + dy * dy);
       double beta = floor_mod((atan2(dy, dx) - Th) + kPi, 2 * kPi) - kPi;
-      const bool enc_ok = !(fabs(beta) > 165.0 * (kPi / 180.0));  // head-on or crossing
+      const bool enc_ok = !(fabs(beta) > 165.0 * (kPi / 180.0));  // head-on or crossing (Q5)
       const bool is_collision = ((Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe)) < 2500.0;
       const bool is_tg = Tf & 1, is_og = Of & 1;
       const bool is_tnav = fabs(Tect) > 3000;
@@ -528,8 +648,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       double r3 = (Oground <= 1000) ? -rd4(0, 50000, Oground) : 0.0;
       double r4 = -rd3(500, 12500, fabs(Oect));
       double r = (r0 + ((((0.0 + r1) + r2) + r3) + r4)) / 5;  // np.sum(5 terms) / 5
-      // get_reward_due_to_ships_termination (reward_function.py:272-314)
-      if (is_collision || is_tg || is_tnav || is_og || is_onav) {
+      if (is_collision || is_tg || is_tnav || is_og || is_onav) {  // :272-314
         const double reward = r + acc;
         double o = 0;
         const bool cond[5] = {is_collision, is_tg, is_tnav, is_og, is_onav};
@@ -561,9 +680,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       bool finish = false;
       if (phase == 0) {
         const bool roa = Of & 8;
-        if (combined_done) {
-          finish = true;
-        } else if (roa) {
+        if (combined_done) finish = true;
+        else if (roa) {
           if (have_iw) phase = 1;
           else finish = true;
         }
@@ -579,33 +697,43 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       } else {
         if (combined_done) finish = true;
       }
-      if (!finish && max_ticks > 0 && ticks >= max_ticks) finish = true;
       if (finish) {
         out_r = acc;
         out_done = combined_done;
         out_bits = bits;
         snap_bits = bits;
-        running = false;
+        ready = true;
       }
+      going = !ready && (max_ticks <= 0 || ticks < max_ticks);
     }
   }
 
   if (!valid || !touched) return;
-  store_ship(S, q, s);
-  if (is_test) {
-    S.sampling_count[env] = sampling_count;
-    S.travel_dist[env] = travel_dist; S.travel_time[env] = travel_time; S.acc[env] = acc;
-    S.n_base[env] = n_base; S.e_base[env] = e_base;
-    S.p_last[env] = p_last; S.chi_last[env] = chi_last;
-    for (int i = 0; i < 4; ++i) S.states4[env * 4 + i] = st4[i];
-    for (int i = 0; i < 8; ++i) S.next_obs8[env * 8 + i] = ns[i];
-    S.snap_bits[env] = snap_bits;
-    if (reward_out) reward_out[env] = out_r;
-    if (done_out) done_out[env] = out_done ? 1 : 0;
-    if (events_out) events_out[env] = out_bits;
+#ifdef SHIPSIM_DEBUG_ENV
+  if (env == SHIPSIM_DEBUG_ENV)
+    printf("[dbg] env %d lie %d end: ready %d ticks %d sc %d n_base %f phase %d have_iw %d\n", env, lie, (int)ready,
+           ticks, sampling_count, n_base, phase, (int)have_iw);
+#endif
+  if (sub == 0) store_ship(S, qc, s);
+  if (lie == 0) {
+    S.sampling_count()[env] = sampling_count;
+    S.travel_dist()[env] = travel_dist; S.travel_time()[env] = travel_time; S.acc()[env] = acc;
+    S.n_base()[env] = n_base; S.e_base()[env] = e_base;
+    S.p_last()[env] = p_last; S.chi_last()[env] = chi_last;
+    for (int i = 0; i < 4; ++i) S.states4()[env * 4 + i] = st4[i];
+    if (ready)
+      for (int i = 0; i < 8; ++i) S.next_obs8()[env * 8 + i] = ns[i];
+    S.snap_bits()[env] = snap_bits;
+    S.dec_flags()[env] = (ready ? DF_AWAITING : 0) | (have_iw ? DF_HAVE_IW : 0) | (phase << DF_PHASE_SHIFT);
+    if (ready) {
+      if (reward_out) reward_out[env] = out_r;
+      if (done_out) done_out[env] = out_done ? 1 : 0;
+      if (events_out) events_out[env] = out_bits;
+    }
     if (ticks_out) ticks_out[env] = ticks;
+    if (ready_out) ready_out[env] = ready ? 1 : 0;
   }
-  if (obs_out) {  // test lane writes obs[0..3], obstacle lane obs[4..7]
+  if (ready && obs_out && sub == 0) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
     for (int i = 0; i < 4; ++i) obs_out[env * 8 + ship * 4 + i] = ns[ship * 4 + i];
   }
 }
@@ -618,11 +746,11 @@ __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevStat
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P.n_envs) return;
   const ShipConst& c = SC[0];
-  const double* rn = S.route_n + (size_t)q * kMaxRoute;
-  const double* re = S.route_e + (size_t)q * kMaxRoute;
+  const double* rn = S.route_n() + (size_t)q * kMaxRoute;
+  const double* re = S.route_e() + (size_t)q * kMaxRoute;
   Ship s;
   load_ship(S, q, s);
-  const double mach_dt = S.mach_dt[q];
+  const double mach_dt = S.mach_dt()[q];
   for (int i = 0; i < k; ++i) control_and_integrate<DETAILED>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false);
   store_ship(S, q, s);
 }
@@ -671,6 +799,34 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+static int lanes_per_env(const shipsim_config* cfg) {
+  int lpe = cfg->lanes_per_env;
+  if (lpe <= 0) {
+    const char* e = getenv("SHIPSIM_LPE");
+    lpe = e ? atoi(e) : 16;
+  }
+  if (lpe != 2 && lpe != 4 && lpe != 8 && lpe != 16) lpe = 16;
+  return lpe;
+}
+
+template <bool D, int CA>
+static void launch_step(shipsim_handle* h, int lpe, const float* action, const uint8_t* active, int32_t max_ticks,
+                        float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
+                        int32_t* ticks_out, uint8_t* ready_out) {
+  const int threads = 64;
+  const int lanes = h->P.n_envs * lpe, blocks = (lanes + threads - 1) / threads;
+#define L(LPE)                                                                                                   \
+  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, \
+                     action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, ready_out)
+  switch (lpe) {
+    case 2: L(2); break;
+    case 4: L(4); break;
+    case 8: L(8); break;
+    default: L(16); break;
+  }
+#undef L
+}
 
 extern "C" {
 
@@ -1002,14 +1158,12 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
   }
   P.min_east = mn_e; P.max_east = mx_e; P.min_north = mn_n; P.max_north = mx_n;
 
-  // constant block: edges, boxes, config routes
-  size_t c_edges = sizeof(Edge) * nv, c_boxes = sizeof(PolyBox) * SHIPSIM_MAX_POLYS;
-  size_t c_routes = sizeof(double) * 2 * kMaxRoute * 2;
-  size_t cbytes = c_edges + c_boxes + c_routes;
+  // constant block: edges | boxes | config routes (ConstBuf layout)
+  size_t cbytes = ConstBuf::kBytes;
   char* hostc = (char*)calloc(1, cbytes);
   Edge* E = (Edge*)hostc;
-  PolyBox* B = (PolyBox*)(hostc + c_edges);
-  double* R = (double*)(hostc + c_edges + c_boxes);
+  PolyBox* B = (PolyBox*)(hostc + sizeof(Edge) * SHIPSIM_MAX_VERTS);
+  double* R = (double*)(hostc + sizeof(Edge) * SHIPSIM_MAX_VERTS + sizeof(PolyBox) * SHIPSIM_MAX_POLYS);
   for (int p = 0; p < cfg->n_polys; ++p) {
     int s0 = cfg->poly_start[p], cnt = cfg->poly_start[p + 1] - s0;
     B[p].first = s0;
@@ -1046,49 +1200,24 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
     *out = h;
     return fail(h, SHIPSIM_EHIP, "hipMemcpy(const): %s", hipGetErrorString(e));
   }
-  h->K.edges = (const Edge*)h->const_block;
-  h->K.boxes = (const PolyBox*)((char*)h->const_block + c_edges);
-  h->K.cfg_route_n = (const double*)((char*)h->const_block + c_edges + c_boxes);
-  h->K.cfg_route_e = h->K.cfg_route_n + 2 * kMaxRoute;
+  h->K.base = (const char*)h->const_block;
   h->K.n_edges = nv;
 
-  // state block
+  // state block (DevState layout: ship arrays | routes | env arrays)
   const size_t S = (size_t)n_envs * ns, N = (size_t)n_envs;
-  size_t bytes = 0;
-  auto take = [&](size_t b) { size_t o = bytes; bytes += (b + 255) & ~(size_t)255; return o; };
-  size_t off_f[SHIPSIM_N_SHIP_FIELDS];
-  for (int i = 0; i < SHIPSIM_N_SHIP_FIELDS; ++i) off_f[i] = take(S * sizeof(double));
-  size_t o_wpt = take(S * 4), o_stop = take(S * 4), o_nr = take(S * 4);
-  size_t o_rn = take(S * kMaxRoute * 8), o_re = take(S * kMaxRoute * 8);
-  size_t o_sc = take(N * 4), o_td = take(N * 8), o_tt = take(N * 8), o_acc = take(N * 8), o_nb = take(N * 8),
-         o_eb = take(N * 8), o_pl = take(N * 8), o_cl = take(N * 8), o_md = take(N * 8), o_s4 = take(N * 16),
-         o_no = take(N * 32), o_sb = take(N * 4), o_wr = take(N * 4);
+  auto r256 = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  h->S.ship_stride = (int64_t)r256(S * sizeof(double));
+  h->S.route_stride = (int64_t)r256(S * kMaxRoute * sizeof(double));
+  h->S.env_stride = (int64_t)r256(N * 8 * sizeof(float));
+  h->S.env_off = DevState::kShipArrays * h->S.ship_stride + 2 * h->S.route_stride;
+  size_t bytes = (size_t)(h->S.env_off + DevState::kEnvArrays * h->S.env_stride);
   e = hipMalloc(&h->dev_block, bytes);
   if (e != hipSuccess) {
     *out = h;
     return fail(h, SHIPSIM_EHIP, "hipMalloc(state %zu B): %s", bytes, hipGetErrorString(e));
   }
   h->dev_bytes = bytes;
-  char* d = (char*)h->dev_block;
-  for (int i = 0; i < SHIPSIM_N_SHIP_FIELDS; ++i) h->S.f[i] = (double*)(d + off_f[i]);
-  h->S.next_wpt = (int32_t*)(d + o_wpt);
-  h->S.stop = (int32_t*)(d + o_stop);
-  h->S.n_route = (int32_t*)(d + o_nr);
-  h->S.route_n = (double*)(d + o_rn);
-  h->S.route_e = (double*)(d + o_re);
-  h->S.sampling_count = (int32_t*)(d + o_sc);
-  h->S.travel_dist = (double*)(d + o_td);
-  h->S.travel_time = (double*)(d + o_tt);
-  h->S.acc = (double*)(d + o_acc);
-  h->S.n_base = (double*)(d + o_nb);
-  h->S.e_base = (double*)(d + o_eb);
-  h->S.p_last = (double*)(d + o_pl);
-  h->S.chi_last = (double*)(d + o_cl);
-  h->S.mach_dt = (double*)(d + o_md);
-  h->S.states4 = (float*)(d + o_s4);
-  h->S.next_obs8 = (float*)(d + o_no);
-  h->S.snap_bits = (uint32_t*)(d + o_sb);
-  h->S.was_reset = (int32_t*)(d + o_wr);
+  h->S.base = (char*)h->dev_block;
   e = hipMemsetAsync(h->dev_block, 0, bytes, h->stream);
   if (e != hipSuccess) {
     *out = h;
@@ -1134,18 +1263,16 @@ int shipsim_reset(shipsim_handle* h, const uint8_t* env_mask, float* obs_out) {
 }
 
 int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks, float* obs_out,
-                 double* reward_out, uint8_t* done_out, uint32_t* events_out, int32_t* ticks_out) {
+                 double* reward_out, uint8_t* done_out, uint32_t* events_out, int32_t* ticks_out,
+                 uint8_t* ready_out) {
   if (!h || !h->dev_block) return SHIPSIM_EINVAL;
   if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "step: only SHIPSIM_KIND_AST has decision steps");
   if (!action) return fail(h, SHIPSIM_EINVAL, "step: action is NULL");
   if (!h->ever_reset) return fail(h, SHIPSIM_ESTATE, "step before reset");
   DeviceGuard g(h->device);
-  if (max_ticks <= 0) max_ticks = (int)(2.0 * h->P.sim_time / h->P.dt) + 16;
-  const int lanes = h->P.n_envs * 2, threads = 64, blocks = (lanes + threads - 1) / threads;
+  const int lpe = lanes_per_env(&h->cfg);
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
-#define LAUNCH(D, CA)                                                                                              \
-  hipLaunchKernelGGL((ast_step_kernel<D, CA>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, action, \
-                     active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out)
+#define LAUNCH(D, CA) launch_step<D, CA>(h, lpe, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, ready_out)
   switch (h->P.collav) {
     case SHIPSIM_COLLAV_NONE: if (det) LAUNCH(true, 0); else LAUNCH(false, 0); break;
     case SHIPSIM_COLLAV_SIMPLE: if (det) LAUNCH(true, 1); else LAUNCH(false, 1); break;
@@ -1175,23 +1302,23 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
 static int field_ptr(shipsim_handle* h, int32_t field, void** p, size_t* bytes) {
   const size_t S = (size_t)h->P.n_envs * h->P.n_ships, N = (size_t)h->P.n_envs;
   if (field >= 0 && field < SHIPSIM_N_SHIP_FIELDS) {
-    if (field == SHIPSIM_F_NEXT_WPT) { *p = h->S.next_wpt; *bytes = S * 4; return 0; }
-    if (field == SHIPSIM_F_STOP) { *p = h->S.stop; *bytes = S * 4; return 0; }
-    *p = h->S.f[field]; *bytes = S * 8;
+    if (field == SHIPSIM_F_NEXT_WPT) { *p = h->S.next_wpt(); *bytes = S * 4; return 0; }
+    if (field == SHIPSIM_F_STOP) { *p = h->S.stop(); *bytes = S * 4; return 0; }
+    *p = h->S.f(field); *bytes = S * 8;
     return 0;
   }
   switch (field) {
-    case SHIPSIM_E_SAMPLING_COUNT: *p = h->S.sampling_count; *bytes = N * 4; return 0;
-    case SHIPSIM_E_TRAVEL_DIST: *p = h->S.travel_dist; *bytes = N * 8; return 0;
-    case SHIPSIM_E_TRAVEL_TIME: *p = h->S.travel_time; *bytes = N * 8; return 0;
-    case SHIPSIM_E_ACC_REWARD: *p = h->S.acc; *bytes = N * 8; return 0;
-    case SHIPSIM_E_N_BASE: *p = h->S.n_base; *bytes = N * 8; return 0;
-    case SHIPSIM_E_E_BASE: *p = h->S.e_base; *bytes = N * 8; return 0;
-    case SHIPSIM_E_SBMPC_P_LAST: *p = h->S.p_last; *bytes = N * 8; return 0;
-    case SHIPSIM_E_SBMPC_CHI_LAST: *p = h->S.chi_last; *bytes = N * 8; return 0;
-    case SHIPSIM_E_ROUTE_LEN: *p = h->S.n_route; *bytes = S * 4; return 0;
-    case SHIPSIM_E_ROUTE_NORTH: *p = h->S.route_n; *bytes = S * kMaxRoute * 8; return 0;
-    case SHIPSIM_E_ROUTE_EAST: *p = h->S.route_e; *bytes = S * kMaxRoute * 8; return 0;
+    case SHIPSIM_E_SAMPLING_COUNT: *p = h->S.sampling_count(); *bytes = N * 4; return 0;
+    case SHIPSIM_E_TRAVEL_DIST: *p = h->S.travel_dist(); *bytes = N * 8; return 0;
+    case SHIPSIM_E_TRAVEL_TIME: *p = h->S.travel_time(); *bytes = N * 8; return 0;
+    case SHIPSIM_E_ACC_REWARD: *p = h->S.acc(); *bytes = N * 8; return 0;
+    case SHIPSIM_E_N_BASE: *p = h->S.n_base(); *bytes = N * 8; return 0;
+    case SHIPSIM_E_E_BASE: *p = h->S.e_base(); *bytes = N * 8; return 0;
+    case SHIPSIM_E_SBMPC_P_LAST: *p = h->S.p_last(); *bytes = N * 8; return 0;
+    case SHIPSIM_E_SBMPC_CHI_LAST: *p = h->S.chi_last(); *bytes = N * 8; return 0;
+    case SHIPSIM_E_ROUTE_LEN: *p = h->S.n_route(); *bytes = S * 4; return 0;
+    case SHIPSIM_E_ROUTE_NORTH: *p = h->S.route_n(); *bytes = S * kMaxRoute * 8; return 0;
+    case SHIPSIM_E_ROUTE_EAST: *p = h->S.route_e(); *bytes = S * kMaxRoute * 8; return 0;
   }
   return 1;
 }

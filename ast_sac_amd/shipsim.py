@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads torch's HIP runtime first; libshipsim binds t
 from . import shipsim_abi as abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libshipsim.so")
+LIB_PATH = os.environ.get("SHIPSIM_LIB") or os.path.join(_HERE, "lib", "libshipsim.so")
 
 _lib = None
 
@@ -40,7 +40,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_num_envs.argtypes = [P]
     L.shipsim_num_envs.restype = C.c_int32
     L.shipsim_reset.argtypes = [P, P, P]
-    L.shipsim_step.argtypes = [P, P, P, C.c_int32, P, P, P, P, P]
+    L.shipsim_step.argtypes = [P, P, P, C.c_int32, P, P, P, P, P, P]
     L.shipsim_tick.argtypes = [P, C.c_int32, P]
     L.shipsim_get_state.argtypes = [P, C.c_int32, P]
     L.shipsim_set_state.argtypes = [P, C.c_int32, P]
@@ -119,7 +119,9 @@ class ShipSim:
         return obs
 
     def step(self, action, active=None, max_ticks=0, out=None):
-        """action: (N,) or (N,1) float32 scoping angles [rad] (already denormalized)."""
+        """One sliced decision step (shipsim_step). action: (N,) or (N,1) float32 scoping angles
+        [rad] (already denormalized); consumed only by envs waiting for a decision. With
+        max_ticks <= 0 every active env runs to its decision point (out['ready'] all ones)."""
         a = self._dev(action, torch.float32).reshape(-1)
         if a.numel() != self.n_envs:
             raise ShipSimError(f"action has {a.numel()} entries, expected {self.n_envs}")
@@ -129,9 +131,11 @@ class ShipSim:
                        reward=torch.empty(self.n_envs, dtype=torch.float64, device=self.device),
                        done=torch.empty(self.n_envs, dtype=torch.uint8, device=self.device),
                        events=torch.empty(self.n_envs, dtype=torch.int32, device=self.device),
-                       ticks=torch.empty(self.n_envs, dtype=torch.int32, device=self.device))
+                       ticks=torch.empty(self.n_envs, dtype=torch.int32, device=self.device),
+                       ready=torch.empty(self.n_envs, dtype=torch.uint8, device=self.device))
         self._check(self.L.shipsim_step(self.h, _ptr(a), _ptr(act), int(max_ticks), _ptr(out["obs"]), _ptr(out["reward"]),
-                                        _ptr(out["done"]), _ptr(out["events"]), _ptr(out["ticks"])), "shipsim_step")
+                                        _ptr(out["done"]), _ptr(out["events"]), _ptr(out["ticks"]),
+                                        _ptr(out.get("ready"))), "shipsim_step")
         self._keep = (a, act)
         return out
 

@@ -104,7 +104,8 @@ class Config(C.Structure):
         ("wind_direction", C.c_double), ("sbmpc_tf", C.c_double), ("sbmpc_dt", C.c_double),
         ("action_low", C.c_float), ("action_high", C.c_float), ("ship", ShipConfig * 2),
         ("n_polys", C.c_int32), ("poly_start", C.c_int32 * (MAX_POLYS + 1)),
-        ("poly_east", C.c_double * MAX_VERTS), ("poly_north", C.c_double * MAX_VERTS)]
+        ("poly_east", C.c_double * MAX_VERTS), ("poly_north", C.c_double * MAX_VERTS),
+        ("lanes_per_env", C.c_int32), ("reserved", C.c_int32 * 7)]
 
 
 # ------------------------------------------------------------------------------------------

@@ -1,10 +1,12 @@
 """Headline benchmark: batched two-ship AST env-steps/sec (BASELINE.json metric) on 1..8 MI355X.
 
-A "step" is one batched MultiShipRLEnv.step() over every env of every rank: each env consumes one
-scoping-angle decision and ticks until its next decision point (RoA + 1 tick) or done (≈156
-env-ticks per decision at dt = 4 s); envs that finished are auto-reset (masked reset kernel)
-inside the step. Actions come from a device-resident synthetic table U(-1, 1) (PCG64 seeded per
-global env id, SURVEY.md §8(d) C3 input) mapped by NormalizedBoxEnv's float32 rule.
+A "step" is one sliced batched MultiShipRLEnv.step() over every env of every rank
+(shipsim_step with max_ticks = --slice): every env runs up to `slice` ticks of its current
+decision (one decision = tick until RoA + 1 tick, or done; ≈130 env-ticks per decision at
+dt = 4 s); envs waiting for a decision first consume a scoping angle; envs whose episode ended
+are auto-reset (masked reset kernel) inside the step. Actions come from a device-resident
+synthetic table U(-1, 1) (PCG64 seeded per global env id, SURVEY.md §8(d) C3 input) mapped by
+NormalizedBoxEnv's float32 rule.
 
 value = env-ticks (one `_step` of one env, both ships + reward/termination) summed over all ranks
         / max-over-ranks wall time of the K timed steps.
@@ -37,6 +39,8 @@ def parse():
     p.add_argument("--envs-per-gpu", type=int, default=4096)
     p.add_argument("--collav", default="sbmpc", choices=["none", "simple", "sbmpc"])
     p.add_argument("--machinery", default="detailed", choices=["detailed", "simplified"])
+    p.add_argument("--slice", type=int, default=64, help="max ticks per env per step call (0 = whole decision)")
+    p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library default)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round1_pmc_traffic.json"))
@@ -81,6 +85,7 @@ def main():
     torch.cuda.set_device(dev)
     mach = abi.MACH_DETAILED if args.machinery == "detailed" else abi.MACH_SIMPLIFIED
     cfg = abi.ast_config(args.collav, machinery=mach)
+    cfg.lanes_per_env = args.lpe
     N = args.envs_per_gpu
     sim = ShipSim(cfg, N, device=dev)
 
@@ -97,7 +102,8 @@ def main():
                reward=torch.empty(N, dtype=torch.float64, device=dev),
                done=torch.empty(N, dtype=torch.uint8, device=dev),
                events=torch.empty(N, dtype=torch.int32, device=dev),
-               ticks=torch.empty(N, dtype=torch.int32, device=dev))
+               ticks=torch.empty(N, dtype=torch.int32, device=dev),
+               ready=torch.empty(N, dtype=torch.uint8, device=dev))
     obs_reset = torch.empty((N, 8), dtype=torch.float32, device=dev)
     total_ticks = torch.zeros((), dtype=torch.int64, device=dev)
     total_decisions = torch.zeros((), dtype=torch.int64, device=dev)
@@ -108,16 +114,17 @@ def main():
         act = table[ep_idx % table_eps, dec_idx, ar]
         if timed_i is not None:
             ev0[timed_i].record()
-        sim.step(act, out=out)
+        sim.step(act, max_ticks=args.slice, out=out)
         if timed_i is not None:
             ev1[timed_i].record()
-        done = out["done"].bool() | (dec_idx + 1 >= n_dec)
+        ready = out["ready"].bool()
+        end = ready & (out["done"].bool() | (dec_idx + 1 >= n_dec))
         total_ticks.add_(out["ticks"].sum())
-        total_decisions.add_(N)
-        dec_idx.add_(1)
-        dec_idx.masked_fill_(done, 0)
-        ep_idx.add_(done.long())
-        sim.reset(mask=done.to(torch.uint8), obs_out=obs_reset)
+        total_decisions.add_(ready.sum())
+        dec_idx.add_(ready.long())
+        dec_idx.masked_fill_(end, 0)
+        ep_idx.add_(end.long())
+        sim.reset(mask=end.to(torch.uint8), obs_out=obs_reset)
 
     sim.reset(obs_out=obs_reset)
     for _ in range(args.warmup):
@@ -184,7 +191,8 @@ def main():
             "config": {"workload": "C3: two-ship AST envs (ShipModelAST PTI machinery, sampled-route LOS, "
                                    "reward_designs), dt 4 s",
                        "envs_per_gpu": N, "global_envs": N * world, "collav": args.collav,
-                       "machinery": args.machinery, "parallelism": f"env-shard x{world}"},
+                       "machinery": args.machinery, "slice_ticks": args.slice, "lanes_per_env": args.lpe or 16,
+                       "parallelism": f"env-shard x{world}"},
             "decisions_per_s": all_dec / elapsed,
             "env_ticks_per_decision": all_ticks / max(all_dec, 1),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

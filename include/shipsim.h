@@ -176,6 +176,10 @@ typedef struct shipsim_config {
   int32_t poly_start[SHIPSIM_MAX_POLYS + 1];
   double poly_east[SHIPSIM_MAX_VERTS];
   double poly_north[SHIPSIM_MAX_VERTS];
+  /* performance knob (no effect on results): device lanes per AST env, 2/4/8/16; 0 = default 16
+   * (or $SHIPSIM_LPE) */
+  int32_t lanes_per_env;
+  int32_t reserved[7];
 } shipsim_config;
 
 /* Per-ship state fields for get/set_state (SoA, double unless noted) */
@@ -241,24 +245,32 @@ int32_t shipsim_num_envs(const shipsim_handle* h);
  * receives the reference's constant initial_states row for reset envs (Q11). */
 int shipsim_reset(shipsim_handle* h, const uint8_t* env_mask, float* obs_out);
 
-/* MultiShipRLEnv.step(action) for all N envs at once (AST kind only).
+/* MultiShipRLEnv.step(action) for all N envs at once (AST kind only), sliced.
+ * Every active env ticks (_step, env.py:563) until its decision point (RoA + one tick, or done —
+ * env.py:700-771) or until it has run `max_ticks` ticks in this call (<= 0: no limit). An env that
+ * paused keeps its decision in progress and resumes in the next call WITHOUT consuming an action;
+ * an env waiting for a decision (after reset or after its previous decision completed) first
+ * consumes action[i] (intermediate-waypoint sampling, env.py:659-696).
  *   action     N float32 scoping angles in radians (already denormalized, i.e. what
  *              NormalizedBoxEnv passes to the wrapped env), device.
  *   active     optional N uint8 mask (NULL = all): envs with 0 are left untouched.
- *   max_ticks  safety bound on ticks per env in this call (<=0: derived from simulation_time).
- * Outputs (device, each may be NULL): obs N x 8 float32, reward N double (un-scaled),
- * done N uint8 (combined_done), events N uint32 (SHIPSIM_EV_* bits), ticks N int32 (_step calls). */
+ * Outputs (device, each may be NULL):
+ *   ready  N uint8: 1 if the env completed a decision in this call; then obs (N x 8 float32),
+ *          reward (N double, un-scaled accumulated reward of the decision), done (N uint8,
+ *          combined_done) and events (N uint32, SHIPSIM_EV_* bits) hold that decision's result;
+ *          rows of envs that did not complete are left untouched.
+ *   ticks  N int32: _step calls executed by the env in this call. */
 int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks,
                  float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
-                 int32_t* ticks_out);
+                 int32_t* ticks_out, uint8_t* ready_out);
 
 /* Raw ticks for the SINGLE and NONIW kinds (and debugging AST): advance every env by k ticks of
  * the reference loop body (run_simplified_model.py:248-249 / env._step). events_out (N uint32,
  * may be NULL) receives the OR of the per-tick env_info bits of the last tick. */
 int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out);
 
-/* Read / write one state field for all envs (device pointer dst/src; ship fields are laid out
- * [ship][env], env fields [env] or [env][SHIPSIM_MAX_ROUTE] for routes). */
+/* Read / write one state field for all envs (device pointer dst/src). Ship fields are laid out
+ * env-major [env][ship] (the device lane order), env fields [env], routes [env][ship][SHIPSIM_MAX_ROUTE]. */
 int shipsim_get_state(shipsim_handle* h, int32_t field, void* dst);
 int shipsim_set_state(shipsim_handle* h, int32_t field, const void* src);
 

@@ -40,7 +40,9 @@ def run_oracle(cfg, tables):
     return out
 
 
-def run_gpu(cfg, tables, device="cuda"):
+def run_gpu(cfg, tables, device="cuda", max_ticks=0):
+    """Replay `tables` through ShipSim. With max_ticks > 0 decisions are sliced: every call runs at
+    most max_ticks ticks per env and the harness keeps calling until each decision completes."""
     import torch
     from ast_sac_amd.shipsim import ShipSim
     n = len(tables)
@@ -48,9 +50,10 @@ def run_gpu(cfg, tables, device="cuda"):
     o0 = sim.reset().cpu().numpy()
     ep = np.zeros(n, int)
     dec = np.zeros(n, int)
+    acc_ticks = np.zeros(n, int)
     rec = [[(o0[i].copy(), [])] for i in range(n)]
     n_eps = np.array([len(t) for t in tables])
-    steps = 0
+    calls = 0
     while True:
         active = ep < n_eps
         if not active.any():
@@ -58,16 +61,21 @@ def run_gpu(cfg, tables, device="cuda"):
         acts = np.zeros(n, np.float32)
         for i in np.nonzero(active)[0]:
             acts[i] = abi.normalized_to_scoping(tables[i][ep[i]][dec[i]])
-        out = sim.step(torch.from_numpy(acts), active=torch.from_numpy(active.astype(np.uint8)))
+        out = sim.step(torch.from_numpy(acts), active=torch.from_numpy(active.astype(np.uint8)), max_ticks=max_ticks)
         o = out["obs"].cpu().numpy()
         r = out["reward"].cpu().numpy()
         d = out["done"].cpu().numpy().astype(bool)
         b = out["events"].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
         t = out["ticks"].cpu().numpy()
-        steps += 1
+        rd = out["ready"].cpu().numpy().astype(bool)
+        calls += 1
         need_reset = np.zeros(n, bool)
         for i in np.nonzero(active)[0]:
-            rec[i][-1][1].append((o[i].copy(), float(r[i]), bool(d[i]), int(b[i]), int(t[i])))
+            acc_ticks[i] += t[i]
+            if not rd[i]:
+                continue
+            rec[i][-1][1].append((o[i].copy(), float(r[i]), bool(d[i]), int(b[i]), int(acc_ticks[i])))
+            acc_ticks[i] = 0
             dec[i] += 1
             if d[i] or dec[i] >= len(tables[i][ep[i]]):
                 ep[i] += 1
@@ -83,7 +91,7 @@ def run_gpu(cfg, tables, device="cuda"):
                                                          abi.E_ACC_REWARD, abi.E_N_BASE, abi.E_E_BASE,
                                                          abi.E_SBMPC_P_LAST, abi.E_SBMPC_CHI_LAST)}
     sim.close()
-    return rec, fields, env_fields, steps
+    return rec, fields, env_fields, calls
 
 
 PERTURBATIONS = (0.0, 1e-15, -1e-15, 1e-13)

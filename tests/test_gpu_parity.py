@@ -111,6 +111,70 @@ def test_ast_env_vs_oracle(torch_cuda, collav, machinery, n_envs, n_eps):
     np.testing.assert_array_equal(env_fields[abi.E_SBMPC_CHI_LAST], envs[:, 7])
 
 
+@pytest.mark.parametrize("collav", ["none", "sbmpc"])
+def test_sliced_steps_are_bitwise_identical(torch_cuda, collav):
+    """Pausing a decision after max_ticks and resuming it in the next call must not change a bit."""
+    cfg = abi.ast_config(collav)
+    tables = H.make_tables(48, 2)
+    full, f_fields, _, calls_full = H.run_gpu(cfg, tables)
+    for mt in (1, 7, 64):
+        sl, s_fields, _, calls = H.run_gpu(cfg, tables, max_ticks=mt)
+        assert calls > calls_full
+        for a, b in zip(full, sl):
+            assert len(a) == len(b)
+            for (a0, ad), (b0, bd) in zip(a, b):
+                np.testing.assert_array_equal(a0, b0)
+                assert len(ad) == len(bd)
+                for x, y in zip(ad, bd):
+                    np.testing.assert_array_equal(x[0], y[0])
+                    assert x[1:] == y[1:]
+        for f in f_fields:
+            np.testing.assert_array_equal(f_fields[f], s_fields[f])
+
+
+@pytest.mark.parametrize("lpe", [2, 4, 16])
+def test_lanes_per_env_variants_identical(torch_cuda, lpe):
+    """The lanes-per-env layout only changes the work split; results are bitwise identical up to the
+    order of the sub-lane min/or reductions (min is exact)."""
+    cfg = abi.ast_config("sbmpc")
+    tables = H.make_tables(40, 2)
+    ref, r_fields, _, _ = H.run_gpu(cfg, tables)
+    cfg2 = abi.ast_config("sbmpc")
+    cfg2.lanes_per_env = lpe
+    got, g_fields, _, _ = H.run_gpu(cfg2, tables)
+    for a, b in zip(ref, got):
+        for (a0, ad), (b0, bd) in zip(a, b):
+            assert len(ad) == len(bd)
+            for x, y in zip(ad, bd):
+                np.testing.assert_array_equal(x[0], y[0])
+                assert x[1:] == y[1:]
+    for f in r_fields:
+        np.testing.assert_array_equal(r_fields[f], g_fields[f])
+
+
+@pytest.mark.parametrize("collav,machinery", [("none", abi.MACH_DETAILED), ("simple", abi.MACH_DETAILED),
+                                               ("sbmpc", abi.MACH_DETAILED), ("sbmpc", abi.MACH_SIMPLIFIED)])
+def test_layout_and_slicing_matrix(torch_cuda, collav, machinery):
+    """Every (lanes-per-env, slice) combination reproduces the LPE=2 whole-decision run bit for bit."""
+    tables = H.make_tables(192, 2, seed=7)
+    cfg = abi.ast_config(collav, machinery=machinery)
+    cfg.lanes_per_env = 2
+    ref, r_fields, _, _ = H.run_gpu(cfg, tables)
+    for lpe, mt in ((8, 0), (8, 3), (8, 32), (16, 5), (4, 11)):
+        c = abi.ast_config(collav, machinery=machinery)
+        c.lanes_per_env = lpe
+        got, g_fields, _, _ = H.run_gpu(c, tables, max_ticks=mt)
+        for a, b in zip(ref, got):
+            assert len(a) == len(b)
+            for (a0, ad), (b0, bd) in zip(a, b):
+                assert len(ad) == len(bd), (lpe, mt)
+                for x, y in zip(ad, bd):
+                    np.testing.assert_array_equal(x[0], y[0])
+                    assert x[1:] == y[1:], (lpe, mt)
+        for f in r_fields:
+            np.testing.assert_array_equal(r_fields[f], g_fields[f], err_msg=f"field {f} lpe {lpe} mt {mt}")
+
+
 def test_ast_env_vs_golden_episodes(golden, torch_cuda):
     """The golden fixture episodes (reference run) replayed on device, one env per collav mode."""
     import torch
