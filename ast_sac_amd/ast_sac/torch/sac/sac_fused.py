@@ -1,0 +1,332 @@
+"""FusedSACTrainer — the SAC update (sac.py:102-300) restructured for MI355X.
+
+The reference update is ~20 tiny GEMMs (B = 256, H = 256) plus ~150 elementwise kernels,
+four optimizer steps and a soft update — launch-bound on any GPU. Restructuring, all exact
+rewrites of the same math:
+
+* every loss is built from the pre-step parameters and each optimizer reads only its own
+  parameters' gradients, so the α → π → Q1 → Q2 step sequence equals one combined step:
+  grads of (α-loss + π-loss) w.r.t. (log α, π) and of (Q1-loss + Q2-loss) w.r.t. (Q1, Q2) are
+  taken from ONE forward graph (two autograd.grad calls; the π-loss gradient that the reference
+  lets flow into Q1/Q2 is zeroed by their zero_grad before their own backward, so it is never
+  computed here), then one fused Adam over two param groups (policy_lr / qf_lr);
+* the actor runs once on [obs; next_obs] (2B rows); twin critics run as one batched GEMM per
+  layer (torch.baddbmm over the stacked [Q1, Q2] weights) on [(obs, ã); (obs, a)] (2B rows);
+  twin targets likewise on (next_obs, ã');
+* the whole step — on-device batch sampling from DeviceReplayBuffer, forward, both grads,
+  Adam, soft target update — is captured once in a HIP graph and replayed (capturable Adam).
+  For data-parallel training the gradients are flattened into one bucket and averaged with a
+  single RCCL all-reduce between two graph halves (one ≈550 KB bucket, xGMI
+  latency-bound; α + π and Q1 + Q2 in one bucket because each optimizer reads only its own).
+
+Numerics: fp32 like the reference; results equal SACTrainer's up to GEMM accumulation order
+(tests/test_sac.py checks both against the captured reference step, tests/golden/sac_step.npz).
+"""
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..utils import pytorch_util as ptu
+from ..core.torch_rl_algorithm import TorchTrainer
+from ..core.distributions import diag_normal_log_prob
+from ..sac.policies.gaussian_policy import LOG_SIG_MIN, LOG_SIG_MAX
+from ...core.eval_util import create_stats_ordered_dict
+from .sac import SACLosses
+
+_LOG2 = float(np.log(2.0))
+_BATCH_KEYS = ("observations", "actions", "rewards", "terminals", "next_observations")
+
+
+def _layers(mlp):
+    return list(mlp.fcs) + [mlp.last_fc]
+
+
+class FusedSACTrainer(TorchTrainer):
+    def __init__(self, env, policy, qf1, qf2, target_qf1, target_qf2, discount=0.99, reward_scale=1.0,
+                 policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None, soft_target_tau=1e-2, target_update_period=1,
+                 plotter=None, render_eval_paths=False, use_automatic_entropy_tuning=True, target_entropy=None,
+                 action_reg_coeff=None, clip_val=np.inf, batch_size=256, use_graph=None, process_group=None):
+        super().__init__()
+        if target_update_period != 1:
+            raise NotImplementedError("FusedSACTrainer soft-updates every step (runner: target_update_period=1)")
+        self.env = env
+        self.policy, self.qf1, self.qf2 = policy, qf1, qf2
+        self.target_qf1, self.target_qf2 = target_qf1, target_qf2
+        self.discount = float(discount)
+        self.reward_scale = float(reward_scale)
+        self.soft_target_tau = float(soft_target_tau)
+        self.target_update_period = 1
+        self.use_automatic_entropy_tuning = use_automatic_entropy_tuning
+        self.action_reg_coeff = action_reg_coeff
+        self.clip_val = float(clip_val)
+        self.batch_size = int(batch_size)
+        self.device = next(policy.parameters()).device
+        dev = self.device
+        if use_automatic_entropy_tuning:
+            self.target_entropy = (-np.prod(env.action_space.shape).item() if target_entropy is None
+                                   else target_entropy)
+        else:
+            self.target_entropy = 0.0
+        self.log_alpha = torch.zeros(1, requires_grad=use_automatic_entropy_tuning, device=dev)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+
+        self.pi_params = ([self.log_alpha] if use_automatic_entropy_tuning else []) + list(policy.parameters())
+        self.q_params = list(qf1.parameters()) + list(qf2.parameters())
+        self.t_params = list(target_qf1.parameters()) + list(target_qf2.parameters())
+        fused = dev.type == "cuda"
+        self.use_graph = fused if use_graph is None else bool(use_graph)
+        self.optimizer = torch.optim.Adam([dict(params=self.pi_params, lr=policy_lr),
+                                           dict(params=self.q_params, lr=qf_lr)],
+                                          fused=fused, capturable=self.use_graph)
+        # one flat gradient bucket; p.grad are persistent views into it
+        params = self.pi_params + self.q_params
+        self._numel = [p.numel() for p in params]
+        self.flat_grad = torch.zeros(sum(self._numel), device=dev)
+        self._grad_views = []
+        off = 0
+        for p, n in zip(params, self._numel):
+            v = self.flat_grad[off:off + n].view_as(p)
+            self._grad_views.append(v)
+            p.grad = v
+            off += n
+        self.noise_fn = None  # callable(shape) -> ε for [obs; next_obs] rows; None = torch.randn
+        self._static = None
+        self._graphs = None
+        self._n_train_steps_total = 0
+        self._need_to_update_eval_statistics = True
+        self.eval_statistics = OrderedDict()
+
+    # ---------------------------------------------------------------- math
+    def _actor(self, x):
+        h = x
+        for fc in self.policy.fcs:
+            h = F.relu(F.linear(h, fc.weight, fc.bias))
+        w = torch.cat([self.policy.last_fc.weight, self.policy.last_fc_log_std.weight], 0)
+        b = torch.cat([self.policy.last_fc.bias, self.policy.last_fc_log_std.bias], 0)
+        out = torch.addmm(b, h, w.t())
+        a_dim = self.policy.last_fc.weight.shape[0]
+        mean, log_std = out[:, :a_dim], out[:, a_dim:]
+        std = torch.exp(torch.clamp(log_std, LOG_SIG_MIN, LOG_SIG_MAX))
+        return mean, std
+
+    @staticmethod
+    def _twin(nets, x):
+        """x: (R, in) shared by both nets → (2, R, out) via one baddbmm per layer."""
+        layers = [_layers(n) for n in nets]
+        h = x.unsqueeze(0).expand(len(nets), -1, -1)
+        n_l = len(layers[0])
+        for i in range(n_l):
+            w = torch.stack([ls[i].weight for ls in layers])          # (2, out, in)
+            b = torch.stack([ls[i].bias for ls in layers]).unsqueeze(1)  # (2, 1, out)
+            h = torch.baddbmm(b, h, w.transpose(1, 2))
+            if i < n_l - 1:
+                h = F.relu(h)
+        return h
+
+    def _eps(self, shape):
+        if self.noise_fn is not None:
+            return self.noise_fn(shape)
+        return torch.randn(shape, device=self.device)
+
+    def _forward_and_grads(self, b):
+        """Losses and gradients for one batch; grads land in self.flat_grad."""
+        obs, act, rew, term, nobs = (b[k] for k in _BATCH_KEYS)
+        B = obs.shape[0]
+        mean, std = self._actor(torch.cat([obs, nobs], 0))
+        z = mean + std * self._eps(mean.shape)
+        a = torch.tanh(z)
+        logp = diag_normal_log_prob(z, mean, std) + (-2.0 * (_LOG2 - z - F.softplus(-2.0 * z)).sum(dim=1))
+        new_a, log_pi = a[:B], logp[:B].unsqueeze(-1)
+        nn_a, nlog_pi = a[B:], logp[B:].unsqueeze(-1)
+        if self.use_automatic_entropy_tuning:
+            alpha_loss = -(self.log_alpha * (log_pi + self.target_entropy).detach()).mean()
+            alpha = self.log_alpha.exp().detach()
+        else:
+            alpha_loss = torch.zeros((), device=self.device)
+            alpha = torch.ones(1, device=self.device)
+        q = self._twin((self.qf1, self.qf2), torch.cat([torch.cat([obs, new_a], 1), torch.cat([obs, act], 1)], 0))
+        q_new = torch.min(q[0, :B], q[1, :B])
+        policy_loss = (alpha * log_pi - q_new).mean()
+        if self.action_reg_coeff:
+            policy_loss = policy_loss + self.action_reg_coeff * (new_a ** 2).mean()
+        q1_pred, q2_pred = q[0, B:], q[1, B:]
+        with torch.no_grad():
+            tq = self._twin((self.target_qf1, self.target_qf2), torch.cat([nobs, nn_a], 1))
+            target_q = torch.min(tq[0], tq[1]) - alpha * nlog_pi
+            q_target = self.reward_scale * rew + (1.0 - term) * self.discount * target_q
+            q_target = torch.clamp(q_target, min=-self.clip_val, max=self.clip_val)
+        qf1_loss = ((q1_pred - q_target) ** 2).mean()
+        qf2_loss = ((q2_pred - q_target) ** 2).mean()
+        g_pi = torch.autograd.grad(policy_loss + alpha_loss, self.pi_params, retain_graph=True)
+        g_q = torch.autograd.grad(qf1_loss + qf2_loss, self.q_params)
+        torch._foreach_copy_(self._grad_views, list(g_pi) + list(g_q))
+        return dict(policy_loss=policy_loss.detach(), qf1_loss=qf1_loss.detach(), qf2_loss=qf2_loss.detach(),
+                    alpha_loss=alpha_loss.detach(), q1_pred=q1_pred.detach(), q2_pred=q2_pred.detach(),
+                    q_target=q_target, log_pi=log_pi.detach(), alpha=alpha.detach(),
+                    pi_mean=torch.tanh(mean[:B]).detach(), pi_std=std[:B].detach())
+
+    def _apply(self):
+        if self.world > 1:
+            self.flat_grad.mul_(1.0 / self.world)
+        self.optimizer.step()
+        with torch.no_grad():
+            tau = self.soft_target_tau
+            torch._foreach_mul_(self.t_params, 1.0 - tau)
+            torch._foreach_add_(self.t_params, self.q_params, alpha=tau)
+
+    def _allreduce(self):
+        if self.world > 1:
+            torch.distributed.all_reduce(self.flat_grad, group=self.pg)
+
+    # ---------------------------------------------------------------- graph
+    def _alloc_static(self, obs_dim, act_dim):
+        B, dev = self.batch_size, self.device
+        self._static = dict(observations=torch.zeros(B, obs_dim, device=dev), actions=torch.zeros(B, act_dim, device=dev),
+                            rewards=torch.zeros(B, 1, device=dev), terminals=torch.zeros(B, 1, device=dev),
+                            next_observations=torch.zeros(B, obs_dim, device=dev))
+
+    def _snapshot_state(self):
+        params = {id(p): p.detach().clone() for p in self.pi_params + self.q_params + self.t_params}
+        st = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in s.items()}
+              for p, s in self.optimizer.state.items()}
+        return params, st
+
+    def _restore_state(self, snap):
+        params, st = snap
+        with torch.no_grad():
+            for p in self.pi_params + self.q_params + self.t_params:
+                p.copy_(params[id(p)])
+            for p, s in self.optimizer.state.items():
+                old = st.get(id(p))
+                for k, v in s.items():
+                    if torch.is_tensor(v):
+                        v.copy_(old[k]) if old is not None else v.zero_()
+
+    def _body_a(self, replay_buffer):
+        if replay_buffer is not None:
+            replay_buffer.random_batch(self.batch_size, out=self._static)
+        self._out = self._forward_and_grads(self._static)
+
+    def _build_graphs(self, replay_buffer):
+        snap = self._snapshot_state()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                self._body_a(replay_buffer)
+                self._allreduce()
+                self._apply()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self._restore_state(snap)
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        pool = torch.cuda.graph_pool_handle()
+        if self.world > 1:
+            with torch.cuda.graph(ga, pool=pool):
+                self._body_a(replay_buffer)
+            with torch.cuda.graph(gb, pool=pool):
+                self._apply()
+        else:
+            with torch.cuda.graph(ga, pool=pool):
+                self._body_a(replay_buffer)
+                self._apply()
+            gb = None
+        torch.cuda.synchronize(self.device)
+        return ga, gb
+
+    def _run_step(self, replay_buffer):
+        key = id(replay_buffer) if replay_buffer is not None else None
+        if self._static is None:
+            obs_dim = self.policy.input_size
+            act_dim = self.policy.last_fc.weight.shape[0]
+            self._alloc_static(obs_dim, act_dim)
+        if not self.use_graph:
+            self._body_a(replay_buffer)
+            self._allreduce()
+            self._apply()
+            return
+        if self._graphs is None or self._graphs[0] != key:
+            self._graphs = (key,) + self._build_graphs(replay_buffer)
+        _, ga, gb = self._graphs
+        ga.replay()
+        if gb is not None:
+            self._allreduce()
+            gb.replay()
+
+    # ---------------------------------------------------------------- API
+    def train_from_torch(self, batch):
+        """One update on an explicit batch (copied into the static batch buffers)."""
+        if self._static is None:
+            self._alloc_static(batch["observations"].shape[1], batch["actions"].shape[1])
+        if batch["observations"].shape[0] != self.batch_size:
+            raise ValueError(f"batch has {batch['observations'].shape[0]} rows, trainer batch_size={self.batch_size}")
+        for k in _BATCH_KEYS:
+            self._static[k].copy_(batch[k].reshape(self._static[k].shape))
+        self._run_step(None)
+        self._after_step()
+
+    def train_from_buffer(self, replay_buffer, n_steps=1):
+        """n_steps updates, each on a fresh uniform batch drawn on-device from a DeviceReplayBuffer."""
+        for _ in range(n_steps):
+            self._num_train_steps += 1
+            self._run_step(replay_buffer)
+            self._after_step()
+
+    def _after_step(self):
+        self._n_train_steps_total += 1
+        if self._need_to_update_eval_statistics:
+            self.eval_statistics = self._stats()
+            self._need_to_update_eval_statistics = False
+
+    def last_losses(self):
+        o = self._out
+        return SACLosses(policy_loss=o["policy_loss"], qf1_loss=o["qf1_loss"], qf2_loss=o["qf2_loss"],
+                         alpha_loss=o["alpha_loss"])
+
+    def _stats(self):
+        o = {k: ptu.get_numpy(v) for k, v in self._out.items()}
+        st = OrderedDict()
+        st["QF1 Loss"] = float(np.mean(o["qf1_loss"]))
+        st["QF2 Loss"] = float(np.mean(o["qf2_loss"]))
+        st["Policy Loss"] = float(np.mean(o["policy_loss"]))
+        st.update(create_stats_ordered_dict("Q1 Predictions", o["q1_pred"]))
+        st.update(create_stats_ordered_dict("Q2 Predictions", o["q2_pred"]))
+        st.update(create_stats_ordered_dict("Q Targets", o["q_target"]))
+        st.update(create_stats_ordered_dict("Log Pis", o["log_pi"]))
+        st.update(create_stats_ordered_dict("policy/mean", o["pi_mean"]))
+        st.update(create_stats_ordered_dict("policy/normal/std", o["pi_std"]))
+        st.update(create_stats_ordered_dict("policy/normal/log_std", np.log(o["pi_std"])))
+        if self.use_automatic_entropy_tuning:
+            st["Alpha"] = float(o["alpha"].reshape(-1)[0])
+            st["Alpha Loss"] = float(o["alpha_loss"])
+        return st
+
+    def broadcast_parameters(self, src=0):
+        """Make every rank start from rank `src`'s networks."""
+        if self.world > 1:
+            with torch.no_grad():
+                for p in self.pi_params + self.q_params + self.t_params:
+                    torch.distributed.broadcast(p.data, src, group=self.pg)
+
+    def get_diagnostics(self):
+        stats = super().get_diagnostics()
+        stats.update(self.eval_statistics)
+        return stats
+
+    def end_epoch(self, epoch):
+        self._need_to_update_eval_statistics = True
+
+    @property
+    def networks(self):
+        return [self.policy, self.qf1, self.qf2, self.target_qf1, self.target_qf2]
+
+    @property
+    def optimizers(self):
+        return [self.optimizer]
+
+    def get_snapshot(self):
+        return dict(policy=self.policy, qf1=self.qf1, qf2=self.qf2, target_qf1=self.target_qf1,
+                    target_qf2=self.target_qf2)

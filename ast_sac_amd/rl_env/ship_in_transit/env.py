@@ -1,0 +1,190 @@
+"""Gym-style environments over the HIP simulator (drop-in for rl_env/ship_in_transit/env.py).
+
+* `BatchedMultiShipRLEnv` — N independent MultiShipRLEnv instances resident on one device;
+  reset/step take and return torch tensors. `step` runs every active env to its decision point
+  (env.py:624-773); `step_async` runs at most `max_ticks` ticks per env and reports which envs
+  completed a decision (GPU-native collectors use this).
+* `MultiShipRLEnv` — the reference's single-env object API (reset() -> np.ndarray(8,) float32,
+  step(action) -> (obs, reward, done, env_info)) as a one-env view of the batched env, so that
+  reference callers (NormalizedBoxEnv, ast_sac_rollout, MdpPathCollector, EnvReplayBuffer,
+  SACTrainer) run unchanged.
+
+Semantics, quirks included, are those of the reference MultiShipRLEnv; the
+numerics run in ast_sac_amd/csrc (fp64) and are checked against the CPU oracle in tests/.
+"""
+import argparse
+
+import numpy as np
+import torch
+
+from ... import shipsim_abi as abi
+from ...shipsim import ShipSim
+from ...spaces import Box
+
+# observation_space / action_space of env.py:86-104
+OBS_LOW = np.array([0, 0, -3000, 0, 0, -np.pi, -3000, 0], dtype=np.float32)
+OBS_HIGH = np.array([10000, 20000, 3000, 10000, 20000, np.pi, 3000, 10], dtype=np.float32)
+
+
+def default_args(**kw):
+    """run/ast-sac_runner.py:27-43 defaults (environment group)."""
+    a = dict(max_sampling_frequency=9, time_step=4, radius_of_acceptance=300, lookahead_distance=1000,
+             collav_mode="sbmpc", ship_draw=False, time_since_last_ship_drawing=30, normalize_action=False)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def config_from_args(args, machinery="detailed"):
+    """The scenario of record (run/env_setup.py) with the env arguments applied."""
+    mach = abi.MACH_DETAILED if machinery in ("detailed", abi.MACH_DETAILED) else abi.MACH_SIMPLIFIED
+    collav = getattr(args, "collav_mode", "sbmpc")
+    cfg = abi.ast_config(collav if collav in abi.COLLAV else "none", time_step=float(args.time_step), machinery=mach)
+    cfg.max_sampling_frequency = int(args.max_sampling_frequency)
+    cfg.env_radius_of_acceptance = float(args.radius_of_acceptance)
+    for s in cfg.ship:
+        s.radius_of_acceptance = float(args.radius_of_acceptance)
+        s.lookahead_distance = float(args.lookahead_distance)
+    cfg.normalize_action = int(bool(getattr(args, "normalize_action", False)))
+    return cfg
+
+
+class BatchedMultiShipRLEnv:
+    def __init__(self, args=None, n_envs=1, device=None, machinery="detailed", cfg=None, lanes_per_env=0):
+        self.args = args if args is not None else default_args()
+        self.cfg = cfg if cfg is not None else config_from_args(self.args, machinery)
+        if lanes_per_env:
+            self.cfg.lanes_per_env = lanes_per_env
+        self.n_envs = int(n_envs)
+        self.sim = ShipSim(self.cfg, self.n_envs, device=device)
+        self.device = self.sim.device
+        self.collav = getattr(self.args, "collav_mode", "sbmpc")
+        self.observation_space = Box(low=OBS_LOW, high=OBS_HIGH, dtype=np.float32)
+        if self.cfg.normalize_action:
+            self.action_space = Box(low=np.array([-1.0], np.float32), high=np.array([1.0], np.float32),
+                                    dtype=np.float32)
+        else:
+            self.action_space = Box(low=np.array([-np.deg2rad(30)], np.float32),
+                                    high=np.array([np.deg2rad(30)], np.float32), dtype=np.float32)
+        self.initial_states = np.array([self.cfg.ship[0].initial_north_position_m, self.cfg.ship[0].initial_east_position_m,
+                                        0.0, self.cfg.ship[1].initial_north_position_m,
+                                        self.cfg.ship[1].initial_east_position_m, self.cfg.ship[1].initial_yaw_angle_rad,
+                                        0.0, self.cfg.ship[1].initial_forward_speed_m_per_s], dtype=np.float32)
+        self._out = None
+
+    # -- reference helpers (env.py:186-196) --
+    def do_normalize_action(self, a_real):
+        return 2.0 * (a_real - self.action_space.low) / (self.action_space.high - self.action_space.low) - 1.0
+
+    def do_denormalize_action(self, a_norm):
+        return (a_norm + 1.0) / 2.0 * (self.action_space.high - self.action_space.low) + self.action_space.low
+
+    def reset(self, mask=None, obs_out=None):
+        """MultiShipRLEnv.reset for the envs in `mask` (all if None); returns (N, 8) float32 —
+        reset rows hold the constant initial_states (env.py:295, Q11); other rows are untouched."""
+        return self.sim.reset(mask=mask, obs_out=obs_out)
+
+    def _info(self, out):
+        ev = out["events"]
+        return dict(events=ev, terminal=(ev & abi.EV_TERMINAL) != 0, test_ship_stop=(ev & abi.EV_TEST_STOP) != 0,
+                    obs_ship_stop=(ev & abi.EV_OBS_STOP) != 0, ticks=out["ticks"])
+
+    def step(self, action, active=None):
+        """MultiShipRLEnv.step for every active env: returns obs (N,8) float32, accumulated reward (N,)
+        float64, combined_done (N,) bool and an info dict of tensors (event bits + flags)."""
+        out = self.sim.step(action, active=active, max_ticks=0)
+        return out["obs"], out["reward"], out["done"].bool(), self._info(out)
+
+    def step_async(self, action, max_ticks=64, active=None, out=None):
+        """Run at most max_ticks ticks per env; envs that reach their decision point have
+        out['ready'] == 1 and their obs/reward/done/events rows are valid."""
+        return self.sim.step(action, active=active, max_ticks=max_ticks, out=out)
+
+    @staticmethod
+    def events_strings(bits):
+        return [abi.events_to_string(int(b)) for b in torch.as_tensor(bits).cpu().tolist()]
+
+    @property
+    def sampling_count(self):
+        return self.sim.get(abi.E_SAMPLING_COUNT)
+
+    def obstacle_routes(self):
+        """(N, L, 2) obstacle-ship route (north, east) incl. sampled intermediate waypoints."""
+        n = self.sim.get(abi.E_ROUTE_NORTH).view(self.n_envs, 2, abi.MAX_ROUTE)[:, 1]
+        e = self.sim.get(abi.E_ROUTE_EAST).view(self.n_envs, 2, abi.MAX_ROUTE)[:, 1]
+        L = self.sim.get(abi.E_ROUTE_LEN).view(self.n_envs, 2)[:, 1]
+        return torch.stack([n, e], -1), L
+
+    def seed(self, seed=None):
+        self.np_random = np.random.default_rng(seed)
+
+    def close(self):
+        self.sim.close()
+
+    # snapshots (logger.save_itr_params pickles the collectors' env): keep the config, not the device state
+    def __getstate__(self):
+        return dict(args=self.args, cfg=bytes(self.cfg), n_envs=self.n_envs, device=str(self.device))
+
+    def __setstate__(self, st):
+        cfg = abi.Config.from_buffer_copy(st["cfg"])
+        self.__init__(st["args"], st["n_envs"], device=st["device"], cfg=cfg)
+
+
+class MultiShipRLEnv:
+    """Single-env object API of rl_env/ship_in_transit/env.py:MultiShipRLEnv over the device env."""
+
+    def __init__(self, args=None, device=None, machinery="detailed", cfg=None, assets=None, map=None):
+        self.args = args if args is not None else default_args()
+        self._b = BatchedMultiShipRLEnv(self.args, 1, device=device, machinery=machinery, cfg=cfg)
+        self.collav = self._b.collav
+        self.observation_space = self._b.observation_space
+        self.action_space = self._b.action_space
+        self.initial_states = self._b.initial_states
+        self.states = self.initial_states
+        self.next_observations = self.initial_states
+        self.accumulated_rewards_list = []
+        self.env_info = {"events": "", "terminal": False, "test_ship_stop": False, "obs_ship_stop": False}
+        self._dev = self._b.device
+
+    do_normalize_action = BatchedMultiShipRLEnv.do_normalize_action
+    do_denormalize_action = BatchedMultiShipRLEnv.do_denormalize_action
+
+    @property
+    def sampling_count(self):
+        return int(self._b.sampling_count[0].item())
+
+    @property
+    def waypoint_samples(self):
+        routes, L = self._b.obstacle_routes()
+        L = int(L[0])
+        r = routes[0, 1:L - 1].cpu().numpy()
+        return [[float(n), float(e)] for n, e in r]
+
+    def reset(self, action=None):
+        obs = self._b.reset()
+        self.accumulated_rewards_list = []
+        self.env_info = {"events": "", "terminal": False, "test_ship_stop": False, "obs_ship_stop": False}
+        return obs[0].cpu().numpy()
+
+    def step(self, action):
+        a = np.asarray(action, dtype=np.float32).reshape(-1)[:1]
+        obs, r, done, info = self._b.step(torch.from_numpy(a))
+        bits = int(info["events"][0].item())
+        env_info = {"events": abi.events_to_string(bits), "terminal": bool(bits & abi.EV_TERMINAL),
+                    "test_ship_stop": bool(bits & abi.EV_TEST_STOP), "obs_ship_stop": bool(bits & abi.EV_OBS_STOP)}
+        reward = float(r[0].item())
+        self.accumulated_rewards_list.append(reward)
+        self.next_observations = obs[0].cpu().numpy()
+        self.env_info = env_info
+        return self.next_observations, reward, bool(done[0].item()), env_info
+
+    def seed(self, seed=None):
+        self.np_random = np.random.default_rng(seed)
+
+    def close(self):
+        self._b.close()
+
+    def __getstate__(self):
+        return dict(args=self.args, cfg=bytes(self._b.cfg), device=str(self._dev))
+
+    def __setstate__(self, st):
+        self.__init__(st["args"], device=st["device"], cfg=abi.Config.from_buffer_copy(st["cfg"]))

@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round1_pmc_traffic.json"))
+    p.add_argument("--sac-steps", type=int, default=300, help="timed SAC grad steps (0 = skip the SAC line)")
+    p.add_argument("--sac-batch", type=int, default=256, help="SAC batch per GPU")
     return p.parse_args()
 
 
@@ -65,6 +67,72 @@ def cpu_baseline(cfg, seconds, n_threads):
     return dict(value=total / dt, unit="env-ticks/s", cores=n_threads, kind="port",
                 sample=f"{n} two-ship AST envs x 1 episode (<=9 decisions, auto from PCG64 table), "
                        f"{int(total)} env-ticks in {dt:.1f} s, oracle/shipsim_oracle.c -O2 OpenMP")
+
+
+def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
+    """SAC grad-steps/s (secondary metric): FusedSACTrainer HIP-graph step (runner networks: 2x256
+    hidden, batch `batch` per GPU, on-device uniform sampling from a 300k-row DeviceReplayBuffer,
+    RCCL gradient all-reduce when world > 1), beside the reference-order eager SACTrainer."""
+    import torch
+    import torch.distributed as dist
+    from ast_sac_amd.ast_sac.torch.networks.mlp import ConcatMlp
+    from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac_amd.ast_sac.torch.sac.sac import SACTrainer
+    from ast_sac_amd.ast_sac.torch.sac.sac_fused import FusedSACTrainer
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+
+    class _Env:
+        class action_space:
+            shape = (1,)
+
+    def nets():
+        torch.manual_seed(0)
+        q = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[256, 256]).to(dev) for _ in range(4)]
+        return TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[256, 256]).to(dev), q
+
+    hp = dict(discount=0.965, soft_target_tau=1e-3, policy_lr=8e-5, qf_lr=8e-5, reward_scale=0.75,
+              action_reg_coeff=0.01, clip_val=100.0)
+    rb = DeviceReplayBuffer(300000, 8, 1, dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    n = 65536
+    rb.add_batch(torch.randn(n, 8, device=dev, generator=g) * 1000, torch.rand(n, 1, device=dev, generator=g) * 2 - 1,
+                 torch.randn(n, 1, device=dev, generator=g), torch.randn(n, 8, device=dev, generator=g) * 1000,
+                 (torch.rand(n, 1, device=dev, generator=g) < 0.1).float())
+
+    def timed(fn, k):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        fn(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt)
+
+    pol, q = nets()
+    tr = FusedSACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3],
+                         batch_size=batch, process_group=pg, **hp)
+    tr.broadcast_parameters(0)
+    tr.train_from_buffer(rb, 10)  # captures the graph
+    dt = timed(lambda k: tr.train_from_buffer(rb, k), steps)
+    res = {"grad_steps_per_s": steps / dt, "ms_per_grad_step": dt / steps * 1e3, "batch_per_gpu": batch,
+           "global_batch": batch * world, "hidden": [256, 256], "dtype": "f32",
+           "impl": "FusedSACTrainer (HIP graph: sample+fwd+grads+fused Adam+soft update"
+                   + (", RCCL all-reduce between graph halves)" if world > 1 else ")")}
+    if world == 1 and eager_steps:
+        pol, q = nets()
+        ref = SACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3], **hp)
+
+        def eager(k):
+            for _ in range(k):
+                ref.train_from_torch(rb.random_batch(batch))
+        eager(3)
+        res["reference_order_eager_grad_steps_per_s"] = eager_steps / timed(eager, eager_steps)
+    return res
 
 
 def main():
@@ -170,6 +238,10 @@ def main():
                 traffic = pmc.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
+    sac = None
+    if args.sac_steps > 0:
+        sac = bench_sac(dev, world, dist.group.WORLD if world > 1 else None, args.sac_steps, args.sac_batch)
+    if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
             nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -200,6 +272,7 @@ def main():
                          "kernel": f"ast_step_kernel (avg {kmean:.3f} ms/launch, "
                                    f"{ticks_per_launch:.0f} env-ticks x {ALGO_BYTES_PER_ENV_TICK} B)"},
             "cpu_baseline": cpu,
+            "sac": sac,
         }
         print(json.dumps(line))
     if world > 1:
