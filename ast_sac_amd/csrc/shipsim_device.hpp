@@ -93,8 +93,8 @@ struct Ship {
 __device__ __forceinline__ double sel(bool c, double a, double b) { return c ? a : b; }
 
 // Python min/max semantics: min(a, b) returns a unless b < a
-__device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
-__device__ __forceinline__ double py_max(double a, double b) { return (b > a) ? b : a; }
+__host__ __device__ __forceinline__ double py_min(double a, double b) { return (b < a) ? b : a; }
+__host__ __device__ __forceinline__ double py_max(double a, double b) { return (b > a) ? b : a; }
 __device__ __forceinline__ double sat(double v, double lo, double hi) { return py_max(lo, py_min(v, hi)); }
 
 // np.remainder / Python float % (floored)
@@ -295,7 +295,7 @@ __device__ __forceinline__ double heading_ctrl(const ShipConst& c, Ship& s, doub
 // map queries (obstacle.py:126-141 over shapely/GEOS; restated GEOS semantics)
 // ---------------------------------------------------------------------------------------------
 // GEOS RayCrossingCounter for one polygon, boundary -> not contained
-__device__ __forceinline__ bool poly_contains(const Edge* __restrict__ edges, int first, int count, double px,
+__host__ __device__ __forceinline__ bool poly_contains(const Edge* __restrict__ edges, int first, int count, double px,
                                               double py) {
   int crossings = 0;
   bool boundary = false;
@@ -321,7 +321,7 @@ __device__ __forceinline__ bool poly_contains(const Edge* __restrict__ edges, in
 }
 
 // if_pos_inside_obstacles :126-129 (bbox rejection is exact for the crossing rule)
-__device__ __forceinline__ bool map_inside(const Edge* __restrict__ edges, const PolyBox* __restrict__ boxes,
+__host__ __device__ __forceinline__ bool map_inside(const Edge* __restrict__ edges, const PolyBox* __restrict__ boxes,
                                            int n_polys, double n, double e) {
   bool inside = false;
   for (int p = 0; p < n_polys; ++p) {

@@ -68,8 +68,13 @@ enum { SF_N = 0, SF_E, SF_YAW, SF_U, SF_V, SF_R, SF_OMEGA, SF_TIME, SF_ECT, SF_E
 
 struct ConstBuf {
   // edges [SHIPSIM_MAX_VERTS] | boxes [SHIPSIM_MAX_POLYS] | config routes n/e [2][kMaxRoute] each
+  // | map grid: cell edge masks [gny][gnx] uint64 | cell containment flags [gny][gnx] uint8
   const char* base;
   int32_t n_edges;
+  int32_t gnx, gny;            // grid cells (0 = no grid: every query runs over the full map)
+  double gx0, gy0, ginv;       // grid origin (east, north) and 1 / cell size
+  const uint64_t* grid_mask;   // edges whose distance to the (slightly enlarged) cell is <= kGroundReach
+  const uint8_t* grid_flag;    // GRID_OUT: cell entirely outside every polygon, GRID_IN: inside one, GRID_MIXED
   __host__ __device__ const Edge* edges() const { return (const Edge*)base; }
   __host__ __device__ const PolyBox* boxes() const { return (const PolyBox*)(base + sizeof(Edge) * SHIPSIM_MAX_VERTS); }
   __host__ __device__ const double* cfg_route_n() const {
@@ -78,7 +83,21 @@ struct ConstBuf {
   __host__ __device__ const double* cfg_route_e() const { return cfg_route_n() + 2 * kMaxRoute; }
   static constexpr size_t kBytes = sizeof(Edge) * SHIPSIM_MAX_VERTS + sizeof(PolyBox) * SHIPSIM_MAX_POLYS +
                                    sizeof(double) * 4 * kMaxRoute;
+  // grid cell of (north, east), or -1 outside the grid / no grid / non-finite position
+  __device__ __forceinline__ int cell(double n, double e) const {
+    const double fx = floor((e - gx0) * ginv), fy = floor((n - gy0) * ginv);
+    if (!(fx >= 0.0 && fx < (double)gnx && fy >= 0.0 && fy < (double)gny)) return -1;
+    return (int)fy * gnx + (int)fx;
+  }
 };
+#define GRID_OUT 0
+#define GRID_IN 1
+#define GRID_MIXED 2
+// The ground-distance reward terms only use the coastline distance when it is <= 1000 m
+// (reward_function.py:109-117: test_ship_grounding_reward / obs_ship_grounding_reward clip at 1 km),
+// so a cell only needs the edges that can come within 1000 m of it: the min over that subset equals
+// the min over all edges whenever the true min is <= 1000 m, and is > 1000 m (or +inf) otherwise.
+constexpr double kGroundReach = 1000.0;
 
 __device__ __forceinline__ void load_ship(const DevState& S, int q, Ship& s) {
   s.n = S.f(SF_N)[q]; s.e = S.f(SF_E)[q]; s.yaw = S.f(SF_YAW)[q];
@@ -392,8 +411,41 @@ __device__ __forceinline__ double map_dist2_part(const EdgeX* __restrict__ E, in
   return best;
 }
 
-__device__ __forceinline__ bool corner_inside(const Edge* __restrict__ edges, const PolyBox* __restrict__ boxes,
-                                              int n_polys, double n, double e) {
+// same value as map_dist2_part over every edge when the true distance is <= kGroundReach (see above)
+__device__ __forceinline__ double map_dist2_grid(const ConstBuf& K, const EdgeX* __restrict__ E, double n, double e,
+                                                 int sub, int nsub) {
+  const int c = K.cell(n, e);
+  if (c < 0) return map_dist2_part(E, K.n_edges, n, e, sub, nsub);
+  uint64_t m = K.grid_mask[c];
+  // this sub-lane takes every nsub-th set bit, starting at the sub-th
+  for (int k = 0; k < sub && m; ++k) m &= m - 1;
+  const double px = e, py = n;
+  double best = INFINITY;
+  while (m) {
+    const int i = __builtin_ctzll(m);
+    for (int k = 0; k < nsub && m; ++k) m &= m - 1;
+    const EdgeX ed = E[i];
+    const double qx = px - ed.ax, qy = py - ed.ay;
+    const double t = qx * ed.dx + qy * ed.dy;
+    const double da = qx * qx + qy * qy;
+    const double rx = px - ed.bx, ry = py - ed.by;
+    const double db = rx * rx + ry * ry;
+    const double cc = (ed.ay - py) * ed.dx - (ed.ax - px) * ed.dy;
+    const double dp = cc * cc * ed.inv_len2;
+    const double d2 = (t <= 0.0) ? da : ((t >= ed.len2) ? db : dp);
+    best = py_min(best, d2);
+  }
+  return best;
+}
+
+// if_pos_inside_obstacles with the grid's exact cell classification (full test on mixed cells)
+__device__ __forceinline__ bool corner_inside(const ConstBuf& K, const Edge* __restrict__ edges,
+                                              const PolyBox* __restrict__ boxes, int n_polys, double n, double e) {
+  const int c = K.cell(n, e);
+  if (c >= 0) {
+    const int f = K.grid_flag[c];
+    if (f != GRID_MIXED) return f == GRID_IN;
+  }
   return map_inside(edges, boxes, n_polys, n, e);
 }
 
@@ -508,7 +560,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       travel_dist = 0;
       travel_time = 0;
       have_iw = true;
-      bool fail = map_inside(lds_edges_raw, lds_boxes, P.n_polys, iw_n, iw_e) ||
+      bool fail = corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, iw_n, iw_e) ||
                   ((iw_n < P.min_north || iw_n > P.max_north) || (iw_e < P.min_east || iw_e > P.max_east));
       if (fail) {  // env.py:673-693 with obs_ship_IW_sampling_failure_reward (multiplier 2)
         out_r = (acc >= 0) ? -acc * 2.0 : acc * 2.0;
@@ -586,14 +638,14 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     bool gr = false;
     if (going) {
 #ifndef SHIPSIM_ABL_NO_MAPDIST
-      d2 = map_dist2_part(lds_edges, K.n_edges, s.n, s.e, sub, NSUB);
+      d2 = map_dist2_grid(K, lds_edges, s.n, s.e, sub, NSUB);
 #endif
       const double margin = c.l_ship / 2;  // check_condition.py:50-78 hull hard points
 #ifndef SHIPSIM_ABL_NO_GROUND
       for (int k = sub; k < 4; k += NSUB) {
         const double cn = (k < 2) ? s.n - margin : s.n + margin;
         const double ce = (k & 1) ? s.e + margin : s.e - margin;
-        if (corner_inside(lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) gr = true;
+        if (corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) gr = true;
       }
 #endif
     }
@@ -771,6 +823,75 @@ struct shipsim_handle {
   int ever_reset;
   char err[512];
 };
+
+// ---------------------------------------------------------------------------------------------
+// map grid (host): exact, conservative cell classification used by corner_inside / map_dist2_grid
+// ---------------------------------------------------------------------------------------------
+static const double kGridCell = 200.0;     // m
+static const double kGridPad = 2000.0;     // m of grid beyond the polygon bounding box
+static const double kGridEps = 1e-3;       // m: cells are enlarged by this before classification
+
+// segment vs closed axis-aligned rectangle (Liang-Barsky clip)
+static bool seg_hits_rect(const Edge& ed, double x0, double y0, double x1, double y1) {
+  double t0 = 0.0, t1 = 1.0;
+  const double dx = ed.bx - ed.ax, dy = ed.by - ed.ay;
+  const double p[4] = {-dx, dx, -dy, dy};
+  const double q[4] = {ed.ax - x0, x1 - ed.ax, ed.ay - y0, y1 - ed.ay};
+  for (int i = 0; i < 4; ++i) {
+    if (p[i] == 0.0) {
+      if (q[i] < 0.0) return false;
+    } else {
+      const double t = q[i] / p[i];
+      if (p[i] < 0.0) { if (t > t1) return false; if (t > t0) t0 = t; }
+      else { if (t < t0) return false; if (t < t1) t1 = t; }
+    }
+  }
+  return true;
+}
+static double point_seg_dist(double px, double py, const Edge& ed) {
+  const double dx = ed.bx - ed.ax, dy = ed.by - ed.ay, l2 = dx * dx + dy * dy;
+  double t = l2 > 0 ? ((px - ed.ax) * dx + (py - ed.ay) * dy) / l2 : 0.0;
+  t = t < 0 ? 0 : (t > 1 ? 1 : t);
+  const double ex = ed.ax + t * dx - px, ey = ed.ay + t * dy - py;
+  return sqrt(ex * ex + ey * ey);
+}
+static double point_rect_dist(double px, double py, double x0, double y0, double x1, double y1) {
+  const double dx = px < x0 ? x0 - px : (px > x1 ? px - x1 : 0.0);
+  const double dy = py < y0 ? y0 - py : (py > y1 ? py - y1 : 0.0);
+  return sqrt(dx * dx + dy * dy);
+}
+static double seg_rect_dist(const Edge& ed, double x0, double y0, double x1, double y1) {
+  if (seg_hits_rect(ed, x0, y0, x1, y1)) return 0.0;
+  double d = point_rect_dist(ed.ax, ed.ay, x0, y0, x1, y1);
+  d = py_min(d, point_rect_dist(ed.bx, ed.by, x0, y0, x1, y1));
+  d = py_min(d, point_seg_dist(x0, y0, ed));
+  d = py_min(d, point_seg_dist(x1, y0, ed));
+  d = py_min(d, point_seg_dist(x0, y1, ed));
+  d = py_min(d, point_seg_dist(x1, y1, ed));
+  return d;
+}
+// Fills mask/flag for a gnx x gny grid. A cell no edge touches is uniformly inside or outside
+// (the polygons' boundary is the union of their edges), so its center decides it; any cell an
+// edge touches is MIXED and gets the full test. Edge masks keep every edge within kGroundReach of
+// the enlarged cell (+1 mm slack on the reach for rounding).
+static void build_grid(const Edge* E, int n_edges, const PolyBox* B, int n_polys, double gx0, double gy0, int gnx,
+                       int gny, uint64_t* mask, uint8_t* flag) {
+  for (int j = 0; j < gny; ++j)
+    for (int i = 0; i < gnx; ++i) {
+      const double x0 = gx0 + i * kGridCell - kGridEps, x1 = gx0 + (i + 1) * kGridCell + kGridEps;
+      const double y0 = gy0 + j * kGridCell - kGridEps, y1 = gy0 + (j + 1) * kGridCell + kGridEps;
+      uint64_t m = 0;
+      bool touched = false;
+      for (int k = 0; k < n_edges; ++k) {
+        const double d = seg_rect_dist(E[k], x0, y0, x1, y1);
+        if (d <= kGroundReach + kGridEps) m |= (uint64_t)1 << k;
+        if (d == 0.0) touched = true;
+      }
+      mask[(size_t)j * gnx + i] = m;
+      const double cx = 0.5 * (x0 + x1), cy = 0.5 * (y0 + y1);
+      flag[(size_t)j * gnx + i] = touched ? GRID_MIXED : (map_inside(E, B, n_polys, cy, cx) ? GRID_IN : GRID_OUT);
+    }
+}
 
 static int fail(shipsim_handle* h, int code, const char* fmt, ...) {
   if (h) {
@@ -1158,8 +1279,14 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
   }
   P.min_east = mn_e; P.max_east = mx_e; P.min_north = mn_n; P.max_north = mx_n;
 
-  // constant block: edges | boxes | config routes (ConstBuf layout)
-  size_t cbytes = ConstBuf::kBytes;
+  // constant block: edges | boxes | config routes | grid (ConstBuf layout)
+  const char* no_grid = getenv("SHIPSIM_NO_GRID");
+  const bool use_grid = nv <= 64 && nv > 0 && !(no_grid && no_grid[0] == '1');
+  const int gnx = use_grid ? (int)ceil((mx_e - mn_e + 2 * kGridPad) / kGridCell) : 0;
+  const int gny = use_grid ? (int)ceil((mx_n - mn_n + 2 * kGridPad) / kGridCell) : 0;
+  const size_t gcells = (size_t)gnx * gny;
+  const size_t grid_off = (ConstBuf::kBytes + 255) & ~(size_t)255;
+  size_t cbytes = grid_off + gcells * (sizeof(uint64_t) + 1);
   char* hostc = (char*)calloc(1, cbytes);
   Edge* E = (Edge*)hostc;
   PolyBox* B = (PolyBox*)(hostc + sizeof(Edge) * SHIPSIM_MAX_VERTS);
@@ -1187,6 +1314,9 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
       R[s * kMaxRoute + i] = cfg->ship[s].route_north[i];
       R[2 * kMaxRoute + s * kMaxRoute + i] = cfg->ship[s].route_east[i];
     }
+  if (use_grid)
+    build_grid(E, nv, B, cfg->n_polys, mn_e - kGridPad, mn_n - kGridPad, gnx, gny, (uint64_t*)(hostc + grid_off),
+               (uint8_t*)(hostc + grid_off + gcells * sizeof(uint64_t)));
   hipError_t e = hipMalloc(&h->const_block, cbytes);
   if (e != hipSuccess) {
     free(hostc);
@@ -1202,6 +1332,14 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
   }
   h->K.base = (const char*)h->const_block;
   h->K.n_edges = nv;
+  h->K.gnx = gnx;
+  h->K.gny = gny;
+  h->K.gx0 = mn_e - kGridPad;
+  h->K.gy0 = mn_n - kGridPad;
+  h->K.ginv = 1.0 / kGridCell;
+  h->K.grid_mask = use_grid ? (const uint64_t*)((const char*)h->const_block + grid_off) : nullptr;
+  h->K.grid_flag = use_grid ? (const uint8_t*)((const char*)h->const_block + grid_off + gcells * sizeof(uint64_t))
+                            : nullptr;
 
   // state block (DevState layout: ship arrays | routes | env arrays)
   const size_t S = (size_t)n_envs * ns, N = (size_t)n_envs;

@@ -67,6 +67,19 @@ def test_batched_collector_matches_single_env_rollout():
     from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
     from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
     from ast_sac_amd.ast_sac.torch.sac.policies.base import MakeDeterministic
+    from ast_sac_amd.ast_sac.torch.utils import pytorch_util as ptu
+    ptu.set_gpu_mode(True)  # as run/ast-sac_runner.py does: numpy observations go to the HIP device
+    try:
+        _collector_vs_single(BatchedMultiShipRLEnv, MultiShipRLEnv, default_args, NormalizedBoxEnv,
+                             BatchedNormalizedBoxEnv, ast_sac_rollout, BatchedPathCollector, DeviceReplayBuffer,
+                             TanhGaussianPolicy, MakeDeterministic)
+    finally:
+        ptu.set_gpu_mode(False)
+
+
+def _collector_vs_single(BatchedMultiShipRLEnv, MultiShipRLEnv, default_args, NormalizedBoxEnv,
+                         BatchedNormalizedBoxEnv, ast_sac_rollout, BatchedPathCollector, DeviceReplayBuffer,
+                         TanhGaussianPolicy, MakeDeterministic):
     torch.manual_seed(3)
     pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[64, 64], init_w=0.5).cuda()
     det = MakeDeterministic(pol)
