@@ -47,7 +47,8 @@ class FusedSACTrainer(TorchTrainer):
     def __init__(self, env, policy, qf1, qf2, target_qf1, target_qf2, discount=0.99, reward_scale=1.0,
                  policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None, soft_target_tau=1e-2, target_update_period=1,
                  plotter=None, render_eval_paths=False, use_automatic_entropy_tuning=True, target_entropy=None,
-                 action_reg_coeff=None, clip_val=np.inf, batch_size=256, use_graph=None, process_group=None):
+                 action_reg_coeff=None, clip_val=np.inf, batch_size=256, use_graph=None, process_group=None,
+                 backend=None):
         super().__init__()
         if target_update_period != 1:
             raise NotImplementedError("FusedSACTrainer soft-updates every step (runner: target_update_period=1)")
@@ -95,9 +96,126 @@ class FusedSACTrainer(TorchTrainer):
         self.noise_fn = None  # callable(shape) -> ε for [obs; next_obs] rows; None = torch.randn
         self._static = None
         self._graphs = None
+        # backend "hip": the fused kernels of libsacfused.so (csrc/sac_kernels.hip); "torch": the
+        # PyTorch-op formulation above. Default: hip on a HIP device when the networks fit it.
+        if backend is None:
+            backend = "hip" if dev.type == "cuda" and self._hip_shapes_ok() else "torch"
+        if backend not in ("hip", "torch"):
+            raise ValueError(f"backend must be 'hip' or 'torch', got {backend!r}")
+        self.backend = backend
+        if backend == "hip":
+            if not self._hip_shapes_ok():
+                raise ValueError("hip backend: needs 2 equal hidden layers (<= 256, multiple of 32), act_dim 1, "
+                                 "obs_dim <= 15 and batch_size % 4 == 0")
+            self._init_hip(policy_lr, qf_lr)
         self._n_train_steps_total = 0
         self._need_to_update_eval_statistics = True
         self.eval_statistics = OrderedDict()
+
+    # ---------------------------------------------------------------- hip backend
+    def _hip_shapes_ok(self):
+        pol, nets = self.policy, (self.qf1, self.qf2, self.target_qf1, self.target_qf2)
+        try:
+            H = pol.fcs[0].weight.shape[0]
+            obs = pol.fcs[0].weight.shape[1]
+            ok = (len(pol.fcs) == 2 and pol.fcs[1].weight.shape == (H, H) and pol.last_fc.weight.shape == (1, H)
+                  and getattr(pol, "last_fc_log_std", None) is not None and H % 32 == 0 and H <= 256
+                  and obs <= 15 and self.batch_size % 4 == 0)
+            for n in nets:
+                ok = ok and len(n.fcs) == 2 and n.fcs[0].weight.shape == (H, obs + 1) \
+                    and n.fcs[1].weight.shape == (H, H) and n.last_fc.weight.shape == (1, H)
+            return bool(ok)
+        except (AttributeError, IndexError):
+            return False
+
+    def _init_hip(self, policy_lr, qf_lr):
+        from ....sacfused import SacFused
+        dev = self.device
+        H = self.policy.fcs[0].weight.shape[0]
+        obs_dim = self.policy.fcs[0].weight.shape[1]
+        pol_params = list(self.policy.parameters())
+        with torch.no_grad():
+            flat = torch.cat([self.log_alpha.detach().reshape(-1)] +
+                             [p.detach().reshape(-1) for p in pol_params + self.q_params]).contiguous()
+            tflat = torch.cat([p.detach().reshape(-1) for p in self.t_params]).contiguous()
+        # the modules' parameters become views of the flat buffers the kernels update in place
+        off = 1
+        for p in pol_params + self.q_params:
+            p.data = flat[off:off + p.numel()].view_as(p)
+            p.grad = None
+            off += p.numel()
+        off = 0
+        for p in self.t_params:
+            p.data = tflat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.log_alpha = flat[0:1]
+        if self.use_automatic_entropy_tuning:
+            self.pi_params = [self.log_alpha] + pol_params
+        self.flat_param, self.flat_target = flat, tflat
+        self.flat_grad = torch.zeros_like(flat)
+        self._adam_m = torch.zeros_like(flat)
+        self._adam_v = torch.zeros_like(flat)
+        self._step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.optimizer = None
+        self._sf = SacFused(obs_dim, H, self.batch_size, dev, self.discount, self.reward_scale, self.soft_target_tau,
+                            self.action_reg_coeff, self.clip_val, float(self.target_entropy), policy_lr, qf_lr,
+                            auto_entropy=self.use_automatic_entropy_tuning, world_size=self.world)
+        if self._sf.n_params != flat.numel() or self._sf.n_targets != tflat.numel():
+            raise RuntimeError("hip backend: flat layout mismatch")
+        self._stats_t = torch.zeros(self._sf.n_stats, device=dev)
+        self._sf.bind(flat, tflat, self.flat_grad, self._adam_m, self._adam_v, self._step_t, self._stats_t)
+        self._seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self._eps_static = None
+        self._replay_key = None
+
+    def _hip_launch(self, replay_buffer, part):
+        sf = self._sf
+        if part in ("a", "ab"):
+            batch = None if replay_buffer is not None else self._static
+            sf.grads(batch, self._eps_static if self.noise_fn is not None else None)
+        if part == "ab":
+            sf.apply()
+        elif part == "b":
+            sf.apply()
+
+    def _hip_step(self, replay_buffer):
+        sf = self._sf
+        if replay_buffer is not None and self._replay_key != id(replay_buffer):
+            st = replay_buffer._store
+            sf.set_replay(st["observations"], st["actions"], st["rewards"], st["terminals"],
+                          st["next_observations"], replay_buffer._size_t, replay_buffer._max, self._seed)
+            self._replay_key = id(replay_buffer)
+            self._graphs = None
+        if self.noise_fn is not None:
+            eps = self.noise_fn((2 * self.batch_size, 1)).reshape(-1)
+            if self._eps_static is None:
+                self._eps_static = torch.empty(2 * self.batch_size, device=self.device)
+                self._graphs = None
+            self._eps_static.copy_(eps)
+        key = (id(replay_buffer) if replay_buffer is not None else None, self.noise_fn is not None)
+        if not self.use_graph:
+            sf.set_stream()
+            self._hip_launch(replay_buffer, "a")
+            self._allreduce()
+            self._hip_launch(replay_buffer, "b")
+            return
+        if self._graphs is None or self._graphs[0] != key:
+            torch.cuda.synchronize(self.device)
+            parts = ("ab",) if self.world == 1 else ("a", "b")
+            graphs = []
+            for part in parts:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    sf.set_stream()
+                    self._hip_launch(replay_buffer, part)
+                graphs.append(g)
+            sf.set_stream()
+            self._graphs = (key, graphs)
+        graphs = self._graphs[1]
+        graphs[0].replay()
+        if len(graphs) > 1:
+            self._allreduce()
+            graphs[1].replay()
 
     # ---------------------------------------------------------------- math
     def _actor(self, x):
@@ -238,6 +356,10 @@ class FusedSACTrainer(TorchTrainer):
         return ga, gb
 
     def _run_step(self, replay_buffer):
+        if self.backend == "hip":
+            if replay_buffer is None and self._static is None:
+                raise RuntimeError("no batch")
+            return self._hip_step(replay_buffer)
         key = id(replay_buffer) if replay_buffer is not None else None
         if self._static is None:
             obs_dim = self.policy.input_size
@@ -282,12 +404,23 @@ class FusedSACTrainer(TorchTrainer):
             self._need_to_update_eval_statistics = False
 
     def last_losses(self):
+        if self.backend == "hip":
+            st = self._stats_t
+            return SACLosses(policy_loss=st[0], qf1_loss=st[1], qf2_loss=st[2], alpha_loss=st[3])
         o = self._out
         return SACLosses(policy_loss=o["policy_loss"], qf1_loss=o["qf1_loss"], qf2_loss=o["qf2_loss"],
                          alpha_loss=o["alpha_loss"])
 
     def _stats(self):
-        o = {k: ptu.get_numpy(v) for k, v in self._out.items()}
+        if self.backend == "hip":
+            st = ptu.get_numpy(self._stats_t)
+            B = self.batch_size
+            rows = st[8:].reshape(6, B)
+            o = dict(qf1_loss=st[1], qf2_loss=st[2], policy_loss=st[0], alpha_loss=st[3], alpha=st[4:5],
+                     q1_pred=rows[0][:, None], q2_pred=rows[1][:, None], q_target=rows[2][:, None],
+                     log_pi=rows[3][:, None], pi_mean=rows[4][:, None], pi_std=rows[5][:, None])
+        else:
+            o = {k: ptu.get_numpy(v) for k, v in self._out.items()}
         st = OrderedDict()
         st["QF1 Loss"] = float(np.mean(o["qf1_loss"]))
         st["QF2 Loss"] = float(np.mean(o["qf2_loss"]))
@@ -308,6 +441,11 @@ class FusedSACTrainer(TorchTrainer):
         """Make every rank start from rank `src`'s networks."""
         if self.world > 1:
             with torch.no_grad():
+                if self.backend == "hip":
+                    torch.distributed.broadcast(self.flat_param, src, group=self.pg)
+                    torch.distributed.broadcast(self.flat_target, src, group=self.pg)
+                    self._sf.sync_params()
+                    return
                 for p in self.pi_params + self.q_params + self.t_params:
                     torch.distributed.broadcast(p.data, src, group=self.pg)
 
@@ -325,7 +463,7 @@ class FusedSACTrainer(TorchTrainer):
 
     @property
     def optimizers(self):
-        return [self.optimizer]
+        return [self.optimizer] if self.optimizer is not None else []
 
     def get_snapshot(self):
         return dict(policy=self.policy, qf1=self.qf1, qf2=self.qf2, target_qf1=self.target_qf1,

@@ -1,0 +1,986 @@
+// sac_kernels.hip — fused SAC update for gfx950 (C ABI: include/sac_fused.h) -> libsacfused.so
+//
+// One grad step of ast_sac/torch/sac/sac.py (compute_loss :156-270, train_from_torch :102-154,
+// update_target_networks :160-166) for TanhGaussianPolicy + twin ConcatMlp critics with two hidden
+// layers of width H and act_dim 1, in three kernels:
+//
+//   sac_rows_kernel  : R batch rows per block. Gathers the batch (or samples it from the replay ring
+//                      with Philox), runs actor(obs), actor(next_obs), Q1/Q2 on (obs, ã) and (obs, a),
+//                      target Q1/Q2 on (next_obs, ã'), the per-row losses, and the whole per-row
+//                      backward (critic input/activation grads, actor activation grads). Everything
+//                      in one SAC update is row-local except the batch means, whose 1/B factors are
+//                      constants, so no grid-wide step is needed until the weight gradients.
+//   sac_wgrad_kernel : every weight/bias gradient = Σ_rows dY[r]ᵀ X[r] (64×64 tiles, 4×4 per thread,
+//                      LDS-staged row chunks) + the loss scalars and d(log α); writes one flat fp32
+//                      gradient in torch parameter order.
+//   sac_apply_kernel : torch.optim.Adam on every element (two lr groups), soft target update
+//                      θ' ← θ'(1−τ) + θτ, and the transposed H×H copies the rows kernel reads.
+//
+// Only the four gradients the reference keeps are formed: the π-loss gradient w.r.t. the critics
+// (which sac.py:123-133 discards with qf*_optimizer.zero_grad()) is never computed; α is treated as a
+// constant inside the π- and Q-losses exactly as after alpha_optimizer.step() in the reference
+// (its grad there is also discarded).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include "sac_fused.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int R = 4;           // batch rows per block in the rows kernel
+constexpr int kXLd = 16;       // leading dim of the per-row input scratch (obs | act)
+constexpr float kLog2 = 0.69314718055994530942f;
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+
+struct Layout {
+  int O, H, B;
+  int64_t p_w1, p_b1, p_w2, p_b2, p_wm, p_bm, p_ws, p_bs;  // policy (params)
+  int64_t q_base[2];                                      // start of qf1 / qf2 in params
+  int64_t q_size;                                         // floats of one critic
+  // offsets inside one critic block
+  int64_t c_w1, c_b1, c_w2, c_b2, c_w3, c_b3;
+  int64_t n_params, n_targets;
+};
+
+struct Scratch {
+  float *a_x, *a_h1, *a_h2, *a_dh1, *a_dh2, *a_dhead;  // actor, obs rows [B][..]
+  float *q_x[2], *q_g1[2], *q_g2[2], *q_dg1[2], *q_dg2[2], *q_dq[2];  // critics, (obs, a) rows
+  float *p_pl, *p_q1l, *p_q2l, *p_la, *p_ga;  // per-row loss partials
+};
+
+struct Hyper {
+  float gamma, rscale, tau, areg, clip, tent, lr_pi, lr_q, beta1, beta2, eps;
+  int auto_ent;
+  float inv_world;
+};
+
+struct RowsArgs {
+  const float* params;
+  const float* targets;
+  const float* T;  // transposed copies: [actor W2ᵀ | q1 W2ᵀ | q2 W2ᵀ | t1 W2ᵀ | t2 W2ᵀ], each H×H
+  const float *obs, *act, *rew, *term, *nobs;
+  const int64_t* size_dev;
+  int64_t capacity;
+  uint64_t seed;
+  int sampled;
+  const float* eps;
+  const int64_t* step;
+  float* stats;
+  Scratch sc;
+  Layout L;
+  Hyper hp;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 (counter-based; one 4-word draw per batch row and step)
+// ---------------------------------------------------------------------------------------------
+__device__ inline void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// block-wide sum of n (<= 32) per-thread partials; result in out[0..n) (LDS), visible after return
+template <int N>
+__device__ inline void block_sum(float (&v)[N], float (*red)[32], float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    float x = v[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    if (lane == 0) red[wave][i] = x;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < N) out[threadIdx.x] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                                (red[2][threadIdx.x] + red[3][threadIdx.x]);
+  __syncthreads();
+}
+
+__device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.0f); }
+__device__ __forceinline__ float softplus(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+
+// acc[i] += Σ_k WT[k*H + j] * in[i][k]  (WT: input-major copy; in: LDS rows of length ld)
+template <int NR>
+__device__ __forceinline__ void matvec_t(const float* __restrict__ WT, int H, int nin, const float* in, int ld,
+                                         int j, float (&acc)[NR]) {
+  int k = 0;
+  for (; k + 4 <= nin; k += 4) {
+    const float w0 = WT[(size_t)(k + 0) * H + j], w1 = WT[(size_t)(k + 1) * H + j];
+    const float w2 = WT[(size_t)(k + 2) * H + j], w3 = WT[(size_t)(k + 3) * H + j];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const float4 x = *reinterpret_cast<const float4*>(in + i * ld + k);
+      acc[i] = fmaf(w0, x.x, acc[i]);
+      acc[i] = fmaf(w1, x.y, acc[i]);
+      acc[i] = fmaf(w2, x.z, acc[i]);
+      acc[i] = fmaf(w3, x.w, acc[i]);
+    }
+  }
+  for (; k < nin; ++k) {
+    const float w = WT[(size_t)k * H + j];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) acc[i] = fmaf(w, in[i * ld + k], acc[i]);
+  }
+}
+
+// per-row scalar slots in LDS
+enum { S_MEAN, S_LSRAW, S_STD, S_Z, S_A, S_LOGP, S_Q1, S_Q2, S_T1, S_T2, S_DQ1, S_DQ2, S_DA, S_DMEAN, S_DLS,
+       S_NSLOT };
+
+__global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
+  const Layout& L = a.L;
+  const int H = L.H, O = L.O, B = L.B;
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * R;
+  const float* P = a.params;
+  const float* TG = a.targets;
+
+  __shared__ float s_x[2 * R][kXLd];                 // actor inputs: obs rows | next_obs rows
+  __shared__ float s_act[R], s_rew[R], s_term[R], s_eps[2 * R];
+  __shared__ __attribute__((aligned(16))) float s_h1[2 * R][SACF_MAX_HIDDEN];
+  __shared__ __attribute__((aligned(16))) float s_h2[2 * R][SACF_MAX_HIDDEN];
+  __shared__ __attribute__((aligned(16))) float s_g1[2][2 * R][SACF_MAX_HIDDEN];  // critic rows: (obs, ã) | (obs, a)
+  __shared__ __attribute__((aligned(16))) float s_g2[2][2 * R][SACF_MAX_HIDDEN];
+  __shared__ float s_red[4][32];
+  __shared__ float s_sum[32];
+  __shared__ float s_row[S_NSLOT][2 * R];
+
+  // ---- batch rows + reparameterisation noise ----
+  if (tid < R) {
+    const int r = r0 + tid;
+    int64_t idx = r;
+    uint32_t c[4] = {(uint32_t)r, (uint32_t)*a.step, (uint32_t)((uint64_t)*a.step >> 32), 0x5AC0u};
+    if (a.sampled || !a.eps) philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+    if (a.sampled) {
+      const int64_t size = *a.size_dev > 0 ? *a.size_dev : 1;
+      const double u = ((double)c[0] + 0.5) * (1.0 / 4294967296.0);
+      idx = (int64_t)(u * (double)size);
+      if (idx >= a.capacity) idx = a.capacity - 1;
+    }
+    float e0, e1;
+    if (a.eps) {
+      e0 = a.eps[r];
+      e1 = a.eps[B + r];
+    } else {  // Box-Muller on two 32-bit uniforms
+      const float u1 = ((float)c[1] + 1.0f) * 2.3283064365386963e-10f;
+      const float u2 = (float)c[2] * 2.3283064365386963e-10f;
+      const float rad = sqrtf(-2.0f * logf(u1));
+      e0 = rad * cosf(6.283185307179586f * u2);
+      e1 = rad * sinf(6.283185307179586f * u2);
+    }
+    for (int m = 0; m < O; ++m) {
+      s_x[tid][m] = a.obs[idx * O + m];
+      s_x[R + tid][m] = a.nobs[idx * O + m];
+    }
+    s_act[tid] = a.act[idx];
+    s_rew[tid] = a.rew[idx];
+    s_term[tid] = a.term[idx];
+    s_eps[tid] = e0;
+    s_eps[R + tid] = e1;
+  }
+  __syncthreads();
+
+  // ---- actor forward on 2R rows (gaussian_policy.py:105-118) ----
+  const int j = tid;
+  const bool col = j < H;
+  if (col) {
+    float acc[2 * R];
+    const float b = P[L.p_b1 + j];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) acc[i] = b;
+    for (int m = 0; m < O; ++m) {
+      const float w = P[L.p_w1 + (int64_t)j * O + m];
+#pragma unroll
+      for (int i = 0; i < 2 * R; ++i) acc[i] = fmaf(w, s_x[i][m], acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) s_h1[i][j] = relu(acc[i]);
+  }
+  __syncthreads();
+  if (col) {
+    float acc[2 * R];
+    const float b = P[L.p_b2 + j];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) acc[i] = b;
+    matvec_t<2 * R>(a.T, H, H, &s_h1[0][0], SACF_MAX_HIDDEN, j, acc);
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) s_h2[i][j] = relu(acc[i]);
+  }
+  __syncthreads();
+  {
+    float v[4 * R];
+    const float wm = col ? P[L.p_wm + j] : 0.0f, ws = col ? P[L.p_ws + j] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) {
+      const float h = col ? s_h2[i][j] : 0.0f;
+      v[i] = wm * h;
+      v[2 * R + i] = ws * h;
+    }
+    block_sum<4 * R>(v, s_red, s_sum);
+  }
+  if (tid < 2 * R) {  // TanhNormal.rsample_and_logprob (distributions.py:346-392)
+    const int i = tid;
+    const float mean = s_sum[i] + P[L.p_bm];
+    const float ls_raw = s_sum[2 * R + i] + P[L.p_bs];
+    const float log_std = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
+    const float std = expf(log_std);
+    const float z = mean + std * s_eps[i];
+    const float act = tanhf(z);
+    const float var = std * std;
+    const float d = z - mean;
+    const float lp = -(d * d) / (2.0f * var) - logf(std) - kLogSqrt2Pi;
+    const float corr = -2.0f * (kLog2 - z - softplus(-2.0f * z));
+    s_row[S_MEAN][i] = mean;
+    s_row[S_LSRAW][i] = ls_raw;
+    s_row[S_STD][i] = std;
+    s_row[S_Z][i] = z;
+    s_row[S_A][i] = act;
+    s_row[S_LOGP][i] = lp + corr;
+  }
+  __syncthreads();
+
+  // ---- critics on (obs, ã) rows 0..R-1 and (obs, a) rows R..2R-1 ----
+  for (int k = 0; k < 2; ++k) {
+    const float* C = P + L.q_base[k];
+    if (col) {
+      float acc[2 * R];
+      const float b = C[L.c_b1 + j];
+      float base[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) base[i] = b;
+      for (int m = 0; m < O; ++m) {
+        const float w = C[L.c_w1 + (int64_t)j * (O + 1) + m];
+#pragma unroll
+        for (int i = 0; i < R; ++i) base[i] = fmaf(w, s_x[i][m], base[i]);
+      }
+      const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        acc[i] = fmaf(wa, s_row[S_A][i], base[i]);
+        acc[R + i] = fmaf(wa, s_act[i], base[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2 * R; ++i) s_g1[k][i][j] = relu(acc[i]);
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < 2; ++k) {
+    if (col) {
+      const float* C = P + L.q_base[k];
+      float acc[2 * R];
+      const float b = C[L.c_b2 + j];
+#pragma unroll
+      for (int i = 0; i < 2 * R; ++i) acc[i] = b;
+      matvec_t<2 * R>(a.T + (size_t)(1 + k) * H * H, H, H, &s_g1[k][0][0], SACF_MAX_HIDDEN, j, acc);
+#pragma unroll
+      for (int i = 0; i < 2 * R; ++i) s_g2[k][i][j] = relu(acc[i]);
+    }
+  }
+  __syncthreads();
+  {
+    float v[4 * R];
+    const float w0 = col ? P[L.q_base[0] + L.c_w3 + j] : 0.0f, w1 = col ? P[L.q_base[1] + L.c_w3 + j] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) {
+      v[i] = col ? w0 * s_g2[0][i][j] : 0.0f;
+      v[2 * R + i] = col ? w1 * s_g2[1][i][j] : 0.0f;
+    }
+    block_sum<4 * R>(v, s_red, s_sum);
+  }
+  if (tid < 2 * R) {
+    s_row[S_Q1][tid] = s_sum[tid] + P[L.q_base[0] + L.c_b3];
+    s_row[S_Q2][tid] = s_sum[2 * R + tid] + P[L.q_base[1] + L.c_b3];
+  }
+  __syncthreads();
+
+  // ---- target critics on (next_obs, ã') (rows R..2R-1 of s_h1/s_h2 are free now) ----
+  for (int k = 0; k < 2; ++k) {
+    const float* C = TG + (int64_t)k * L.q_size;
+    if (col) {
+      float acc[R];
+      const float b = C[L.c_b1 + j];
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = b;
+      for (int m = 0; m < O; ++m) {
+        const float w = C[L.c_w1 + (int64_t)j * (O + 1) + m];
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] = fmaf(w, s_x[R + i][m], acc[i]);
+      }
+      const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
+#pragma unroll
+      for (int i = 0; i < R; ++i) s_h1[R + i][j] = relu(fmaf(wa, s_row[S_A][R + i], acc[i]));
+    }
+    __syncthreads();
+    if (col) {
+      float acc[R];
+      const float b = C[L.c_b2 + j];
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = b;
+      matvec_t<R>(a.T + (size_t)(3 + k) * H * H, H, H, &s_h1[R][0], SACF_MAX_HIDDEN, j, acc);
+#pragma unroll
+      for (int i = 0; i < R; ++i) s_h2[R + i][j] = relu(acc[i]);
+    }
+    __syncthreads();
+    float v[R];
+    const float w3 = col ? C[L.c_w3 + j] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < R; ++i) v[i] = col ? w3 * s_h2[R + i][j] : 0.0f;
+    block_sum<R>(v, s_red, s_sum);
+    if (tid < R) s_row[k == 0 ? S_T1 : S_T2][tid] = s_sum[tid] + C[L.c_b3];
+    __syncthreads();
+  }
+
+  // ---- losses and output gradients per row (sac.py:170-247) ----
+  const float log_alpha = P[0];
+  const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
+  const float invB = 1.0f / (float)B;
+  if (tid < R) {
+    const int i = tid, r = r0 + i;
+    const float q1a = s_row[S_Q1][i], q2a = s_row[S_Q2][i];
+    const float q1b = s_row[S_Q1][R + i], q2b = s_row[S_Q2][R + i];
+    const float tq = fminf(s_row[S_T1][i], s_row[S_T2][i]) - alpha * s_row[S_LOGP][R + i];
+    float qt = a.hp.rscale * s_rew[i] + ((1.0f - s_term[i]) * a.hp.gamma) * tq;
+    qt = fminf(fmaxf(qt, -a.hp.clip), a.hp.clip);
+    const float qmin = fminf(q1a, q2a);
+    // torch.minimum backward: the smaller input takes the gradient, ties split it in half
+    const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
+    const float w2 = 1.0f - w1;
+    s_row[S_DQ1][i] = -w1 * invB;
+    s_row[S_DQ2][i] = -w2 * invB;
+    const float dq1b = (2.0f * invB) * (q1b - qt), dq2b = (2.0f * invB) * (q2b - qt);
+    s_row[S_DQ1][R + i] = dq1b;
+    s_row[S_DQ2][R + i] = dq2b;
+    a.sc.q_dq[0][r] = dq1b;
+    a.sc.q_dq[1][r] = dq2b;
+    const float logp = s_row[S_LOGP][i], act = s_row[S_A][i];
+    a.sc.p_pl[r] = alpha * logp - qmin + (a.hp.areg != 0.0f ? a.hp.areg * (act * act) : 0.0f);
+    a.sc.p_q1l[r] = (q1b - qt) * (q1b - qt);
+    a.sc.p_q2l[r] = (q2b - qt) * (q2b - qt);
+    a.sc.p_la[r] = -(log_alpha * (logp + a.hp.tent));
+    a.sc.p_ga[r] = -(logp + a.hp.tent);
+    float* st = a.stats + 8;
+    st[r] = q1b;
+    st[B + r] = q2b;
+    st[2 * B + r] = qt;
+    st[3 * B + r] = logp;
+    st[4 * B + r] = tanhf(s_row[S_MEAN][i]);
+    st[5 * B + r] = s_row[S_STD][i];
+    for (int m = 0; m < kXLd; ++m) {
+      const float x = m < O ? s_x[i][m] : (m == O ? s_act[i] : 0.0f);
+      a.sc.q_x[0][(int64_t)r * kXLd + m] = x;
+      a.sc.q_x[1][(int64_t)r * kXLd + m] = x;
+      a.sc.a_x[(int64_t)r * kXLd + m] = m < O ? s_x[i][m] : 0.0f;
+    }
+  }
+  __syncthreads();
+
+  // ---- critic backward: dg2 = dq·w3 ⊙ [g2 > 0], dg1 = (W2ᵀ dg2) ⊙ [g1 > 0] ----
+  for (int k = 0; k < 2; ++k) {
+    const float* C = P + L.q_base[k];
+    const float* dq = s_row[k == 0 ? S_DQ1 : S_DQ2];
+    if (col) {
+      const float w3 = C[L.c_w3 + j];
+#pragma unroll
+      for (int i = 0; i < 2 * R; ++i) {
+        const float g2 = s_g2[k][i][j];
+        const float dg2 = g2 > 0.0f ? dq[i] * w3 : 0.0f;
+        if (i >= R) {
+          const int64_t o = (int64_t)(r0 + i - R) * H + j;
+          a.sc.q_g2[k][o] = g2;
+          a.sc.q_dg2[k][o] = dg2;
+        }
+        s_g2[k][i][j] = dg2;
+      }
+    }
+  }
+  __syncthreads();
+  {
+    float v[2 * R];  // d(ã) partials for the policy rows, both critics
+    for (int k = 0; k < 2; ++k) {
+      const float* C = P + L.q_base[k];
+      if (col) {
+        float acc[2 * R];
+#pragma unroll
+        for (int i = 0; i < 2 * R; ++i) acc[i] = 0.0f;
+        // Σ_j W2[j][m]·dg2[i][j] with m = this column: W2 row-major reads are coalesced over m
+        const float* W2 = C + L.c_w2;
+        for (int jj = 0; jj < H; jj += 4) {
+          const float w0 = W2[(int64_t)(jj + 0) * H + j], w1 = W2[(int64_t)(jj + 1) * H + j];
+          const float w2 = W2[(int64_t)(jj + 2) * H + j], w3 = W2[(int64_t)(jj + 3) * H + j];
+#pragma unroll
+          for (int i = 0; i < 2 * R; ++i) {
+            const float4 d = *reinterpret_cast<const float4*>(&s_g2[k][i][jj]);
+            acc[i] = fmaf(w0, d.x, acc[i]);
+            acc[i] = fmaf(w1, d.y, acc[i]);
+            acc[i] = fmaf(w2, d.z, acc[i]);
+            acc[i] = fmaf(w3, d.w, acc[i]);
+          }
+        }
+        const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
+#pragma unroll
+        for (int i = 0; i < 2 * R; ++i) {
+          const float g1 = s_g1[k][i][j];
+          const float dg1 = g1 > 0.0f ? acc[i] : 0.0f;
+          if (i < R) {
+            v[k * R + i] = wa * dg1;
+          } else {
+            const int64_t o = (int64_t)(r0 + i - R) * H + j;
+            a.sc.q_g1[k][o] = g1;  // (obs, a) rows feed the weight gradients
+            a.sc.q_dg1[k][o] = dg1;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) v[k * R + i] = 0.0f;
+      }
+    }
+    block_sum<2 * R>(v, s_red, s_sum);
+  }
+
+  // ---- actor backward on the obs rows ----
+  if (tid < R) {
+    const int i = tid, r = r0 + i;
+    const float act = s_row[S_A][i], z = s_row[S_Z][i], mean = s_row[S_MEAN][i], std = s_row[S_STD][i];
+    const float ls_raw = s_row[S_LSRAW][i];
+    float dA = s_sum[i] + s_sum[R + i];
+    if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
+    const float ainv = alpha * invB;
+    const float d = z - mean, var = std * std;
+    const float sig = 1.0f / (1.0f + expf(2.0f * z));  // sigmoid(-2z)
+    const float gz = dA * (1.0f - act * act) + ainv * (-(d / var) + (2.0f - 4.0f * sig));
+    const float dmean = gz + ainv * (d / var);
+    const float dstd = gz * s_eps[i] + ainv * ((d * d) / (var * std) - 1.0f / std);
+    const float dls = (ls_raw >= -20.0f && ls_raw <= 2.0f) ? dstd * std : 0.0f;
+    s_row[S_DMEAN][i] = dmean;
+    s_row[S_DLS][i] = dls;
+    a.sc.a_dhead[(int64_t)r * 2] = dmean;
+    a.sc.a_dhead[(int64_t)r * 2 + 1] = dls;
+  }
+  __syncthreads();
+  if (col) {
+    const float wm = P[L.p_wm + j], ws = P[L.p_ws + j];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float h2 = s_h2[i][j];
+      const float dh2 = h2 > 0.0f ? (wm * s_row[S_DMEAN][i] + ws * s_row[S_DLS][i]) : 0.0f;
+      const int64_t o = (int64_t)(r0 + i) * H + j;
+      a.sc.a_h2[o] = h2;
+      a.sc.a_dh2[o] = dh2;
+      s_h2[i][j] = dh2;
+    }
+  }
+  __syncthreads();
+  if (col) {
+    float acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = 0.0f;
+    const float* W2 = P + L.p_w2;
+    for (int jj = 0; jj < H; jj += 4) {
+      const float w0 = W2[(int64_t)(jj + 0) * H + j], w1 = W2[(int64_t)(jj + 1) * H + j];
+      const float w2 = W2[(int64_t)(jj + 2) * H + j], w3 = W2[(int64_t)(jj + 3) * H + j];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const float4 dd = *reinterpret_cast<const float4*>(&s_h2[i][jj]);
+        acc[i] = fmaf(w0, dd.x, acc[i]);
+        acc[i] = fmaf(w1, dd.y, acc[i]);
+        acc[i] = fmaf(w2, dd.z, acc[i]);
+        acc[i] = fmaf(w3, dd.w, acc[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const float h1 = s_h1[i][j];
+      const int64_t o = (int64_t)(r0 + i) * H + j;
+      a.sc.a_h1[o] = h1;
+      a.sc.a_dh1[o] = h1 > 0.0f ? acc[i] : 0.0f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight gradients: out[j][k] = Σ_r dY[r·ldY + j] · X[r·ldX + k]  (X == nullptr: ones -> bias)
+// ---------------------------------------------------------------------------------------------
+struct GMat {
+  const float* dY;
+  const float* X;
+  int ldY, ldX, M, N;
+  int64_t out_off;
+};
+struct GTask {
+  int mat, j0, k0;
+};
+constexpr int kMaxMats = 24;
+struct WgradArgs {
+  GMat mats[kMaxMats];
+  const GTask* tasks;
+  int n_tasks;
+  float* grads;
+  int B;
+  Scratch sc;
+  const float* params;
+  int64_t* step;
+  float* stats;
+  Hyper hp;
+};
+
+__global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x == a.n_tasks) {  // scalars: losses, α and d(log α); step += 1
+    float v[5] = {0, 0, 0, 0, 0};
+    for (int r = tid; r < a.B; r += kThreads) {
+      v[0] += a.sc.p_pl[r];
+      v[1] += a.sc.p_q1l[r];
+      v[2] += a.sc.p_q2l[r];
+      v[3] += a.sc.p_la[r];
+      v[4] += a.sc.p_ga[r];
+    }
+    __shared__ float red[4][32];
+    __shared__ float sum[32];
+    block_sum<5>(v, red, sum);
+    if (tid == 0) {
+      const float invB = 1.0f / (float)a.B;
+      a.stats[0] = sum[0] * invB;
+      a.stats[1] = sum[1] * invB;
+      a.stats[2] = sum[2] * invB;
+      a.stats[3] = a.hp.auto_ent ? sum[3] * invB : 0.0f;
+      a.stats[4] = a.hp.auto_ent ? expf(a.params[0]) : 1.0f;
+      a.grads[0] = a.hp.auto_ent ? sum[4] * invB : 0.0f;
+      *a.step += 1;
+    }
+    return;
+  }
+  const GTask t = a.tasks[blockIdx.x];
+  const GMat m = a.mats[t.mat];
+  __shared__ float sY[32][64 + 1];
+  __shared__ float sX[32][64 + 1];
+  const int tj = tid >> 4, tk = tid & 15;
+  float acc[4][4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = 0.0f;
+  for (int rb = 0; rb < a.B; rb += 32) {
+    for (int e = tid; e < 32 * 64; e += kThreads) {
+      const int rr = e >> 6, cc = e & 63, r = rb + rr;
+      const int jj = t.j0 + cc, kk = t.k0 + cc;
+      sY[rr][cc] = (r < a.B && jj < m.M) ? m.dY[(int64_t)r * m.ldY + jj] : 0.0f;
+      sX[rr][cc] = (r < a.B && kk < m.N) ? (m.X ? m.X[(int64_t)r * m.ldX + kk] : 1.0f) : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int rr = 0; rr < 32; ++rr) {
+      float y[4], x[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) y[p] = sY[rr][tj * 4 + p];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = sX[rr][tk * 4 + q];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[p][q] = fmaf(y[p], x[q], acc[p][q]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int jj = t.j0 + tj * 4 + p;
+    if (jj >= m.M) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = t.k0 + tk * 4 + q;
+      if (kk < m.N) a.grads[m.out_off + (int64_t)jj * m.N + kk] = acc[p][q];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Adam (torch.optim.Adam, amsgrad=False, no weight decay) + soft target update + transposes
+// ---------------------------------------------------------------------------------------------
+struct ApplyArgs {
+  float* params;
+  float* targets;
+  const float* grads;
+  float* m;
+  float* v;
+  const int64_t* step;
+  float* T;
+  Layout L;
+  Hyper hp;
+};
+
+__global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const Layout& L = a.L;
+  if (e >= L.n_params) return;
+  if (e == 0 && !a.hp.auto_ent) return;
+  const float g = a.grads[e] * a.hp.inv_world;
+  const bool is_q = e >= L.q_base[0];
+  const double lr = is_q ? a.hp.lr_q : a.hp.lr_pi;
+  const double t = (double)*a.step;
+  const double bc1 = 1.0 - pow((double)a.hp.beta1, t);
+  const double bc2 = 1.0 - pow((double)a.hp.beta2, t);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  float m = a.m[e], v = a.v[e];
+  m = m + (1.0f - a.hp.beta1) * (g - m);             // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+  const float denom = sqrtf(v) / bc2_sqrt + a.hp.eps;
+  const float p = a.params[e] + (-step_size) * (m / denom);
+  a.m[e] = m;
+  a.v[e] = v;
+  a.params[e] = p;
+  const int H = L.H;
+  if (e >= L.p_w2 && e < L.p_w2 + (int64_t)H * H) {
+    const int64_t l = e - L.p_w2;
+    a.T[(l % H) * H + l / H] = p;
+  }
+  if (is_q) {
+    const int k = e >= L.q_base[1] ? 1 : 0;
+    const int64_t qe = e - L.q_base[0];
+    const float tp = a.targets[qe] * (1.0f - a.hp.tau) + p * a.hp.tau;
+    a.targets[qe] = tp;
+    const int64_t l = e - L.q_base[k] - L.c_w2;
+    if (l >= 0 && l < (int64_t)H * H) {
+      a.T[(size_t)(1 + k) * H * H + (l % H) * H + l / H] = p;
+      a.T[(size_t)(3 + k) * H * H + (l % H) * H + l / H] = tp;
+    }
+  }
+}
+
+__global__ void sac_transpose_kernel(const float* params, const float* targets, float* T, Layout L) {
+  const int64_t HH = (int64_t)L.H * L.H;
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= 5 * HH) return;
+  const int which = (int)(e / HH);
+  const int64_t l = e % HH;
+  const float* src = which == 0 ? params + L.p_w2
+                     : which <= 2 ? params + L.q_base[which - 1] + L.c_w2
+                                  : targets + (int64_t)(which - 3) * L.q_size + L.c_w2;
+  T[which * HH + (l % L.H) * L.H + l / L.H] = src[l];
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+struct sacf_handle {
+  sacf_config cfg;
+  Layout L;
+  Hyper hp;
+  int device;
+  hipStream_t stream;
+  float *params, *targets, *grads, *adam_m, *adam_v, *stats;
+  int64_t* step;
+  const float *r_obs, *r_act, *r_rew, *r_term, *r_nobs;
+  const int64_t* r_size;
+  int64_t r_cap;
+  uint64_t seed;
+  float* T;
+  float* scratch;
+  Scratch sc;
+  GTask* tasks;
+  int n_tasks;
+  GMat mats[kMaxMats];
+  int n_mats;
+  char err[512];
+};
+
+static int sfail(sacf_handle* h, int code, const char* fmt, ...) {
+  if (h) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(h->err, sizeof(h->err), fmt, ap);
+    va_end(ap);
+  }
+  return code;
+}
+
+struct SDev {
+  int prev;
+  explicit SDev(int d) {
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(d);
+  }
+  ~SDev() { (void)hipSetDevice(prev); }
+};
+
+extern "C" {
+
+int32_t sacf_abi_version(void) { return SACF_ABI_VERSION; }
+
+int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** out) {
+  if (!out) return SACF_EINVAL;
+  *out = nullptr;
+  if (!cfg || cfg->abi_version != SACF_ABI_VERSION) return SACF_EINVAL;
+  const int O = cfg->obs_dim, H = cfg->hidden, B = cfg->batch;
+  if (O < 1 || O + 1 > kXLd || H < 32 || H > SACF_MAX_HIDDEN || H % 32 || B < R || B % R || cfg->world_size < 1)
+    return SACF_EINVAL;
+  sacf_handle* h = new (std::nothrow) sacf_handle();
+  if (!h) return SACF_EINVAL;
+  h->cfg = *cfg;
+  h->device = device;
+  h->stream = (hipStream_t)stream;
+  Layout& L = h->L;
+  L.O = O;
+  L.H = H;
+  L.B = B;
+  int64_t o = 1;  // log_alpha at 0
+  L.p_w1 = o; o += (int64_t)H * O;
+  L.p_b1 = o; o += H;
+  L.p_w2 = o; o += (int64_t)H * H;
+  L.p_b2 = o; o += H;
+  L.p_wm = o; o += H;
+  L.p_bm = o; o += 1;
+  L.p_ws = o; o += H;
+  L.p_bs = o; o += 1;
+  int64_t c = 0;
+  L.c_w1 = c; c += (int64_t)H * (O + 1);
+  L.c_b1 = c; c += H;
+  L.c_w2 = c; c += (int64_t)H * H;
+  L.c_b2 = c; c += H;
+  L.c_w3 = c; c += H;
+  L.c_b3 = c; c += 1;
+  L.q_size = c;
+  L.q_base[0] = o;
+  L.q_base[1] = o + c;
+  L.n_params = o + 2 * c;
+  L.n_targets = 2 * c;
+  Hyper& hp = h->hp;
+  hp.gamma = cfg->discount;
+  hp.rscale = cfg->reward_scale;
+  hp.tau = cfg->soft_target_tau;
+  hp.areg = cfg->action_reg_coeff;
+  hp.clip = cfg->clip_val;
+  hp.tent = cfg->target_entropy;
+  hp.lr_pi = cfg->policy_lr;
+  hp.lr_q = cfg->qf_lr;
+  hp.beta1 = cfg->beta1;
+  hp.beta2 = cfg->beta2;
+  hp.eps = cfg->adam_eps;
+  hp.auto_ent = cfg->auto_entropy;
+  hp.inv_world = 1.0f / (float)cfg->world_size;
+
+  SDev g(device);
+  // scratch: actor 4·B·H + B·16 + 2B; critics 2·(4·B·H + B·16 + B); partials 5B
+  const int64_t BH = (int64_t)B * H;
+  const int64_t n_scr = 4 * BH + B * kXLd + 2 * B + 2 * (4 * BH + B * kXLd + B) + 5 * B;
+  hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
+  if (e != hipSuccess) {
+    *out = h;
+    return sfail(h, SACF_EHIP, "hipMalloc(scratch): %s", hipGetErrorString(e));
+  }
+  float* s = h->scratch;
+  Scratch& sc = h->sc;
+  sc.a_x = s; s += B * kXLd;
+  sc.a_h1 = s; s += BH;
+  sc.a_h2 = s; s += BH;
+  sc.a_dh1 = s; s += BH;
+  sc.a_dh2 = s; s += BH;
+  sc.a_dhead = s; s += 2 * B;
+  for (int k = 0; k < 2; ++k) {
+    sc.q_x[k] = s; s += B * kXLd;
+    sc.q_g1[k] = s; s += BH;
+    sc.q_g2[k] = s; s += BH;
+    sc.q_dg1[k] = s; s += BH;
+    sc.q_dg2[k] = s; s += BH;
+    sc.q_dq[k] = s; s += B;
+  }
+  sc.p_pl = s; s += B;
+  sc.p_q1l = s; s += B;
+  sc.p_q2l = s; s += B;
+  sc.p_la = s; s += B;
+  sc.p_ga = s; s += B;
+  e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);
+  if (e != hipSuccess) {
+    *out = h;
+    return sfail(h, SACF_EHIP, "hipMalloc(T): %s", hipGetErrorString(e));
+  }
+  // weight-gradient matrices and their 64×64 tiles
+  int nm = 0;
+  auto add = [&](const float* dY, int ldY, const float* X, int ldX, int M, int N, int64_t off) {
+    h->mats[nm++] = GMat{dY, X, ldY, ldX, M, N, off};
+  };
+  add(sc.a_dh1, H, sc.a_x, kXLd, H, O, L.p_w1);
+  add(sc.a_dh1, H, nullptr, 0, H, 1, L.p_b1);
+  add(sc.a_dh2, H, sc.a_h1, H, H, H, L.p_w2);
+  add(sc.a_dh2, H, nullptr, 0, H, 1, L.p_b2);
+  add(sc.a_dhead, 2, sc.a_h2, H, 1, H, L.p_wm);
+  add(sc.a_dhead, 2, nullptr, 0, 1, 1, L.p_bm);
+  add(sc.a_dhead + 1, 2, sc.a_h2, H, 1, H, L.p_ws);
+  add(sc.a_dhead + 1, 2, nullptr, 0, 1, 1, L.p_bs);
+  for (int k = 0; k < 2; ++k) {
+    const int64_t b = L.q_base[k];
+    add(sc.q_dg1[k], H, sc.q_x[k], kXLd, H, O + 1, b + L.c_w1);
+    add(sc.q_dg1[k], H, nullptr, 0, H, 1, b + L.c_b1);
+    add(sc.q_dg2[k], H, sc.q_g1[k], H, H, H, b + L.c_w2);
+    add(sc.q_dg2[k], H, nullptr, 0, H, 1, b + L.c_b2);
+    add(sc.q_dq[k], 1, sc.q_g2[k], H, 1, H, b + L.c_w3);
+    add(sc.q_dq[k], 1, nullptr, 0, 1, 1, b + L.c_b3);
+  }
+  h->n_mats = nm;
+  std::vector<GTask> tasks;
+  // the big H×H tiles first so they start early
+  for (int pass = 0; pass < 2; ++pass)
+    for (int mi = 0; mi < nm; ++mi) {
+      const GMat& m = h->mats[mi];
+      const bool big = m.M == H && m.N == H;
+      if ((pass == 0) != big) continue;
+      for (int j0 = 0; j0 < m.M; j0 += 64)
+        for (int k0 = 0; k0 < m.N; k0 += 64) tasks.push_back(GTask{mi, j0, k0});
+    }
+  h->n_tasks = (int)tasks.size();
+  e = hipMalloc(&h->tasks, sizeof(GTask) * tasks.size());
+  if (e == hipSuccess) e = hipMemcpy(h->tasks, tasks.data(), sizeof(GTask) * tasks.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    *out = h;
+    return sfail(h, SACF_EHIP, "tasks: %s", hipGetErrorString(e));
+  }
+  *out = h;
+  return SACF_OK;
+}
+
+int sacf_destroy(sacf_handle* h) {
+  if (!h) return SACF_OK;
+  SDev g(h->device);
+  if (h->scratch) (void)hipFree(h->scratch);
+  if (h->T) (void)hipFree(h->T);
+  if (h->tasks) (void)hipFree(h->tasks);
+  delete h;
+  return SACF_OK;
+}
+
+const char* sacf_last_error(const sacf_handle* h) { return h ? h->err : "null handle"; }
+int64_t sacf_param_count(const sacf_handle* h) { return h ? h->L.n_params : -1; }
+int64_t sacf_target_count(const sacf_handle* h) { return h ? h->L.n_targets : -1; }
+int64_t sacf_stats_count(const sacf_handle* h) { return h ? 8 + 6 * (int64_t)h->L.B : -1; }
+
+int sacf_set_stream(sacf_handle* h, void* stream) {
+  if (!h) return SACF_EINVAL;
+  h->stream = (hipStream_t)stream;
+  return SACF_OK;
+}
+
+int sacf_bind(sacf_handle* h, float* params, float* targets, float* grads, float* adam_m, float* adam_v,
+              int64_t* step, float* stats) {
+  if (!h || !params || !targets || !grads || !adam_m || !adam_v || !step || !stats)
+    return sfail(h, SACF_EINVAL, "sacf_bind: null buffer");
+  h->params = params;
+  h->targets = targets;
+  h->grads = grads;
+  h->adam_m = adam_m;
+  h->adam_v = adam_v;
+  h->step = step;
+  h->stats = stats;
+  return sacf_sync_params(h);
+}
+
+int sacf_sync_params(sacf_handle* h) {
+  if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_sync_params: not bound");
+  SDev g(h->device);
+  const int64_t n = 5 * (int64_t)h->L.H * h->L.H;
+  hipLaunchKernelGGL(sac_transpose_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     h->stream, h->params, h->targets, h->T, h->L);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "transpose: %s", hipGetErrorString(e));
+}
+
+int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
+                    const float* next_obs, const int64_t* size_dev, int64_t capacity, uint64_t seed) {
+  if (!h || !obs || !act || !rew || !term || !next_obs || !size_dev || capacity < 1)
+    return sfail(h, SACF_EINVAL, "sacf_set_replay: bad argument");
+  h->r_obs = obs;
+  h->r_act = act;
+  h->r_rew = rew;
+  h->r_term = term;
+  h->r_nobs = next_obs;
+  h->r_size = size_dev;
+  h->r_cap = capacity;
+  h->seed = seed;
+  return SACF_OK;
+}
+
+int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
+               const float* next_obs, const float* eps) {
+  if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_grads: buffers not bound");
+  RowsArgs a;
+  memset(&a, 0, sizeof(a));
+  a.params = h->params;
+  a.targets = h->targets;
+  a.T = h->T;
+  if (obs) {
+    if (!act || !rew || !term || !next_obs) return sfail(h, SACF_EINVAL, "sacf_grads: partial batch");
+    a.obs = obs; a.act = act; a.rew = rew; a.term = term; a.nobs = next_obs;
+    a.sampled = 0;
+  } else {
+    if (!h->r_obs) return sfail(h, SACF_ESTATE, "sacf_grads: no batch and no replay bound");
+    a.obs = h->r_obs; a.act = h->r_act; a.rew = h->r_rew; a.term = h->r_term; a.nobs = h->r_nobs;
+    a.size_dev = h->r_size;
+    a.capacity = h->r_cap;
+    a.sampled = 1;
+  }
+  a.seed = h->seed;
+  a.eps = eps;
+  a.step = h->step;
+  a.stats = h->stats;
+  a.sc = h->sc;
+  a.L = h->L;
+  a.hp = h->hp;
+  SDev g(h->device);
+  hipLaunchKernelGGL(sac_rows_kernel, dim3(h->L.B / R), dim3(kThreads), 0, h->stream, a);
+  WgradArgs w;
+  memset(&w, 0, sizeof(w));
+  for (int i = 0; i < h->n_mats; ++i) w.mats[i] = h->mats[i];
+  w.tasks = h->tasks;
+  w.n_tasks = h->n_tasks;
+  w.grads = h->grads;
+  w.B = h->L.B;
+  w.sc = h->sc;
+  w.params = h->params;
+  w.step = h->step;
+  w.stats = h->stats;
+  w.hp = h->hp;
+  hipLaunchKernelGGL(sac_wgrad_kernel, dim3(h->n_tasks + 1), dim3(kThreads), 0, h->stream, w);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
+}
+
+int sacf_apply(sacf_handle* h) {
+  if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_apply: buffers not bound");
+  ApplyArgs a;
+  a.params = h->params;
+  a.targets = h->targets;
+  a.grads = h->grads;
+  a.m = h->adam_m;
+  a.v = h->adam_v;
+  a.step = h->step;
+  a.T = h->T;
+  a.L = h->L;
+  a.hp = h->hp;
+  SDev g(h->device);
+  hipLaunchKernelGGL(sac_apply_kernel, dim3((unsigned)((h->L.n_params + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     h->stream, a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_apply: %s", hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -113,16 +113,21 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         return float(dt)
 
-    pol, q = nets()
-    tr = FusedSACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3],
-                         batch_size=batch, process_group=pg, **hp)
-    tr.broadcast_parameters(0)
-    tr.train_from_buffer(rb, 10)  # captures the graph
-    dt = timed(lambda k: tr.train_from_buffer(rb, k), steps)
+    def fused(backend):
+        pol, q = nets()
+        tr = FusedSACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3],
+                             batch_size=batch, process_group=pg, backend=backend, **hp)
+        tr.broadcast_parameters(0)
+        tr.train_from_buffer(rb, 10)  # captures the graph
+        return timed(lambda k: tr.train_from_buffer(rb, k), steps)
+
+    dt = fused("hip")
     res = {"grad_steps_per_s": steps / dt, "ms_per_grad_step": dt / steps * 1e3, "batch_per_gpu": batch,
            "global_batch": batch * world, "hidden": [256, 256], "dtype": "f32",
-           "impl": "FusedSACTrainer (HIP graph: sample+fwd+grads+fused Adam+soft update"
-                   + (", RCCL all-reduce between graph halves)" if world > 1 else ")")}
+           "impl": "FusedSACTrainer hip backend (csrc/sac_kernels.hip: rows + weight-grad + Adam kernels, "
+                   "HIP graph" + (", RCCL all-reduce between graph halves)" if world > 1 else ")")}
+    if world == 1:
+        res["torch_ops_graph_grad_steps_per_s"] = steps / fused("torch")
     if world == 1 and eager_steps:
         pol, q = nets()
         ref = SACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3], **hp)

@@ -1,0 +1,97 @@
+/*
+ * sac_fused.h — C ABI of the fused SAC update kernels (gfx950), libsacfused.so.
+ *
+ * Replaces the per-op PyTorch graph of one SACTrainer.train_from_torch call
+ * (ast_sac/torch/sac/sac.py:102-154 compute_loss + train_from_torch, :156-166 soft update,
+ * torch.optim.Adam for log_alpha / policy / qf1 / qf2) for the runner's networks:
+ *   policy  TanhGaussianPolicy(obs_dim -> H -> H -> (mean, log_std)), act_dim = 1
+ *   qf1/qf2 ConcatMlp(obs_dim + 1 -> H -> H -> 1), targets likewise
+ * with three launches per grad step:
+ *   sacf_grads : rows kernel (batch gather/sampling, every forward, losses, per-row backward)
+ *                + weight-gradient kernel (flat fp32 gradient of [log_alpha | policy | qf1 | qf2])
+ *   sacf_apply : Adam (torch.optim.Adam semantics, betas/eps as configured) on every parameter,
+ *                soft target update, refresh of the library's transposed weight copies.
+ * Between the two a caller may all-reduce the flat gradient (data parallel); sacf_apply divides
+ * it by world_size.
+ *
+ * Memory: the caller owns the flat buffers (torch tensors) bound with sacf_bind; the library owns
+ * its scratch (per-row activations, ≈12·B·H floats) and transposed copies of the H×H weights.
+ * Flat layout (fp32, torch parameter order and (out, in) row-major weights):
+ *   params : [log_alpha] policy{fc0.w (H×O), fc0.b (H), fc1.w (H×H), fc1.b (H), last_fc.w (H),
+ *            last_fc.b (1), last_fc_log_std.w (H), last_fc_log_std.b (1)}
+ *            qf1{fc0.w (H×(O+1)), fc0.b, fc1.w (H×H), fc1.b, last_fc.w (H), last_fc.b (1)} qf2{…}
+ *   targets: target_qf1{…} target_qf2{…}  (same layout as the qf part)
+ * Conventions: 0 = success, negative SACF_E* otherwise; asynchronous on the handle's stream;
+ * a handle is not thread-safe.
+ */
+#ifndef SAC_FUSED_H
+#define SAC_FUSED_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SACF_ABI_VERSION 1
+#define SACF_OK 0
+#define SACF_EINVAL -1
+#define SACF_EHIP -2
+#define SACF_ESTATE -3
+#define SACF_MAX_OBS 16
+#define SACF_MAX_HIDDEN 256
+
+typedef struct sacf_config {
+  int32_t abi_version;   /* = SACF_ABI_VERSION */
+  int32_t obs_dim;       /* <= SACF_MAX_OBS (8 for the AST env) */
+  int32_t hidden;        /* H, multiple of 32, <= SACF_MAX_HIDDEN (runner: 256) */
+  int32_t batch;         /* B per call (per rank), multiple of 4 */
+  float discount;        /* sac.py:31  γ */
+  float reward_scale;    /* sac.py:32 */
+  float soft_target_tau; /* sac.py:37  τ */
+  float action_reg_coeff;/* runner: 0.01 (0 disables) */
+  float clip_val;        /* q-target clamp (runner: 100; +inf disables) */
+  float target_entropy;  /* sac.py:62-64: −|A| */
+  float policy_lr;       /* lr of log_alpha and the policy */
+  float qf_lr;
+  float beta1, beta2, adam_eps; /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
+  int32_t auto_entropy;  /* use_automatic_entropy_tuning */
+  int32_t world_size;    /* gradient is divided by this in sacf_apply */
+  int32_t reserved[6];
+} sacf_config;
+
+typedef struct sacf_handle sacf_handle;
+
+int32_t sacf_abi_version(void);
+int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** out);
+int sacf_destroy(sacf_handle* h);
+const char* sacf_last_error(const sacf_handle* h);
+/* launches go to this stream from now on (e.g. torch's current / capturing stream) */
+int sacf_set_stream(sacf_handle* h, void* stream);
+/* element counts of the flat params / targets buffers */
+int64_t sacf_param_count(const sacf_handle* h);
+int64_t sacf_target_count(const sacf_handle* h);
+/* stats buffer: [policy_loss, qf1_loss, qf2_loss, alpha_loss, alpha, 0, 0, 0] then per row
+ * q1_pred[B], q2_pred[B], q_target[B], log_pi[B], tanh(mean)[B], std[B] */
+int64_t sacf_stats_count(const sacf_handle* h);
+/* Bind caller-owned device buffers (params/targets/grads/adam_m/adam_v: param or target count
+ * floats; step: one int64 = number of completed updates, read by Adam bias correction and the RNG). */
+int sacf_bind(sacf_handle* h, float* params, float* targets, float* grads, float* adam_m, float* adam_v,
+              int64_t* step, float* stats);
+/* Re-derive the library's transposed weight copies after params/targets changed outside the library. */
+int sacf_sync_params(sacf_handle* h);
+/* Replay ring (DeviceReplayBuffer storage, float32 rows) sampled uniformly with replacement. */
+int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
+                    const float* next_obs, const int64_t* size_dev, int64_t capacity, uint64_t seed);
+/* Gradient of one update into `grads` (and step += 1). With obs == NULL the batch is sampled from
+ * the replay ring; with eps == NULL the 2·B reparameterisation normals come from the in-kernel
+ * Philox stream, else eps = [B normals for obs rows | B normals for next_obs rows]. */
+int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
+               const float* next_obs, const float* eps);
+/* Adam + soft target update from `grads` (divided by world_size). */
+int sacf_apply(sacf_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

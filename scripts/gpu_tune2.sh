@@ -8,7 +8,7 @@ tail -4 $O/pytest_gpu_$TAG.log
 B="python bench.py --no-cpu-baseline --sac-steps 0"
 for ca in none sbmpc; do
   for lpe in 2 4 8 16; do
-    timeout -k 10 300 $B --collav $ca --lpe $lpe > $O/t_${TAG}_${ca}_lpe$lpe.log 2>&1; hard $? bench_$ca_$lpe
+    timeout -k 10 300 $B --collav $ca --lpe $lpe > $O/t_${TAG}_${ca}_lpe$lpe.log 2>&1; hard $? bench_${ca}_${lpe}
     echo "$ca lpe$lpe grid: $(python -c "import json;d=json.loads(open('$O/t_${TAG}_${ca}_lpe$lpe.log').read().strip().splitlines()[-1]);print(round(d['value']/1e6,1),'M', round(d['roofline']['frac']*100,3),'%')")"
   done
   SHIPSIM_NO_GRID=1 timeout -k 10 300 $B --collav $ca > $O/t_${TAG}_${ca}_nogrid.log 2>&1; hard $? bench_nogrid

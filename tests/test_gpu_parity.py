@@ -234,7 +234,8 @@ def test_map_grid_is_exact(torch_cuda, collav, monkeypatch):
         for _ in range(60):
             o = sim.step(tab[dec.clamp(max=8), ar], max_ticks=40)
             ready = o["ready"].bool()
-            outs.append(torch.cat([o["obs"].double().reshape(-1), torch.where(ready, o["reward"], 0).reshape(-1),
+            obs = torch.where(ready.unsqueeze(1), o["obs"], 0)  # obs rows are only written for ready envs
+            outs.append(torch.cat([obs.double().reshape(-1), torch.where(ready, o["reward"], 0).reshape(-1),
                                    torch.where(ready, o["events"], 0).double(), o["ticks"].double()]).cpu())
             end = ready & (o["done"].bool() | (dec >= 8))
             dec = torch.where(ready, dec + 1, dec).masked_fill(end, 0)

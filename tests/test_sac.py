@@ -81,7 +81,7 @@ def test_sac_trainer_matches_reference_step(golden):
 
 def _run_fused(fx, device, use_graph):
     nets, kw, B = _build(fx, device)
-    tr = FusedSACTrainer(env=_Env, **nets, **kw, batch_size=B, use_graph=use_graph)
+    tr = FusedSACTrainer(env=_Env, **nets, **kw, batch_size=B, use_graph=use_graph, backend="torch")
     cur = {}
     tr.noise_fn = lambda shape: cur["eps"]
     for s in range(_n_steps(fx)):
@@ -162,3 +162,110 @@ def test_device_replay_buffer_ring_order():
     assert rb.num_steps_can_sample() == 5
     b = rb.random_batch(64)
     assert set(b["observations"][:, 0].tolist()) <= {4.0, 5.0, 6.0, 7.0, 8.0}
+
+
+# ------------------------------------------------------------------------------------------------
+# HIP backend (csrc/sac_kernels.hip): fused rows / weight-gradient / Adam kernels
+# ------------------------------------------------------------------------------------------------
+def _seeded_nets(H, device, seed=0):
+    torch.manual_seed(seed)
+    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[H, H])
+    qs = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[H, H]) for _ in range(4)]
+    return pol.to(device), [q.to(device) for q in qs]
+
+
+def _rand_batch(B, device, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    b = dict(observations=torch.rand(B, 8, generator=g) * 2000 - 1000, actions=torch.rand(B, 1, generator=g) * 2 - 1,
+             rewards=torch.randn(B, 1, generator=g) * 3, terminals=(torch.rand(B, 1, generator=g) < 0.2).float(),
+             next_observations=torch.rand(B, 8, generator=g) * 2000 - 1000)
+    eps = torch.randn(2 * B, 1, generator=g)
+    return {k: v.to(device) for k, v in b.items()}, eps.to(device)
+
+
+def _trainer(backend, H, B, device, use_graph=False, seed=0):
+    pol, qs = _seeded_nets(H, device, seed)
+    return FusedSACTrainer(env=_Env, policy=pol, qf1=qs[0], qf2=qs[1], target_qf1=qs[2], target_qf2=qs[3],
+                           discount=0.965, reward_scale=0.75, policy_lr=8e-5, qf_lr=8e-5, soft_target_tau=1e-3,
+                           action_reg_coeff=0.01, clip_val=100.0, batch_size=B, use_graph=use_graph, backend=backend)
+
+
+def _assert_grads_close(g_hip, g_ref, tr, what):
+    """Per parameter tensor: |Δ| <= 1e-4·|ref| + 1e-5·max|ref| (fp32, different summation order)."""
+    off = 0
+    for name, p in [("log_alpha", tr.log_alpha)] + [(f"p{i}", p) for i, p in enumerate(tr.pi_params[1:] + tr.q_params)]:
+        n = p.numel()
+        a, b = g_hip[off:off + n], g_ref[off:off + n]
+        tol = 1e-4 * b.abs() + 1e-5 * b.abs().max() + 1e-12
+        assert bool(((a - b).abs() <= tol).all()), f"{what} {name}: max |Δ| {(a - b).abs().max().item():.3e}"
+        off += n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,B", [(32, 64), (256, 256)])
+def test_hip_sac_gradients_match_torch_autograd(H, B):
+    """One update's flat gradient (α | π | Q1 | Q2) from the fused kernels == torch autograd's."""
+    batch, eps = _rand_batch(B, "cuda")
+    ref = _trainer("torch", H, B, "cuda")
+    hip = _trainer("hip", H, B, "cuda")
+    for tr in (ref, hip):
+        tr.noise_fn = lambda shape: eps
+        tr.train_from_torch(batch)
+    torch.cuda.synchronize()
+    lr, lh = ref.last_losses(), hip.last_losses()
+    for a, b in zip(lh, lr):
+        assert abs(float(a) - float(b)) <= 1e-5 * abs(float(b)) + 1e-6
+    _assert_grads_close(hip.flat_grad, ref.flat_grad, ref, f"H={H}")
+
+
+@pytest.mark.gpu
+def test_hip_sac_matches_reference_step(golden):
+    """Three captured reference steps (tests/golden/sac_step.npz): losses within 1e-5, parameters within
+    fp32 tolerance except where Adam's normalised step flips sign on a near-zero gradient (bounded by
+    2·lr per step, and required to be rare)."""
+    fx = golden("sac_step")
+    nets, kw, B = _build(fx, "cuda")
+    tr = FusedSACTrainer(env=_Env, **nets, **kw, batch_size=B, use_graph=True, backend="hip")
+    cur = {}
+    tr.noise_fn = lambda shape: cur["eps"]
+    lr = kw["policy_lr"]
+    for s in range(_n_steps(fx)):
+        noise = fx[f"step{s}/noise"]
+        cur["eps"] = torch.from_numpy(np.concatenate([noise[0], noise[1]], 0)).cuda()
+        tr.train_from_torch(_batch(fx, s, "cuda"))
+        l = tr.last_losses()
+        got = np.array([float(l.policy_loss), float(l.qf1_loss), float(l.qf2_loss), float(l.alpha_loss)])
+        np.testing.assert_allclose(got, fx[f"step{s}/losses"], rtol=1e-5, atol=1e-6)
+        n_bad, n_all = 0, 0
+        for name, net in nets.items():
+            for pn, p in net.named_parameters():
+                ref = fx[f"step{s}/{name}/{pn}"]
+                d = np.abs(p.detach().cpu().numpy() - ref)
+                assert d.max() <= 2 * lr * (s + 1) + 1e-6, f"step {s} {name}.{pn} {d.max():.3e}"
+                n_bad += int((d > 1e-6 + 1e-5 * np.abs(ref)).sum())
+                n_all += d.size
+        assert n_bad <= max(2, n_all // 200), f"step {s}: {n_bad}/{n_all} parameters off"
+        np.testing.assert_allclose(tr.log_alpha.detach().cpu().numpy(), fx[f"step{s}/log_alpha"], rtol=1e-5,
+                                   atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_hip_sac_graph_replay_equals_eager_launches():
+    """Replay-buffer sampling + Philox noise inside the HIP graph gives bitwise the same training as
+    launching the kernels one by one."""
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    rb = DeviceReplayBuffer(5000, 8, 1, "cuda")
+    b, _ = _rand_batch(3000, "cuda", seed=4)
+    rb.add_batch(b["observations"], b["actions"], b["rewards"], b["next_observations"], b["terminals"])
+    res = []
+    for g in (False, True):
+        tr = _trainer("hip", 256, 256, "cuda", use_graph=g, seed=7)
+        tr._sf.set_replay(*[rb._store[k] for k in ("observations", "actions", "rewards", "terminals",
+                                                     "next_observations")], rb._size_t, rb._max, 1234)
+        tr._seed = 1234
+        tr.train_from_buffer(rb, 20)
+        torch.cuda.synchronize()
+        res.append(torch.cat([tr.flat_param, tr.flat_target]).cpu())
+        assert int(tr._step_t.item()) == 20
+        assert np.isfinite(float(tr.last_losses().qf1_loss))
+    assert torch.equal(res[0], res[1])
