@@ -205,6 +205,27 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   const double q11 = -sp, q12 = cp, q21 = cp, q22 = sp;
   double sp0, cp0;
   sincos(wrap_pmpi(psi_d), &sp0, &cp0);
+  double dChi0 = Chi_ca - in.chi_last;
+  const double H2 = 25 * (1 - P_ca) + 30 * (Chi_ca * Chi_ca) + 20 * fabs(in.p_last - P_ca) +
+                    ((dChi0 > 0) ? 20 * dChi0 * dChi0 : (dChi0 < 0 ? 30 * dChi0 * dChi0 : 0));
+  // Exact skip of the horizon loop: H0 can only be non-zero at samples with dist < max_d_safe.
+  // After sample 0 both predictions are straight lines (the own ship's sway is zeroed after the
+  // first step), so the relative position is P1 + k·W, k = 0..n_samp-2; if its continuous minimum
+  // (and sample 0) stays above max_d_safe by a margin far beyond the rounding of the incremental
+  // update below, every sample's H0 is 0 and the cost is H2 alone.
+  {
+    const double vox = r11 * in.ob_u + r12 * in.ob_v, voy = r21 * in.ob_u + r22 * in.ob_v;
+    const double e0x = in.ob_x - in.os_x, e0y = in.ob_y - in.os_y;
+    const double p1x = (in.ob_x + vox * DT) - (in.os_x + DT * (q11 * ud + q12 * in.os_v));
+    const double p1y = (in.ob_y + voy * DT) - (in.os_y + DT * (q21 * ud + q22 * in.os_v));
+    const double wx = (vox - q11 * ud) * DT, wy = (voy - q21 * ud) * DT;
+    const double ww = wx * wx + wy * wy;
+    double k = ww > 0 ? -(p1x * wx + p1y * wy) / ww : 0.0;
+    k = k < 0 ? 0 : (k > n_samp - 2 ? n_samp - 2 : k);
+    const double mx = p1x + k * wx, my = p1y + k * wy;
+    const double lim = max_d_safe + 1e-3;
+    if (e0x * e0x + e0y * e0y > lim * lim && mx * mx + my * my > lim * lim) return 0.0 + H2;
+  }
   double ox = in.ob_x, oy = in.ob_y, sx = in.os_x, sy = in.os_y, sv = in.os_v;
   double H1 = 0, t = 0;
   for (int i = 0; i < n_samp; ++i) {
@@ -244,9 +265,6 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     double H0 = C * R + 0.0 * 0;
     if (H0 > H1) H1 = H0;
   }
-  double dchi = Chi_ca - in.chi_last;
-  double dChi = (dchi > 0) ? 20 * dchi * dchi : (dchi < 0 ? 30 * dchi * dchi : 0);
-  double H2 = 25 * (1 - P_ca) + 30 * (Chi_ca * Chi_ca) + 20 * fabs(in.p_last - P_ca) + dChi;
   return H1 + H2;
 }
 
