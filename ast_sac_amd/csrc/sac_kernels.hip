@@ -36,7 +36,7 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int R = 4;           // batch rows per block in the rows kernel
+constexpr int R = 4;           // batch granularity: B must be a multiple of R (rows-kernel tiles)
 constexpr int kXLd = 16;       // leading dim of the per-row input scratch (obs | act)
 constexpr float kLog2 = 0.69314718055994530942f;
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
@@ -118,54 +118,102 @@ __device__ inline void block_sum(float (&v)[N], float (*red)[32], float* out) {
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.0f); }
 __device__ __forceinline__ float softplus(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
-// acc[i] += Σ_k WT[k*H + j] * in[i][k]  (WT: input-major copy; in: LDS rows of length ld)
-template <int NR>
-__device__ __forceinline__ void matvec_t(const float* __restrict__ WT, int H, int nin, const float* in, int ld,
-                                         int j, float (&acc)[NR]) {
-  int k = 0;
-  for (; k + 4 <= nin; k += 4) {
-    const float w0 = WT[(size_t)(k + 0) * H + j], w1 = WT[(size_t)(k + 1) * H + j];
-    const float w2 = WT[(size_t)(k + 2) * H + j], w3 = WT[(size_t)(k + 3) * H + j];
+// ---------------------------------------------------------------------------------------------
+// rows kernel: RR batch rows per block, KS k-groups of kCols threads (split-K matvecs)
+// ---------------------------------------------------------------------------------------------
+constexpr int kCols = 256;  // column threads per k-group (>= H)
+
+// acc[i] += Σ_{k in this k-group's slice} WT[k*H + j] · in[i][k]. With W row-major (out, in) the
+// same indexing computes the backward product Σ_jj W[jj][m] · d[i][jj] for column m.
+template <int NR, int KS>
+__device__ __forceinline__ void mv_part(const float* __restrict__ WT, int H, const float* in, int ld, int j, int kg,
+                                        float (&acc)[NR]) {
+  const int len = H / KS, k0 = kg * len, k1 = k0 + len;
+#pragma unroll 2
+  for (int k = k0; k < k1; k += 8) {
+    float w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = WT[(size_t)(k + u) * H + j];
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const float4 x = *reinterpret_cast<const float4*>(in + i * ld + k);
-      acc[i] = fmaf(w0, x.x, acc[i]);
-      acc[i] = fmaf(w1, x.y, acc[i]);
-      acc[i] = fmaf(w2, x.z, acc[i]);
-      acc[i] = fmaf(w3, x.w, acc[i]);
+      const float4 x0 = *reinterpret_cast<const float4*>(in + i * ld + k);
+      const float4 x1 = *reinterpret_cast<const float4*>(in + i * ld + k + 4);
+      acc[i] = fmaf(w[0], x0.x, acc[i]);
+      acc[i] = fmaf(w[1], x0.y, acc[i]);
+      acc[i] = fmaf(w[2], x0.z, acc[i]);
+      acc[i] = fmaf(w[3], x0.w, acc[i]);
+      acc[i] = fmaf(w[4], x1.x, acc[i]);
+      acc[i] = fmaf(w[5], x1.y, acc[i]);
+      acc[i] = fmaf(w[6], x1.z, acc[i]);
+      acc[i] = fmaf(w[7], x1.w, acc[i]);
     }
-  }
-  for (; k < nin; ++k) {
-    const float w = WT[(size_t)k * H + j];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) acc[i] = fmaf(w, in[i * ld + k], acc[i]);
   }
 }
 
-// per-row scalar slots in LDS
-enum { S_MEAN, S_LSRAW, S_STD, S_Z, S_A, S_LOGP, S_Q1, S_Q2, S_T1, S_T2, S_DQ1, S_DQ2, S_DA, S_DMEAN, S_DLS,
-       S_NSLOT };
+// sum the k-groups' partials into the kg == 0 threads (every thread of the block must call this)
+template <int NR, int KS>
+__device__ __forceinline__ void kreduce(float (&acc)[NR], float* part, int j, int kg) {
+  if (KS == 1) return;
+  if (kg > 0)
+#pragma unroll
+    for (int i = 0; i < NR; ++i) part[((kg - 1) * NR + i) * kCols + j] = acc[i];
+  __syncthreads();
+  if (kg == 0)
+    for (int g = 1; g < KS; ++g)
+#pragma unroll
+      for (int i = 0; i < NR; ++i) acc[i] += part[((g - 1) * NR + i) * kCols + j];
+  __syncthreads();
+}
 
-__global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
+// block-wide sum over NW waves of N (<= 32) per-thread partials -> out[0..N)
+template <int N, int NW>
+__device__ inline void block_sum_w(float (&v)[N], float (*red)[32], float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    float x = v[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    if (lane == 0) red[wave][i] = x;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < N) {
+    float t = 0.0f;
+    for (int w = 0; w < NW; ++w) t += red[w][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// per-row scalar slots in LDS
+enum { S_MEAN, S_LSRAW, S_STD, S_Z, S_A, S_LOGP, S_Q1, S_Q2, S_T1, S_T2, S_DQ1, S_DQ2, S_DMEAN, S_DLS, S_NSLOT };
+
+template <int RR, int KS>
+__global__ __launch_bounds__(kCols* KS) void sac_rows_kernel(RowsArgs a) {
+  constexpr int NW = kCols * KS / 64;
   const Layout& L = a.L;
   const int H = L.H, O = L.O, B = L.B;
   const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * R;
+  const int j = tid % kCols, kg = tid / kCols;
+  const bool col = j < H;
+  const bool lead = kg == 0 && col;  // finalises column j
+  const int r0 = blockIdx.x * RR;
   const float* P = a.params;
   const float* TG = a.targets;
 
-  __shared__ float s_x[2 * R][kXLd];                 // actor inputs: obs rows | next_obs rows
-  __shared__ float s_act[R], s_rew[R], s_term[R], s_eps[2 * R];
-  __shared__ __attribute__((aligned(16))) float s_h1[2 * R][SACF_MAX_HIDDEN];
-  __shared__ __attribute__((aligned(16))) float s_h2[2 * R][SACF_MAX_HIDDEN];
-  __shared__ __attribute__((aligned(16))) float s_g1[2][2 * R][SACF_MAX_HIDDEN];  // critic rows: (obs, ã) | (obs, a)
-  __shared__ __attribute__((aligned(16))) float s_g2[2][2 * R][SACF_MAX_HIDDEN];
-  __shared__ float s_red[4][32];
+  __shared__ float s_x[2 * RR][kXLd];  // actor inputs: obs rows | next_obs rows
+  __shared__ float s_act[RR], s_rew[RR], s_term[RR], s_eps[2 * RR];
+  __shared__ __attribute__((aligned(16))) float s_h1[2 * RR][SACF_MAX_HIDDEN];
+  __shared__ __attribute__((aligned(16))) float s_h2[2 * RR][SACF_MAX_HIDDEN];
+  __shared__ __attribute__((aligned(16))) float s_g1[2][2 * RR][SACF_MAX_HIDDEN];  // critic rows: (obs, ã) | (obs, a)
+  __shared__ __attribute__((aligned(16))) float s_g2[2][2 * RR][SACF_MAX_HIDDEN];
+  __shared__ float s_part[(KS > 1 ? KS - 1 : 1) * 2 * RR * kCols];
+  __shared__ float s_red[NW][32];
   __shared__ float s_sum[32];
-  __shared__ float s_row[S_NSLOT][2 * R];
+  __shared__ float s_row[S_NSLOT][2 * RR];
 
   // ---- batch rows + reparameterisation noise ----
-  if (tid < R) {
+  if (tid < RR) {
     const int r = r0 + tid;
     int64_t idx = r;
     uint32_t c[4] = {(uint32_t)r, (uint32_t)*a.step, (uint32_t)((uint64_t)*a.step >> 32), 0x5AC0u};
@@ -189,58 +237,58 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
     }
     for (int m = 0; m < O; ++m) {
       s_x[tid][m] = a.obs[idx * O + m];
-      s_x[R + tid][m] = a.nobs[idx * O + m];
+      s_x[RR + tid][m] = a.nobs[idx * O + m];
     }
     s_act[tid] = a.act[idx];
     s_rew[tid] = a.rew[idx];
     s_term[tid] = a.term[idx];
     s_eps[tid] = e0;
-    s_eps[R + tid] = e1;
+    s_eps[RR + tid] = e1;
   }
   __syncthreads();
 
-  // ---- actor forward on 2R rows (gaussian_policy.py:105-118) ----
-  const int j = tid;
-  const bool col = j < H;
-  if (col) {
-    float acc[2 * R];
+  // ---- actor forward on 2RR rows (gaussian_policy.py:105-118) ----
+  if (lead) {
+    float acc[2 * RR];
     const float b = P[L.p_b1 + j];
 #pragma unroll
-    for (int i = 0; i < 2 * R; ++i) acc[i] = b;
+    for (int i = 0; i < 2 * RR; ++i) acc[i] = b;
     for (int m = 0; m < O; ++m) {
       const float w = P[L.p_w1 + (int64_t)j * O + m];
 #pragma unroll
-      for (int i = 0; i < 2 * R; ++i) acc[i] = fmaf(w, s_x[i][m], acc[i]);
+      for (int i = 0; i < 2 * RR; ++i) acc[i] = fmaf(w, s_x[i][m], acc[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 2 * R; ++i) s_h1[i][j] = relu(acc[i]);
-  }
-  __syncthreads();
-  if (col) {
-    float acc[2 * R];
-    const float b = P[L.p_b2 + j];
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) acc[i] = b;
-    matvec_t<2 * R>(a.T, H, H, &s_h1[0][0], SACF_MAX_HIDDEN, j, acc);
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) s_h2[i][j] = relu(acc[i]);
+    for (int i = 0; i < 2 * RR; ++i) s_h1[i][j] = relu(acc[i]);
   }
   __syncthreads();
   {
-    float v[4 * R];
-    const float wm = col ? P[L.p_wm + j] : 0.0f, ws = col ? P[L.p_ws + j] : 0.0f;
+    float acc[2 * RR];
+    const float b = lead ? P[L.p_b2 + j] : 0.0f;
 #pragma unroll
-    for (int i = 0; i < 2 * R; ++i) {
-      const float h = col ? s_h2[i][j] : 0.0f;
-      v[i] = wm * h;
-      v[2 * R + i] = ws * h;
-    }
-    block_sum<4 * R>(v, s_red, s_sum);
+    for (int i = 0; i < 2 * RR; ++i) acc[i] = b;
+    if (col) mv_part<2 * RR, KS>(a.T, H, &s_h1[0][0], SACF_MAX_HIDDEN, j, kg, acc);
+    kreduce<2 * RR, KS>(acc, s_part, j, kg);
+    if (lead)
+#pragma unroll
+      for (int i = 0; i < 2 * RR; ++i) s_h2[i][j] = relu(acc[i]);
   }
-  if (tid < 2 * R) {  // TanhNormal.rsample_and_logprob (distributions.py:346-392)
+  __syncthreads();
+  {
+    float v[4 * RR];
+    const float wm = lead ? P[L.p_wm + j] : 0.0f, ws = lead ? P[L.p_ws + j] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2 * RR; ++i) {
+      const float h = lead ? s_h2[i][j] : 0.0f;
+      v[i] = wm * h;
+      v[2 * RR + i] = ws * h;
+    }
+    block_sum_w<4 * RR, NW>(v, s_red, s_sum);
+  }
+  if (tid < 2 * RR) {  // TanhNormal.rsample_and_logprob (distributions.py:346-392)
     const int i = tid;
     const float mean = s_sum[i] + P[L.p_bm];
-    const float ls_raw = s_sum[2 * R + i] + P[L.p_bs];
+    const float ls_raw = s_sum[2 * RR + i] + P[L.p_bs];
     const float log_std = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
     const float std = expf(log_std);
     const float z = mean + std * s_eps[i];
@@ -258,94 +306,93 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
   }
   __syncthreads();
 
-  // ---- critics on (obs, ã) rows 0..R-1 and (obs, a) rows R..2R-1 ----
-  for (int k = 0; k < 2; ++k) {
-    const float* C = P + L.q_base[k];
-    if (col) {
-      float acc[2 * R];
+  // ---- critics on (obs, ã) rows 0..RR-1 and (obs, a) rows RR..2RR-1 ----
+  if (lead) {
+    for (int k = 0; k < 2; ++k) {
+      const float* C = P + L.q_base[k];
+      float base[RR];
       const float b = C[L.c_b1 + j];
-      float base[R];
 #pragma unroll
-      for (int i = 0; i < R; ++i) base[i] = b;
+      for (int i = 0; i < RR; ++i) base[i] = b;
       for (int m = 0; m < O; ++m) {
         const float w = C[L.c_w1 + (int64_t)j * (O + 1) + m];
 #pragma unroll
-        for (int i = 0; i < R; ++i) base[i] = fmaf(w, s_x[i][m], base[i]);
+        for (int i = 0; i < RR; ++i) base[i] = fmaf(w, s_x[i][m], base[i]);
       }
       const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        acc[i] = fmaf(wa, s_row[S_A][i], base[i]);
-        acc[R + i] = fmaf(wa, s_act[i], base[i]);
+      for (int i = 0; i < RR; ++i) {
+        s_g1[k][i][j] = relu(fmaf(wa, s_row[S_A][i], base[i]));
+        s_g1[k][RR + i][j] = relu(fmaf(wa, s_act[i], base[i]));
       }
-#pragma unroll
-      for (int i = 0; i < 2 * R; ++i) s_g1[k][i][j] = relu(acc[i]);
     }
   }
   __syncthreads();
   for (int k = 0; k < 2; ++k) {
-    if (col) {
-      const float* C = P + L.q_base[k];
-      float acc[2 * R];
-      const float b = C[L.c_b2 + j];
+    const float* C = P + L.q_base[k];
+    float acc[2 * RR];
+    const float b = lead ? C[L.c_b2 + j] : 0.0f;
 #pragma unroll
-      for (int i = 0; i < 2 * R; ++i) acc[i] = b;
-      matvec_t<2 * R>(a.T + (size_t)(1 + k) * H * H, H, H, &s_g1[k][0][0], SACF_MAX_HIDDEN, j, acc);
+    for (int i = 0; i < 2 * RR; ++i) acc[i] = b;
+    if (col) mv_part<2 * RR, KS>(a.T + (size_t)(1 + k) * H * H, H, &s_g1[k][0][0], SACF_MAX_HIDDEN, j, kg, acc);
+    kreduce<2 * RR, KS>(acc, s_part, j, kg);
+    if (lead)
 #pragma unroll
-      for (int i = 0; i < 2 * R; ++i) s_g2[k][i][j] = relu(acc[i]);
-    }
+      for (int i = 0; i < 2 * RR; ++i) s_g2[k][i][j] = relu(acc[i]);
   }
   __syncthreads();
   {
-    float v[4 * R];
-    const float w0 = col ? P[L.q_base[0] + L.c_w3 + j] : 0.0f, w1 = col ? P[L.q_base[1] + L.c_w3 + j] : 0.0f;
+    float v[4 * RR];
+    const float w0 = lead ? P[L.q_base[0] + L.c_w3 + j] : 0.0f, w1 = lead ? P[L.q_base[1] + L.c_w3 + j] : 0.0f;
 #pragma unroll
-    for (int i = 0; i < 2 * R; ++i) {
-      v[i] = col ? w0 * s_g2[0][i][j] : 0.0f;
-      v[2 * R + i] = col ? w1 * s_g2[1][i][j] : 0.0f;
+    for (int i = 0; i < 2 * RR; ++i) {
+      v[i] = lead ? w0 * s_g2[0][i][j] : 0.0f;
+      v[2 * RR + i] = lead ? w1 * s_g2[1][i][j] : 0.0f;
     }
-    block_sum<4 * R>(v, s_red, s_sum);
+    block_sum_w<4 * RR, NW>(v, s_red, s_sum);
   }
-  if (tid < 2 * R) {
+  if (tid < 2 * RR) {
     s_row[S_Q1][tid] = s_sum[tid] + P[L.q_base[0] + L.c_b3];
-    s_row[S_Q2][tid] = s_sum[2 * R + tid] + P[L.q_base[1] + L.c_b3];
+    s_row[S_Q2][tid] = s_sum[2 * RR + tid] + P[L.q_base[1] + L.c_b3];
   }
   __syncthreads();
 
-  // ---- target critics on (next_obs, ã') (rows R..2R-1 of s_h1/s_h2 are free now) ----
+  // ---- target critics on (next_obs, ã') (rows RR..2RR-1 of s_h1/s_h2 are free now) ----
   for (int k = 0; k < 2; ++k) {
     const float* C = TG + (int64_t)k * L.q_size;
-    if (col) {
-      float acc[R];
+    if (lead) {
+      float acc[RR];
       const float b = C[L.c_b1 + j];
 #pragma unroll
-      for (int i = 0; i < R; ++i) acc[i] = b;
+      for (int i = 0; i < RR; ++i) acc[i] = b;
       for (int m = 0; m < O; ++m) {
         const float w = C[L.c_w1 + (int64_t)j * (O + 1) + m];
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = fmaf(w, s_x[R + i][m], acc[i]);
+        for (int i = 0; i < RR; ++i) acc[i] = fmaf(w, s_x[RR + i][m], acc[i]);
       }
       const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
 #pragma unroll
-      for (int i = 0; i < R; ++i) s_h1[R + i][j] = relu(fmaf(wa, s_row[S_A][R + i], acc[i]));
+      for (int i = 0; i < RR; ++i) s_h1[RR + i][j] = relu(fmaf(wa, s_row[S_A][RR + i], acc[i]));
     }
     __syncthreads();
-    if (col) {
-      float acc[R];
-      const float b = C[L.c_b2 + j];
+    {
+      float acc[RR];
+      const float b = lead ? C[L.c_b2 + j] : 0.0f;
 #pragma unroll
-      for (int i = 0; i < R; ++i) acc[i] = b;
-      matvec_t<R>(a.T + (size_t)(3 + k) * H * H, H, H, &s_h1[R][0], SACF_MAX_HIDDEN, j, acc);
+      for (int i = 0; i < RR; ++i) acc[i] = b;
+      if (col) mv_part<RR, KS>(a.T + (size_t)(3 + k) * H * H, H, &s_h1[RR][0], SACF_MAX_HIDDEN, j, kg, acc);
+      kreduce<RR, KS>(acc, s_part, j, kg);
+      if (lead)
 #pragma unroll
-      for (int i = 0; i < R; ++i) s_h2[R + i][j] = relu(acc[i]);
+        for (int i = 0; i < RR; ++i) s_h2[RR + i][j] = relu(acc[i]);
     }
     __syncthreads();
-    float v[R];
-    const float w3 = col ? C[L.c_w3 + j] : 0.0f;
+    float v[RR];
+    const float w3 = lead ? C[L.c_w3 + j] : 0.0f;
 #pragma unroll
-    for (int i = 0; i < R; ++i) v[i] = col ? w3 * s_h2[R + i][j] : 0.0f;
-    block_sum<R>(v, s_red, s_sum);
-    if (tid < R) s_row[k == 0 ? S_T1 : S_T2][tid] = s_sum[tid] + C[L.c_b3];
+    for (int i = 0; i < RR; ++i) v[i] = lead ? w3 * s_h2[RR + i][j] : 0.0f;
+    block_sum_w<RR, NW>(v, s_red, s_sum);
+    if (tid < RR) s_row[k == 0 ? S_T1 : S_T2][tid] = s_sum[tid] + C[L.c_b3];
     __syncthreads();
   }
 
@@ -353,11 +400,11 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
   const float invB = 1.0f / (float)B;
-  if (tid < R) {
+  if (tid < RR) {
     const int i = tid, r = r0 + i;
     const float q1a = s_row[S_Q1][i], q2a = s_row[S_Q2][i];
-    const float q1b = s_row[S_Q1][R + i], q2b = s_row[S_Q2][R + i];
-    const float tq = fminf(s_row[S_T1][i], s_row[S_T2][i]) - alpha * s_row[S_LOGP][R + i];
+    const float q1b = s_row[S_Q1][RR + i], q2b = s_row[S_Q2][RR + i];
+    const float tq = fminf(s_row[S_T1][i], s_row[S_T2][i]) - alpha * s_row[S_LOGP][RR + i];
     float qt = a.hp.rscale * s_rew[i] + ((1.0f - s_term[i]) * a.hp.gamma) * tq;
     qt = fminf(fmaxf(qt, -a.hp.clip), a.hp.clip);
     const float qmin = fminf(q1a, q2a);
@@ -367,8 +414,8 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
     s_row[S_DQ1][i] = -w1 * invB;
     s_row[S_DQ2][i] = -w2 * invB;
     const float dq1b = (2.0f * invB) * (q1b - qt), dq2b = (2.0f * invB) * (q2b - qt);
-    s_row[S_DQ1][R + i] = dq1b;
-    s_row[S_DQ2][R + i] = dq2b;
+    s_row[S_DQ1][RR + i] = dq1b;
+    s_row[S_DQ2][RR + i] = dq2b;
     a.sc.q_dq[0][r] = dq1b;
     a.sc.q_dq[1][r] = dq2b;
     const float logp = s_row[S_LOGP][i], act = s_row[S_A][i];
@@ -394,17 +441,17 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
   __syncthreads();
 
   // ---- critic backward: dg2 = dq·w3 ⊙ [g2 > 0], dg1 = (W2ᵀ dg2) ⊙ [g1 > 0] ----
-  for (int k = 0; k < 2; ++k) {
-    const float* C = P + L.q_base[k];
-    const float* dq = s_row[k == 0 ? S_DQ1 : S_DQ2];
-    if (col) {
+  if (lead) {
+    for (int k = 0; k < 2; ++k) {
+      const float* C = P + L.q_base[k];
+      const float* dq = s_row[k == 0 ? S_DQ1 : S_DQ2];
       const float w3 = C[L.c_w3 + j];
 #pragma unroll
-      for (int i = 0; i < 2 * R; ++i) {
+      for (int i = 0; i < 2 * RR; ++i) {
         const float g2 = s_g2[k][i][j];
         const float dg2 = g2 > 0.0f ? dq[i] * w3 : 0.0f;
-        if (i >= R) {
-          const int64_t o = (int64_t)(r0 + i - R) * H + j;
+        if (i >= RR) {
+          const int64_t o = (int64_t)(r0 + i - RR) * H + j;
           a.sc.q_g2[k][o] = g2;
           a.sc.q_dg2[k][o] = dg2;
         }
@@ -414,54 +461,38 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
   }
   __syncthreads();
   {
-    float v[2 * R];  // d(ã) partials for the policy rows, both critics
+    float v[2 * RR];  // d(ã) partials for the policy rows, both critics
     for (int k = 0; k < 2; ++k) {
       const float* C = P + L.q_base[k];
-      if (col) {
-        float acc[2 * R];
+      float acc[2 * RR];
 #pragma unroll
-        for (int i = 0; i < 2 * R; ++i) acc[i] = 0.0f;
-        // Σ_j W2[j][m]·dg2[i][j] with m = this column: W2 row-major reads are coalesced over m
-        const float* W2 = C + L.c_w2;
-        for (int jj = 0; jj < H; jj += 4) {
-          const float w0 = W2[(int64_t)(jj + 0) * H + j], w1 = W2[(int64_t)(jj + 1) * H + j];
-          const float w2 = W2[(int64_t)(jj + 2) * H + j], w3 = W2[(int64_t)(jj + 3) * H + j];
+      for (int i = 0; i < 2 * RR; ++i) acc[i] = 0.0f;
+      // Σ_jj W2[jj][m]·dg2[i][jj] with m = this column: W2 row-major reads are coalesced over m
+      if (col) mv_part<2 * RR, KS>(C + L.c_w2, H, &s_g2[k][0][0], SACF_MAX_HIDDEN, j, kg, acc);
+      kreduce<2 * RR, KS>(acc, s_part, j, kg);
+      const float wa = lead ? C[L.c_w1 + (int64_t)j * (O + 1) + O] : 0.0f;
 #pragma unroll
-          for (int i = 0; i < 2 * R; ++i) {
-            const float4 d = *reinterpret_cast<const float4*>(&s_g2[k][i][jj]);
-            acc[i] = fmaf(w0, d.x, acc[i]);
-            acc[i] = fmaf(w1, d.y, acc[i]);
-            acc[i] = fmaf(w2, d.z, acc[i]);
-            acc[i] = fmaf(w3, d.w, acc[i]);
-          }
+      for (int i = 0; i < 2 * RR; ++i) {
+        const float g1 = lead ? s_g1[k][i][j] : 0.0f;
+        const float dg1 = g1 > 0.0f ? acc[i] : 0.0f;
+        if (i < RR) {
+          v[k * RR + i] = wa * dg1;
+        } else if (lead) {
+          const int64_t o = (int64_t)(r0 + i - RR) * H + j;
+          a.sc.q_g1[k][o] = g1;  // (obs, a) rows feed the weight gradients
+          a.sc.q_dg1[k][o] = dg1;
         }
-        const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
-#pragma unroll
-        for (int i = 0; i < 2 * R; ++i) {
-          const float g1 = s_g1[k][i][j];
-          const float dg1 = g1 > 0.0f ? acc[i] : 0.0f;
-          if (i < R) {
-            v[k * R + i] = wa * dg1;
-          } else {
-            const int64_t o = (int64_t)(r0 + i - R) * H + j;
-            a.sc.q_g1[k][o] = g1;  // (obs, a) rows feed the weight gradients
-            a.sc.q_dg1[k][o] = dg1;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < R; ++i) v[k * R + i] = 0.0f;
       }
     }
-    block_sum<2 * R>(v, s_red, s_sum);
+    block_sum_w<2 * RR, NW>(v, s_red, s_sum);
   }
 
   // ---- actor backward on the obs rows ----
-  if (tid < R) {
+  if (tid < RR) {
     const int i = tid, r = r0 + i;
     const float act = s_row[S_A][i], z = s_row[S_Z][i], mean = s_row[S_MEAN][i], std = s_row[S_STD][i];
     const float ls_raw = s_row[S_LSRAW][i];
-    float dA = s_sum[i] + s_sum[R + i];
+    float dA = s_sum[i] + s_sum[RR + i];
     if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
     const float ainv = alpha * invB;
     const float d = z - mean, var = std * std;
@@ -476,10 +507,10 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
     a.sc.a_dhead[(int64_t)r * 2 + 1] = dls;
   }
   __syncthreads();
-  if (col) {
+  if (lead) {
     const float wm = P[L.p_wm + j], ws = P[L.p_ws + j];
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
+    for (int i = 0; i < RR; ++i) {
       const float h2 = s_h2[i][j];
       const float dh2 = h2 > 0.0f ? (wm * s_row[S_DMEAN][i] + ws * s_row[S_DLS][i]) : 0.0f;
       const int64_t o = (int64_t)(r0 + i) * H + j;
@@ -489,29 +520,20 @@ __global__ __launch_bounds__(kThreads) void sac_rows_kernel(RowsArgs a) {
     }
   }
   __syncthreads();
-  if (col) {
-    float acc[R];
+  {
+    float acc[RR];
 #pragma unroll
-    for (int i = 0; i < R; ++i) acc[i] = 0.0f;
-    const float* W2 = P + L.p_w2;
-    for (int jj = 0; jj < H; jj += 4) {
-      const float w0 = W2[(int64_t)(jj + 0) * H + j], w1 = W2[(int64_t)(jj + 1) * H + j];
-      const float w2 = W2[(int64_t)(jj + 2) * H + j], w3 = W2[(int64_t)(jj + 3) * H + j];
+    for (int i = 0; i < RR; ++i) acc[i] = 0.0f;
+    if (col) mv_part<RR, KS>(P + L.p_w2, H, &s_h2[0][0], SACF_MAX_HIDDEN, j, kg, acc);
+    kreduce<RR, KS>(acc, s_part, j, kg);
+    if (lead) {
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const float4 dd = *reinterpret_cast<const float4*>(&s_h2[i][jj]);
-        acc[i] = fmaf(w0, dd.x, acc[i]);
-        acc[i] = fmaf(w1, dd.y, acc[i]);
-        acc[i] = fmaf(w2, dd.z, acc[i]);
-        acc[i] = fmaf(w3, dd.w, acc[i]);
+      for (int i = 0; i < RR; ++i) {
+        const float h1 = s_h1[i][j];
+        const int64_t o = (int64_t)(r0 + i) * H + j;
+        a.sc.a_h1[o] = h1;
+        a.sc.a_dh1[o] = h1 > 0.0f ? acc[i] : 0.0f;
       }
-    }
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const float h1 = s_h1[i][j];
-      const int64_t o = (int64_t)(r0 + i) * H + j;
-      a.sc.a_h1[o] = h1;
-      a.sc.a_dh1[o] = h1 > 0.0f ? acc[i] : 0.0f;
     }
   }
 }
@@ -946,7 +968,23 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   a.L = h->L;
   a.hp = h->hp;
   SDev g(h->device);
-  hipLaunchKernelGGL(sac_rows_kernel, dim3(h->L.B / R), dim3(kThreads), 0, h->stream, a);
+  // rows-kernel shape: RR batch rows per block x KS k-groups (SACF_ROWS=RRxKS overrides, e.g. 4x1).
+  // Measured on MI355X, H = 256, B = 256 (grad steps/s): 4x1 5131, 2x2 7430, 2x4 8364, 1x4 9682.
+  int rr = 1, ks = 4;
+  if (const char* e = getenv("SACF_ROWS")) {
+    if (sscanf(e, "%dx%d", &rr, &ks) != 2) rr = 1, ks = 4;
+  }
+  if (h->L.H / ks < 8 || (h->L.H / ks) % 8) ks = 1;
+#define ROWS(RR_, KS_) \
+  hipLaunchKernelGGL((sac_rows_kernel<RR_, KS_>), dim3(h->L.B / RR_), dim3(kCols * KS_), 0, h->stream, a)
+  if (rr == 4 && ks == 1) ROWS(4, 1);
+  else if (rr == 4 && ks == 2) ROWS(4, 2);
+  else if (rr == 2 && ks == 2) ROWS(2, 2);
+  else if (rr == 1 && ks == 4) ROWS(1, 4);
+  else if (rr == 2 && ks == 4) ROWS(2, 4);
+  else if (ks == 1) ROWS(2, 1);
+  else ROWS(1, 4);
+#undef ROWS
   WgradArgs w;
   memset(&w, 0, sizeof(w));
   for (int i = 0; i < h->n_mats; ++i) w.mats[i] = h->mats[i];

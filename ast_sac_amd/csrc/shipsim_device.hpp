@@ -86,6 +86,7 @@ struct Ship {
   double spd_a, spd_b;            // ship-speed PI ei | thrust PID ei ; shaft PI ei | thrust PID prev
   double log_rudder, log_thrust, log_ect, log_n, log_e;  // simulation_results[-1]
   double wp_prev_n, wp_prev_e, wp_n, wp_e;  // navigate.north/east[k-1], [k] (register cache)
+  double seg_alpha, seg_sin, seg_cos;        // atan2 / sincos of the cached segment (los_guidance)
   double end_n, end_e;            // navigate.north/east[-1]
   int32_t next_wpt, n_route, stop;
 };
@@ -219,11 +220,8 @@ __device__ __forceinline__ void integrate(Ship& s, const Deriv& d, double dt, do
 // ---------------------------------------------------------------------------------------------
 // LOS_guidance.py:100-117 (k = next_wpt; waypoints k-1, k are register-cached)
 __device__ __forceinline__ double los_guidance(const ShipConst& c, Ship& s, double x, double y) {
-  double dx = s.wp_n - s.wp_prev_n;
-  double dy = s.wp_e - s.wp_prev_e;
-  double alpha_k = atan2(dy, dx);
-  double sa, ca;
-  sincos(alpha_k, &sa, &ca);
+  // alpha_k = atan2(dy, dx) and its sin/cos depend on the segment only: cached by segment_changed()
+  const double alpha_k = s.seg_alpha, sa = s.seg_sin, ca = s.seg_cos;
   double e_ct = -(x - s.wp_prev_n) * sa + (y - s.wp_prev_e) * ca;
   s.e_ct = e_ct;
   if (e_ct * e_ct >= c.los_r2) {
@@ -242,6 +240,14 @@ __device__ __forceinline__ bool next_wpt_advance(const ShipConst& c, const Ship&
   return (dn * dn + de * de <= c.ra2) && (s.n_route > s.next_wpt + 1);
 }
 
+// LOS_guidance.py:104-106 per-segment terms: recompute whenever wp_prev_* / wp_* change
+__device__ __forceinline__ void segment_changed(Ship& s) {
+  const double dx = s.wp_n - s.wp_prev_n;
+  const double dy = s.wp_e - s.wp_prev_e;
+  s.seg_alpha = atan2(dy, dx);
+  sincos(s.seg_alpha, &s.seg_sin, &s.seg_cos);
+}
+
 // reload the cached LOS segment (k-1, k) from the route table
 __device__ __forceinline__ void load_segment(Ship& s, const double* __restrict__ rn, const double* __restrict__ re) {
   s.wp_prev_n = rn[s.next_wpt - 1];
@@ -250,6 +256,7 @@ __device__ __forceinline__ void load_segment(Ship& s, const double* __restrict__
   s.wp_e = re[s.next_wpt];
   s.end_n = rn[s.n_route - 1];
   s.end_e = re[s.n_route - 1];
+  segment_changed(s);
 }
 
 // PidController.pid_ctrl controllers.py:106-118

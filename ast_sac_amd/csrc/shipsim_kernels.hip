@@ -58,6 +58,20 @@ struct DevState {
   static constexpr int kEnvArrays = 14;
   static constexpr int kShipArrays = 22;
 };
+#ifdef SHIPSIM_PHASE_TIMING
+// timing build only (scripts/phase_timing.sh): per-phase wall-clock cycles summed over waves
+__device__ unsigned long long g_phase_cycles[8];
+#define PT_MARK(k)                                                     \
+  do {                                                                 \
+    const unsigned long long _t = wall_clock64();                      \
+    pt_acc[k] += _t - pt_last;                                         \
+    pt_last = _t;                                                      \
+  } while (0)
+#else
+#define PT_MARK(k) \
+  do {             \
+  } while (0)
+#endif
 // dec_flags bits (per env, persistent across calls)
 #define DF_AWAITING 1
 #define DF_HAVE_IW 2
@@ -180,6 +194,9 @@ __device__ __forceinline__ double shfl_d(double x, int src) {
   return __hiloint2double(hi, lo);
 }
 
+constexpr double kCosPhiAh = 0.36650122672429719;  // cos(68.5°) (only used against a 1e-9 band)
+constexpr double kSinPhiAh = 0.93041756798202460;  // sin(68.5°)
+
 __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
   const double os_l = 25.0;  // ShipLinearModel default length (sbmpc_misc.py:86, Q7)
   const double d_safe = 1000.0, d_close = 2000.0;
@@ -226,6 +243,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     const double lim = max_d_safe + 1e-3;
     if (e0x * e0x + e0y * e0y > lim * lim && mx * mx + my * my > lim * lim) return 0.0 + H2;
   }
+  const double lim2 = (max_d_safe * (1.0 + 1e-9)) * (max_d_safe * (1.0 + 1e-9));
   double ox = in.ob_x, oy = in.ob_y, sx = in.os_x, sy = in.os_y, sv = in.os_v;
   double H1 = 0, t = 0;
   for (int i = 0; i < n_samp; ++i) {
@@ -238,29 +256,44 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     }
     t += DT;
     double d0 = ox - sx, d1 = oy - sy;
-    double dist = sqrt(d0 * d0 + d1 * d1);
+    const double d2s = d0 * d0 + d1 * d1;
     double R = 0, C = 0;
     // R and C stay 0 unless dist < d_safe_i <= max_d_safe, so the sector geometry (atan2, wrap,
     // norms) is only evaluated there; identical results to the reference's `dist < d_close` block.
+    // d2s >= lim2 already implies sqrt(d2s) >= max_d_safe, so the sqrt is skipped for far samples.
+    if (d2s < lim2) {
+    const double dist = sqrt(d2s);
     if (dist < d_close && dist < max_d_safe) {
       double ss = (i == 0) ? sp0 : sp, cs = (i == 0) ? cp0 : cp;
       double vs0 = -ss * ud + cs * sv;
       double vs1 = cs * ud + ss * sv;
-      double phi_o = wrap_pmpi(atan2(-d1, -d0) - in.ob_psi + kPi / 2);
+      // sector of phi_o = wrap(atan2(-d1, -d0) - psi_o + pi/2) against PHI_AH == PHI_OT = θ: e is
+      // (-d0, -d1) rotated by pi/2 - psi_o, so phi_o = angle(e); phi_o > θ <=> sin(angle(e) - θ) >= 0
+      // and e_y > 0. Within 1e-9 rad of a decision boundary the reference expression is evaluated.
+      const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
+      const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
+      int sector;  // 0: phi_o < PHI_AH, 1: phi_o > PHI_OT, 2: equal
+      if (fabs(cr) > 1e-9 * dist && fabs(ey) > 1e-9 * dist) {
+        sector = (cr >= 0 && ey > 0) ? 1 : 0;
+      } else {
+        const double phi_o = wrap_pmpi(atan2(-d1, -d0) - in.ob_psi + kPi / 2);
+        sector = (phi_o < PHI_AH) ? 0 : ((phi_o > PHI_OT) ? 1 : 2);
+      }
       double d_safe_i;
-      if (phi_o < PHI_AH) d_safe_i = d_safe + in.obs_l / 2;
-      else if (phi_o > PHI_OT) d_safe_i = 0.5 * d_safe + in.obs_l / 2;
+      if (sector == 0) d_safe_i = d_safe + in.obs_l / 2;
+      else if (sector == 1) d_safe_i = 0.5 * d_safe + in.obs_l / 2;
       else d_safe_i = d_safe + in.obs_w / 2;
       double dot = vs0 * vo0 + vs1 * vo1;
       double ns = sqrt(vs0 * vs0 + vs1 * vs1);
       if (dot > cos_ot * ns * no && ns > no) d_safe_i = d_safe + os_l / 2 + in.obs_l / 2;
       if (dist < d_safe_i) {
-        R = (1 / pow(fabs(t - 0.0), 1.0)) * pow(d_safe / dist, 4.0);
+        R = (1 / fabs(t - 0.0)) * pow(d_safe / dist, 4.0);  // pow(|t|, 1.0) == |t| exactly
         double k_coll = 1e-6 * os_l * in.obs_l;
         double w0 = vs0 - vo0, w1 = vs1 - vo1;
         double nrm = sqrt(w0 * w0 + w1 * w1);
         C = k_coll * (nrm * nrm);
       }
+    }
     }
     double H0 = C * R + 0.0 * 0;
     if (H0 > H1) H1 = H0;
@@ -572,7 +605,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         int L = s.n_route;
         rn[L] = s.end_n; re[L] = s.end_e;
         rn[L - 1] = iw_n; re[L - 1] = iw_e;
-        if (s.next_wpt == L - 1) { s.wp_n = iw_n; s.wp_e = iw_e; }
+        if (s.next_wpt == L - 1) {
+          s.wp_n = iw_n;
+          s.wp_e = iw_e;
+          segment_changed(s);
+        }
         s.n_route = L + 1;
       }
       travel_dist = 0;
@@ -595,6 +632,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 
   const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
   bool going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
+#ifdef SHIPSIM_PHASE_TIMING
+  unsigned long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long pt_last = wall_clock64();
+#endif
   while (__any(going)) {
     // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
@@ -626,6 +667,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       }
     }
 
+    PT_MARK(0);
     // ---- ship ticks (test_step :345-445 / obs_step :447-536) ----
     double my_speed_out = 0.0, dtravel = 0.0, dtime = 0.0;
     if (going) {
@@ -651,6 +693,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         }
       }
     }
+    PT_MARK(1);
     // ---- own-ship map queries, split over the ship's sub-lanes ----
     double d2 = INFINITY;
     bool gr = false;
@@ -674,6 +717,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       gri |= __shfl_xor(gri, m, 64);
     }
     const double my_ground = sqrt(d2);
+    PT_MARK(2);
     bool my_end = false, my_outside = false, my_roa = false;
     if (going) {
       my_end = sqrt((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e)) <= 200;
@@ -704,14 +748,14 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       ns[3] = (float)On; ns[4] = (float)Oe; ns[5] = (float)Oyaw; ns[6] = (float)Ospeed; ns[7] = (float)Oect;
       st4[0] = ns[0]; st4[1] = ns[1]; st4[2] = ns[3]; st4[3] = ns[4];
       // get_reward_and_env_info (reward_function.py:59-270)
-      double dx = On - Tn, dy = Oe - Te;
-      double dist = sqrt(dx * dx + dy * dy);
-      double beta = floor_mod((atan2(dy, dx) - Th) + kPi, 2 * kPi) - kPi;
-      const bool enc_ok = !(fabs(beta) > 165.0 * (kPi / 180.0));  // head-on or crossing (Q5)
       const bool is_collision = ((Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe)) < 2500.0;
       const bool is_tg = Tf & 1, is_og = Of & 1;
       const bool is_tnav = fabs(Tect) > 3000;
       const bool is_onav = (travel_dist > P.AB_seg * 2) || (travel_time > INFINITY) || (fabs(Oect) > 500);
+      double dx = On - Tn, dy = Oe - Te;
+      double dist = sqrt(dx * dx + dy * dy);
+      double beta = floor_mod((atan2(dy, dx) - Th) + kPi, 2 * kPi) - kPi;
+      const bool enc_ok = !(fabs(beta) > 165.0 * (kPi / 180.0));  // head-on or crossing (Q5)
       double r0 = (dist < 10000 && enc_ok) ? rd4(0, 200000000, dist) : 0.0;
       double r1 = (Tground <= 1000) ? rd4(0, 175000, Tground) : 0.0;
       double r2 = rd3(3000, 1250000, fabs(Tect));
@@ -776,7 +820,12 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       }
       going = !ready && (max_ticks <= 0 || ticks < max_ticks);
     }
+    PT_MARK(3);
   }
+#ifdef SHIPSIM_PHASE_TIMING
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 4; ++k) atomicAdd(&g_phase_cycles[k], pt_acc[k]);
+#endif
 
   if (!valid || !touched) return;
 #ifdef SHIPSIM_DEBUG_ENV
@@ -970,6 +1019,15 @@ static void launch_step(shipsim_handle* h, int lpe, const float* action, const u
 extern "C" {
 
 int32_t shipsim_abi_version(void) { return SHIPSIM_ABI_VERSION; }
+
+#ifdef SHIPSIM_PHASE_TIMING
+// timing builds only (not part of the ABI): read and clear the per-phase cycle sums
+int shipsim_debug_phase_cycles(unsigned long long* out8) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 const char* shipsim_build_info(void) {
   return "shipsim gfx950 HIP (fp64, lane-pair AST kernel, wave-cooperative SBMPC) built " __DATE__ " " __TIME__;

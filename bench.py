@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round1_pmc_traffic.json"))
     p.add_argument("--sac-steps", type=int, default=300, help="timed SAC grad steps (0 = skip the SAC line)")
     p.add_argument("--sac-batch", type=int, default=256, help="SAC batch per GPU")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, one GPU per rank) | gloo (rehearsal)")
     return p.parse_args()
 
 
@@ -151,9 +152,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":  # multi-rank rehearsal on fewer GPUs than ranks
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     mach = abi.MACH_DETAILED if args.machinery == "detailed" else abi.MACH_SIMPLIFIED
