@@ -247,6 +247,26 @@ def ast_config(collav="sbmpc", time_step=4, machinery=MACH_DETAILED):
     return cfg
 
 
+# MachineryModeParams of run/env_setup.py:62-81 (main_engine_capacity 2160 kW, diesel_gen_capacity 510 kW)
+MACHINERY_MODES = {
+    "PTO": (2160e3, 0.0, SG_GEN),         # pto_mode :62-67
+    "PTI": (0.0, 2 * 510e3, SG_MOTOR),    # pti_mode :69-74 (the mode the runner uses, :82-84)
+    "MEC": (2160e3, 510e3, SG_OFF),       # mec_mode :76-81
+}
+
+
+def set_machinery_mode(cfg, mode, ships=(0, 1)):
+    """Select the active MachineryMode of the given ships (MachineryModes([mode]) with
+    machinery_operating_mode=0): PTO / PTI / MEC with the env_setup capacities."""
+    me, el, sg = MACHINERY_MODES[mode]
+    for i in ships:
+        s = cfg.ship[i]
+        s.main_engine_capacity = me
+        s.electrical_capacity = el
+        s.shaft_generator_state = sg
+    return cfg
+
+
 def c1_config(collav="none", time_step=30):
     """run_colav/run_simplified_model.py:55-233 (MultiShipNonIWEnv)."""
     cfg = _base(KIND_NONIW, collav, time_step, MACH_SIMPLIFIED)

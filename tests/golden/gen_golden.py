@@ -557,6 +557,103 @@ def gen_rl():
     np.savez_compressed(os.path.join(OUT, "rl_env_simplified.npz"), **out)
 
 
+class _machinery_mode:
+    """Build run/env_setup.py's scenario with MachineryModes([<mode>]) instead of [pti_mode]
+    (env_setup.py:62-84 constructs pto/pti/mec modes; the runner only uses PTI). The mode objects
+    the reference creates are captured and the requested one is handed to MachineryModes."""
+
+    def __init__(self, state):  # 'GEN' (PTO), 'MOTOR' (PTI), 'OFF' (MEC)
+        self.state = state
+
+    def __enter__(self):
+        import run.env_setup as es
+        from rl_env.ship_in_transit.sub_systems import ship_engine as se
+        made = []
+        state = self.state
+
+        class RecMode(se.MachineryMode):
+            def __init__(self, params):
+                super().__init__(params)
+                made.append(self)
+
+        class PickModes(se.MachineryModes):
+            def __init__(self, list_of_modes):
+                super().__init__([m for m in made if m.shaft_generator_state == state])
+
+        self._es, self._saved = es, (es.MachineryMode, es.MachineryModes)
+        es.MachineryMode, es.MachineryModes = RecMode, PickModes
+        return self
+
+    def __exit__(self, *exc):
+        self._es.MachineryMode, self._es.MachineryModes = self._saved
+
+
+MODE_TAGS = {"GEN": "pto", "MOTOR": "pti", "OFF": "mec"}
+
+
+def gen_modes():
+    """C5 machinery modes PTO / MEC: decision-level episodes like gen_rl (F4) for collav none/sbmpc."""
+    from run.env_setup import prepare_multiship_rl_env
+    tabs = action_tables()[:3]
+    out = {}
+    for state in ("GEN", "OFF"):
+        for collav in ("none", "sbmpc"):
+            with _machinery_mode(state):
+                env, _ = prepare_multiship_rl_env(rl_args(collav))
+            eps = run_rl_episodes(env, tabs)
+            pack_episodes(f"{MODE_TAGS[state]}_{collav}", eps, out)
+            for i, e in enumerate(eps):
+                print("modes", state, collav, "ep", i, "ticks", [d["nticks"] for d in e["dec"]],
+                      "bits", hex(e["dec"][-1]["bits"]), "fuel", e["test_log"][-1, -1])
+    out["log_cols"] = np.array(AST_KEYS)
+    np.savez_compressed(os.path.join(OUT, "rl_env_modes.npz"), **out)
+
+
+REWARD_TRACKER_FIELDS = ("ship_collision", "test_ship_grounding", "test_ship_nav_failure", "obs_ship_grounding",
+                         "obs_ship_nav_failure", "from_test_ship", "from_obs_ship", "total")
+
+
+def gen_traj():
+    """f1: the full simulation_results dict (every key, reference order) of both ships, the
+    RewardTracker lists, ShipAssets.time_list / integrator_term, waypoint_sampling_times and the
+    animation lists, for a few episodes (machinery modes x collav, incl. a sampling failure)."""
+    from run.env_setup import prepare_multiship_rl_env
+    tabs = action_tables()
+    cases = [("MOTOR", "none", (1, 3)), ("MOTOR", "sbmpc", (2,)), ("MOTOR", "simple", (1,)),
+             ("GEN", "none", (2,)), ("OFF", "none", (1,))]
+    out = {}
+    for state, collav, tab_ids in cases:
+        with _machinery_mode(state):
+            env, _ = prepare_multiship_rl_env(rl_args(collav))
+        for k, ti in enumerate(tab_ids):
+            p = f"{MODE_TAGS[state]}_{collav}_ep{k}"
+            env.reset()
+            acts = []
+            for a_norm in tabs[ti]:
+                a = scaled_action(a_norm)
+                acts.append(a[0])
+                _, _, d, _ = env.step(a.copy())
+                if d:
+                    break
+            out[p + "_a"] = np.array(acts, np.float32)
+            for name, ship in (("test", env.test), ("obs", env.obs)):
+                sr = ship.ship_model.simulation_results
+                keys = list(sr.keys())
+                out[p + f"_{name}_keys"] = np.array(keys)
+                out[p + f"_{name}_sr"] = np.array([sr[key] for key in keys], np.float64).T
+                out[p + f"_{name}_time_list"] = np.array(ship.time_list, np.float64)
+                out[p + f"_{name}_integrator_term"] = np.array(ship.integrator_term, np.float64)
+            for f in REWARD_TRACKER_FIELDS:
+                out[p + f"_rt_{f}"] = np.array(getattr(env.reward_tracker, f), np.float64)
+            out[p + "_wst"] = np.array(env.waypoint_sampling_times, np.float64)
+            out[p + "_waypoint_samples"] = np.array(env.waypoint_samples, np.float64).reshape(-1, 2)
+            out[p + "_is_collision"] = np.array(env.is_collision_list, np.int64)
+            out[p + "_imminent"] = np.array(env.is_collision_imminent_list, np.int64)
+            print("traj", p, "rows", out[p + "_test_sr"].shape, "keys", len(out[p + "_test_keys"]),
+                  "rt", len(out[p + "_rt_total"]), "wst", out[p + "_wst"])
+    np.savez_compressed(os.path.join(OUT, "rl_env_traj.npz"), **out)
+
+
 # ----------------------------------------------------------------------------------------------
 # F5 SBMPC known answers, F6 geometry / reward pure functions
 # ----------------------------------------------------------------------------------------------
@@ -718,3 +815,7 @@ if __name__ == "__main__":
         gen_sac()
     if "rl" in what:
         gen_rl()
+    if "modes" in what:
+        gen_modes()
+    if "traj" in what:
+        gen_traj()
