@@ -38,6 +38,11 @@ struct ShipConst {
   double avail_me, avail_el, cap_me, cap_el;   // available powers; torque caps avail/5*pi/30
   double d_me, d_hsg, r_me, r_hsg, jp, kp_prop, thrust_coeff, shaft_speed_max;
   double init_omega;
+  // MachineryMode.distribute_load / BaseMachineryModel.fuel_consumption (ship_engine.py:46-76, 259-295):
+  // logging only (trajectory recording); capacities of the active mode, hotel load, fuel coefficients
+  double mode_me, mode_el, hotel, avail_prop;
+  double fa_me, fb_me, fc_me, fa_dg, fb_dg, fc_dg;
+  int32_t sg_state, pad_sg_;
   // controllers (controllers.py:45-209; run_colav ThrustFromSpeedSetPoint)
   double kp_ship_speed, ki_ship_speed, kp_shaft_speed, ki_shaft_speed, init_shaft_ei;
   double spd_kp, spd_ki, spd_kd, max_thrust;
@@ -289,6 +294,34 @@ __device__ __forceinline__ double speed_ctrl(const ShipConst& c, Ship& s, double
   }
   double t = pid(s.spd_a, s.spd_b, c.spd_kp, c.spd_kd, c.spd_ki, dt, setpoint, u);
   return sat(t, -c.max_thrust, c.max_thrust);
+}
+
+// BaseMachineryModel.fuel_consumption (ship_engine.py:266-295) with MachineryMode.distribute_load
+// (:46-76) and spec_fuel_cons (:259-264): f = {fuel_cons_me, fuel_cons_electrical, fuel_cons}
+__device__ __forceinline__ void fuel_consumption(const ShipConst& c, double load, double dt, double f[3]) {
+  const double total = load * c.avail_prop;
+  double l_me, l_el, p_me, p_el;
+  if (c.sg_state == SHIPSIM_SG_MOTOR) {
+    l_me = py_min(total, c.mode_me);
+    l_el = total + c.hotel - l_me;
+    p_el = l_el / c.mode_el;
+    p_me = (c.mode_me == 0) ? 0.0 : l_me / c.mode_me;
+  } else if (c.sg_state == SHIPSIM_SG_GEN) {
+    l_el = py_min(c.hotel, c.mode_el);
+    l_me = total + c.hotel - l_el;
+    p_me = l_me / c.mode_me;
+    p_el = (c.mode_el == 0) ? 0.0 : l_el / c.mode_el;
+  } else {
+    l_me = total;
+    l_el = c.hotel;
+    p_me = l_me / c.mode_me;
+    p_el = l_el / c.mode_el;
+  }
+  const double rate_me = (l_me == 0) ? 0.0 : l_me * ((c.fa_me * (p_me * p_me) + c.fb_me * p_me + c.fc_me) / 3.6e9);
+  const double rate_el = (p_el == 0) ? 0.0 : l_el * ((c.fa_dg * (p_el * p_el) + c.fb_dg * p_el + c.fc_dg) / 3.6e9);
+  f[0] = f[0] + rate_me * dt;
+  f[1] = f[1] + rate_el * dt;
+  f[2] = f[2] + (rate_me + rate_el) * dt;
 }
 
 // HeadingByReferenceController.rudder_angle_from_heading_setpoint :246-255

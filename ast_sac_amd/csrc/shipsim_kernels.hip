@@ -113,6 +113,23 @@ struct ConstBuf {
 // the min over all edges whenever the true min is <= 1000 m, and is > 1000 m (or +inf) otherwise.
 constexpr double kGroundReach = 1000.0;
 
+// Trajectory record (shipsim_set_trajectory): simulation_results rows per ship, RewardTracker rows per
+// env. Row t of a ship is its t-th store_simulation_data since reset (row 0 = init_step); env row t is
+// the reward of tick t + 1 of the episode. Rows past `cap` are dropped; len keeps counting.
+struct Traj {
+  double* ship;   // [q][cap][SHIPSIM_TRAJ_SHIP_COLS]
+  double* env;    // [env][cap][SHIPSIM_TRAJ_ENV_COLS] (may be null)
+  double* fuel;   // [q][3] fuel accumulators (library-owned)
+  int32_t* len;   // [env] ship rows recorded since reset
+  int32_t cap;
+  __device__ __forceinline__ double* ship_row(int q, int t) const {
+    return (t >= 0 && t < cap) ? ship + ((size_t)q * cap + t) * SHIPSIM_TRAJ_SHIP_COLS : nullptr;
+  }
+  __device__ __forceinline__ double* env_row(int e, int t) const {
+    return (env && t >= 0 && t < cap) ? env + ((size_t)e * cap + t) * SHIPSIM_TRAJ_ENV_COLS : nullptr;
+  }
+};
+
 __device__ __forceinline__ void load_ship(const DevState& S, int q, Ship& s) {
   s.n = S.f(SF_N)[q]; s.e = S.f(SF_E)[q]; s.yaw = S.f(SF_YAW)[q];
   s.u = S.f(SF_U)[q]; s.v = S.f(SF_V)[q]; s.r = S.f(SF_R)[q];
@@ -149,12 +166,12 @@ __device__ __forceinline__ const ShipConst* stage_consts(const Params& P, ShipCo
 
 // one controlled ship tick: autopilot -> speed control -> store -> update -> integrate -> next_time
 // (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339)
-template <bool DETAILED>
+template <bool DETAILED, bool REC = false>
 __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const Params& P, Ship& s,
                                                       const double* __restrict__ rn, const double* __restrict__ re,
                                                       double offset, double speed_factor, double mach_dt,
                                                       int simple_collav_flag /*0 none, 1 rl(-15deg), 2 noniw(+15)*/,
-                                                      bool imminent) {
+                                                      bool imminent, double* row = nullptr, double* fuel = nullptr) {
   const double N = s.n, E = s.e, H = s.yaw, U = s.u;
   if (next_wpt_advance(c, s, N, E)) {
     s.next_wpt += 1;
@@ -175,8 +192,34 @@ __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const 
   s.log_n = N;
   s.log_e = E;
   s.log_thrust = DETAILED ? (c.thrust_coeff * s.omega * fabs(s.omega)) / 1000 : ctrl;
+  if (REC) {  // the full store_simulation_data row (ship_model.py:903-942) + ShipAssets trackers
+    if (DETAILED) fuel_consumption(c, ctrl, mach_dt, fuel);
+    if (row) {
+      row[SHIPSIM_TS_TIME] = s.time; row[SHIPSIM_TS_NORTH] = N; row[SHIPSIM_TS_EAST] = E;
+      row[SHIPSIM_TS_YAW] = H; row[SHIPSIM_TS_RUDDER] = rudder; row[SHIPSIM_TS_U] = U;
+      row[SHIPSIM_TS_V] = s.v; row[SHIPSIM_TS_R] = s.r; row[SHIPSIM_TS_OMEGA] = DETAILED ? s.omega : 0.0;
+      row[SHIPSIM_TS_THRUST] = DETAILED ? c.thrust_coeff * s.omega * fabs(s.omega) : ctrl;
+      row[SHIPSIM_TS_E_CT] = s.e_ct; row[SHIPSIM_TS_E_PSI] = fabs(H - href); row[SHIPSIM_TS_LOAD] = ctrl;
+      row[SHIPSIM_TS_FUEL_ME] = DETAILED ? fuel[0] : 0.0; row[SHIPSIM_TS_FUEL_EL] = DETAILED ? fuel[1] : 0.0;
+      row[SHIPSIM_TS_FUEL] = DETAILED ? fuel[2] : 0.0; row[SHIPSIM_TS_E_CT_INT] = s.e_ct_int;
+      row[SHIPSIM_TS_NEXT_WPT] = (double)s.next_wpt; row[SHIPSIM_TS_REPEAT] = 0.0;
+      row[SHIPSIM_TS_TIME_LIST] = s.time;
+    }
+  }
   Deriv d = differentials(c, P, s, ctrl, rudder, DETAILED);
   integrate(s, d, P.dt, mach_dt, DETAILED);
+}
+
+// store_last_simulation_data (ship_model.py:946-957) of a stopped ship: the previous row repeated
+// with the current time; ShipAssets.time_list gets the time after the first next_time (env.py:451-465)
+__device__ __forceinline__ void record_last(const Traj& T, int q, int t, double time, double time_list) {
+  double* row = T.ship_row(q, t);
+  const double* prev = T.ship_row(q, t - 1);
+  if (!row || !prev) return;
+  for (int k = 0; k < SHIPSIM_TRAJ_SHIP_COLS; ++k) row[k] = prev[k];
+  row[SHIPSIM_TS_TIME] = time;
+  row[SHIPSIM_TS_REPEAT] = 1.0;
+  row[SHIPSIM_TS_TIME_LIST] = time_list;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -197,10 +240,100 @@ __device__ __forceinline__ double shfl_d(double x, int src) {
 constexpr double kCosPhiAh = 0.36650122672429719;  // cos(68.5°) (only used against a 1e-9 band)
 constexpr double kSinPhiAh = 0.93041756798202460;  // sin(68.5°)
 
+// sqrt(d2s) < D, decided without the sqrt unless d2s is within 1e-12 of D² (sqrt is correctly
+// rounded and monotone, so outside that band the comparison cannot change)
+__device__ __forceinline__ bool dist_lt(double d2s, double D) {
+  const double D2 = D * D;
+  if (d2s < D2 * (1.0 - 1e-12)) return true;
+  if (d2s > D2 * (1.0 + 1e-12)) return false;
+  return sqrt(d2s) < D;
+}
+
+// d_safe_i from the obstacle's sector (sbmpc.py:237-244), see sbmpc_sample_cost
+__device__ __forceinline__ double sbmpc_dsafe_sector(const SbIn& in, double so, double co, double d0, double d1,
+                                                     double d2s, double ds_ah, double ds_ot, double ds_eq) {
+  const double PHI_AH = 68.5 * (kPi / 180.0), PHI_OT = 68.5 * (kPi / 180.0);
+  const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
+  const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
+  if (cr * cr > 1e-18 * d2s && ey * ey > 1e-18 * d2s) return (cr >= 0 && ey > 0) ? ds_ot : ds_ah;
+  const double phi_o = wrap_pmpi(atan2(-d1, -d0) - in.ob_psi + kPi / 2);
+  return (phi_o < PHI_AH) ? ds_ah : ((phi_o > PHI_OT) ? ds_ot : ds_eq);
+}
+
+// Per-sample collision cost H0 = C·R of sbmpc.py:205-289 (KAPPA_ = 0) for one prediction sample with
+// obstacle-minus-own-ship offset (d0, d1); (ss, cs, sv) are the own ship's sin/cos(psi_) and sway
+// at that sample. R and C stay 0 unless dist < d_safe_i <= max_d_safe, so the sector geometry (atan2,
+// wrap, norms) is only evaluated there; identical results to the reference's `dist < d_close` block.
+__device__ __forceinline__ double sbmpc_sample_cost(const SbIn& in, double so, double co, double vo0, double vo1,
+                                                    double no, double t, double d0, double d1, double d2s,
+                                                    double ss, double cs, double ud, double sv, double max_d_safe,
+                                                    double lim2, double cos_ot) {
+  const double os_l = 25.0, d_safe = 1000.0, d_close = 2000.0;
+  const double PHI_AH = 68.5 * (kPi / 180.0), PHI_OT = 68.5 * (kPi / 180.0);
+  if (!(d2s < lim2)) return 0.0;  // d2s >= lim2 already implies sqrt(d2s) >= max_d_safe
+  const double dist = sqrt(d2s);
+  if (!(dist < d_close && dist < max_d_safe)) return 0.0;
+  double vs0 = -ss * ud + cs * sv;
+  double vs1 = cs * ud + ss * sv;
+  // sector of phi_o = wrap(atan2(-d1, -d0) - psi_o + pi/2) against PHI_AH == PHI_OT = θ: e is
+  // (-d0, -d1) rotated by pi/2 - psi_o, so phi_o = angle(e); phi_o > θ <=> sin(angle(e) - θ) >= 0
+  // and e_y > 0. Within 1e-9 rad of a decision boundary the reference expression is evaluated.
+  const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
+  const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
+  int sector;  // 0: phi_o < PHI_AH, 1: phi_o > PHI_OT, 2: equal
+  if (fabs(cr) > 1e-9 * dist && fabs(ey) > 1e-9 * dist) {
+    sector = (cr >= 0 && ey > 0) ? 1 : 0;
+  } else {
+    const double phi_o = wrap_pmpi(atan2(-d1, -d0) - in.ob_psi + kPi / 2);
+    sector = (phi_o < PHI_AH) ? 0 : ((phi_o > PHI_OT) ? 1 : 2);
+  }
+  double d_safe_i;
+  if (sector == 0) d_safe_i = d_safe + in.obs_l / 2;
+  else if (sector == 1) d_safe_i = 0.5 * d_safe + in.obs_l / 2;
+  else d_safe_i = d_safe + in.obs_w / 2;
+  double dot = vs0 * vo0 + vs1 * vo1;
+  double ns = sqrt(vs0 * vs0 + vs1 * vs1);
+  if (dot > cos_ot * ns * no && ns > no) d_safe_i = d_safe + os_l / 2 + in.obs_l / 2;
+  if (!(dist < d_safe_i)) return 0.0;
+  const double R = (1 / fabs(t - 0.0)) * pow(d_safe / dist, 4.0);  // pow(|t|, 1.0) == |t| exactly
+  const double k_coll = 1e-6 * os_l * in.obs_l;
+  const double w0 = vs0 - vo0, w1 = vs1 - vo1;
+  const double nrm = sqrt(w0 * w0 + w1 * w1);
+  const double C = k_coll * (nrm * nrm);
+  return C * R + 0.0 * 0;
+}
+
+// sbmpc.py:190-298 cost_func for one (Chi_ca, P_ca) scenario, sample by sample as the reference.
+// Kept as the exact fallback of sbmpc_scenario_cost (near-ties between samples).
+__device__ __noinline__ double sbmpc_scenario_cost_direct(const SbIn& in, int n_samp, double DT, double ud,
+                                                          double sp, double cp, double sp0, double cp0, double so,
+                                                          double co, double vo0, double vo1, double no,
+                                                          double max_d_safe, double lim2, double cos_ot, double H2) {
+  const double r11 = -so, r12 = co, r21 = co, r22 = so;
+  const double q11 = -sp, q12 = cp, q21 = cp, q22 = sp;
+  double ox = in.ob_x, oy = in.ob_y, sx = in.os_x, sy = in.os_y, sv = in.os_v;
+  double H1 = 0, t = 0;
+  for (int i = 0; i < n_samp; ++i) {
+    if (i > 0) {
+      ox = ox + (r11 * in.ob_u + r12 * in.ob_v) * DT;
+      oy = oy + (r21 * in.ob_u + r22 * in.ob_v) * DT;
+      sx = sx + DT * (q11 * ud + q12 * sv);
+      sy = sy + DT * (q21 * ud + q22 * sv);
+      sv = 0.0;
+    }
+    t += DT;
+    const double d0 = ox - sx, d1 = oy - sy;
+    const double H0 = sbmpc_sample_cost(in, so, co, vo0, vo1, no, t, d0, d1, d0 * d0 + d1 * d1, (i == 0) ? sp0 : sp,
+                                        (i == 0) ? cp0 : cp, ud, sv, max_d_safe, lim2, cos_ot);
+    if (H0 > H1) H1 = H0;
+  }
+  return H1 + H2;
+}
+
 __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
   const double os_l = 25.0;  // ShipLinearModel default length (sbmpc_misc.py:86, Q7)
   const double d_safe = 1000.0, d_close = 2000.0;
-  const double PHI_AH = 68.5 * (kPi / 180.0), PHI_OT = 68.5 * (kPi / 180.0);
+  const double PHI_OT = 68.5 * (kPi / 180.0);
   const double cos_ot = cos(PHI_OT * (kPi / 180.0));  // np.cos(np.deg2rad(PHI_OT_)) — PHI_OT_ already in rad
   const double max_d_safe = py_max(py_max(d_safe + in.obs_l / 2, 0.5 * d_safe + in.obs_l / 2),
                                    py_max(d_safe + in.obs_w / 2, d_safe + os_l / 2 + in.obs_l / 2));
@@ -244,58 +377,70 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     if (e0x * e0x + e0y * e0y > lim * lim && mx * mx + my * my > lim * lim) return 0.0 + H2;
   }
   const double lim2 = (max_d_safe * (1.0 + 1e-9)) * (max_d_safe * (1.0 + 1e-9));
+  // Sample 0 (own ship at wrap(psi_d) with its current sway) exactly as the reference.
+  const double e0x = in.ob_x - in.os_x, e0y = in.ob_y - in.os_y;
+  double H1 = 0;
+  {
+    const double H0 = sbmpc_sample_cost(in, so, co, vo0, vo1, no, DT, e0x, e0y, e0x * e0x + e0y * e0y, sp0, cp0, ud,
+                                        in.os_v, max_d_safe, lim2, cos_ot);
+    if (H0 > H1) H1 = H0;
+  }
+  // Samples 1..n-1: the own ship's velocity is constant (sway zeroed), so C and the overtaking
+  // override of d_safe_i are sample-independent, and H0 = C·R with R = d_safe^4 / (t·dist^4).
+  // max_i fl(C·R_i) = fl(C·max_i R_i) (rounding is monotone), so only the sample with the largest
+  // R needs the exact pow: members are ranked by s = t·d2s² (within ~1e-14 of the exact ordering);
+  // a runner-up within 1e-10 of the best sends the scenario to the sample-by-sample evaluation.
+  const double vs0 = -sp * ud + cp * 0.0, vs1 = cp * ud + sp * 0.0;
+  const double dot1 = vs0 * vo0 + vs1 * vo1;
+  const double ns1 = sqrt(vs0 * vs0 + vs1 * vs1);
+  const bool ovr = dot1 > cos_ot * ns1 * no && ns1 > no;
+  const double ds_ah = d_safe + in.obs_l / 2, ds_ot = 0.5 * d_safe + in.obs_l / 2, ds_eq = d_safe + in.obs_w / 2;
+  const double ds_ovr = d_safe + os_l / 2 + in.obs_l / 2;
+  const double ds_lo = py_min(py_min(ds_ah, ds_ot), ds_eq), ds_hi = py_max(py_max(ds_ah, ds_ot), ds_eq);
   double ox = in.ob_x, oy = in.ob_y, sx = in.os_x, sy = in.os_y, sv = in.os_v;
-  double H1 = 0, t = 0;
-  for (int i = 0; i < n_samp; ++i) {
-    if (i > 0) {
-      ox = ox + (r11 * in.ob_u + r12 * in.ob_v) * DT;
-      oy = oy + (r21 * in.ob_u + r22 * in.ob_v) * DT;
-      sx = sx + DT * (q11 * ud + q12 * sv);
-      sy = sy + DT * (q21 * ud + q22 * sv);
-      sv = 0.0;
-    }
+  double t = DT;
+  double s1 = INFINITY, s2 = INFINITY, t1 = 0.0, q1 = 0.0;
+  for (int i = 1; i < n_samp; ++i) {
+    ox = ox + (r11 * in.ob_u + r12 * in.ob_v) * DT;
+    oy = oy + (r21 * in.ob_u + r22 * in.ob_v) * DT;
+    sx = sx + DT * (q11 * ud + q12 * sv);
+    sy = sy + DT * (q21 * ud + q22 * sv);
+    sv = 0.0;
     t += DT;
-    double d0 = ox - sx, d1 = oy - sy;
+    const double d0 = ox - sx, d1 = oy - sy;
     const double d2s = d0 * d0 + d1 * d1;
-    double R = 0, C = 0;
-    // R and C stay 0 unless dist < d_safe_i <= max_d_safe, so the sector geometry (atan2, wrap,
-    // norms) is only evaluated there; identical results to the reference's `dist < d_close` block.
-    // d2s >= lim2 already implies sqrt(d2s) >= max_d_safe, so the sqrt is skipped for far samples.
     if (d2s < lim2) {
-    const double dist = sqrt(d2s);
-    if (dist < d_close && dist < max_d_safe) {
-      double ss = (i == 0) ? sp0 : sp, cs = (i == 0) ? cp0 : cp;
-      double vs0 = -ss * ud + cs * sv;
-      double vs1 = cs * ud + ss * sv;
-      // sector of phi_o = wrap(atan2(-d1, -d0) - psi_o + pi/2) against PHI_AH == PHI_OT = θ: e is
-      // (-d0, -d1) rotated by pi/2 - psi_o, so phi_o = angle(e); phi_o > θ <=> sin(angle(e) - θ) >= 0
-      // and e_y > 0. Within 1e-9 rad of a decision boundary the reference expression is evaluated.
-      const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
-      const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
-      int sector;  // 0: phi_o < PHI_AH, 1: phi_o > PHI_OT, 2: equal
-      if (fabs(cr) > 1e-9 * dist && fabs(ey) > 1e-9 * dist) {
-        sector = (cr >= 0 && ey > 0) ? 1 : 0;
+      bool member;
+      if (ovr) {
+        member = dist_lt(d2s, ds_ovr);
+      } else if (dist_lt(d2s, ds_lo)) {
+        member = true;
+      } else if (!dist_lt(d2s, ds_hi)) {
+        member = false;
       } else {
-        const double phi_o = wrap_pmpi(atan2(-d1, -d0) - in.ob_psi + kPi / 2);
-        sector = (phi_o < PHI_AH) ? 0 : ((phi_o > PHI_OT) ? 1 : 2);
+        member = dist_lt(d2s, sbmpc_dsafe_sector(in, so, co, d0, d1, d2s, ds_ah, ds_ot, ds_eq));
       }
-      double d_safe_i;
-      if (sector == 0) d_safe_i = d_safe + in.obs_l / 2;
-      else if (sector == 1) d_safe_i = 0.5 * d_safe + in.obs_l / 2;
-      else d_safe_i = d_safe + in.obs_w / 2;
-      double dot = vs0 * vo0 + vs1 * vo1;
-      double ns = sqrt(vs0 * vs0 + vs1 * vs1);
-      if (dot > cos_ot * ns * no && ns > no) d_safe_i = d_safe + os_l / 2 + in.obs_l / 2;
-      if (dist < d_safe_i) {
-        R = (1 / fabs(t - 0.0)) * pow(d_safe / dist, 4.0);  // pow(|t|, 1.0) == |t| exactly
-        double k_coll = 1e-6 * os_l * in.obs_l;
-        double w0 = vs0 - vo0, w1 = vs1 - vo1;
-        double nrm = sqrt(w0 * w0 + w1 * w1);
-        C = k_coll * (nrm * nrm);
+      member = member && dist_lt(d2s, d_close);
+      if (member) {
+        const double s = t * d2s * d2s;
+        if (s < s1) {
+          s2 = s1;
+          s1 = s; t1 = t; q1 = d2s;
+        } else if (s < s2) {
+          s2 = s;
+        }
       }
     }
-    }
-    double H0 = C * R + 0.0 * 0;
+  }
+  if (s1 < INFINITY) {
+    if (s2 <= s1 * (1.0 + 1e-10))
+      return sbmpc_scenario_cost_direct(in, n_samp, DT, ud, sp, cp, sp0, cp0, so, co, vo0, vo1, no, max_d_safe, lim2,
+                                        cos_ot, H2);
+    const double R = (1 / fabs(t1 - 0.0)) * pow(d_safe / sqrt(q1), 4.0);
+    const double k_coll = 1e-6 * os_l * in.obs_l;
+    const double w0 = vs0 - vo0, w1 = vs1 - vo1;
+    const double nrm = sqrt(w0 * w0 + w1 * w1);
+    const double H0 = (k_coll * (nrm * nrm)) * R + 0.0 * 0;
     if (H0 > H1) H1 = H0;
   }
   return H1 + H2;
@@ -393,9 +538,9 @@ __global__ void init_kernel(const Params P, DevState S, ConstBuf K) {
 }
 
 // MultiShipRLEnv.reset (env.py:238-295): reset assets + IW sampler + snapshot, then init_step
-template <bool DETAILED>
-__global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, ConstBuf K, const uint8_t* mask,
-                                                   float* obs_out) {
+template <bool DETAILED, bool REC>
+__global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, ConstBuf K, Traj T,
+                                                   const uint8_t* mask, float* obs_out) {
   __shared__ ShipConst lds_sc[2];
   const ShipConst* SC = stage_consts(P, lds_sc);
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -420,8 +565,14 @@ __global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, 
   load_segment(s, rn, re);
   const double mach_dt = P.mach_dt_reset;
   // init_step (env.py:307-339): one control + integrate tick, no collision avoidance
-  control_and_integrate<DETAILED>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false);
+  double fuel[3] = {0.0, 0.0, 0.0};  // machinery reset restores the fuel accumulators (ship_engine.py:468-481)
+  control_and_integrate<DETAILED, REC>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false, REC ? T.ship_row(q, 0) : nullptr,
+                                       fuel);
   store_ship(S, q, s);
+  if (REC) {
+    for (int k = 0; k < 3; ++k) T.fuel[(size_t)q * 3 + k] = fuel[k];
+    if (ship == 0) T.len[env] = 1;
+  }
   if (ship == 0) {
     S.sampling_count()[env] = 0;
     S.travel_dist()[env] = 0; S.travel_time()[env] = 0; S.acc()[env] = 0;
@@ -514,8 +665,8 @@ __device__ __forceinline__ double xor_shfl_d(double x, int mask) {
 // for a decision consume action[env] first (IW sampling). LPE lanes per env: lane & 1 selects the
 // ship, the LPE/2 sub-lanes of a ship hold identical state, run the control chain redundantly and
 // split the map queries (edges for the coastline distance, hull corners for grounding).
-template <bool DETAILED, int COLLAV, int LPE>
-__global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K,
+template <bool DETAILED, int COLLAV, int LPE, bool REC>
+__global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K, Traj T,
                                                       const float* __restrict__ action,
                                                       const uint8_t* __restrict__ active_mask, int max_ticks,
                                                       float* obs_out, double* reward_out, uint8_t* done_out,
@@ -574,6 +725,12 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 
   float ns[8];
   for (int i = 0; i < 8; ++i) ns[i] = S.next_obs8()[envc * 8 + i];
+  int rec_t = 0;
+  double fuel[3] = {0.0, 0.0, 0.0};
+  if (REC) {
+    rec_t = T.len[envc];
+    for (int k = 0; k < 3; ++k) fuel[k] = T.fuel[(size_t)qc * 3 + k];
+  }
   double out_r = 0.0;
   bool out_done = false, ready = false;
   uint32_t out_bits = 0;
@@ -641,6 +798,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
     double sf = 1.0, off = 0.0;
+    bool sb_active = false;
     if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
       bool need = false;
       SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -660,6 +818,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       pb = shfl_d(pb, env_lane0);
       cb = shfl_d(cb, env_lane0);
       const int need0 = __shfl((int)need, env_lane0, 64);
+      sb_active = need0;
       if (going) {
         if (need0) { p_last = pb; chi_last = cb; }
         else { p_last = 1; chi_last = 0; }
@@ -673,6 +832,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     if (going) {
       if (!is_test && s.stop) {
         // frozen obstacle ship: store_last_simulation_data + two next_time (Q9)
+        if (REC && sub == 0) record_last(T, qc, rec_t, s.time, s.time + P.dt);
         s.time = s.time + P.dt;
         s.time = s.time + P.dt;
       } else {
@@ -683,8 +843,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
           float dn = st4[0] - st4[2], de = st4[1] - st4[3];
           imminent = (dn * dn + de * de) < 9000000.0f;
         }
-        control_and_integrate<DETAILED>(c, P, s, rn, re, -off, sf, mach_dt,
-                                        (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) ? 1 : 0, imminent);
+        control_and_integrate<DETAILED, REC>(c, P, s, rn, re, -off, sf, mach_dt,
+                                             (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) ? 1 : 0, imminent,
+                                             (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel);
         my_speed_out = U;
         if (!is_test) {  // travel tracker (env.py:527-534, Q6)
           double tn = s.log_n - prev_log_n, te = s.log_e - prev_log_e;
@@ -788,6 +949,20 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       if (obs_stop) bits |= SHIPSIM_EV_OBS_STOP;
       if (obs_stop && !terminal && !is_test) s.stop = 1;
       const bool combined_done = terminal || (test_stop && !terminal);
+      if (REC) {  // RewardTracker.update (reward_function.py:181-186) + env.py:613-620 animation lists
+        double* er = (lie == 0) ? T.env_row(env, rec_t - 1) : nullptr;
+        if (er) {
+          er[SHIPSIM_TE_R_COLLISION] = r0 / 5; er[SHIPSIM_TE_R_TEST_GROUNDING] = r1 / 5;
+          er[SHIPSIM_TE_R_TEST_NAV] = r2 / 5; er[SHIPSIM_TE_R_OBS_GROUNDING] = r3 / 5;
+          er[SHIPSIM_TE_R_OBS_NAV] = r4 / 5; er[SHIPSIM_TE_R_TOTAL] = r; er[SHIPSIM_TE_BITS] = (double)bits;
+          const bool imm = (COLLAV == SHIPSIM_COLLAV_SBMPC)
+                               ? sb_active
+                               : ((Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe)) < 9000000.0;
+          er[SHIPSIM_TE_FLAGS] = (double)((is_collision ? SHIPSIM_TE_FLAG_COLLISION : 0) |
+                                          (imm ? SHIPSIM_TE_FLAG_IMMINENT : 0));
+        }
+        rec_t += 1;
+      }
       // ---- env.py:700-771 decision logic ----
       acc += r;
       ticks += 1;
@@ -834,6 +1009,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
            ticks, sampling_count, n_base, phase, (int)have_iw);
 #endif
   if (sub == 0) store_ship(S, qc, s);
+  if (REC) {
+    if (sub == 0)
+      for (int k = 0; k < 3; ++k) T.fuel[(size_t)qc * 3 + k] = fuel[k];
+    if (lie == 0) T.len[env] = rec_t;
+  }
   if (lie == 0) {
     S.sampling_count()[env] = sampling_count;
     S.travel_dist()[env] = travel_dist; S.travel_time()[env] = travel_time; S.acc()[env] = acc;
@@ -874,6 +1054,29 @@ __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevStat
   store_ship(S, q, s);
 }
 
+// SBMPC.get_optimal_ctrl_offset (sbmpc.py:113-185) for a batch of independent single-obstacle
+// requests (shipsim_sbmpc_eval): one request per lane, optimisations served wave-cooperatively.
+__global__ __launch_bounds__(64) void sbmpc_eval_kernel(int n, double tf, double dt, const double* __restrict__ in,
+                                                        double* __restrict__ out) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const bool valid = i < n;
+  const double* r = in + (size_t)(valid ? i : 0) * SHIPSIM_SBMPC_IN;
+  SbIn q;
+  q.p_last = r[0]; q.chi_last = r[1]; q.u_d = r[2]; q.chi_d = r[3];
+  q.os_x = r[4]; q.os_y = r[5]; q.os_v = r[8];  // os_state (x, y, psi, u, v, r): linear_pred uses x, y, v
+  q.ob_x = r[10]; q.ob_y = r[11]; q.ob_psi = r[12]; q.ob_u = r[13]; q.ob_v = r[14];
+  q.obs_l = r[15]; q.obs_w = r[16];
+  const double d0 = q.ob_x - q.os_x, d1 = q.ob_y - q.os_y;
+  const bool active = valid && sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_ (sbmpc.py:154-159)
+  double pb = 1.0, cb = 0.0;
+  sbmpc_cooperative(active, q, (int)(tf / dt), dt, pb, cb);
+  if (valid) {
+    out[(size_t)i * 3 + 0] = active ? pb : 1.0;
+    out[(size_t)i * 3 + 1] = active ? cb : 0.0;
+    out[(size_t)i * 3 + 2] = active ? 1.0 : 0.0;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -886,6 +1089,8 @@ struct shipsim_handle {
   hipStream_t stream;
   void* dev_block;
   void* const_block;
+  void* fuel_block;  // trajectory fuel accumulators
+  Traj T;
   size_t dev_bytes;
   int ever_reset;
   char err[512];
@@ -1003,15 +1208,21 @@ static void launch_step(shipsim_handle* h, int lpe, const float* action, const u
                         float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
                         int32_t* ticks_out, uint8_t* ready_out) {
   const int threads = 64;
+  if (h->T.ship) lpe = 16;  // recording kernels are built for the default layout only
   const int lanes = h->P.n_envs * lpe, blocks = (lanes + threads - 1) / threads;
-#define L(LPE)                                                                                                   \
-  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, \
-                     action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, ready_out)
+#define L(LPE, REC)                                                                                              \
+  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, REC>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S,  \
+                     h->K, h->T, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, \
+                     ready_out)
+  if (h->T.ship) {
+    L(16, true);
+    return;
+  }
   switch (lpe) {
-    case 2: L(2); break;
-    case 4: L(4); break;
-    case 8: L(8); break;
-    default: L(16); break;
+    case 2: L(2, false); break;
+    case 4: L(4, false); break;
+    case 8: L(8, false); break;
+    default: L(16, false); break;
   }
 #undef L
 }
@@ -1222,6 +1433,17 @@ static void make_ship_const(const shipsim_config* cfg, const shipsim_ship_config
   k->thrust_coeff = pow(c->propeller_diameter, 4) * c->propeller_speed_to_thrust_force_coefficient;
   k->shaft_speed_max = 1.1 * (c->rated_speed_main_engine_rpm * M_PI / 30) * k->r_me;
   k->init_omega = c->initial_propeller_shaft_speed_rad_per_s;
+  k->mode_me = me;
+  k->mode_el = el;
+  k->hotel = hl;
+  k->avail_prop = (c->shaft_generator_state == SHIPSIM_SG_MOTOR) ? me + el - hl
+                  : (c->shaft_generator_state == SHIPSIM_SG_GEN) ? me - hl : me;  // :32-44
+  k->sg_state = c->shaft_generator_state;
+  // run/env_setup.py:85-104: SpecificFuelConsumptionWartila6L26 (ME) / Baudouin6M26Dot3 (DG),
+  // ship_engine.py:88-112 (BaseMachineryModel.fuel_consumption uses these, not the
+  // ShipMachineryModel.specific_fuel_coeffs_* literals)
+  k->fa_me = 128.9; k->fb_me = -168.9; k->fc_me = 246.8;
+  k->fa_dg = 108.7; k->fb_dg = -289.9; k->fc_dg = 324.9;
   k->kp_ship_speed = c->kp_ship_speed;
   k->ki_ship_speed = c->ki_ship_speed;
   k->kp_shaft_speed = c->kp_shaft_speed;
@@ -1453,6 +1675,7 @@ int shipsim_destroy(shipsim_handle* h) {
     else (void)hipDeviceSynchronize();
     if (h->dev_block) (void)hipFree(h->dev_block);
     if (h->const_block) (void)hipFree(h->const_block);
+    if (h->fuel_block) (void)hipFree(h->fuel_block);
   }
   delete h;
   return SHIPSIM_OK;
@@ -1467,10 +1690,15 @@ int shipsim_reset(shipsim_handle* h, const uint8_t* env_mask, float* obs_out) {
     return fail(h, SHIPSIM_EINVAL, "reset: kind %d not supported on device", h->P.kind);
   DeviceGuard g(h->device);
   int S = h->P.n_envs * h->P.n_ships, threads = 256, blocks = (S + threads - 1) / threads;
-  if (h->P.machinery == SHIPSIM_MACH_DETAILED)
-    hipLaunchKernelGGL(reset_kernel<true>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, env_mask, obs_out);
-  else
-    hipLaunchKernelGGL(reset_kernel<false>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, env_mask, obs_out);
+  const bool rec = h->T.ship != nullptr;
+#define RL(D, REC) \
+  hipLaunchKernelGGL((reset_kernel<D, REC>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, h->T, env_mask, obs_out)
+  if (h->P.machinery == SHIPSIM_MACH_DETAILED) {
+    if (rec) RL(true, true); else RL(true, false);
+  } else {
+    if (rec) RL(false, true); else RL(false, false);
+  }
+#undef RL
   HIPCHK(h, hipGetLastError());
   h->ever_reset = 1;
   return SHIPSIM_OK;
@@ -1555,6 +1783,35 @@ int shipsim_set_state(shipsim_handle* h, int32_t field, const void* src) {
   DeviceGuard g(h->device);
   HIPCHK(h, hipMemcpyAsync(p, src, b, hipMemcpyDefault, h->stream));
   return SHIPSIM_OK;
+}
+
+int shipsim_set_trajectory(shipsim_handle* h, double* ship_rows, double* env_rows, int32_t capacity,
+                           int32_t* lengths) {
+  if (!h || !h->dev_block) return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "set_trajectory: SHIPSIM_KIND_AST only");
+  if (!ship_rows) {
+    memset(&h->T, 0, sizeof(h->T));
+    return SHIPSIM_OK;
+  }
+  if (capacity <= 0 || !lengths) return fail(h, SHIPSIM_EINVAL, "set_trajectory: capacity %d / lengths", capacity);
+  DeviceGuard g(h->device);
+  const size_t fb = (size_t)h->P.n_envs * h->P.n_ships * 3 * sizeof(double);
+  if (!h->fuel_block) HIPCHK(h, hipMalloc(&h->fuel_block, fb));
+  HIPCHK(h, hipMemsetAsync(h->fuel_block, 0, fb, h->stream));
+  HIPCHK(h, hipMemsetAsync(lengths, 0, (size_t)h->P.n_envs * sizeof(int32_t), h->stream));
+  h->T.ship = ship_rows;
+  h->T.env = env_rows;
+  h->T.fuel = (double*)h->fuel_block;
+  h->T.len = lengths;
+  h->T.cap = capacity;
+  return SHIPSIM_OK;
+}
+
+int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double* out, void* stream) {
+  if (n < 0 || (n > 0 && (!in || !out)) || !(dt > 0) || tf / dt > 4096) return SHIPSIM_EINVAL;
+  if (n == 0) return SHIPSIM_OK;
+  hipLaunchKernelGGL(sbmpc_eval_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, tf, dt, in, out);
+  return hipGetLastError() == hipSuccess ? SHIPSIM_OK : SHIPSIM_EHIP;
 }
 
 int shipsim_synchronize(shipsim_handle* h) {

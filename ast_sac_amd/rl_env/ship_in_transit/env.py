@@ -20,6 +20,7 @@ import torch
 from ... import shipsim_abi as abi
 from ...shipsim import ShipSim
 from ...spaces import Box
+from .trajectory import EpisodeRecord, RewardTracker
 
 # observation_space / action_space of env.py:86-104
 OBS_LOW = np.array([0, 0, -3000, 0, 0, -np.pi, -3000, 0], dtype=np.float32)
@@ -117,6 +118,21 @@ class BatchedMultiShipRLEnv:
     def seed(self, seed=None):
         self.np_random = np.random.default_rng(seed)
 
+    # -- trajectory recording (simulation_results export) --
+    def record_trajectories(self, capacity=None):
+        """Record every tick of every env (both ships' simulation_results rows + RewardTracker rows)
+        into device buffers; rows start at the next reset. capacity defaults to the longest episode
+        (simulation_time / time_step + 2 rows)."""
+        if capacity is None:
+            capacity = int(np.ceil(self.cfg.simulation_time / self.cfg.time_step)) + 8
+        return self.sim.set_trajectory(capacity)
+
+    def episode_record(self, env_index=0):
+        """EpisodeRecord of one env (host copy of its rows since its last reset)."""
+        if getattr(self.sim, "traj", None) is None:
+            raise RuntimeError("trajectory recording is off: call record_trajectories() before reset()")
+        return EpisodeRecord(self.sim.traj, env_index, self.cfg, self.sim.n_ships)
+
     def close(self):
         self.sim.close()
 
@@ -129,12 +145,98 @@ class BatchedMultiShipRLEnv:
         self.__init__(st["args"], st["n_envs"], device=st["device"], cfg=cfg)
 
 
-class MultiShipRLEnv:
-    """Single-env object API of rl_env/ship_in_transit/env.py:MultiShipRLEnv over the device env."""
+class _Int:
+    """EulerInt view (utils.py:27-53): dt / sim_time, time read from the device."""
 
-    def __init__(self, args=None, device=None, machinery="detailed", cfg=None, assets=None, map=None):
+    def __init__(self, env, ship):
+        self._env, self._ship = env, ship
+        self.dt = float(env._b.cfg.time_step)
+        self.sim_time = float(env._b.cfg.simulation_time)
+
+    @property
+    def time(self):
+        return float(self._env._b.sim.get(abi.F_TIME)[self._ship].item())
+
+
+class _ShipModelView:
+    """ShipModelAST / SimpleShipModel attributes the reference's post-processing reads."""
+
+    def __init__(self, env, ship):
+        self._env, self._ship = env, ship
+        self.int = _Int(env, ship)
+        c = env._b.cfg.ship[ship]
+        self.l_ship, self.w_ship = c.length_of_ship, c.width_of_ship
+
+    def _field(self, f):
+        return float(self._env._b.sim.get(f)[self._ship].item())
+
+    north = property(lambda self: self._field(abi.F_NORTH))
+    east = property(lambda self: self._field(abi.F_EAST))
+    yaw_angle = property(lambda self: self._field(abi.F_YAW))
+    forward_speed = property(lambda self: self._field(abi.F_U))
+    sideways_speed = property(lambda self: self._field(abi.F_V))
+    yaw_rate = property(lambda self: self._field(abi.F_R))
+
+    @property
+    def simulation_results(self):
+        return self._env._record().simulation_results(self._ship)
+
+
+class _NavigateView:
+    def __init__(self, env, ship):
+        self._env, self._ship = env, ship
+
+    def _route(self):
+        return self._env._route(self._ship)
+
+    north = property(lambda self: [float(x) for x in self._route()[:, 0]])
+    east = property(lambda self: [float(x) for x in self._route()[:, 1]])
+    e_ct = property(lambda self: float(self._env._b.sim.get(abi.F_E_CT)[self._ship].item()))
+    e_ct_int = property(lambda self: float(self._env._b.sim.get(abi.F_E_CT_INT)[self._ship].item()))
+
+
+class _AutoPilotView:
+    def __init__(self, env, ship):
+        self.navigate = _NavigateView(env, ship)
+        self._env, self._ship = env, ship
+
+    next_wpt = property(lambda self: int(self._env._b.sim.get(abi.F_NEXT_WPT)[self._ship].item()))
+
+
+class ShipAssetView:
+    """ShipAssets (env.py:29-39) of one ship of the N = 1 device env, for the reference's plotting /
+    post-analysis code: ship_model.simulation_results (needs record_trajectory=True), ship_model.int,
+    auto_pilot.navigate.north/east, time_list, integrator_term, stop_flag, desired_forward_speed."""
+
+    def __init__(self, env, ship):
+        self._env, self._ship = env, ship
+        self.ship_model = _ShipModelView(env, ship)
+        self.auto_pilot = _AutoPilotView(env, ship)
+        self.desired_forward_speed = float(env._b.cfg.ship[ship].desired_forward_speed)
+        self.type_tag = "test_ship" if ship == 0 else "obs_ship"
+
+    time_list = property(lambda self: self._env._record().time_list(self._ship))
+    integrator_term = property(lambda self: self._env._record().integrator_term(self._ship))
+    stop_flag = property(lambda self: bool(self._env._b.sim.get(abi.F_STOP)[self._ship].item()))
+
+
+class MultiShipRLEnv:
+    """Single-env object API of rl_env/ship_in_transit/env.py:MultiShipRLEnv over the device env.
+    With record_trajectory=True every tick is recorded on the device and the reference's
+    post-processing surface is available: test/obs/assets (ShipAssetView), reward_tracker,
+    waypoint_sampling_times, is_collision_list, is_collision_imminent_list."""
+
+    def __init__(self, args=None, device=None, machinery="detailed", cfg=None, assets=None, map=None,
+                 record_trajectory=False, trajectory_capacity=None):
         self.args = args if args is not None else default_args()
         self._b = BatchedMultiShipRLEnv(self.args, 1, device=device, machinery=machinery, cfg=cfg)
+        self.record_trajectory = bool(record_trajectory)
+        if self.record_trajectory:
+            self._b.record_trajectories(trajectory_capacity)
+        self.test, self.obs = ShipAssetView(self, 0), ShipAssetView(self, 1)
+        self.assets = [self.test, self.obs]
+        self.waypoint_sampling_times = []
+        self._extra_totals = []
         self.collav = self._b.collav
         self.observation_space = self._b.observation_space
         self.action_space = self._b.action_space
@@ -159,16 +261,51 @@ class MultiShipRLEnv:
         r = routes[0, 1:L - 1].cpu().numpy()
         return [[float(n), float(e)] for n, e in r]
 
+    def _record(self):
+        if not self.record_trajectory:
+            raise RuntimeError("construct MultiShipRLEnv(record_trajectory=True) to read simulation results")
+        return self._b.episode_record(0)
+
+    def _route(self, ship):
+        routes = self._b.sim.get(abi.E_ROUTE_NORTH).view(2, abi.MAX_ROUTE)[ship].cpu().numpy()
+        routes_e = self._b.sim.get(abi.E_ROUTE_EAST).view(2, abi.MAX_ROUTE)[ship].cpu().numpy()
+        L = int(self._b.sim.get(abi.E_ROUTE_LEN)[ship].item())
+        return np.stack([routes[:L], routes_e[:L]], 1)
+
+    @property
+    def reward_tracker(self):
+        rt = self._record().reward_tracker()
+        for r in self._extra_totals:  # update_r_total_only on sampling failures (env.py:690)
+            rt.update_r_total_only(r)
+        return rt
+
+    @property
+    def is_collision_list(self):
+        return self._record().is_collision_list()
+
+    @property
+    def is_collision_imminent_list(self):
+        if self.collav not in ("simple", "sbmpc"):
+            return []
+        return self._record().is_collision_imminent_list()
+
     def reset(self, action=None):
         obs = self._b.reset()
+        self.waypoint_sampling_times = []
+        self._extra_totals = []
         self.accumulated_rewards_list = []
         self.env_info = {"events": "", "terminal": False, "test_ship_stop": False, "obs_ship_stop": False}
         return obs[0].cpu().numpy()
 
     def step(self, action):
         a = np.asarray(action, dtype=np.float32).reshape(-1)[:1]
+        if self.sampling_count < self._b.cfg.max_sampling_frequency:  # env.py:663-665
+            t_obs = float(self._b.sim.get(abi.F_TIME)[1].item())
+            self.waypoint_sampling_times.append(t_obs - float(self._b.cfg.time_step))
         obs, r, done, info = self._b.step(torch.from_numpy(a))
         bits = int(info["events"][0].item())
+        if bits & abi.EV_SAMPLING_FAILURE:
+            self._extra_totals.append(float(r[0].item()))
         env_info = {"events": abi.events_to_string(bits), "terminal": bool(bits & abi.EV_TERMINAL),
                     "test_ship_stop": bool(bits & abi.EV_TEST_STOP), "obs_ship_stop": bool(bits & abi.EV_OBS_STOP)}
         reward = float(r[0].item())
@@ -184,7 +321,8 @@ class MultiShipRLEnv:
         self._b.close()
 
     def __getstate__(self):
-        return dict(args=self.args, cfg=bytes(self._b.cfg), device=str(self._dev))
+        return dict(args=self.args, cfg=bytes(self._b.cfg), device=str(self._dev), record=self.record_trajectory)
 
     def __setstate__(self, st):
-        self.__init__(st["args"], device=st["device"], cfg=abi.Config.from_buffer_copy(st["cfg"]))
+        self.__init__(st["args"], device=st["device"], cfg=abi.Config.from_buffer_copy(st["cfg"]),
+                      record_trajectory=st.get("record", False))

@@ -45,6 +45,8 @@ def load_library(path=LIB_PATH):
     L.shipsim_get_state.argtypes = [P, C.c_int32, P]
     L.shipsim_set_state.argtypes = [P, C.c_int32, P]
     L.shipsim_synchronize.argtypes = [P]
+    L.shipsim_set_trajectory.argtypes = [P, P, P, C.c_int32, P]
+    L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
     if L.shipsim_abi_version() != abi.ABI_VERSION:
         raise ShipSimError(f"ABI mismatch: library {L.shipsim_abi_version()} vs binding {abi.ABI_VERSION}")
     _lib = L
@@ -53,7 +55,8 @@ def load_library(path=LIB_PATH):
 
 EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_default_config", "shipsim_create",
                     "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
-                    "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize")
+                    "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
+                    "shipsim_set_trajectory", "shipsim_sbmpc_eval")
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
@@ -164,5 +167,41 @@ class ShipSim:
         self._check(self.L.shipsim_set_state(self.h, int(field), _ptr(t)), "shipsim_set_state")
         self._keep_set = t
 
+    # -- trajectory recording (include/shipsim.h: shipsim_set_trajectory) --
+    def set_trajectory(self, capacity, env_rows=True):
+        """Record every tick's simulation_results row (both ships) and RewardTracker row into device
+        tensors of `capacity` rows per env; returns dict(ship=(N*2, cap, 20) f64, env=(N, cap, 8) f64,
+        len=(N,) int32, cap). Rows start at the next reset."""
+        S = self.n_envs * self.n_ships
+        cap = int(capacity)
+        t = dict(ship=torch.zeros((S, cap, abi.TRAJ_SHIP_COLS), dtype=torch.float64, device=self.device),
+                 env=torch.zeros((self.n_envs, cap, abi.TRAJ_ENV_COLS), dtype=torch.float64, device=self.device)
+                 if env_rows else None,
+                 len=torch.zeros(self.n_envs, dtype=torch.int32, device=self.device), cap=cap)
+        self._check(self.L.shipsim_set_trajectory(self.h, _ptr(t["ship"]), _ptr(t["env"]), cap, _ptr(t["len"])),
+                    "shipsim_set_trajectory")
+        self.traj = t
+        return t
+
+    def clear_trajectory(self):
+        self._check(self.L.shipsim_set_trajectory(self.h, None, None, 0, None), "shipsim_set_trajectory")
+        self.traj = None
+
     def synchronize(self):
         self._check(self.L.shipsim_synchronize(self.h), "shipsim_synchronize")
+
+
+def sbmpc_eval(requests, tf=1000.0, dt=20.0, device="cuda"):
+    """SBMPC.get_optimal_ctrl_offset on the device for a batch of (n, 17) requests
+    [P_ca_last, Chi_ca_last, u_d, chi_d, os_state(6), obstacle(5), obs_l, obs_w] -> (n, 3) tensor
+    [speed factor, course offset, active] (shipsim_sbmpc_eval)."""
+    L = load_library()
+    x = torch.as_tensor(requests, dtype=torch.float64, device=device).contiguous()
+    if x.dim() != 2 or x.shape[1] != abi.SBMPC_IN:
+        raise ShipSimError(f"requests must be (n, {abi.SBMPC_IN})")
+    out = torch.empty((x.shape[0], 3), dtype=torch.float64, device=x.device)
+    stream = torch.cuda.current_stream(x.device)
+    rc = L.shipsim_sbmpc_eval(int(x.shape[0]), float(tf), float(dt), _ptr(x), _ptr(out), C.c_void_p(stream.cuda_stream))
+    if rc:
+        raise ShipSimError(f"shipsim_sbmpc_eval failed ({rc})")
+    return out

@@ -13,7 +13,7 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_ROUTE = 16
 MAX_POLYS = 16
 MAX_VERTS = 128
@@ -63,6 +63,16 @@ N_SHIP_FIELDS = 19
 E_SAMPLING_COUNT, E_TRAVEL_DIST, E_TRAVEL_TIME, E_ACC_REWARD, E_N_BASE, E_E_BASE = range(100, 106)
 E_SBMPC_P_LAST, E_SBMPC_CHI_LAST, E_ROUTE_LEN, E_ROUTE_NORTH, E_ROUTE_EAST = range(106, 111)
 INT_FIELDS = {F_NEXT_WPT, F_STOP, E_SAMPLING_COUNT, E_ROUTE_LEN}
+
+# trajectory record columns (shipsim_set_trajectory)
+TRAJ_SHIP_COLS = 20
+(TS_TIME, TS_NORTH, TS_EAST, TS_YAW, TS_RUDDER, TS_U, TS_V, TS_R, TS_OMEGA, TS_THRUST, TS_E_CT, TS_E_PSI, TS_LOAD,
+ TS_FUEL_ME, TS_FUEL_EL, TS_FUEL, TS_E_CT_INT, TS_NEXT_WPT, TS_REPEAT, TS_TIME_LIST) = range(20)
+TRAJ_ENV_COLS = 8
+(TE_R_COLLISION, TE_R_TEST_GROUNDING, TE_R_TEST_NAV, TE_R_OBS_GROUNDING, TE_R_OBS_NAV, TE_R_TOTAL, TE_BITS,
+ TE_FLAGS) = range(8)
+TE_FLAG_COLLISION, TE_FLAG_IMMINENT = 1, 2
+SBMPC_IN = 17
 
 
 def events_to_string(bits):

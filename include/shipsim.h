@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 1
+#define SHIPSIM_ABI_VERSION 2
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -273,6 +273,64 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out);
  * env-major [env][ship] (the device lane order), env fields [env], routes [env][ship][SHIPSIM_MAX_ROUTE]. */
 int shipsim_get_state(shipsim_handle* h, int32_t field, void* dst);
 int shipsim_set_state(shipsim_handle* h, int32_t field, const void* src);
+
+/* ---- trajectory recording (f1: simulation_results export) ----------------------------------
+ * Per-tick rows of ShipModelAST/SimpleShipModel.store_simulation_data (ship_model.py:903-957,
+ * run_colav/.../ship_model.py:418-444) for both ships, plus the RewardTracker entry of every tick
+ * (reward_function.py:30-57, 181-186) and the animation lists of env.py:612-620. Row t of a ship is its
+ * t-th store since the env's last reset (row 0 = init_step, env.py:329); env row t belongs to tick
+ * t + 1. Values are raw (SI units, radians); the Python facade derives the reference's keys and units.
+ * Ship row columns: */
+#define SHIPSIM_TRAJ_SHIP_COLS 20
+#define SHIPSIM_TS_TIME 0       /* int.time at the store */
+#define SHIPSIM_TS_NORTH 1
+#define SHIPSIM_TS_EAST 2
+#define SHIPSIM_TS_YAW 3        /* rad */
+#define SHIPSIM_TS_RUDDER 4     /* rad */
+#define SHIPSIM_TS_U 5
+#define SHIPSIM_TS_V 6
+#define SHIPSIM_TS_R 7          /* rad/s */
+#define SHIPSIM_TS_OMEGA 8      /* propeller shaft speed rad/s (detailed) */
+#define SHIPSIM_TS_THRUST 9     /* N: propeller thrust (detailed) | commanded thrust force (simplified) */
+#define SHIPSIM_TS_E_CT 10      /* auto_pilot.get_cross_track_error() */
+#define SHIPSIM_TS_E_PSI 11     /* auto_pilot.get_heading_error() = |heading_mea - heading_ref| (rad, Q8) */
+#define SHIPSIM_TS_LOAD 12      /* engine throttle = load_perc (detailed) | thrust command (simplified) */
+#define SHIPSIM_TS_FUEL_ME 13   /* accumulated fuel kg (detailed; machinery int.dt, Q1) */
+#define SHIPSIM_TS_FUEL_EL 14
+#define SHIPSIM_TS_FUEL 15
+#define SHIPSIM_TS_E_CT_INT 16  /* navigate.e_ct_int after the tick (ShipAssets.integrator_term) */
+#define SHIPSIM_TS_NEXT_WPT 17
+#define SHIPSIM_TS_REPEAT 18    /* 1: store_last_simulation_data row of a stopped ship */
+#define SHIPSIM_TS_TIME_LIST 19 /* ShipAssets.time_list entry of the tick */
+/* Env row columns: */
+#define SHIPSIM_TRAJ_ENV_COLS 8
+#define SHIPSIM_TE_R_COLLISION 0      /* RewardTracker.ship_collision (already / 5) */
+#define SHIPSIM_TE_R_TEST_GROUNDING 1
+#define SHIPSIM_TE_R_TEST_NAV 2
+#define SHIPSIM_TE_R_OBS_GROUNDING 3
+#define SHIPSIM_TE_R_OBS_NAV 4
+#define SHIPSIM_TE_R_TOTAL 5          /* RewardTracker.total (after the termination multipliers) */
+#define SHIPSIM_TE_BITS 6             /* SHIPSIM_EV_* bits of the tick */
+#define SHIPSIM_TE_FLAGS 7            /* SHIPSIM_TE_FLAG_* */
+#define SHIPSIM_TE_FLAG_COLLISION 1   /* is_collision_list entry */
+#define SHIPSIM_TE_FLAG_IMMINENT 2    /* is_collision_imminent_list entry (simple: distance, sbmpc: active) */
+
+/* Enable recording into caller-owned device buffers: ship_rows n_envs*n_ships x capacity x
+ * SHIPSIM_TRAJ_SHIP_COLS doubles ([env][ship][row][col]), env_rows n_envs x capacity x
+ * SHIPSIM_TRAJ_ENV_COLS doubles (may be NULL), lengths n_envs int32 (ship rows recorded since the env's
+ * last reset; rows past capacity are dropped while the count goes on). Lengths are zeroed here and by
+ * every reset; enable before the reset that starts the episodes to record. ship_rows NULL disables.
+ * AST kind only; recording steps run the lanes_per_env = 16 kernels (identical results). */
+int shipsim_set_trajectory(shipsim_handle* h, double* ship_rows, double* env_rows, int32_t capacity,
+                           int32_t* lengths);
+
+/* SBMPC.get_optimal_ctrl_offset (sbmpc.py:113-185) for n independent single-obstacle requests on the
+ * device, stateless (P_ca_last_ / Chi_ca_last_ are inputs). in: n x SHIPSIM_SBMPC_IN doubles
+ * [P_ca_last, Chi_ca_last, u_d, chi_d, os_state(6: x, y, psi, u, v, r), obstacle(5: x, y, psi, u, v),
+ *  obstacle length, obstacle width]; out: n x 3 doubles [speed factor, course offset, active].
+ * SBMPC(tf, dt) horizon; stream is a hipStream_t (NULL = default); device pointers. */
+#define SHIPSIM_SBMPC_IN 17
+int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double* out, void* stream);
 
 /* Block until all work queued on the handle's stream is done. */
 int shipsim_synchronize(shipsim_handle* h);

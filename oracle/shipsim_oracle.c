@@ -413,6 +413,10 @@ typedef struct {
   int has_log;
   /* optional per-tick log sink */
   double* log_buf;
+  /* optional raw-row sink in the device trajectory layout (include/shipsim.h SHIPSIM_TS_*) */
+  double* raw_buf;
+  int raw_cap, raw_len;
+  double last_raw[SHIPSIM_TRAJ_SHIP_COLS];
   int log_cap, log_len;
   double last_row[13];
 } o_asset;
@@ -454,6 +458,7 @@ static void asset_reset(o_asset* a, int quirk) { /* env.py:252-271 */
   a->stop_flag = 0;
   a->has_log = 0;
   a->log_len = 0;
+  a->raw_len = 0;
 }
 
 /* throttle (detailed, controllers.py:185-189, Q2: measured_shaft_speed = forward speed) or thrust
@@ -487,9 +492,24 @@ static void asset_store(o_asset* a, double ctrl, double rudder) {
   a->log_rudder = rudder; a->log_thrust = thrust_logged;
   a->has_log = 1;
   if (a->log_buf && a->log_len < a->log_cap) memcpy(a->log_buf + 13 * a->log_len++, row, sizeof(row));
+  /* the same store as raw values: SI units / radians, the throttle (load_perc) and all three fuel
+   * accumulators, plus ShipAssets.integrator_term / time_list of the tick (env.py:429-430) */
+  double raw[SHIPSIM_TRAJ_SHIP_COLS] = {m->time, m->north, m->east, m->yaw, rudder, m->u, m->v, m->r,
+                                        m->detailed ? m->omega : 0.0, m->detailed ? mach_thrust(m) : ctrl,
+                                        a->ap.nav.e_ct, fabs(a->ap.heading_mea - a->ap.heading_ref), ctrl,
+                                        m->detailed ? m->fuel_cons_me : 0.0, m->detailed ? m->fuel_cons_el : 0.0,
+                                        m->detailed ? m->fuel_cons : 0.0, a->ap.nav.e_ct_int, (double)a->ap.next_wpt,
+                                        0.0, m->time};
+  memcpy(a->last_raw, raw, sizeof(raw));
+  if (a->raw_buf && a->raw_len < a->raw_cap) memcpy(a->raw_buf + SHIPSIM_TRAJ_SHIP_COLS * a->raw_len++, raw, sizeof(raw));
 }
 /* store_last_simulation_data (ship_model.py:946-957): repeat the last row with the current time */
 static void asset_store_last(o_asset* a) {
+  a->last_raw[SHIPSIM_TS_TIME] = a->m.time;
+  a->last_raw[SHIPSIM_TS_REPEAT] = 1.0;
+  a->last_raw[SHIPSIM_TS_TIME_LIST] = a->m.time + a->m.dt; /* time_list after the first next_time (env.py:454-462) */
+  if (a->raw_buf && a->raw_len < a->raw_cap)
+    memcpy(a->raw_buf + SHIPSIM_TRAJ_SHIP_COLS * a->raw_len++, a->last_raw, sizeof(a->last_raw));
   a->last_row[0] = a->m.time;
   if (a->log_buf && a->log_len < a->log_cap) memcpy(a->log_buf + 13 * a->log_len++, a->last_row, sizeof(a->last_row));
 }
@@ -806,6 +826,10 @@ void oracle_env_set_log(o_env* env, int ship, double* buf, int cap) {
   env->a[ship].log_buf = buf; env->a[ship].log_cap = cap; env->a[ship].log_len = 0;
 }
 int oracle_env_log_len(const o_env* env, int ship) { return env->a[ship].log_len; }
+void oracle_env_set_raw(o_env* env, int ship, double* buf, int cap) {
+  env->a[ship].raw_buf = buf; env->a[ship].raw_cap = cap; env->a[ship].raw_len = 0;
+}
+int oracle_env_raw_len(const o_env* env, int ship) { return env->a[ship].raw_len; }
 void oracle_env_set_rtick(o_env* env, double* buf, int cap) { env->rtick_buf = buf; env->rtick_cap = cap; env->rtick_len = 0; }
 int oracle_env_rtick_len(const o_env* env) { return env->rtick_len; }
 

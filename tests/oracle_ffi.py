@@ -31,6 +31,8 @@ def lib():
         L.oracle_env_destroy.argtypes = [P]
         L.oracle_env_set_log.argtypes = [P, C.c_int, dp, C.c_int]
         L.oracle_env_log_len.argtypes = [P, C.c_int]
+        L.oracle_env_set_raw.argtypes = [P, C.c_int, dp, C.c_int]
+        L.oracle_env_raw_len.argtypes = [P, C.c_int]
         L.oracle_env_set_rtick.argtypes = [P, dp, C.c_int]
         L.oracle_env_rtick_len.argtypes = [P]
         L.oracle_env_reset.argtypes = [P, fp]
@@ -66,12 +68,16 @@ class OracleEnv:
         self.cfg = cfg
         self.h = lib().oracle_env_create(C.byref(cfg))
         self.logs = []
+        self.raws = []
         self.rtick = None
         if log_cap:
             for s in range(cfg.n_ships):
                 buf = np.zeros((log_cap, 13))
                 lib().oracle_env_set_log(self.h, s, buf, log_cap)
                 self.logs.append(buf)
+                raw = np.zeros((log_cap, abi.TRAJ_SHIP_COLS))
+                lib().oracle_env_set_raw(self.h, s, raw, log_cap)
+                self.raws.append(raw)
             self.rtick = np.zeros(log_cap)
             lib().oracle_env_set_rtick(self.h, self.rtick, log_cap)
 
@@ -83,6 +89,10 @@ class OracleEnv:
 
     def log(self, ship):
         return self.logs[ship][:lib().oracle_env_log_len(self.h, ship)].copy()
+
+    def raw_rows(self, ship):
+        """Raw rows in the device trajectory layout (include/shipsim.h SHIPSIM_TS_*)."""
+        return self.raws[ship][:lib().oracle_env_raw_len(self.h, ship)].copy()
 
     def rewards_per_tick(self):
         return self.rtick[:lib().oracle_env_rtick_len(self.h)].copy()

@@ -61,6 +61,10 @@ def test_header_constants_match_binding():
              "EV_TERMINAL": abi.EV_TERMINAL, "EV_TEST_STOP": abi.EV_TEST_STOP, "EV_OBS_STOP": abi.EV_OBS_STOP,
              "F_NEXT_WPT": abi.F_NEXT_WPT, "F_STOP": abi.F_STOP, "N_SHIP_FIELDS": abi.N_SHIP_FIELDS,
              "E_SAMPLING_COUNT": abi.E_SAMPLING_COUNT, "E_ROUTE_EAST": abi.E_ROUTE_EAST}
+    for name in dir(abi):  # trajectory record layout and SBMPC batch layout, every column
+        if name.startswith(("TS_", "TE_", "TRAJ_", "SBMPC_IN")):
+            pairs[name] = getattr(abi, name)
+    assert "TS_TIME_LIST" in pairs and "TE_FLAG_IMMINENT" in pairs
     for k, v in pairs.items():
         assert d[k] == v, k
     assert C.sizeof(abi.Config) > 0

@@ -1,0 +1,242 @@
+"""Device trajectory recording, PTO/MEC machinery modes (C5) and the batched
+SBMPC entry point, against the golden reference fixtures and the CPU oracle. Needs an MI355X."""
+import numpy as np
+import pytest
+
+import gpu_harness as H
+import oracle_ffi as O
+from ast_sac_amd import shipsim_abi as abi
+from parity import assert_close, rel_err
+
+pytestmark = pytest.mark.gpu
+
+MODE_NAMES = {"pto": "PTO", "pti": "PTI", "mec": "MEC"}
+TRAJ_CASES = [("pti", "none", 2), ("pti", "sbmpc", 1), ("pti", "simple", 1), ("pto", "none", 1), ("mec", "none", 1)]
+CMD_KEYS = ("commanded load fraction me [-]", "commanded load fraction hsg [-]", "power me [kw]",
+            "power electrical [kw]", "power [kw]", "propulsion power [kw]", "fuel rate me [kg/s]",
+            "fuel rate hsg [kg/s]", "fuel rate [kg/s]", "motor torque [Nm]")
+RT_FIELDS = ("ship_collision", "test_ship_grounding", "test_ship_nav_failure", "obs_ship_grounding",
+             "obs_ship_nav_failure", "from_test_ship", "from_obs_ship", "total")
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+@pytest.mark.parametrize("mode,collav,n_eps", TRAJ_CASES)
+def test_single_env_trajectory_matches_reference(golden, torch_cuda, mode, collav, n_eps):
+    """MultiShipRLEnv(record_trajectory=True): simulation_results of both ships (all 27 keys, reference
+    order), time_list, integrator_term, RewardTracker (incl. the sampling-failure total),
+    waypoint_sampling_times and the animation lists equal the reference run."""
+    from ast_sac_amd.rl_env.ship_in_transit.env import MultiShipRLEnv, default_args
+    g = golden("rl_env_traj")
+    cfg = abi.set_machinery_mode(abi.ast_config(collav), MODE_NAMES[mode])
+    env = MultiShipRLEnv(default_args(collav_mode=collav), cfg=cfg, record_trajectory=True)
+    for ep in range(n_eps):
+        p = f"{mode}_{collav}_ep{ep}"
+        env.reset()
+        for a in g[p + "_a"]:
+            if env.step(np.array([a], np.float32))[2]:
+                break
+        for ship, name in ((env.test, "test"), (env.obs, "obs")):
+            sr = ship.ship_model.simulation_results
+            keys = [str(k) for k in g[p + f"_{name}_keys"]]
+            assert list(sr) == keys
+            got = np.array([sr[k] for k in keys], np.float64).T
+            ref = g[p + f"_{name}_sr"]
+            assert got.shape == ref.shape, (p, name)
+            # State, rudder, thrust, fuel and guidance columns at the north-star 1e-5. The columns
+            # derived from the commanded load (the throttle = output of the saturating ship-speed ->
+            # shaft-speed PI cascade) are held to 1e-4: with SBMPC speed factors active, libm ulps
+            # between the device and NumPy move the throttle by ~1e-5 relative while the states they
+            # integrate into stay within 1e-6.
+            cmd = [i for i, k in enumerate(keys) if k in CMD_KEYS]
+            rest = [i for i in range(len(keys)) if i not in cmd]
+            assert_close(got[:, rest], ref[:, rest], what=f"{p} {name} simulation_results")
+            assert_close(got[:, cmd], ref[:, cmd], rtol=1e-4, what=f"{p} {name} load-derived columns")
+            assert_close(np.array(ship.time_list), g[p + f"_{name}_time_list"], what=p + " time_list")
+            assert_close(np.array(ship.integrator_term), g[p + f"_{name}_integrator_term"], what=p + " integrator")
+        rt = env.reward_tracker
+        for f in RT_FIELDS:
+            ref = g[p + f"_rt_{f}"]
+            got = np.array(getattr(rt, f))
+            assert got.shape == ref.shape, (p, f)
+            np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-9, err_msg=f"{p} reward_tracker.{f}")
+        np.testing.assert_allclose(env.waypoint_sampling_times, g[p + "_wst"], rtol=0, atol=1e-9)
+        # np.tan on the float32 scoping angle is not correctly rounded in NumPy (SIMD); the device
+        # rounds tan(double) to float32: a float32 ulp (~1e-8 relative) may separate the samples
+        np.testing.assert_allclose(np.array(env.waypoint_samples).reshape(-1, 2), g[p + "_waypoint_samples"],
+                                   rtol=1e-6, atol=0)
+        np.testing.assert_array_equal(np.array(env.is_collision_list, np.int64), g[p + "_is_collision"])
+        np.testing.assert_array_equal(np.array(env.is_collision_imminent_list, np.int64), g[p + "_imminent"])
+    env.close()
+
+
+def _perturbed(cfg, eps):
+    import copy
+    c = copy.deepcopy(cfg)
+    c.ship[0].initial_north_position_m *= 1 + eps
+    c.ship[1].initial_east_position_m *= 1 - eps
+    return c
+
+
+def _rows_vs_oracle(cfg, acts, rec, n_dec):
+    """(worst error / tolerance, message) of an env's recorded rows against an oracle episode."""
+    orc = O.OracleEnv(cfg, log_cap=4000)
+    orc.reset()
+    k = 0
+    for a in acts:
+        k += 1
+        if orc.step(a)[2]:
+            break
+    if k != n_dec:
+        return np.inf, f"{k} decisions vs {n_dec}"
+    worst, msg = 0.0, ""
+    for s in (0, 1):
+        raw = orc.raw_rows(s)
+        if rec.n_rows != len(raw):
+            return np.inf, f"ship {s}: {rec.n_rows} rows vs {len(raw)}"
+        got = rec.ship_rows[s]
+        if not (np.array_equal(got[:, abi.TS_REPEAT], raw[:, abi.TS_REPEAT])
+                and np.array_equal(got[:, abi.TS_NEXT_WPT], raw[:, abi.TS_NEXT_WPT])):
+            return np.inf, f"ship {s}: repeat / waypoint columns differ"
+        # the throttle (TS_LOAD) is d(throttle)/du ~ 50 * 205.25 ~ 1e4 times more sensitive than the
+        # surge speed it is computed from (controllers.py:185-189), so it is held to 1e-4
+        cols = [c for c in range(abi.TRAJ_SHIP_COLS) if c != abi.TS_LOAD]
+        e = float(rel_err(got[:, cols], raw[:, cols]).max()) / 1e-5
+        e = max(e, float(rel_err(got[:, abi.TS_LOAD], raw[:, abi.TS_LOAD]).max()) / 1e-4)
+        if e > worst:
+            worst, msg = e, f"ship {s}: worst error {e:.2f} x tolerance"
+    e = float(rel_err(rec.env_rows[:, abi.TE_R_TOTAL], orc.rewards_per_tick()).max()) / 1e-5
+    if e > worst:
+        worst, msg = e, f"reward per tick: {e:.2f} x tolerance"
+    return worst, msg
+
+
+@pytest.mark.parametrize("collav,mode", [("none", "PTI"), ("sbmpc", "PTI"), ("simple", "MEC"), ("none", "PTO")])
+def test_batched_trajectory_rows_equal_oracle(torch_cuda, collav, mode):
+    """Every env of a batch records exactly the oracle's raw rows (stopped-ship repeats included),
+    across resets, with sliced stepping; recording does not change the simulation."""
+    torch = torch_cuda
+    from ast_sac_amd.rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, default_args
+    n = 48
+    cfg = abi.set_machinery_mode(abi.ast_config(collav), mode)
+    tables = H.make_tables(n, 1)
+    acts = np.stack([abi.normalized_to_scoping(t[0]) for t in tables])  # (n, 9)
+    env = BatchedMultiShipRLEnv(default_args(collav_mode=collav), n, cfg=cfg)
+    env.record_trajectories()
+    env.reset()
+    dec = np.zeros(n, int)
+    active = np.ones(n, bool)
+    results = {}
+    for _ in range(4000):
+        if not active.any():
+            break
+        a = torch.from_numpy(acts[np.arange(n), np.minimum(dec, 8)].astype(np.float32))
+        out = env.step_async(a, max_ticks=37, active=torch.from_numpy(active.astype(np.uint8)))
+        rd = out["ready"].cpu().numpy().astype(bool) & active
+        dn = out["done"].cpu().numpy().astype(bool)
+        for i in np.nonzero(rd)[0]:
+            results.setdefault(i, []).append((out["obs"][i].cpu().numpy().copy(), float(out["reward"][i])))
+            dec[i] += 1
+            if dn[i] or dec[i] >= 9:
+                active[i] = False
+    assert not active.any()
+    chosen = []
+    for i in range(n):
+        rec = env.episode_record(i)
+        best = None
+        for v, eps in enumerate(H.PERTURBATIONS):  # ill-conditioned envs: see gpu_harness.run_oracle_variants
+            err = _rows_vs_oracle(_perturbed(cfg, eps), acts[i], rec, len(results[i]))
+            if best is None or err[0] < best[0]:
+                best = (err[0], err[1], v)
+            if err[0] <= 1.0:
+                break
+        assert best[0] <= 1.0, f"env {i}: {best[1]}"
+        chosen.append(best[2])
+    assert np.mean(np.array(chosen) != 0) <= 0.1, chosen
+    env.close()
+
+
+@pytest.mark.parametrize("mode", ["PTO", "MEC"])
+@pytest.mark.parametrize("collav", ["none", "sbmpc"])
+def test_machinery_modes_vs_oracle(torch_cuda, mode, collav):
+    """C5 machinery modes on device vs the oracle, several episodes per env."""
+    cfg = abi.set_machinery_mode(abi.ast_config(collav), mode)
+    tables = H.make_tables(96, 2)
+    gpu, _, _, _ = H.run_gpu(cfg, tables)
+    orcs = H.run_oracle_variants(cfg, tables)
+    worst, msgs, chosen = H.compare(gpu, orcs)
+    assert not msgs, "\n".join(msgs[:20])
+    assert worst <= 1e-5
+    assert (chosen != 0).mean() <= 0.1
+
+
+def test_sbmpc_eval_matches_oracle(golden, torch_cuda):
+    """shipsim_sbmpc_eval (wave-cooperative SBMPC) vs the oracle: the golden known answers (a
+    sequence carrying P_ca_last/Chi_ca_last) and 4096 random near-encounter requests."""
+    from ast_sac_amd.shipsim import sbmpc_eval
+    g = golden("sbmpc_geometry_reward")
+    reqs, refs = [], []
+    p_last, chi_last = 1.0, 0.0
+    for row, out in zip(g["sbmpc_in"], g["sbmpc_out"]):
+        reqs.append(np.concatenate([[p_last, chi_last], row[:13], [80.0, 16.0]]))
+        refs.append(out[:3])
+        p_last, chi_last = out[3], out[4]
+    got = sbmpc_eval(np.array(reqs)).cpu().numpy()
+    np.testing.assert_array_equal(got, np.array(refs))
+    rng = np.random.Generator(np.random.PCG64(5))
+    n = 4096
+    os_ = np.stack([rng.uniform(0, 20000, n), rng.uniform(0, 10000, n), rng.uniform(-np.pi, np.pi, n),
+                    rng.uniform(0, 6, n), rng.uniform(-0.5, 0.5, n), rng.uniform(-0.01, 0.01, n)], 1)
+    ang, rad = rng.uniform(-np.pi, np.pi, n), rng.uniform(20, 2200, n)
+    ob = np.stack([os_[:, 0] + rad * np.cos(ang), os_[:, 1] + rad * np.sin(ang), rng.uniform(-np.pi, np.pi, n),
+                   rng.uniform(0, 6, n), rng.uniform(-0.5, 0.5, n)], 1)
+    last = np.stack([rng.choice([0.4, 0.6, 0.8, 1.0], n), np.deg2rad(rng.choice(np.arange(-30, 31, 10), n))], 1)
+    req = np.concatenate([last, rng.uniform(3, 5, (n, 1)), rng.uniform(-4, 4, (n, 1)), os_, ob,
+                          np.full((n, 1), 80.0), np.full((n, 1), 16.0)], 1)
+    got = sbmpc_eval(req).cpu().numpy()
+    ref = np.array([O.sbmpc(r[0], r[1], r[2], r[3], r[4:10], r[10:15])[0] for r in req])
+    assert got[:, 2].sum() > n // 2  # most requests are active encounters
+    mism = np.nonzero((got != ref).any(axis=1))[0]
+    # an exact argmin tie can only differ through libm ulps; it must stay a rarity
+    assert len(mism) <= n // 1000, (len(mism), req[mism[:3]], got[mism[:3]], ref[mism[:3]])
+
+
+def test_trained_policy_replay_from_snapshot(torch_cuda, tmp_path):
+    """f3: a snapshot written by the package logger replays through SimulatePolicyEnvSetup with the
+    reference's post-processing surface (DataFrames of every simulation_results key)."""
+    torch = torch_cuda
+    from ast_sac_amd.ast_sac.core.logging import logger
+    from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac_amd.ast_sac.torch.sac.policies.base import MakeDeterministic
+    from ast_sac_amd.ast_sac.torch.utils import pytorch_util as ptu
+    from ast_sac_amd.ast_sac.env_wrapper.normalized_box_env import NormalizedBoxEnv
+    from ast_sac_amd.ast_sac.samplers.data_collector.rollout_functions import ast_sac_rollout
+    from ast_sac_amd.rl_env.ship_in_transit.env import MultiShipRLEnv, default_args
+    from ast_sac_amd.rl_env.ship_in_transit.trajectory import AST_RESULT_KEYS
+    from ast_sac_amd.run.ast_sac_run_trained_policy import SimulatePolicyEnvSetup
+    torch.manual_seed(7)
+    pol = MakeDeterministic(TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[64, 64], init_w=0.5))
+    logger.set_snapshot_dir(str(tmp_path))
+    logger.set_snapshot_mode("last")
+    logger.save_itr_params(0, {"evaluation/policy": pol})
+    try:
+        setup = SimulatePolicyEnvSetup(str(tmp_path / "params.pkl"), 9, True, default_args(collav_mode="none"))
+        path = setup.simulate_policy()
+        assert list(setup.ts_results_df.columns) == list(AST_RESULT_KEYS)
+        assert len(setup.ts_results_df) == len(setup.os_results_df) > 100
+        assert len(setup.waypoint_sampling_times) == len(path["actions"])
+        # the same policy on a non-recording env gives the same episode (recording is side-effect free)
+        ref = ast_sac_rollout(NormalizedBoxEnv(MultiShipRLEnv(default_args(collav_mode="none"))), setup.policy, 9)
+        np.testing.assert_array_equal(ref["rewards"], path["rewards"])
+        np.testing.assert_array_equal(ref["next_observations"], path["next_observations"])
+        rt = setup.env.wrapped_env.reward_tracker
+        np.testing.assert_allclose(np.cumsum(rt.total)[-1], path["rewards"].sum(), rtol=1e-9)
+    finally:
+        ptu.set_gpu_mode(False)
+        logger.set_snapshot_dir(None)

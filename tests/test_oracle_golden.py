@@ -61,11 +61,12 @@ def test_ast_single_ship_and_machinery_dt_quirk(golden):
     assert_close(env.ship_state(0)[[0, 1, 2, 3, 4, 5, 6]], g["after_reset_final"], what="after reset final")
 
 
-def _run_episodes(golden, fname, collav, machinery, cols):
+def _run_episodes(golden, fname, collav, machinery, cols, cfg=None, prefix=None):
     g = golden(fname)
-    env = O.OracleEnv(abi.ast_config(collav, machinery=machinery), log_cap=4000)
-    for ep in range(int(g[f"{collav}_n_episodes"])):
-        p = f"{collav}_ep{ep}"
+    prefix = prefix or collav
+    env = O.OracleEnv(cfg if cfg is not None else abi.ast_config(collav, machinery=machinery), log_cap=4000)
+    for ep in range(int(g[f"{prefix}_n_episodes"])):
+        p = f"{prefix}_ep{ep}"
         np.testing.assert_array_equal(env.reset(), g[p + "_o0"])
         n_dec = len(g[p + "_a"])
         got = {k: [] for k in ("obs", "reward", "done", "bits", "nticks")}
@@ -107,6 +108,48 @@ def test_rl_env_detailed_episodes(golden, collav):
 @pytest.mark.parametrize("collav", ["none", "sbmpc"])
 def test_rl_env_simplified_episodes(golden, collav):
     _run_episodes(golden, "rl_env_simplified", collav, abi.MACH_SIMPLIFIED, SR_COLS)
+
+
+MODE_NAMES = {"pto": "PTO", "pti": "PTI", "mec": "MEC"}
+
+
+@pytest.mark.parametrize("mode", ["pto", "mec"])
+@pytest.mark.parametrize("collav", ["none", "sbmpc"])
+def test_rl_env_machinery_modes(golden, mode, collav):
+    """C5: MachineryModes([pto_mode]) / ([mec_mode]) of run/env_setup.py:62-81 instead of PTI."""
+    cfg = abi.set_machinery_mode(abi.ast_config(collav), MODE_NAMES[mode])
+    _run_episodes(golden, "rl_env_modes", collav, abi.MACH_DETAILED, AST_COLS, cfg=cfg, prefix=f"{mode}_{collav}")
+
+
+TRAJ_CASES = [("pti", "none", 2), ("pti", "sbmpc", 1), ("pti", "simple", 1), ("pto", "none", 1), ("mec", "none", 1)]
+
+
+@pytest.mark.parametrize("mode,collav,n_eps", TRAJ_CASES)
+def test_trajectory_schema_from_oracle_rows(golden, mode, collav, n_eps):
+    """f1: raw rows in the device trajectory layout (the oracle's) -> the reference's full
+    simulation_results dict (all 27 ShipModelAST keys, reference order), time_list, integrator_term."""
+    from ast_sac_amd.rl_env.ship_in_transit.trajectory import simulation_results, AST_RESULT_KEYS
+    g = golden("rl_env_traj")
+    cfg = abi.set_machinery_mode(abi.ast_config(collav), MODE_NAMES[mode])
+    env = O.OracleEnv(cfg, log_cap=4000)
+    for ep in range(n_eps):
+        p = f"{mode}_{collav}_ep{ep}"
+        env.reset()
+        for a in g[p + "_a"]:
+            if env.step(a)[2]:
+                break
+        for s, name in ((0, "test"), (1, "obs")):
+            keys = [str(k) for k in g[p + f"_{name}_keys"]]
+            assert tuple(keys) == AST_RESULT_KEYS
+            raw = env.raw_rows(s)
+            sr = simulation_results(raw, cfg.ship[s], detailed=True, as_lists=False)
+            assert list(sr) == keys
+            ref = g[p + f"_{name}_sr"]
+            assert len(raw) == len(ref), (p, name)
+            got = np.stack([sr[k] for k in keys], 1)
+            assert_close(got, ref, what=f"{p} {name} simulation_results")
+            assert_close(raw[1:, abi.TS_TIME_LIST], g[p + f"_{name}_time_list"], what=p + " time_list")
+            assert_close(raw[1:, abi.TS_E_CT_INT], g[p + f"_{name}_integrator_term"], what=p + " integrator_term")
 
 
 def test_sbmpc_known_answers(golden):
