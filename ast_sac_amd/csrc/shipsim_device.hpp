@@ -105,7 +105,14 @@ __device__ __forceinline__ double sat(double v, double lo, double hi) { return p
 
 // np.remainder / Python float % (floored)
 __device__ __forceinline__ double floor_mod(double a, double b) {
-  double m = fmod(a, b);
+  // fmod is exact; for b > 0 and |a| < 2b it is a, a - b or a + b, each exact by Sterbenz' lemma
+  // (b <= |a| <= 2b), so the library call is only needed for larger ratios.
+  double m;
+  if (b > 0 && a > -2 * b && a < 2 * b) {
+    m = (a >= b) ? a - b : ((a <= -b) ? a + b : a);
+  } else {
+    m = fmod(a, b);
+  }
   if (m != 0.0) {
     if ((b < 0) != (m < 0)) m += b;
   } else {
@@ -132,25 +139,51 @@ struct Deriv {
   double dn, de, dyaw, du, dv, dr, domega;
 };
 
-// get_wind_force :497-517
-__device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, const Ship& s, double tau[3]) {
+// swap a double with the lane two below/above (lane ^ 2) — DPP quad_perm [2,3,0,1]: in the AST
+// lane layout (lane = env*LPE + 2*sub + ship) this pairs sub-lanes 2k and 2k+1 of the same ship
+__device__ __forceinline__ double sub_pair_swap(double x) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// sincos of two angles: with PAIRED, sub-lane pairs of a ship evaluate one each in a single call
+// (`odd` = odd sub-lane) and exchange the results; the values are those of two separate calls.
+template <bool PAIRED>
+__device__ __forceinline__ void sincos2(double a, double b, bool odd, double& sa, double& ca, double& sb, double& cb) {
+  if (PAIRED) {
+    double s_, c_;
+    sincos(odd ? b : a, &s_, &c_);
+    const double so = sub_pair_swap(s_), co = sub_pair_swap(c_);
+    sa = odd ? so : s_; ca = odd ? co : c_;
+    sb = odd ? s_ : so; cb = odd ? c_ : co;
+  } else {
+    sincos(a, &sa, &ca);
+    sincos(b, &sb, &cb);
+  }
+}
+
+// get_wind_force :497-517 (sw, cw = sin/cos(wind_direction - yaw))
+template <bool PAIRED>
+__device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, const Ship& s, double sw, double cw,
+                                           bool odd, double tau[3]) {
 #ifdef SHIPSIM_ABL_NO_WIND
   tau[0] = tau[1] = tau[2] = 0.0;
   return;
 #endif
-  double sw, cw;
-  sincos(P.wind_dir - s.yaw, &sw, &cw);
   double uw = P.wind_speed * cw;
   double vw = P.wind_speed * sw;
   double u_rw = uw - s.u;
   double v_rw = vw - s.v;
   double gamma_rw = -atan2(v_rw, u_rw);
   double wind_rw2 = u_rw * u_rw + v_rw * v_rw;
-  double sg, cg;
-  sincos(gamma_rw, &sg, &cg);
+  double sg, cg, s2g, c2g;
+  sincos2<PAIRED>(gamma_rw, 2 * gamma_rw, odd, sg, cg, s2g, c2g);  // sin(2 * gamma_rw) as sincos(.).sin
+  (void)c2g;
   double c_x = -c.cx * cg;
   double c_y = c.cy * sg;
-  double c_n = c.cn * sin(2 * gamma_rw);
+  double c_n = c.cn * s2g;
   double tau_coeff = 0.5 * c.rho_a * wind_rw2;
   tau[0] = tau_coeff * c_x * c.proj_area_f;
   tau[1] = tau_coeff * c_y * c.proj_area_l;
@@ -160,11 +193,12 @@ __device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, 
 // update_differentials (ShipModelAST :882-888 / SimpleShipModel run_colav :399-404):
 // three_dof_kinematics :519-528, shaft_eq + thrust (ship_engine.py:403-443), three_dof_kinetics
 // :834-864 with rudder :866-880. `ctrl` is the engine throttle (detailed) or thrust force (simplified).
+template <bool PAIRED = false>
 __device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params& P, const Ship& s, double ctrl,
-                                               double delta, bool detailed) {
+                                               double delta, bool detailed, bool odd = false) {
   Deriv d;
-  double sy, cy;
-  sincos(s.yaw, &sy, &cy);
+  double sy, cy, sw, cw;
+  sincos2<PAIRED>(s.yaw, P.wind_dir - s.yaw, odd, sy, cy, sw, cw);
   d.dn = cy * s.u + (-sy) * s.v + 0 * s.r;
   d.de = sy * s.u + cy * s.v + 0 * s.r;
   d.dyaw = 0 * s.u + 0 * s.v + 1 * s.r;
@@ -185,7 +219,7 @@ __device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params&
   double fv = -c.c_rudder_v * delta * (s.u - vc0);
   double fr = -c.c_rudder_r * delta * (s.u - vc0);
   double tau[3];
-  wind_force(c, P, s, tau);
+  wind_force<PAIRED>(c, P, s, sw, cw, odd, tau);
   double u_r = s.u - vc0;
   double v_r = s.v - vc1;
   double x_g = 0.0;
@@ -223,10 +257,11 @@ __device__ __forceinline__ void integrate(Ship& s, const Deriv& d, double dt, do
 // ---------------------------------------------------------------------------------------------
 // guidance & control
 // ---------------------------------------------------------------------------------------------
-// LOS_guidance.py:100-117 (k = next_wpt; waypoints k-1, k are register-cached)
-__device__ __forceinline__ double los_guidance(const ShipConst& c, Ship& s, double x, double y) {
+// LOS_guidance.py:100-117 (k = next_wpt; waypoints k-1, k are register-cached): the state update
+// (e_ct, windup-limited e_ct_int) and the argument of the course correction atan
+__device__ __forceinline__ double los_update(const ShipConst& c, Ship& s, double x, double y) {
   // alpha_k = atan2(dy, dx) and its sin/cos depend on the segment only: cached by segment_changed()
-  const double alpha_k = s.seg_alpha, sa = s.seg_sin, ca = s.seg_cos;
+  const double sa = s.seg_sin, ca = s.seg_cos;
   double e_ct = -(x - s.wp_prev_n) * sa + (y - s.wp_prev_e) * ca;
   s.e_ct = e_ct;
   if (e_ct * e_ct >= c.los_r2) {
@@ -235,8 +270,11 @@ __device__ __forceinline__ double los_guidance(const ShipConst& c, Ship& s, doub
   }
   double delta = py_max(1e-6, sqrt(c.los_r2 - e_ct * e_ct));
   if (fabs(s.e_ct_int + e_ct / delta) <= c.los_limit) s.e_ct_int += e_ct / delta;
-  double chi_r = atan(-e_ct / delta - s.e_ct_int * c.los_ki);
-  return alpha_k + chi_r;
+  return -e_ct / delta - s.e_ct_int * c.los_ki;
+}
+__device__ __forceinline__ double los_guidance(const ShipConst& c, Ship& s, double x, double y) {
+  const double arg = los_update(c, s, x, y);
+  return s.seg_alpha + atan(arg);
 }
 
 // LOS_guidance.py:83-98: true when the index advances (caller reloads the segment cache)

@@ -166,12 +166,14 @@ __device__ __forceinline__ const ShipConst* stage_consts(const Params& P, ShipCo
 
 // one controlled ship tick: autopilot -> speed control -> store -> update -> integrate -> next_time
 // (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339)
-template <bool DETAILED, bool REC = false>
+// PAIRED: sub-lanes 2k / 2k+1 of the ship share the batched sincos calls (odd = this lane is 2k+1)
+template <bool DETAILED, bool REC = false, bool PAIRED = false>
 __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const Params& P, Ship& s,
                                                       const double* __restrict__ rn, const double* __restrict__ re,
                                                       double offset, double speed_factor, double mach_dt,
                                                       int simple_collav_flag /*0 none, 1 rl(-15deg), 2 noniw(+15)*/,
-                                                      bool imminent, double* row = nullptr, double* fuel = nullptr) {
+                                                      bool imminent, double* row = nullptr, double* fuel = nullptr,
+                                                      bool odd = false) {
   const double N = s.n, E = s.e, H = s.yaw, U = s.u;
   if (next_wpt_advance(c, s, N, E)) {
     s.next_wpt += 1;
@@ -206,7 +208,7 @@ __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const 
       row[SHIPSIM_TS_TIME_LIST] = s.time;
     }
   }
-  Deriv d = differentials(c, P, s, ctrl, rudder, DETAILED);
+  Deriv d = differentials<PAIRED>(c, P, s, ctrl, rudder, DETAILED, odd);
   integrate(s, d, P.dt, mach_dt, DETAILED);
 }
 
@@ -305,7 +307,7 @@ __device__ __forceinline__ double sbmpc_sample_cost(const SbIn& in, double so, d
 
 // sbmpc.py:190-298 cost_func for one (Chi_ca, P_ca) scenario, sample by sample as the reference.
 // Kept as the exact fallback of sbmpc_scenario_cost (near-ties between samples).
-__device__ __noinline__ double sbmpc_scenario_cost_direct(const SbIn& in, int n_samp, double DT, double ud,
+__device__ __forceinline__ double sbmpc_scenario_cost_direct(const SbIn& in, int n_samp, double DT, double ud,
                                                           double sp, double cp, double sp0, double cp0, double so,
                                                           double co, double vo0, double vo1, double no,
                                                           double max_d_safe, double lim2, double cos_ot, double H2) {
@@ -353,8 +355,9 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   double sp, cp;
   sincos(psi_d, &sp, &cp);
   const double q11 = -sp, q12 = cp, q21 = cp, q22 = sp;
-  double sp0, cp0;
-  sincos(wrap_pmpi(psi_d), &sp0, &cp0);
+  double sp0 = sp, cp0 = cp;
+  const double psi_w = wrap_pmpi(psi_d);
+  if (psi_w != psi_d) sincos(psi_w, &sp0, &cp0);
   double dChi0 = Chi_ca - in.chi_last;
   const double H2 = 25 * (1 - P_ca) + 30 * (Chi_ca * Chi_ca) + 20 * fabs(in.p_last - P_ca) +
                     ((dChi0 > 0) ? 20 * dChi0 * dChi0 : (dChi0 < 0 ? 30 * dChi0 * dChi0 : 0));
@@ -397,15 +400,21 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   const double ds_ah = d_safe + in.obs_l / 2, ds_ot = 0.5 * d_safe + in.obs_l / 2, ds_eq = d_safe + in.obs_w / 2;
   const double ds_ovr = d_safe + os_l / 2 + in.obs_l / 2;
   const double ds_lo = py_min(py_min(ds_ah, ds_ot), ds_eq), ds_hi = py_max(py_max(ds_ah, ds_ot), ds_eq);
-  double ox = in.ob_x, oy = in.ob_y, sx = in.os_x, sy = in.os_y, sv = in.os_v;
+  // position increments: the obstacle's are constant, the own ship's use its sway at sample 1
+  // only (linear_pred zeroes v after the first step)
+  const double dox = (r11 * in.ob_u + r12 * in.ob_v) * DT, doy = (r21 * in.ob_u + r22 * in.ob_v) * DT;
+  const double dsx = DT * (q11 * ud + q12 * 0.0), dsy = DT * (q21 * ud + q22 * 0.0);
+  double ox = in.ob_x, oy = in.ob_y;
+  double sx = in.os_x + DT * (q11 * ud + q12 * in.os_v), sy = in.os_y + DT * (q21 * ud + q22 * in.os_v);
   double t = DT;
   double s1 = INFINITY, s2 = INFINITY, t1 = 0.0, q1 = 0.0;
   for (int i = 1; i < n_samp; ++i) {
-    ox = ox + (r11 * in.ob_u + r12 * in.ob_v) * DT;
-    oy = oy + (r21 * in.ob_u + r22 * in.ob_v) * DT;
-    sx = sx + DT * (q11 * ud + q12 * sv);
-    sy = sy + DT * (q21 * ud + q22 * sv);
-    sv = 0.0;
+    ox = ox + dox;
+    oy = oy + doy;
+    if (i > 1) {
+      sx = sx + dsx;
+      sy = sy + dsy;
+    }
     t += DT;
     const double d0 = ox - sx, d1 = oy - sy;
     const double d2s = d0 * d0 + d1 * d1;
@@ -803,15 +812,17 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       bool need = false;
       SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       if (going && is_test) {
-        // env.py:362-363: next_wpt result discarded; los_guidance integrates e_ct_int (Q3)
-        double chi_d = los_guidance(c, s, s.n, s.e);
-        in.u_d = c.desired_speed; in.chi_d = -chi_d;
+        // env.py:362-363: next_wpt result discarded; los_guidance integrates e_ct_int (Q3). The
+        // course (atan) only feeds the optimisation, so it is evaluated for requesting envs only.
+        const double los_arg = los_update(c, s, s.n, s.e);
+        double d0 = pe - s.e, d1 = pn - s.n;
+        need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
+        if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
+        in.u_d = c.desired_speed;
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
         in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
         in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
         in.p_last = p_last; in.chi_last = chi_last;
-        double d0 = pe - s.e, d1 = pn - s.n;
-        need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
       }
       double pb = 1.0, cb = 0.0;
       sbmpc_cooperative(need && sub == 0, in, n_samp, P.sbmpc_dt, pb, cb);
@@ -843,9 +854,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
           float dn = st4[0] - st4[2], de = st4[1] - st4[3];
           imminent = (dn * dn + de * de) < 9000000.0f;
         }
-        control_and_integrate<DETAILED, REC>(c, P, s, rn, re, -off, sf, mach_dt,
-                                             (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) ? 1 : 0, imminent,
-                                             (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel);
+        control_and_integrate<DETAILED, REC, (NSUB >= 2)>(c, P, s, rn, re, -off, sf, mach_dt,
+                                                          (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) ? 1 : 0,
+                                                          imminent, (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr,
+                                                          fuel, (sub & 1) != 0);
         my_speed_out = U;
         if (!is_test) {  // travel tracker (env.py:527-534, Q6)
           double tn = s.log_n - prev_log_n, te = s.log_e - prev_log_e;
@@ -917,11 +929,30 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       double dist = sqrt(dx * dx + dy * dy);
       double beta = floor_mod((atan2(dy, dx) - Th) + kPi, 2 * kPi) - kPi;
       const bool enc_ok = !(fabs(beta) > 165.0 * (kPi / 180.0));  // head-on or crossing (Q5)
-      double r0 = (dist < 10000 && enc_ok) ? rd4(0, 200000000, dist) : 0.0;
-      double r1 = (Tground <= 1000) ? rd4(0, 175000, Tground) : 0.0;
-      double r2 = rd3(3000, 1250000, fabs(Tect));
-      double r3 = (Oground <= 1000) ? -rd4(0, 50000, Oground) : 0.0;
-      double r4 = -rd3(500, 12500, fabs(Oect));
+      // the five shaped terms of reward_designs.py:33-55 (RewardDesign4 / 3): one exp each,
+      // evaluated by five lanes of the env in one call when LPE >= 8, then gathered
+      const double xv[5] = {dist, Tground, fabs(Tect), Oground, fabs(Oect)};
+      const double tg[5] = {0.0, 0.0, 3000.0, 0.0, 500.0};
+      const double of[5] = {200000000.0, 175000.0, 1250000.0, 50000.0, 12500.0};
+      double ex[5];
+      if (LPE >= 8) {
+        const int j = lie & 7;
+        const double xj = (j == 0) ? xv[0] : (j == 1) ? xv[1] : (j == 2) ? xv[2] : (j == 3) ? xv[3] : xv[4];
+        const double tj = (j == 2) ? tg[2] : (j == 4) ? tg[4] : 0.0;
+        const double oj = (j == 0) ? of[0] : (j == 1) ? of[1] : (j == 2) ? of[2] : (j == 3) ? of[3] : of[4];
+        const double ej = exp(-((xj - tj) * (xj - tj)) / oj);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ex[k] = shfl_d(ej, env_lane0 + k);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ex[k] = exp(-((xv[k] - tg[k]) * (xv[k] - tg[k])) / of[k]);
+      }
+      // rd4(t, off, v) = v < t ? 1 : exp(.), rd3(t, off, v) = v < t ? exp(.) : 1
+      double r0 = (dist < 10000 && enc_ok) ? ((xv[0] < 0.0) ? 1.0 : ex[0]) : 0.0;
+      double r1 = (Tground <= 1000) ? ((xv[1] < 0.0) ? 1.0 : ex[1]) : 0.0;
+      double r2 = (xv[2] < 3000.0) ? ex[2] : 1.0;
+      double r3 = (Oground <= 1000) ? -((xv[3] < 0.0) ? 1.0 : ex[3]) : 0.0;
+      double r4 = -((xv[4] < 500.0) ? ex[4] : 1.0);
       double r = (r0 + ((((0.0 + r1) + r2) + r3) + r4)) / 5;  // np.sum(5 terms) / 5
       if (is_collision || is_tg || is_tnav || is_og || is_onav) {  // :272-314
         const double reward = r + acc;
