@@ -242,26 +242,6 @@ __device__ __forceinline__ double shfl_d(double x, int src) {
 constexpr double kCosPhiAh = 0.36650122672429719;  // cos(68.5°) (only used against a 1e-9 band)
 constexpr double kSinPhiAh = 0.93041756798202460;  // sin(68.5°)
 
-// sqrt(d2s) < D, decided without the sqrt unless d2s is within 1e-12 of D² (sqrt is correctly
-// rounded and monotone, so outside that band the comparison cannot change)
-__device__ __forceinline__ bool dist_lt(double d2s, double D) {
-  const double D2 = D * D;
-  if (d2s < D2 * (1.0 - 1e-12)) return true;
-  if (d2s > D2 * (1.0 + 1e-12)) return false;
-  return sqrt(d2s) < D;
-}
-
-// d_safe_i from the obstacle's sector (sbmpc.py:237-244), see sbmpc_sample_cost
-__device__ __forceinline__ double sbmpc_dsafe_sector(const SbIn& in, double so, double co, double d0, double d1,
-                                                     double d2s, double ds_ah, double ds_ot, double ds_eq) {
-  const double PHI_AH = 68.5 * (kPi / 180.0), PHI_OT = 68.5 * (kPi / 180.0);
-  const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
-  const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
-  if (cr * cr > 1e-18 * d2s && ey * ey > 1e-18 * d2s) return (cr >= 0 && ey > 0) ? ds_ot : ds_ah;
-  const double phi_o = wrap_pmpi(atan2(-d1, -d0) - in.ob_psi + kPi / 2);
-  return (phi_o < PHI_AH) ? ds_ah : ((phi_o > PHI_OT) ? ds_ot : ds_eq);
-}
-
 // Per-sample collision cost H0 = C·R of sbmpc.py:205-289 (KAPPA_ = 0) for one prediction sample with
 // obstacle-minus-own-ship offset (d0, d1); (ss, cs, sv) are the own ship's sin/cos(psi_) and sway
 // at that sample. R and C stay 0 unless dist < d_safe_i <= max_d_safe, so the sector geometry (atan2,
@@ -332,7 +312,33 @@ __device__ __forceinline__ double sbmpc_scenario_cost_direct(const SbIn& in, int
   return H1 + H2;
 }
 
+#ifdef SHIPSIM_PHASE_TIMING
+// timing build: split of one scenario evaluation into g_phase_cycles[4..7]
+struct SbTimer {
+  unsigned long long t0, acc[4] = {0, 0, 0, 0};
+  __device__ SbTimer() : t0(wall_clock64()) {}
+  __device__ void mark(int k) {
+    const unsigned long long t = wall_clock64();
+    acc[k] += t - t0;
+    t0 = t;
+  }
+  __device__ ~SbTimer() {
+    mark(3);
+    if ((threadIdx.x & 31) == 0)
+      for (int k = 0; k < 4; ++k) atomicAdd(&g_phase_cycles[4 + k], acc[k]);
+  }
+};
+#define SB_MARK(k) sb_timer.mark(k)
+#else
+#define SB_MARK(k) \
+  do {             \
+  } while (0)
+#endif
+
 __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
+#ifdef SHIPSIM_PHASE_TIMING
+  SbTimer sb_timer;
+#endif
   const double os_l = 25.0;  // ShipLinearModel default length (sbmpc_misc.py:86, Q7)
   const double d_safe = 1000.0, d_close = 2000.0;
   const double PHI_OT = 68.5 * (kPi / 180.0);
@@ -377,6 +383,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     k = k < 0 ? 0 : (k > n_samp - 2 ? n_samp - 2 : k);
     const double mx = p1x + k * wx, my = p1y + k * wy;
     const double lim = max_d_safe + 1e-3;
+    SB_MARK(0);
     if (e0x * e0x + e0y * e0y > lim * lim && mx * mx + my * my > lim * lim) return 0.0 + H2;
   }
   const double lim2 = (max_d_safe * (1.0 + 1e-9)) * (max_d_safe * (1.0 + 1e-9));
@@ -388,6 +395,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
                                         in.os_v, max_d_safe, lim2, cos_ot);
     if (H0 > H1) H1 = H0;
   }
+  SB_MARK(1);
   // Samples 1..n-1: the own ship's velocity is constant (sway zeroed), so C and the overtaking
   // override of d_safe_i are sample-independent, and H0 = C·R with R = d_safe^4 / (t·dist^4).
   // max_i fl(C·R_i) = fl(C·max_i R_i) (rounding is monotone), so only the sample with the largest
@@ -397,9 +405,13 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   const double dot1 = vs0 * vo0 + vs1 * vo1;
   const double ns1 = sqrt(vs0 * vs0 + vs1 * vs1);
   const bool ovr = dot1 > cos_ot * ns1 * no && ns1 > no;
-  const double ds_ah = d_safe + in.obs_l / 2, ds_ot = 0.5 * d_safe + in.obs_l / 2, ds_eq = d_safe + in.obs_w / 2;
+  const double ds_ah = d_safe + in.obs_l / 2, ds_ot = 0.5 * d_safe + in.obs_l / 2;  // :239-242
   const double ds_ovr = d_safe + os_l / 2 + in.obs_l / 2;
-  const double ds_lo = py_min(py_min(ds_ah, ds_ot), ds_eq), ds_hi = py_max(py_max(ds_ah, ds_ot), ds_eq);
+  // Branch-free horizon: membership dist < d_safe_i (and < d_close) is decided on d2s against the
+  // squared thresholds; a sample within 1e-12 of a threshold, or whose sector is within 1e-9 of
+  // the PHI_AH / PHI_OT boundary, marks the scenario `unc` and it is re-evaluated sample by sample.
+  constexpr double kEps = 1e-12;
+  const double ah2 = ds_ah * ds_ah, ot2 = ds_ot * ds_ot, ovr2 = ds_ovr * ds_ovr, cl2 = d_close * d_close;
   // position increments: the obstacle's are constant, the own ship's use its sway at sample 1
   // only (linear_pred zeroes v after the first step)
   const double dox = (r11 * in.ob_u + r12 * in.ob_v) * DT, doy = (r21 * in.ob_u + r22 * in.ob_v) * DT;
@@ -408,6 +420,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   double sx = in.os_x + DT * (q11 * ud + q12 * in.os_v), sy = in.os_y + DT * (q21 * ud + q22 * in.os_v);
   double t = DT;
   double s1 = INFINITY, s2 = INFINITY, t1 = 0.0, q1 = 0.0;
+  bool unc = false;
   for (int i = 1; i < n_samp; ++i) {
     ox = ox + dox;
     oy = oy + doy;
@@ -418,29 +431,26 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     t += DT;
     const double d0 = ox - sx, d1 = oy - sy;
     const double d2s = d0 * d0 + d1 * d1;
-    if (d2s < lim2) {
-      bool member;
-      if (ovr) {
-        member = dist_lt(d2s, ds_ovr);
-      } else if (dist_lt(d2s, ds_lo)) {
-        member = true;
-      } else if (!dist_lt(d2s, ds_hi)) {
-        member = false;
-      } else {
-        member = dist_lt(d2s, sbmpc_dsafe_sector(in, so, co, d0, d1, d2s, ds_ah, ds_ot, ds_eq));
-      }
-      member = member && dist_lt(d2s, d_close);
-      if (member) {
-        const double s = t * d2s * d2s;
-        if (s < s1) {
-          s2 = s1;
-          s1 = s; t1 = t; q1 = d2s;
-        } else if (s < s2) {
-          s2 = s;
-        }
-      }
+    if (d2s < lim2) {  // samples beyond max_d_safe contribute nothing
+      // sector of phi_o (see sbmpc_sample_cost): overtaking sector iff cr >= 0 and ey > 0
+      const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
+      const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
+      const bool sec_ok = cr * cr > 1e-18 * d2s && ey * ey > 1e-18 * d2s;
+      const double D2 = ovr ? ovr2 : ((cr >= 0 && ey > 0) ? ot2 : ah2);
+      const bool member = d2s < D2 * (1.0 - kEps) && d2s < cl2 * (1.0 - kEps);
+      unc = unc || (!ovr && !sec_ok) || fabs(d2s - D2) <= kEps * D2 || fabs(d2s - cl2) <= kEps * cl2;
+      const double sc = member ? t * d2s * d2s : INFINITY;
+      const bool lt1 = sc < s1;
+      s2 = lt1 ? s1 : (sc < s2 ? sc : s2);
+      t1 = lt1 ? t : t1;
+      q1 = lt1 ? d2s : q1;
+      s1 = lt1 ? sc : s1;
     }
   }
+  if (unc)
+    return sbmpc_scenario_cost_direct(in, n_samp, DT, ud, sp, cp, sp0, cp0, so, co, vo0, vo1, no, max_d_safe, lim2,
+                                      cos_ot, H2);
+  SB_MARK(2);
   if (s1 < INFINITY) {
     if (s2 <= s1 * (1.0 + 1e-10))
       return sbmpc_scenario_cost_direct(in, n_samp, DT, ud, sp, cp, sp0, cp0, so, co, vo0, vo1, no, max_d_safe, lim2,

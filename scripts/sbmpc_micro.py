@@ -6,7 +6,13 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from ast_sac_amd.shipsim import sbmpc_eval  # noqa: E402
+from ast_sac_amd.shipsim import sbmpc_eval, load_library  # noqa: E402
+import ctypes as C  # noqa: E402
+L = load_library()
+timing = hasattr(L, "shipsim_debug_phase_cycles")
+if timing:
+    L.shipsim_debug_phase_cycles.argtypes = [C.c_void_p]
+    buf = (C.c_ulonglong * 8)()
 
 rng = np.random.Generator(np.random.PCG64(5))
 n = 65536
@@ -23,6 +29,8 @@ for rad_hi, tag in ((2000, "encounters within D_INIT"), (1000, "close (< 1 km)")
     for _ in range(3):
         sbmpc_eval(x)
     torch.cuda.synchronize()
+    if timing:
+        L.shipsim_debug_phase_cycles(buf)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(10):
@@ -33,3 +41,8 @@ for rad_hi, tag in ((2000, "encounters within D_INIT"), (1000, "close (< 1 km)")
     passes = 32  # 64 requests per wave, two per pass; 1024 waves = one per SIMD
     print(f"{tag}: {ms:.3f} ms for {n} requests -> {ms * 1e3 / passes:.2f} us "
           f"({ms * 1e-3 / passes * 2.4e9:.0f} cycles at 2.4 GHz) per pass")
+    if timing:
+        L.shipsim_debug_phase_cycles(buf)
+        cyc = np.array(buf[4:8], dtype=np.float64)
+        print("   scenario split: setup+skip %.1f%%, sample0 %.1f%%, horizon loop %.1f%%, final/fallback %.1f%%"
+              % tuple(100 * cyc / max(cyc.sum(), 1)))
