@@ -341,8 +341,9 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
 #endif
   const double os_l = 25.0;  // ShipLinearModel default length (sbmpc_misc.py:86, Q7)
   const double d_safe = 1000.0, d_close = 2000.0;
-  const double PHI_OT = 68.5 * (kPi / 180.0);
-  const double cos_ot = cos(PHI_OT * (kPi / 180.0));  // np.cos(np.deg2rad(PHI_OT_)) — PHI_OT_ already in rad
+  // np.cos(np.deg2rad(PHI_OT_)) — PHI_OT_ is already in radians (sbmpc.py:248): a constant, taken
+  // as the correctly rounded double of cos(68.5·(π/180)²) (NumPy and glibc agree on it)
+  constexpr double cos_ot = 0.9997823068017366;
   const double max_d_safe = py_max(py_max(d_safe + in.obs_l / 2, 0.5 * d_safe + in.obs_l / 2),
                                    py_max(d_safe + in.obs_w / 2, d_safe + os_l / 2 + in.obs_l / 2));
   const double CHI_DEG = -30.0 + 10.0 * ichi;

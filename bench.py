@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--envs-per-gpu", type=int, default=4096)
     p.add_argument("--collav", default="sbmpc", choices=["none", "simple", "sbmpc"])
     p.add_argument("--machinery", default="detailed", choices=["detailed", "simplified"])
-    p.add_argument("--slice", type=int, default=64, help="max ticks per env per step call (0 = whole decision)")
+    p.add_argument("--slice", type=int, default=128, help="max ticks per env per step call (0 = whole decision)")
     p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library default)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
