@@ -422,6 +422,9 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   double t = DT;
   double s1 = INFINITY, s2 = INFINITY, t1 = 0.0, q1 = 0.0;
   bool unc = false;
+#ifdef SHIPSIM_ABL_NO_SBLOOP
+  n_samp = 1;  // ablation build only: no horizon samples after sample 0
+#endif
   for (int i = 1; i < n_samp; ++i) {
     ox = ox + dox;
     oy = oy + doy;
