@@ -186,8 +186,9 @@ def main():
     obs_reset = torch.empty((N, 8), dtype=torch.float32, device=dev)
     total_ticks = torch.zeros((), dtype=torch.int64, device=dev)
     total_decisions = torch.zeros((), dtype=torch.int64, device=dev)
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    n_ev = args.steps + args.warmup  # every launch is bracketed (warmup ones too, to compare with rocprof)
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
 
     def one_step(timed_i=None):
         act = table[ep_idx % table_eps, dec_idx, ar]
@@ -206,8 +207,8 @@ def main():
         sim.reset(mask=end.to(torch.uint8), obs_out=obs_reset)
 
     sim.reset(obs_out=obs_reset)
-    for _ in range(args.warmup):
-        one_step()
+    for i in range(args.warmup):
+        one_step(args.steps + i)
     total_ticks.zero_()
     total_decisions.zero_()
     torch.cuda.synchronize()
@@ -223,7 +224,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    kern_ms = np.array([a.elapsed_time(b) for a, b in zip(ev0, ev1)])
+    all_ms = np.array([a.elapsed_time(b) for a, b in zip(ev0, ev1)])
+    kern_ms = all_ms[:args.steps]
     local_ticks = int(total_ticks.item())
     stats = torch.tensor([elapsed, float(local_ticks), float(total_decisions.item()), float(kern_ms.mean())],
                          dtype=torch.float64, device=dev)
@@ -281,7 +283,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"ast_step_kernel (avg {kmean:.3f} ms/launch, "
-                                   f"{ticks_per_launch:.0f} env-ticks x {ALGO_BYTES_PER_ENV_TICK} B)"},
+                                   f"{ticks_per_launch:.0f} env-ticks x {ALGO_BYTES_PER_ENV_TICK} B)",
+                         "kernel_ms_timed": kmean, "kernel_ms_all_launches": float(all_ms.mean()),
+                         "launches": int(len(all_ms))},
             "cpu_baseline": cpu,
             "sac": sac,
         }

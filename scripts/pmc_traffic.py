@@ -31,7 +31,8 @@ def main(fetch_dir, write_dir, out, collav="sbmpc", envs=4096):
                fetch_size_kb_raw=sum(fe) / len(fe), write_size_kb=sum(wr) / len(wr),
                fetch_bytes_corrected=fetch_b, write_bytes=write_b, hbm_bytes_per_launch=fetch_b + write_b,
                note="FETCH_SIZE x2 (gfx950 wide-read correction, MI355X_MICROARCH.md HBM section); "
-                    "bench.py --steps 10 --warmup 4 --no-cpu-baseline --sac-steps 0, slice 64, LPE default")
+                    "python3 bench.py --no-cpu-baseline --sac-steps 0 (default steps/warmup/slice), averaged over "
+                    "every ast_step_kernel dispatch of the run")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
