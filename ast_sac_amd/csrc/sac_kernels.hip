@@ -551,10 +551,16 @@ struct GTask {
   int mat, j0, k0;
 };
 constexpr int kMaxMats = 24;
+// Row split of the weight gradients: grid.y = kParts blocks per tile each reduce B / kParts rows
+// into partial gradient p (same layout as the flat gradient); sac_gsum_kernel adds the kParts
+// partials in a fixed order (deterministic) into the gradient.
+constexpr int kParts = 4;
 struct WgradArgs {
   GMat mats[kMaxMats];
   const GTask* tasks;
   int n_tasks;
+  float* partials;          // [kParts][n_params]
+  int64_t n_params;
   float* grads;
   int B;
   Scratch sc;
@@ -567,6 +573,7 @@ struct WgradArgs {
 __global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
   const int tid = threadIdx.x;
   if ((int)blockIdx.x == a.n_tasks) {  // scalars: losses, α and d(log α); step += 1
+    if (blockIdx.y != 0) return;
     float v[5] = {0, 0, 0, 0, 0};
     for (int r = tid; r < a.B; r += kThreads) {
       v[0] += a.sc.p_pl[r];
@@ -600,12 +607,15 @@ __global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
   for (int p = 0; p < 4; ++p)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[p][q] = 0.0f;
-  for (int rb = 0; rb < a.B; rb += 32) {
+  const int part = blockIdx.y;
+  const int rows = (a.B + kParts - 1) / kParts;
+  const int r_lo = part * rows, r_hi = min(a.B, r_lo + rows);
+  for (int rb = r_lo; rb < r_hi; rb += 32) {
     for (int e = tid; e < 32 * 64; e += kThreads) {
       const int rr = e >> 6, cc = e & 63, r = rb + rr;
       const int jj = t.j0 + cc, kk = t.k0 + cc;
-      sY[rr][cc] = (r < a.B && jj < m.M) ? m.dY[(int64_t)r * m.ldY + jj] : 0.0f;
-      sX[rr][cc] = (r < a.B && kk < m.N) ? (m.X ? m.X[(int64_t)r * m.ldX + kk] : 1.0f) : 0.0f;
+      sY[rr][cc] = (r < r_hi && jj < m.M) ? m.dY[(int64_t)r * m.ldY + jj] : 0.0f;
+      sX[rr][cc] = (r < r_hi && kk < m.N) ? (m.X ? m.X[(int64_t)r * m.ldX + kk] : 1.0f) : 0.0f;
     }
     __syncthreads();
 #pragma unroll 4
@@ -622,6 +632,7 @@ __global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
     }
     __syncthreads();
   }
+  float* P = a.partials + (size_t)part * a.n_params;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int jj = t.j0 + tj * 4 + p;
@@ -629,9 +640,20 @@ __global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int kk = t.k0 + tk * 4 + q;
-      if (kk < m.N) a.grads[m.out_off + (int64_t)jj * m.N + kk] = acc[p][q];
+      if (kk < m.N) P[m.out_off + (int64_t)jj * m.N + kk] = acc[p][q];
     }
   }
+}
+
+// gradient = Σ_p partial_p (p = 0..kParts-1 in order); element 0 (d log α) is the scalar block's
+__global__ __launch_bounds__(kThreads) void sac_gsum_kernel(const float* __restrict__ partials, float* grads,
+                                                            int64_t n_params) {
+  const int64_t e = 1 + (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= n_params) return;
+  float g = partials[e];
+#pragma unroll
+  for (int p = 1; p < kParts; ++p) g += partials[(size_t)p * n_params + e];
+  grads[e] = g;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -722,6 +744,7 @@ struct sacf_handle {
   Scratch sc;
   GTask* tasks;
   int n_tasks;
+  float* partials;
   GMat mats[kMaxMats];
   int n_mats;
   char err[512];
@@ -871,6 +894,11 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
         for (int k0 = 0; k0 < m.N; k0 += 64) tasks.push_back(GTask{mi, j0, k0});
     }
   h->n_tasks = (int)tasks.size();
+  e = hipMalloc(&h->partials, sizeof(float) * kParts * L.n_params);
+  if (e != hipSuccess) {
+    *out = h;
+    return sfail(h, SACF_EHIP, "partials: %s", hipGetErrorString(e));
+  }
   e = hipMalloc(&h->tasks, sizeof(GTask) * tasks.size());
   if (e == hipSuccess) e = hipMemcpy(h->tasks, tasks.data(), sizeof(GTask) * tasks.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -887,6 +915,7 @@ int sacf_destroy(sacf_handle* h) {
   if (h->scratch) (void)hipFree(h->scratch);
   if (h->T) (void)hipFree(h->T);
   if (h->tasks) (void)hipFree(h->tasks);
+  if (h->partials) (void)hipFree(h->partials);
   delete h;
   return SACF_OK;
 }
@@ -990,6 +1019,8 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   for (int i = 0; i < h->n_mats; ++i) w.mats[i] = h->mats[i];
   w.tasks = h->tasks;
   w.n_tasks = h->n_tasks;
+  w.partials = h->partials;
+  w.n_params = h->L.n_params;
   w.grads = h->grads;
   w.B = h->L.B;
   w.sc = h->sc;
@@ -997,7 +1028,9 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   w.step = h->step;
   w.stats = h->stats;
   w.hp = h->hp;
-  hipLaunchKernelGGL(sac_wgrad_kernel, dim3(h->n_tasks + 1), dim3(kThreads), 0, h->stream, w);
+  hipLaunchKernelGGL(sac_wgrad_kernel, dim3(h->n_tasks + 1, kParts), dim3(kThreads), 0, h->stream, w);
+  hipLaunchKernelGGL(sac_gsum_kernel, dim3((unsigned)((h->L.n_params - 1 + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     h->stream, h->partials, h->grads, h->L.n_params);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
 }
