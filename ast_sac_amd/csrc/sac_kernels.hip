@@ -554,7 +554,7 @@ constexpr int kMaxMats = 24;
 // Row split of the weight gradients: grid.y = kParts blocks per tile each reduce B / kParts rows
 // into partial gradient p (same layout as the flat gradient); sac_gsum_kernel adds the kParts
 // partials in a fixed order (deterministic) into the gradient.
-constexpr int kParts = 4;
+constexpr int kParts = 8;
 struct WgradArgs {
   GMat mats[kMaxMats];
   const GTask* tasks;
