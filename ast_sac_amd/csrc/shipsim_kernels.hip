@@ -55,7 +55,9 @@ struct DevState {
   __host__ __device__ uint32_t* snap_bits() const { return (uint32_t*)ev(11); }
   __host__ __device__ int32_t* was_reset() const { return (int32_t*)ev(12); }
   __host__ __device__ int32_t* dec_flags() const { return (int32_t*)ev(13); }  // DF_* (sliced stepping)
-  static constexpr int kEnvArrays = 14;
+  __host__ __device__ double* legacy_states() const { return (double*)ev(14); }  // [env][4] legacy self.states
+  __host__ __device__ int32_t* legacy_flags() const { return (int32_t*)ev(15); }  // 1: still the f32 initial_states
+  static constexpr int kEnvArrays = 16;
   static constexpr int kShipArrays = 22;
 };
 #ifdef SHIPSIM_PHASE_TIMING
@@ -557,6 +559,8 @@ __global__ void init_kernel(const Params P, DevState S, ConstBuf K) {
     S.snap_bits()[env] = 0;
     S.was_reset()[env] = 0;
     S.dec_flags()[env] = DF_AWAITING;
+    for (int i = 0; i < 4; ++i) S.legacy_states()[env * 4 + i] = 0.0;
+    S.legacy_flags()[env] = 1;
   }
 }
 
@@ -1097,6 +1101,145 @@ __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevStat
   const double mach_dt = S.mach_dt()[q];
   for (int i = 0; i < k; ++i) control_and_integrate<DETAILED>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false);
   store_ship(S, q, s);
+}
+
+// Legacy per-tick MultiShipEnv.step (rl_env/ship_in_transit/env.py:1104-1173), k steps per launch.
+// Two lanes per env (lane & 1 = ship); the termination flags of get_termination_status
+// (termination_flags.py:5-70) are evaluated in fp64 on the next_states, as the reference does on
+// its Python-float list.
+template <bool DETAILED, int COLLAV>
+__global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevState S, ConstBuf K, int k,
+                                                         double* __restrict__ states_out, uint8_t* __restrict__ done_out,
+                                                         uint32_t* __restrict__ status_out) {
+  __shared__ ShipConst lds_sc[2];
+  __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
+  __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
+  const ShipConst* SC = stage_consts(P, lds_sc);
+  for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) lds_edges_raw[i] = K.edges()[i];
+  for (int i = threadIdx.x; i < P.n_polys; i += blockDim.x) lds_boxes[i] = K.boxes()[i];
+  __syncthreads();
+
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int env = gl >> 1;
+  const int ship = gl & 1;
+  const bool is_test = ship == 0;
+  const bool valid = env < P.n_envs;
+  const int envc = valid ? env : 0;
+  const int qc = envc * 2 + ship;
+  const ShipConst& c = SC[ship];
+  const double* rn = S.route_n() + (size_t)qc * kMaxRoute;
+  const double* re = S.route_e() + (size_t)qc * kMaxRoute;
+  Ship s;
+  load_ship(S, qc, s);
+  double p_last = S.p_last()[envc], chi_last = S.chi_last()[envc];
+  const double mach_dt = S.mach_dt()[envc];
+  double* lst = S.legacy_states() + (size_t)envc * 4;  // self.states [test n, e, obs n, e]
+  double st[4] = {lst[0], lst[1], lst[2], lst[3]};
+  bool st_f32 = S.legacy_flags()[envc] & 1;
+  const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
+
+  double out8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t status = 0;
+  bool done = false, ticked = false;
+  bool going = valid;
+  for (int it = 0; it < k; ++it) {
+    if (!__any(going)) break;
+    const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
+    const double pu = pair_swap(s.u), pv = pair_swap(s.v);
+    double sf = 1.0, off = 0.0;
+    if (COLLAV == SHIPSIM_COLLAV_SBMPC) {  // test_step :938-963 (obstacle ship before it moves)
+      bool need = false;
+      SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      if (going && is_test) {
+        const double los_arg = los_update(c, s, s.n, s.e);
+        const double d0 = pe - s.e, d1 = pn - s.n;
+        need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
+        if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
+        in.u_d = c.desired_speed;
+        in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
+        in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
+        in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
+        in.p_last = p_last; in.chi_last = chi_last;
+      }
+      double pb = 1.0, cb = 0.0;
+      sbmpc_cooperative(need, in, n_samp, P.sbmpc_dt, pb, cb);
+      if (going && is_test) {
+        if (need) { p_last = pb; chi_last = cb; sf = pb; off = cb; }
+        else { p_last = 1; chi_last = 0; }
+      }
+    }
+    double speed_out = 0.0;
+    if (going) {
+      if (!is_test && s.stop) {  // obs_step :1029-1056: store_last + two next_time, speed reported 0
+        s.time = s.time + P.dt;
+        s.time = s.time + P.dt;
+      } else {
+        bool imminent = false;
+        if (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) {  // is_collision_imminent(self.states[0:2], [3:5])
+          if (st_f32) {
+            const float dn = P.initial_states[0] - P.initial_states[3], de = P.initial_states[1] - P.initial_states[4];
+            imminent = (dn * dn + de * de) < 9000000.0f;
+          } else {
+            imminent = ((st[0] - st[2]) * (st[0] - st[2]) + (st[1] - st[3]) * (st[1] - st[3])) < 9000000.0;
+          }
+        }
+        speed_out = s.u;
+        control_and_integrate<DETAILED>(c, P, s, rn, re, -off, sf, mach_dt,
+                                        (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) ? 1 : 0, imminent);
+      }
+    }
+    // own-ship flags on the post-tick state (check_condition.py)
+    bool my_end = false, my_out = false, my_gr = false;
+    if (going) {
+      const double margin = c.l_ship / 2;
+      my_end = sqrt((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e)) <= 200;
+      my_out = (s.n < P.min_north + margin || s.n > P.max_north - margin) ||
+               (s.e < P.min_east + margin || s.e > P.max_east - margin);
+      for (int q = 0; q < 4; ++q) {
+        const double cn = (q < 2) ? s.n - margin : s.n + margin;
+        const double ce = (q & 1) ? s.e + margin : s.e - margin;
+        if (corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) my_gr = true;
+      }
+    }
+    const bool my_nav = fabs(s.log_ect) > 500;  // is_ship_navigation_failure (e_tol 500, both ships)
+    const int my_flags = (my_end ? 1 : 0) | (my_out ? 2 : 0) | (my_gr ? 4 : 0) | (my_nav ? 8 : 0);
+    const int o_flags = pair_swap_i(my_flags);
+    const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
+    const double o_ect = pair_swap(s.log_ect), o_speed = pair_swap(speed_out);
+    if (going) {
+      const double Tn = is_test ? s.n : o_n, Te = is_test ? s.e : o_e;
+      const double On = is_test ? o_n : s.n, Oe = is_test ? o_e : s.e;
+      const int Tf = is_test ? my_flags : o_flags, Of = is_test ? o_flags : my_flags;
+      out8[0] = Tn; out8[1] = Te; out8[2] = is_test ? s.log_ect : o_ect;
+      out8[3] = On; out8[4] = Oe; out8[5] = is_test ? o_yaw : s.yaw;
+      out8[6] = is_test ? o_speed : speed_out; out8[7] = is_test ? o_ect : s.log_ect;
+      const double cd = (Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe);
+      status = (uint32_t)(Tf & 15) | (cd < 9000000.0 ? SHIPSIM_LT_NEAR_COLLISION : 0u) |
+               (cd < 2500.0 ? SHIPSIM_LT_COLLISION : 0u) | ((uint32_t)(Of & 15) << 6);
+      done = (status & (SHIPSIM_LT_TEST_REACHED | SHIPSIM_LT_TEST_OUTSIDE | SHIPSIM_LT_TEST_GROUNDED |
+                        SHIPSIM_LT_TEST_NAV_FAILURE | SHIPSIM_LT_COLLISION | SHIPSIM_LT_OBS_GROUNDED |
+                        SHIPSIM_LT_OBS_NAV_FAILURE)) != 0;
+      // stop_int_obs = obs_is_outside and obs_is_reached (:1168-1171)
+      if (!is_test && (Of & 2) && (Of & 1)) s.stop = 1;
+      st[0] = Tn; st[1] = Te; st[2] = On; st[3] = Oe;
+      st_f32 = false;
+      ticked = true;
+      going = !done;
+    }
+  }
+  if (!valid) return;
+  store_ship(S, qc, s);
+  if (is_test) {
+    S.p_last()[env] = p_last; S.chi_last()[env] = chi_last;
+    for (int i = 0; i < 4; ++i) lst[i] = st[i];
+    S.legacy_flags()[env] = st_f32 ? 1 : 0;
+    if (ticked) {
+      if (states_out)
+        for (int i = 0; i < 8; ++i) states_out[(size_t)env * 8 + i] = out8[i];
+      if (done_out) done_out[env] = done ? 1 : 0;
+      if (status_out) status_out[env] = status;
+    }
+  }
 }
 
 // SBMPC.get_optimal_ctrl_offset (sbmpc.py:113-185) for a batch of independent single-obstacle
@@ -1782,6 +1925,26 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
     hipLaunchKernelGGL(single_tick_kernel<true>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
   else
     hipLaunchKernelGGL(single_tick_kernel<false>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
+  HIPCHK(h, hipGetLastError());
+  return SHIPSIM_OK;
+}
+
+int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_t* done_out, uint32_t* status_out) {
+  if (!h || !h->dev_block || k < 0) return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "legacy_step: AST kind only");
+  if (k == 0) return SHIPSIM_OK;
+  DeviceGuard g(h->device);
+  const int threads = 64, blocks = (2 * h->P.n_envs + threads - 1) / threads;
+#define LEGACY(D, CA)                                                                                      \
+  hipLaunchKernelGGL((legacy_step_kernel<D, CA>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k, \
+                     states_out, done_out, status_out)
+  const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
+  switch (h->P.collav) {
+    case SHIPSIM_COLLAV_SBMPC: if (det) LEGACY(true, SHIPSIM_COLLAV_SBMPC); else LEGACY(false, SHIPSIM_COLLAV_SBMPC); break;
+    case SHIPSIM_COLLAV_SIMPLE: if (det) LEGACY(true, SHIPSIM_COLLAV_SIMPLE); else LEGACY(false, SHIPSIM_COLLAV_SIMPLE); break;
+    default: if (det) LEGACY(true, SHIPSIM_COLLAV_NONE); else LEGACY(false, SHIPSIM_COLLAV_NONE); break;
+  }
+#undef LEGACY
   HIPCHK(h, hipGetLastError());
   return SHIPSIM_OK;
 }

@@ -20,7 +20,7 @@ import torch
 from ... import shipsim_abi as abi
 from ...shipsim import ShipSim
 from ...spaces import Box
-from .trajectory import EpisodeRecord, RewardTracker
+from .trajectory import EpisodeRecord, RewardTracker, ShipSnapshots
 
 # observation_space / action_space of env.py:86-104
 OBS_LOW = np.array([0, 0, -3000, 0, 0, -np.pi, -3000, 0], dtype=np.float32)
@@ -119,6 +119,11 @@ class BatchedMultiShipRLEnv:
         self.np_random = np.random.default_rng(seed)
 
     # -- trajectory recording (simulation_results export) --
+    def legacy_step(self, k=1, out=None):
+        """k ticks of the legacy per-tick MultiShipEnv.step() (env.py:1104-1173) for every env:
+        dict(states (N, 8) float64 next_states, done (N,) uint8, status (N,) int32 LT_* bits)."""
+        return self.sim.legacy_step(k, out=out)
+
     def record_trajectories(self, capacity=None):
         """Record every tick of every env (both ships' simulation_results rows + RewardTracker rows)
         into device buffers; rows start at the next reset. capacity defaults to the longest episode
@@ -180,6 +185,11 @@ class _ShipModelView:
     @property
     def simulation_results(self):
         return self._env._record().simulation_results(self._ship)
+
+    @property
+    def ship_drawings(self):
+        """[[x arrays], [y arrays]] of the ShipDraw snapshots since the last reset (ship_draw=True)."""
+        return self._env._ship_drawings(self._ship)
 
 
 class _NavigateView:
@@ -246,6 +256,9 @@ class MultiShipRLEnv:
         self.accumulated_rewards_list = []
         self.env_info = {"events": "", "terminal": False, "test_ship_stop": False, "obs_ship_stop": False}
         self._dev = self._b.device
+        # ShipDraw snapshots (env.py:118-120, :573-579): the timer is env-level and survives reset
+        self.ship_draw = bool(getattr(self.args, "ship_draw", False))
+        self._snap = ShipSnapshots(self._b.cfg.time_step, float(getattr(self.args, "time_since_last_ship_drawing", 30)))
 
     do_normalize_action = BatchedMultiShipRLEnv.do_normalize_action
     do_denormalize_action = BatchedMultiShipRLEnv.do_denormalize_action
@@ -295,7 +308,26 @@ class MultiShipRLEnv:
         self._extra_totals = []
         self.accumulated_rewards_list = []
         self.env_info = {"events": "", "terminal": False, "test_ship_stop": False, "obs_ship_stop": False}
+        self._snap.reset()  # ship_model.reset() restores the empty drawings; the timer carries on
         return obs[0].cpu().numpy()
+
+    @property
+    def time_since_last_ship_drawing(self):
+        return self._snap.timer
+
+    def _ship_drawings(self, ship):
+        self._record()
+        return self._snap.drawings[ship]
+
+    def _ship_snapshots(self, n_ticks):
+        """ShipDraw snapshots of this call's ticks, at each firing tick's post-tick state read from
+        the device trajectory rows (or the state now, for the last tick / a stopped ship)."""
+        fire = self._snap.advance(n_ticks)
+        if not fire or not self.record_trajectory:
+            return
+        rec, sim = self._record(), self._b.sim
+        now = [tuple(float(sim.get(f)[s].item()) for f in (abi.F_NORTH, abi.F_EAST, abi.F_YAW)) for s in (0, 1)]
+        self._snap.draw(fire, rec.ship_rows, now)
 
     def step(self, action):
         a = np.asarray(action, dtype=np.float32).reshape(-1)[:1]
@@ -304,6 +336,8 @@ class MultiShipRLEnv:
             self.waypoint_sampling_times.append(t_obs - float(self._b.cfg.time_step))
         obs, r, done, info = self._b.step(torch.from_numpy(a))
         bits = int(info["events"][0].item())
+        if self.ship_draw:
+            self._ship_snapshots(int(info["ticks"][0].item()))
         if bits & abi.EV_SAMPLING_FAILURE:
             self._extra_totals.append(float(r[0].item()))
         env_info = {"events": abi.events_to_string(bits), "terminal": bool(bits & abi.EV_TERMINAL),
@@ -326,3 +360,75 @@ class MultiShipRLEnv:
     def __setstate__(self, st):
         self.__init__(st["args"], device=st["device"], cfg=abi.Config.from_buffer_copy(st["cfg"]),
                       record_trajectory=st.get("record", False))
+
+
+class MultiShipEnv:
+    """The legacy per-tick env of rl_env/ship_in_transit/env.py:783-1181 over the device (N = 1 view):
+    reset() -> initial_states; step() -> (next_states: list of 8 floats, done, termination_cond: list
+    of the 10 get_termination_status flags). One tick per step, no intermediate waypoints, no reward;
+    the ships are the scenario of record (assets/map arguments are accepted for signature parity and
+    must describe that scenario; the configuration comes from `args` / `cfg`)."""
+
+    def __init__(self, assets=None, map=None, ship_draw=False, collav=None, time_since_last_ship_drawing=30,
+                 args=None, device=None, machinery="detailed", cfg=None):
+        self.args = args if args is not None else default_args()
+        self.collav = collav if collav is not None else getattr(self.args, "collav_mode", "sbmpc")
+        if cfg is None:
+            cfg = config_from_args(argparse.Namespace(**{**vars(self.args), "collav_mode": self.collav}), machinery)
+        self._b = BatchedMultiShipRLEnv(self.args, 1, device=device, machinery=machinery, cfg=cfg)
+        self.test, self.obs = ShipAssetView(self, 0), ShipAssetView(self, 1)
+        self.assets = [self.test, self.obs]
+        self.observation_space = self._b.observation_space
+        self.action_space = Box(low=np.array([-np.pi / 6], np.float32), high=np.array([np.pi / 6], np.float32),
+                                dtype=np.float32)
+        self.obsv_dim, self.action_dim = 8, 1
+        self.initial_states = self._b.initial_states
+        self.states = self.initial_states
+        self.next_states = self.initial_states
+        self.map = map
+        self.ship_draw = bool(ship_draw)
+        self._snap = ShipSnapshots(self._b.cfg.time_step, float(time_since_last_ship_drawing))
+        self._out = None
+        self.record_trajectory = False
+
+    @property
+    def time_since_last_ship_drawing(self):
+        return self._snap.timer
+
+    def _record(self):
+        raise RuntimeError("the legacy MultiShipEnv keeps no simulation_results on the device")
+
+    def _ship_drawings(self, ship):
+        return self._snap.drawings[ship]
+
+    def _route(self, ship):
+        return MultiShipRLEnv._route(self, ship)
+
+    def reset(self):
+        self._b.reset()
+        self._snap.reset()
+        return self.initial_states
+
+    def step(self):
+        self._out = self._b.legacy_step(1, out=self._out)
+        states = [float(x) for x in self._out["states"][0].cpu().tolist()]
+        bits = int(self._out["status"][0].item())
+        done = bool(self._out["done"][0].item())
+        if self.ship_draw:
+            fire = self._snap.advance(1)
+            if fire:
+                empty = np.empty((0, abi.TRAJ_SHIP_COLS))
+                self._snap.draw(fire, [empty, empty], [(states[0], states[1], self.test.ship_model.yaw_angle),
+                                                       (states[3], states[4], states[5])])
+        self.states = states
+        cond = [bool(bits >> i & 1) for i in range(10)]
+        return states, done, cond
+
+    def seed(self, seed=None):
+        self.np_random = np.random.default_rng(seed)
+
+    def ensure_scalar(self, x):
+        return float(x[0]) if isinstance(x, (np.ndarray, list)) else float(x)
+
+    def close(self):
+        self._b.close()

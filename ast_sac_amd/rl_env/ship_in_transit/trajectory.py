@@ -168,6 +168,80 @@ class RewardTracker:
         self.total.append(r_total)
 
 
+class ShipDraw:
+    """Map-view ship outline (utils/utils.py:56-101): an 80 m x 20 m pentagon, rotated by the yaw
+    angle and translated to (north, east). Snapshots are x = north-frame, y = east-frame arrays of 6
+    points (closed outline), as ship_model.ship_snap_shot (ship_model.py:612-624) stores them."""
+    l = 80.0
+    b = 20.0
+
+    def local_coords(self):
+        l, b = self.l, self.b
+        x = np.array([-l / 2, l / 4, l / 2, l / 4, -l / 2, -l / 2])
+        y = np.array([-b / 2, -b / 2, 0.0, b / 2, b / 2, -b / 2])
+        return x, y
+
+    def rotate_coords(self, x, y, psi):
+        return np.cos(psi) * x - np.sin(psi) * y, np.sin(psi) * x + np.cos(psi) * y
+
+    def translate_coords(self, x_ned, y_ned, north, east):
+        return x_ned + north, y_ned + east
+
+    def snapshot(self, north, east, yaw):
+        x, y = self.local_coords()
+        xr, yr = self.rotate_coords(x, y, yaw)
+        return self.translate_coords(xr, yr, north, east)
+
+
+def post_tick_state(ship_rows, tick, final_state):
+    """(north, east, yaw) of one ship right after episode tick `tick` (1-based; row 0 is the
+    init_step row, row j is stored by tick j before integrating). The next row holds it unless that
+    row is a store_last_simulation_data repeat (ship stopped, state frozen) or not yet written, in
+    which case the ship's state now (`final_state`) is it."""
+    nxt = tick + 1
+    if nxt < len(ship_rows) and ship_rows[nxt, abi.TS_REPEAT] == 0:
+        r = ship_rows[nxt]
+        return r[abi.TS_NORTH], r[abi.TS_EAST], r[abi.TS_YAW]
+    return final_state
+
+
+class ShipSnapshots:
+    """The env-level drawing timer and both ships' `ship_drawings` (env.py:118-120, :573-579).
+    The timer starts at args.time_since_last_ship_drawing, survives reset (only __init__ sets it);
+    each _step: snapshot both ships if timer > 30, then timer += dt. Drawings are cleared by reset
+    (ship_model.reset restores the empty lists)."""
+
+    def __init__(self, dt, timer0=30.0, n_ships=2):
+        self.dt = float(dt)
+        self.timer = float(timer0)
+        self.n_ships = n_ships
+        self.drawer = ShipDraw()
+        self.reset()
+
+    def reset(self):
+        self.drawings = [[[], []] for _ in range(self.n_ships)]
+        self.ticks = 0
+
+    def advance(self, n_ticks):
+        """Runs the timer over the next n_ticks episode ticks; returns the ticks that snapshot."""
+        fire = []
+        for j in range(self.ticks + 1, self.ticks + n_ticks + 1):
+            if self.timer > 30:
+                fire.append(j)
+                self.timer = 0
+            self.timer += self.dt
+        self.ticks += n_ticks
+        return fire
+
+    def draw(self, fire, ship_rows, now):
+        """ship_rows[s]: the ship's trajectory rows this episode; now[s]: its (north, east, yaw) now."""
+        for s in range(self.n_ships):
+            for j in fire:
+                x, y = self.drawer.snapshot(*post_tick_state(ship_rows[s], j, now[s]))
+                self.drawings[s][0].append(x)
+                self.drawings[s][1].append(y)
+
+
 class EpisodeRecord:
     """One env's record since its last reset, read back from the device buffers."""
 

@@ -47,6 +47,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_synchronize.argtypes = [P]
     L.shipsim_set_trajectory.argtypes = [P, P, P, C.c_int32, P]
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
+    L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     if L.shipsim_abi_version() != abi.ABI_VERSION:
         raise ShipSimError(f"ABI mismatch: library {L.shipsim_abi_version()} vs binding {abi.ABI_VERSION}")
     _lib = L
@@ -56,7 +57,7 @@ def load_library(path=LIB_PATH):
 EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_default_config", "shipsim_create",
                     "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
-                    "shipsim_set_trajectory", "shipsim_sbmpc_eval")
+                    "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step")
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
@@ -144,6 +145,18 @@ class ShipSim:
 
     def tick(self, k=1):
         self._check(self.L.shipsim_tick(self.h, int(k), None), "shipsim_tick")
+
+    def legacy_step(self, k=1, out=None):
+        """k legacy MultiShipEnv.step() ticks of every env (shipsim_legacy_step): dict(states=(N, 8) f64
+        next_states, done=(N,) u8, status=(N,) i32 termination bits LT_*) of each env's last tick."""
+        N = self.n_envs
+        if out is None:
+            out = dict(states=torch.zeros((N, 8), dtype=torch.float64, device=self.device),
+                       done=torch.zeros(N, dtype=torch.uint8, device=self.device),
+                       status=torch.zeros(N, dtype=torch.int32, device=self.device))
+        self._check(self.L.shipsim_legacy_step(self.h, int(k), _ptr(out["states"]), _ptr(out["done"]),
+                                               _ptr(out["status"])), "shipsim_legacy_step")
+        return out
 
     def _field_shape(self, field):
         S, N = self.n_envs * self.n_ships, self.n_envs

@@ -13,7 +13,7 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_ROUTE = 16
 MAX_POLYS = 16
 MAX_VERTS = 128
@@ -23,6 +23,20 @@ COLLAV_NONE, COLLAV_SIMPLE, COLLAV_SBMPC = 0, 1, 2
 COLLAV = {"none": COLLAV_NONE, None: COLLAV_NONE, "simple": COLLAV_SIMPLE, "sbmpc": COLLAV_SBMPC}
 MACH_SIMPLIFIED, MACH_DETAILED = 0, 1
 SG_GEN, SG_MOTOR, SG_OFF = 0, 1, 2
+
+# legacy MultiShipEnv termination_conditions bits (shipsim_legacy_step, termination_flags.py:66-68)
+LT_TEST_REACHED = 1 << 0
+LT_TEST_OUTSIDE = 1 << 1
+LT_TEST_GROUNDED = 1 << 2
+LT_TEST_NAV_FAILURE = 1 << 3
+LT_NEAR_COLLISION = 1 << 4
+LT_COLLISION = 1 << 5
+LT_OBS_REACHED = 1 << 6
+LT_OBS_OUTSIDE = 1 << 7
+LT_OBS_GROUNDED = 1 << 8
+LT_OBS_NAV_FAILURE = 1 << 9
+LT_DONE_MASK = (LT_TEST_REACHED | LT_TEST_OUTSIDE | LT_TEST_GROUNDED | LT_TEST_NAV_FAILURE | LT_COLLISION
+                | LT_OBS_GROUNDED | LT_OBS_NAV_FAILURE)
 
 EV_COLLISION = 1 << 0
 EV_TEST_GROUNDING = 1 << 1

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 2
+#define SHIPSIM_ABI_VERSION 3
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -331,6 +331,30 @@ int shipsim_set_trajectory(shipsim_handle* h, double* ship_rows, double* env_row
  * SBMPC(tf, dt) horizon; stream is a hipStream_t (NULL = default); device pointers. */
 #define SHIPSIM_SBMPC_IN 17
 int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double* out, void* stream);
+
+/* ---- legacy per-tick MultiShipEnv (rl_env/ship_in_transit/env.py:783-1181) ----
+ * AST kind. Each of the k ticks is one MultiShipEnv.step() (:1104-1173) of every env: test_step
+ * (:923-1023, SBMPC / simple collision avoidance as configured) + obs_step (:1025-1102) +
+ * get_termination_status (evaluation/termination_flags.py:5-70). No intermediate waypoints, no reward.
+ * Envs start from shipsim_reset (MultiShipEnv.reset/init_step, :855-921 — same placement as the RL
+ * reset); the simple collision check reads the previous step's next_states (the float32
+ * initial_states before the first step after create), which survive reset, as in the reference.
+ * An env whose step reports done stops ticking for the rest of the call (k = 1: the reference's
+ * per-call semantics). Outputs of the env's last tick (device, each may be NULL):
+ *   states  N x 8 doubles: next_states [test n, e, e_ct, obs n, e, yaw, speed, e_ct]
+ *   done    N uint8: test reached/outside/grounded/nav failure, collision, obs grounded/nav failure
+ *   status  N uint32: bit i = termination_conditions[i] (SHIPSIM_LT_*) */
+#define SHIPSIM_LT_TEST_REACHED (1u << 0)
+#define SHIPSIM_LT_TEST_OUTSIDE (1u << 1)
+#define SHIPSIM_LT_TEST_GROUNDED (1u << 2)
+#define SHIPSIM_LT_TEST_NAV_FAILURE (1u << 3)  /* |e_ct| > 500 */
+#define SHIPSIM_LT_NEAR_COLLISION (1u << 4)    /* distance < 3000 m */
+#define SHIPSIM_LT_COLLISION (1u << 5)         /* distance < 50 m */
+#define SHIPSIM_LT_OBS_REACHED (1u << 6)
+#define SHIPSIM_LT_OBS_OUTSIDE (1u << 7)
+#define SHIPSIM_LT_OBS_GROUNDED (1u << 8)
+#define SHIPSIM_LT_OBS_NAV_FAILURE (1u << 9)
+int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_t* done_out, uint32_t* status_out);
 
 /* Block until all work queued on the handle's stream is done. */
 int shipsim_synchronize(shipsim_handle* h);

@@ -778,6 +778,10 @@ typedef struct {
   double last_reward_tick;
   int ticks_total;
   double* rtick_buf; int rtick_cap, rtick_len;
+  /* legacy MultiShipEnv self.states: the float32 initial_states until its first step, then the
+   * Python-float next_states list of the previous step (kept across reset, env.py:855-888) */
+  double lstates[8];
+  int lstates_f32;
 } o_env;
 
 static void env_init_iw(o_env* env) { /* init_get_intermediate_waypoints env.py:143-169 */
@@ -817,6 +821,7 @@ o_env* oracle_env_create(const shipsim_config* cfg) {
     s[6] = 0.0f; s[7] = (float)env->a[1].m.u;
     memcpy(env->states, s, sizeof(env->states));
     memcpy(env->next_observations, s, sizeof(env->states));
+    env->lstates_f32 = 1;
   }
   return env;
 }
@@ -1093,6 +1098,75 @@ int oracle_env_step(o_env* env, float a, int max_ticks, float obs8[8], double* r
   *done_out = combined_done;
   *bits_out = bits;
   return ticks;
+}
+
+/* ---------------- legacy MultiShipEnv (rl_env/ship_in_transit/env.py:783-1181) ---------------- */
+/* step() :1104-1173: one tick of both ships + get_termination_status (termination_flags.py:5-70).
+ * out8 = next_states (Python floats), status bit i = termination_conditions[i]; returns done. */
+int oracle_legacy_step(o_env* env, double out8[8], uint32_t* status) {
+  o_asset* T = &env->a[0];
+  o_asset* O = &env->a[1];
+  /* test_step :923-1023 (the test ship has no stop path) */
+  {
+    double n = T->m.north, e = T->m.east, h = T->m.yaw, u = T->m.u;
+    double sf = 1.0, off = 0.0;
+    if (env->cfg.collav == SHIPSIM_COLLAV_SBMPC) sbmpc_block(env, T, n, e, &sf, &off);
+    double rudder = ap_rudder(&T->ap, n, e, h, -off);
+    double thr = speed_ctrl(T, T->desired_speed * sf, u);
+    if (env->cfg.collav == SHIPSIM_COLLAV_SIMPLE) {
+      int imm;
+      if (env->lstates_f32) {
+        imm = imminent_f32(env->initial_states);
+      } else { /* is_collision_imminent on Python floats */
+        const double* st = env->lstates;
+        imm = ((st[0] - st[3]) * (st[0] - st[3]) + (st[1] - st[4]) * (st[1] - st[4])) < 9000000.0;
+      }
+      if (imm) {
+        thr *= 0.5;
+        thr = py_min(py_max(thr, 0.0), 1.1);
+        rudder += DEG2RAD(-15.0);
+        rudder = py_min(py_max(rudder, -T->ap.max_rudder), T->ap.max_rudder);
+      }
+    }
+    ship_tick(T, rudder, thr);
+    out8[0] = T->m.north; out8[1] = T->m.east; out8[2] = T->log_ect;
+  }
+  /* obs_step :1025-1102 */
+  if (O->stop_flag) {
+    asset_store_last(O);
+    next_time(&O->m);
+    next_time(&O->m);
+    out8[3] = O->m.north; out8[4] = O->m.east; out8[5] = O->m.yaw; out8[6] = 0.0; out8[7] = O->log_ect;
+  } else {
+    double n = O->m.north, e = O->m.east, h = O->m.yaw, u = O->m.u;
+    double rudder = ap_rudder(&O->ap, n, e, h, 0.0);
+    double thr = speed_ctrl(O, O->desired_speed, u);
+    ship_tick(O, rudder, thr);
+    out8[3] = O->m.north; out8[4] = O->m.east; out8[5] = O->m.yaw; out8[6] = u; out8[7] = O->log_ect;
+  }
+  memcpy(env->lstates, out8, sizeof(env->lstates));
+  env->lstates_f32 = 0;
+  const o_map* mp = &env->map;
+  double tn = out8[0], te = out8[1], on = out8[3], oe = out8[4];
+  double cd = (tn - on) * (tn - on) + (te - oe) * (te - oe);
+  int c[10];
+  c[0] = is_reaches_endpoint(T->ap.nav.north[T->ap.nav.n - 1], T->ap.nav.east[T->ap.nav.n - 1], tn, te);
+  c[1] = is_pos_outside_horizon(mp, tn, te, T->m.l_ship);
+  c[2] = is_pos_inside_obstacles(mp, tn, te, T->m.l_ship);
+  c[3] = fabs(out8[2]) > 500; /* is_ship_navigation_failure, e_tol 500 for both ships */
+  c[4] = cd < 9000000.0;      /* is_collision_imminent */
+  c[5] = cd < 2500.0;         /* is_ship_collision */
+  c[6] = is_reaches_endpoint(O->ap.nav.north[O->ap.nav.n - 1], O->ap.nav.east[O->ap.nav.n - 1], on, oe);
+  c[7] = is_pos_outside_horizon(mp, on, oe, O->m.l_ship);
+  c[8] = is_pos_inside_obstacles(mp, on, oe, O->m.l_ship);
+  c[9] = fabs(out8[7]) > 500;
+  uint32_t bits = 0;
+  for (int i = 0; i < 10; ++i)
+    if (c[i]) bits |= 1u << i;
+  *status = bits;
+  if (c[7] && c[6]) O->stop_flag = 1; /* stop_int_obs = obs_is_outside and obs_is_reached */
+  env->ticks_total++;
+  return c[0] || c[1] || c[2] || c[3] || c[5] || c[8] || c[9];
 }
 
 /* ---------------- C1: MultiShipNonIWEnv (run_colav/env.py:37-677) ---------------- */

@@ -654,6 +654,75 @@ def gen_traj():
     np.savez_compressed(os.path.join(OUT, "rl_env_traj.npz"), **out)
 
 
+def gen_draw():
+    """f4: ShipDraw snapshots (env.py:573-579, ship_model.py:612-624) with ship_draw=True over
+    consecutive episodes of one env object (the drawing timer is env-level and survives reset,
+    the drawings do not), plus the per-ship stop tick so the frozen-state case is visible."""
+    from run.env_setup import prepare_multiship_rl_env
+    tabs = action_tables()
+    out = {}
+    for collav, tab_ids in (("none", (1, 3, 0)), ("sbmpc", (2, 4))):
+        args = rl_args(collav)
+        args.ship_draw = True
+        env, _ = prepare_multiship_rl_env(args)
+        for k, ti in enumerate(tab_ids):
+            p = f"{collav}_ep{k}"
+            env.reset()
+            acts = []
+            for a_norm in tabs[ti]:
+                a = scaled_action(a_norm)
+                acts.append(a[0])
+                _, _, d, _ = env.step(a.copy())
+                if d:
+                    break
+            out[p + "_a"] = np.array(acts, np.float32)
+            out[p + "_timer"] = np.float64(env.time_since_last_ship_drawing)
+            for name, ship in (("test", env.test), ("obs", env.obs)):
+                dr = ship.ship_model.ship_drawings
+                out[p + f"_{name}_draw"] = np.array([np.stack([x, y]) for x, y in zip(dr[0], dr[1])],
+                                                    np.float64).reshape(-1, 2, 6)
+                out[p + f"_{name}_rows"] = np.int64(len(ship.ship_model.simulation_results["time [s]"]))
+            print("draw", p, "snapshots", out[p + "_test_draw"].shape[0], out[p + "_obs_draw"].shape[0],
+                  "rows", out[p + "_test_rows"], "timer", out[p + "_timer"])
+    np.savez_compressed(os.path.join(OUT, "rl_env_draw.npz"), **out)
+
+
+def gen_legacy(max_ticks=3000):
+    """f4: the legacy per-tick MultiShipEnv (env.py:783-1181) on the scenario of record: per tick the
+    next_states list, the 10 get_termination_status flags and done, for two consecutive episodes of one
+    env object (self.states and the SBMPC memory survive reset), plus the ShipDraw snapshots."""
+    from run.env_setup import prepare_multiship_rl_env
+    from rl_env.ship_in_transit.env import MultiShipEnv
+    out = {}
+    for collav in ("none", "simple", "sbmpc"):
+        args = rl_args(collav)
+        rl_env, assets = prepare_multiship_rl_env(args)
+        env = MultiShipEnv(assets=assets, map=rl_env.map, ship_draw=True, collav=collav,
+                           time_since_last_ship_drawing=30, args=args)
+        for ep in range(2):
+            p = f"{collav}_ep{ep}"
+            env.reset()
+            states, conds, dones = [], [], []
+            for _ in range(max_ticks):
+                ns, done, cond = env.step()
+                states.append(ns)
+                conds.append([bool(c) for c in cond])
+                dones.append(bool(done))
+                if done:
+                    break
+            out[p + "_states"] = np.array(states, np.float64)
+            out[p + "_cond"] = np.array(conds, np.int8)
+            out[p + "_done"] = np.array(dones, np.int8)
+            out[p + "_obs_stop"] = np.int8(env.obs.stop_flag)
+            for name, ship in (("test", env.test), ("obs", env.obs)):
+                dr = ship.ship_model.ship_drawings
+                out[p + f"_{name}_draw"] = np.array([np.stack([x, y]) for x, y in zip(dr[0], dr[1])],
+                                                    np.float64).reshape(-1, 2, 6)
+            print("legacy", p, "ticks", len(dones), "done", dones[-1], "cond", np.nonzero(conds[-1])[0],
+                  "obs_stop", env.obs.stop_flag, "near", int(np.sum(out[p + "_cond"][:, 4])))
+    np.savez_compressed(os.path.join(OUT, "rl_env_legacy.npz"), **out)
+
+
 # ----------------------------------------------------------------------------------------------
 # F5 SBMPC known answers, F6 geometry / reward pure functions
 # ----------------------------------------------------------------------------------------------
@@ -819,3 +888,7 @@ if __name__ == "__main__":
         gen_modes()
     if "traj" in what:
         gen_traj()
+    if "draw" in what:
+        gen_draw()
+    if "legacy" in what:
+        gen_legacy()

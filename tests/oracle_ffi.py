@@ -39,6 +39,7 @@ def lib():
         L.oracle_env_step.argtypes = [P, C.c_float, C.c_int, fp, C.POINTER(C.c_double), C.POINTER(C.c_int),
                                       C.POINTER(C.c_uint32)]
         L.oracle_single_run.argtypes = [P, C.c_int]
+        L.oracle_legacy_step.argtypes = [P, dp, C.POINTER(C.c_uint32)]
         L.oracle_c1_run.argtypes = [P, C.c_int, up, ip]
         L.oracle_c2_run.argtypes = [cfgp, C.c_int, dp, C.c_int, C.c_void_p, dp, C.c_int]
         L.oracle_ast_rollouts.restype = C.c_longlong
@@ -110,6 +111,13 @@ class OracleEnv:
         ticks = lib().oracle_env_step(self.h, float(np.float32(a)), max_ticks, o, C.byref(r), C.byref(d),
                                       C.byref(b))
         return o, r.value, bool(d.value), int(b.value), ticks
+
+    def legacy_step(self):
+        """legacy MultiShipEnv.step(): (next_states (8,) float64, done, termination bits)."""
+        out = np.zeros(8)
+        b = C.c_uint32()
+        d = lib().oracle_legacy_step(self.h, out, C.byref(b))
+        return out, bool(d), int(b.value)
 
     def run_single(self, k):
         return lib().oracle_single_run(self.h, k)

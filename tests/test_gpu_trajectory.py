@@ -240,3 +240,26 @@ def test_trained_policy_replay_from_snapshot(torch_cuda, tmp_path):
     finally:
         ptu.set_gpu_mode(False)
         logger.set_snapshot_dir(None)
+
+
+@pytest.mark.parametrize("collav,n_eps", [("none", 3), ("sbmpc", 2)])
+def test_ship_drawings_match_reference(golden, torch_cuda, collav, n_eps):
+    """f4: MultiShipRLEnv(ship_draw=True, record_trajectory=True): test/obs ship_model.ship_drawings
+    and the env-level drawing timer over consecutive episodes of one env object."""
+    from ast_sac_amd.rl_env.ship_in_transit.env import MultiShipRLEnv, default_args
+    g = golden("rl_env_draw")
+    env = MultiShipRLEnv(default_args(collav_mode=collav, ship_draw=True), record_trajectory=True)
+    for ep in range(n_eps):
+        p = f"{collav}_ep{ep}"
+        env.reset()
+        for a in g[p + "_a"]:
+            if env.step(np.array([a], np.float32))[2]:
+                break
+        assert env.time_since_last_ship_drawing == g[p + "_timer"], p
+        for ship, name in ((env.test, "test"), (env.obs, "obs")):
+            dr = ship.ship_model.ship_drawings
+            got = np.array([np.stack([x, y]) for x, y in zip(dr[0], dr[1])]).reshape(-1, 2, 6)
+            ref = g[p + f"_{name}_draw"]
+            assert got.shape == ref.shape, (p, name, got.shape, ref.shape)
+            assert_close(got.reshape(len(got), -1), ref.reshape(len(ref), -1), what=f"{p} {name} ship_drawings")
+    env.close()
