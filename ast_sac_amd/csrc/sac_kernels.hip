@@ -4,17 +4,21 @@
 // update_target_networks :160-166) for TanhGaussianPolicy + twin ConcatMlp critics with two hidden
 // layers of width H and act_dim 1, in three kernels:
 //
-//   sac_rows_kernel  : R batch rows per block. Gathers the batch (or samples it from the replay ring
-//                      with Philox), runs actor(obs), actor(next_obs), Q1/Q2 on (obs, ã) and (obs, a),
-//                      target Q1/Q2 on (next_obs, ã'), the per-row losses, and the whole per-row
-//                      backward (critic input/activation grads, actor activation grads). Everything
-//                      in one SAC update is row-local except the batch means, whose 1/B factors are
-//                      constants, so no grid-wide step is needed until the weight gradients.
+//   sac_rows_g4_kernel: one batch row per block (default; sac_rows_kernel<RR, KS> is the general
+//                      shape). Gathers the batch (or samples it from the replay ring with Philox),
+//                      runs actor(obs), actor(next_obs), Q1/Q2 on (obs, ã) and (obs, a), target
+//                      Q1/Q2 on (next_obs, ã'), the per-row losses, and the whole per-row backward.
+//                      Everything in one SAC update is row-local except the batch means, whose 1/B
+//                      factors are constants, so no grid-wide step is needed until the weight
+//                      gradients. Bound: every block streams 8 H x H fp32 matrices (2 MB at H = 256)
+//                      from L2; scripts/mb_weight_read.hip measures that alone at ≈19 µs on MI355X.
 //   sac_wgrad_kernel : every weight/bias gradient = Σ_rows dY[r]ᵀ X[r] (64×64 tiles, 4×4 per thread,
-//                      LDS-staged row chunks) + the loss scalars and d(log α); writes one flat fp32
-//                      gradient in torch parameter order.
-//   sac_apply_kernel : torch.optim.Adam on every element (two lr groups), soft target update
-//                      θ' ← θ'(1−τ) + θτ, and the transposed H×H copies the rows kernel reads.
+//                      LDS-staged row chunks, rows split kParts ways into partial gradients) + the loss
+//                      scalars, d(log α) and this step's Adam bias corrections.
+//   sac_gsum_kernel  : (data parallel only) Σ of the partials into the flat gradient before the all-reduce.
+//   sac_apply_kernel : Σ partials (single process), torch.optim.Adam on every element (two lr groups),
+//                      soft target update θ' ← θ'(1−τ) + θτ, and the transposed H×H copies the rows
+//                      kernel reads (32×32 tiles through LDS).
 //
 // Only the four gradients the reference keeps are formed: the π-loss gradient w.r.t. the critics
 // (which sac.py:123-133 discards with qf*_optimizer.zero_grad()) is never computed; α is treated as a
@@ -36,6 +40,19 @@
 namespace {
 
 constexpr int kThreads = 256;
+
+#ifdef SACF_PHASE_TIMING
+// timing build only: shader-clock stamps of block 0 at the phase boundaries of sac_rows_g4_kernel
+__device__ unsigned long long g_sac_stamp[16];
+#define SAC_MARK(k)                                                              \
+  do {                                                                           \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_sac_stamp[k] = clock64();         \
+  } while (0)
+#else
+#define SAC_MARK(k) \
+  do {              \
+  } while (0)
+#endif
 constexpr int R = 4;           // batch granularity: B must be a multiple of R (rows-kernel tiles)
 constexpr int kXLd = 16;       // leading dim of the per-row input scratch (obs | act)
 constexpr float kLog2 = 0.69314718055994530942f;
@@ -539,6 +556,313 @@ __global__ __launch_bounds__(kCols* KS) void sac_rows_kernel(RowsArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// rows kernel, one batch row per block, four 256-thread groups working on independent matrices:
+// the six critic / target-critic rows of the forward pass are one phase (group g = Q1, Q2, T1, T2,
+// each over the full K), the twin-critic backward is one phase (two groups per critic, split-K 2).
+// Same math as sac_rows_kernel<1, 4>; 4 H x H matvec phases per block instead of 8.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kCols * 4) void sac_rows_g4_kernel(RowsArgs a) {
+  constexpr int NW = kCols * 4 / 64;
+  const Layout& L = a.L;
+  const int H = L.H, O = L.O, B = L.B;
+  const int tid = threadIdx.x;
+  const int j = tid % kCols, kg = tid / kCols;
+  const bool col = j < H;
+  const bool lead = kg == 0 && col;
+  const int r = blockIdx.x;
+  const float* P = a.params;
+  const float* TG = a.targets;
+  SAC_MARK(0);
+
+  __shared__ float s_x[2][kXLd];  // obs row | next_obs row
+  __shared__ float s_act, s_rew, s_term, s_eps[2];
+  __shared__ __attribute__((aligned(16))) float s_h1[2][SACF_MAX_HIDDEN];     // actor: obs | next_obs
+  __shared__ __attribute__((aligned(16))) float s_h2[2][SACF_MAX_HIDDEN];
+  __shared__ __attribute__((aligned(16))) float s_g1[4][2][SACF_MAX_HIDDEN];  // Q1, Q2: (obs, ã) | (obs, a); T1, T2: row 0
+  __shared__ __attribute__((aligned(16))) float s_g2[4][2][SACF_MAX_HIDDEN];
+  __shared__ float s_part[3 * 2 * kCols];
+  __shared__ float s_red[NW][32];
+  __shared__ float s_sum[32];
+  __shared__ float s_row[S_NSLOT][2];
+
+  // ---- batch row + reparameterisation noise ----
+  if (tid == 0) {
+    int64_t idx = r;
+    uint32_t c[4] = {(uint32_t)r, (uint32_t)*a.step, (uint32_t)((uint64_t)*a.step >> 32), 0x5AC0u};
+    if (a.sampled || !a.eps) philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+    if (a.sampled) {
+      const int64_t size = *a.size_dev > 0 ? *a.size_dev : 1;
+      const double u = ((double)c[0] + 0.5) * (1.0 / 4294967296.0);
+      idx = (int64_t)(u * (double)size);
+      if (idx >= a.capacity) idx = a.capacity - 1;
+    }
+    float e0, e1;
+    if (a.eps) {
+      e0 = a.eps[r];
+      e1 = a.eps[B + r];
+    } else {
+      const float u1 = ((float)c[1] + 1.0f) * 2.3283064365386963e-10f;
+      const float u2 = (float)c[2] * 2.3283064365386963e-10f;
+      const float rad = sqrtf(-2.0f * logf(u1));
+      e0 = rad * cosf(6.283185307179586f * u2);
+      e1 = rad * sinf(6.283185307179586f * u2);
+    }
+    for (int m = 0; m < O; ++m) {
+      s_x[0][m] = a.obs[idx * O + m];
+      s_x[1][m] = a.nobs[idx * O + m];
+    }
+    s_act = a.act[idx];
+    s_rew = a.rew[idx];
+    s_term = a.term[idx];
+    s_eps[0] = e0;
+    s_eps[1] = e1;
+  }
+  __syncthreads();
+  SAC_MARK(1);
+
+  // ---- actor forward on obs and next_obs ----
+  if (lead) {
+    float acc[2];
+    const float b = P[L.p_b1 + j];
+    acc[0] = b;
+    acc[1] = b;
+    for (int m = 0; m < O; ++m) {
+      const float w = P[L.p_w1 + (int64_t)j * O + m];
+      acc[0] = fmaf(w, s_x[0][m], acc[0]);
+      acc[1] = fmaf(w, s_x[1][m], acc[1]);
+    }
+    s_h1[0][j] = relu(acc[0]);
+    s_h1[1][j] = relu(acc[1]);
+  }
+  __syncthreads();
+  SAC_MARK(2);
+  {
+    float acc[2];
+    const float b = lead ? P[L.p_b2 + j] : 0.0f;
+    acc[0] = b;
+    acc[1] = b;
+    if (col) mv_part<2, 4>(a.T, H, &s_h1[0][0], SACF_MAX_HIDDEN, j, kg, acc);
+    kreduce<2, 4>(acc, s_part, j, kg);
+    if (lead) {
+      s_h2[0][j] = relu(acc[0]);
+      s_h2[1][j] = relu(acc[1]);
+    }
+  }
+  __syncthreads();
+  SAC_MARK(3);
+  {
+    float v[4];
+    const float wm = lead ? P[L.p_wm + j] : 0.0f, ws = lead ? P[L.p_ws + j] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float h = lead ? s_h2[i][j] : 0.0f;
+      v[i] = wm * h;
+      v[2 + i] = ws * h;
+    }
+    block_sum_w<4, NW>(v, s_red, s_sum);
+  }
+  if (tid < 2) {  // TanhNormal.rsample_and_logprob (distributions.py:346-392)
+    const int i = tid;
+    const float mean = s_sum[i] + P[L.p_bm];
+    const float ls_raw = s_sum[2 + i] + P[L.p_bs];
+    const float log_std = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
+    const float std = expf(log_std);
+    const float z = mean + std * s_eps[i];
+    const float act = tanhf(z);
+    const float var = std * std;
+    const float d = z - mean;
+    const float lp = -(d * d) / (2.0f * var) - logf(std) - kLogSqrt2Pi;
+    const float corr = -2.0f * (kLog2 - z - softplus(-2.0f * z));
+    s_row[S_MEAN][i] = mean;
+    s_row[S_LSRAW][i] = ls_raw;
+    s_row[S_STD][i] = std;
+    s_row[S_Z][i] = z;
+    s_row[S_A][i] = act;
+    s_row[S_LOGP][i] = lp + corr;
+  }
+  __syncthreads();
+  SAC_MARK(4);
+
+  // ---- first layers: group g = Q1, Q2 on (obs, ã) | (obs, a); T1, T2 on (next_obs, ã') ----
+  const bool is_t = kg >= 2;
+  const float* C = is_t ? TG + (int64_t)(kg - 2) * L.q_size : P + L.q_base[kg];
+  if (col) {
+    const float* xin = s_x[is_t ? 1 : 0];
+    float base = C[L.c_b1 + j];
+    for (int m = 0; m < O; ++m) base = fmaf(C[L.c_w1 + (int64_t)j * (O + 1) + m], xin[m], base);
+    const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
+    if (is_t) {
+      s_g1[kg][0][j] = relu(fmaf(wa, s_row[S_A][1], base));
+    } else {
+      s_g1[kg][0][j] = relu(fmaf(wa, s_row[S_A][0], base));
+      s_g1[kg][1][j] = relu(fmaf(wa, s_act, base));
+    }
+  }
+  __syncthreads();
+  SAC_MARK(5);
+  // ---- second layers, all four at once (full K per group) ----
+  if (col) {
+    const float b = C[L.c_b2 + j];
+    float acc[2] = {b, b};
+    const float* WT = a.T + (size_t)(1 + kg) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
+    if (is_t) {
+      float a1[1] = {b};
+      mv_part<1, 1>(WT, H, &s_g1[kg][0][0], SACF_MAX_HIDDEN, j, 0, a1);
+      acc[0] = a1[0];
+    } else {
+      mv_part<2, 1>(WT, H, &s_g1[kg][0][0], SACF_MAX_HIDDEN, j, 0, acc);
+    }
+    s_g2[kg][0][j] = relu(acc[0]);
+    if (!is_t) s_g2[kg][1][j] = relu(acc[1]);
+  }
+  __syncthreads();
+  SAC_MARK(6);
+  {
+    // heads: Q1 (2 rows), Q2 (2 rows), T1, T2 -> v[0..5]
+    float v[6] = {0, 0, 0, 0, 0, 0};
+    if (col) {
+      const float w3 = C[L.c_w3 + j];
+      if (is_t) {
+        v[4 + (kg - 2)] = w3 * s_g2[kg][0][j];
+      } else {
+        v[2 * kg] = w3 * s_g2[kg][0][j];
+        v[2 * kg + 1] = w3 * s_g2[kg][1][j];
+      }
+    }
+    block_sum_w<6, NW>(v, s_red, s_sum);
+  }
+  const float log_alpha = P[0];
+  const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
+  const float invB = 1.0f / (float)B;
+  if (tid == 0) {  // losses and output gradients (sac.py:170-247)
+    const float q1a = s_sum[0] + P[L.q_base[0] + L.c_b3], q1b = s_sum[1] + P[L.q_base[0] + L.c_b3];
+    const float q2a = s_sum[2] + P[L.q_base[1] + L.c_b3], q2b = s_sum[3] + P[L.q_base[1] + L.c_b3];
+    const float t1 = s_sum[4] + TG[L.c_b3], t2 = s_sum[5] + TG[L.q_size + L.c_b3];
+    const float tq = fminf(t1, t2) - alpha * s_row[S_LOGP][1];
+    float qt = a.hp.rscale * s_rew + ((1.0f - s_term) * a.hp.gamma) * tq;
+    qt = fminf(fmaxf(qt, -a.hp.clip), a.hp.clip);
+    const float qmin = fminf(q1a, q2a);
+    const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
+    const float w2 = 1.0f - w1;
+    s_row[S_DQ1][0] = -w1 * invB;
+    s_row[S_DQ2][0] = -w2 * invB;
+    const float dq1b = (2.0f * invB) * (q1b - qt), dq2b = (2.0f * invB) * (q2b - qt);
+    s_row[S_DQ1][1] = dq1b;
+    s_row[S_DQ2][1] = dq2b;
+    a.sc.q_dq[0][r] = dq1b;
+    a.sc.q_dq[1][r] = dq2b;
+    const float logp = s_row[S_LOGP][0], act = s_row[S_A][0];
+    a.sc.p_pl[r] = alpha * logp - qmin + (a.hp.areg != 0.0f ? a.hp.areg * (act * act) : 0.0f);
+    a.sc.p_q1l[r] = (q1b - qt) * (q1b - qt);
+    a.sc.p_q2l[r] = (q2b - qt) * (q2b - qt);
+    a.sc.p_la[r] = -(log_alpha * (logp + a.hp.tent));
+    a.sc.p_ga[r] = -(logp + a.hp.tent);
+    float* st = a.stats + 8;
+    st[r] = q1b;
+    st[B + r] = q2b;
+    st[2 * B + r] = qt;
+    st[3 * B + r] = logp;
+    st[4 * B + r] = tanhf(s_row[S_MEAN][0]);
+    st[5 * B + r] = s_row[S_STD][0];
+  } else if (tid >= 64 && tid < 64 + kXLd) {
+    const int m = tid - 64;
+    const float x = m < O ? s_x[0][m] : (m == O ? s_act : 0.0f);
+    a.sc.q_x[0][(int64_t)r * kXLd + m] = x;
+    a.sc.q_x[1][(int64_t)r * kXLd + m] = x;
+    a.sc.a_x[(int64_t)r * kXLd + m] = m < O ? s_x[0][m] : 0.0f;
+  }
+  __syncthreads();
+  SAC_MARK(7);
+
+  // ---- critic backward: dg2 = dq·w3 ⊙ [g2 > 0] (groups 0, 1), then dg1 = (W2ᵀ dg2) ⊙ [g1 > 0] ----
+  if (col && kg < 2) {
+    const float* dq = s_row[kg == 0 ? S_DQ1 : S_DQ2];
+    const float w3 = C[L.c_w3 + j];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float g2 = s_g2[kg][i][j];
+      const float dg2 = g2 > 0.0f ? dq[i] * w3 : 0.0f;
+      if (i == 1) {
+        const int64_t o = (int64_t)r * H + j;
+        a.sc.q_g2[kg][o] = g2;
+        a.sc.q_dg2[kg][o] = dg2;
+      }
+      s_g2[kg][i][j] = dg2;
+    }
+  }
+  __syncthreads();
+  SAC_MARK(8);
+  {
+    // groups 0, 1 -> critic 0 (k halves), groups 2, 3 -> critic 1
+    const int k = kg >> 1, half = kg & 1;
+    const float* Ck = P + L.q_base[k];
+    float acc[2] = {0.0f, 0.0f};
+    if (col) mv_part<2, 2>(Ck + L.c_w2, H, &s_g2[k][0][0], SACF_MAX_HIDDEN, j, half, acc);
+    if (half) {
+      s_part[(k * 2 + 0) * kCols + j] = acc[0];
+      s_part[(k * 2 + 1) * kCols + j] = acc[1];
+    }
+    __syncthreads();
+    float v[2] = {0.0f, 0.0f};
+    if (!half && col) {
+      acc[0] += s_part[(k * 2 + 0) * kCols + j];
+      acc[1] += s_part[(k * 2 + 1) * kCols + j];
+      const float wa = Ck[L.c_w1 + (int64_t)j * (O + 1) + O];
+      const float g1a = s_g1[k][0][j], g1b = s_g1[k][1][j];
+      v[k] = wa * (g1a > 0.0f ? acc[0] : 0.0f);
+      const int64_t o = (int64_t)r * H + j;
+      a.sc.q_g1[k][o] = g1b;
+      a.sc.q_dg1[k][o] = g1b > 0.0f ? acc[1] : 0.0f;
+    }
+    block_sum_w<2, NW>(v, s_red, s_sum);
+  }
+
+  // ---- actor backward on the obs row ----
+  if (tid == 0) {
+    const float act = s_row[S_A][0], z = s_row[S_Z][0], mean = s_row[S_MEAN][0], std = s_row[S_STD][0];
+    const float ls_raw = s_row[S_LSRAW][0];
+    float dA = s_sum[0] + s_sum[1];
+    if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
+    const float ainv = alpha * invB;
+    const float d = z - mean, var = std * std;
+    const float sig = 1.0f / (1.0f + expf(2.0f * z));  // sigmoid(-2z)
+    const float gz = dA * (1.0f - act * act) + ainv * (-(d / var) + (2.0f - 4.0f * sig));
+    const float dmean = gz + ainv * (d / var);
+    const float dstd = gz * s_eps[0] + ainv * ((d * d) / (var * std) - 1.0f / std);
+    const float dls = (ls_raw >= -20.0f && ls_raw <= 2.0f) ? dstd * std : 0.0f;
+    s_row[S_DMEAN][0] = dmean;
+    s_row[S_DLS][0] = dls;
+    a.sc.a_dhead[(int64_t)r * 2] = dmean;
+    a.sc.a_dhead[(int64_t)r * 2 + 1] = dls;
+  }
+  __syncthreads();
+  SAC_MARK(9);
+  if (lead) {
+    const float wm = P[L.p_wm + j], ws = P[L.p_ws + j];
+    const float h2 = s_h2[0][j];
+    const float dh2 = h2 > 0.0f ? (wm * s_row[S_DMEAN][0] + ws * s_row[S_DLS][0]) : 0.0f;
+    const int64_t o = (int64_t)r * H + j;
+    a.sc.a_h2[o] = h2;
+    a.sc.a_dh2[o] = dh2;
+    s_h2[0][j] = dh2;
+  }
+  __syncthreads();
+  SAC_MARK(10);
+  {
+    float acc[1] = {0.0f};
+    if (col) mv_part<1, 4>(P + L.p_w2, H, &s_h2[0][0], SACF_MAX_HIDDEN, j, kg, acc);
+    kreduce<1, 4>(acc, s_part, j, kg);
+    if (lead) {
+      const float h1 = s_h1[0][j];
+      const int64_t o = (int64_t)r * H + j;
+      a.sc.a_h1[o] = h1;
+      a.sc.a_dh1[o] = h1 > 0.0f ? acc[0] : 0.0f;
+    }
+  }
+  SAC_MARK(11);
+}
+
+// ---------------------------------------------------------------------------------------------
 // weight gradients: out[j][k] = Σ_r dY[r·ldY + j] · X[r·ldX + k]  (X == nullptr: ones -> bias)
 // ---------------------------------------------------------------------------------------------
 struct GMat {
@@ -593,7 +917,15 @@ __global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
       a.stats[3] = a.hp.auto_ent ? sum[3] * invB : 0.0f;
       a.stats[4] = a.hp.auto_ent ? expf(a.params[0]) : 1.0f;
       a.grads[0] = a.hp.auto_ent ? sum[4] * invB : 0.0f;
-      *a.step += 1;
+      const int64_t step = *a.step + 1;
+      *a.step = step;
+      // Adam bias corrections of this step for sac_apply_kernel (stats[5..7])
+      const double t = (double)step;
+      const double bc1 = 1.0 - pow((double)a.hp.beta1, t);
+      const double bc2 = 1.0 - pow((double)a.hp.beta2, t);
+      a.stats[5] = (float)(a.hp.lr_pi / bc1);
+      a.stats[6] = (float)(a.hp.lr_q / bc1);
+      a.stats[7] = (float)sqrt(bc2);
     }
     return;
   }
@@ -662,52 +994,98 @@ __global__ __launch_bounds__(kThreads) void sac_gsum_kernel(const float* __restr
 struct ApplyArgs {
   float* params;
   float* targets;
-  const float* grads;
+  float* grads;
+  const float* partials;  // non-null: the gradient is Σ of the kParts partials (single process, no all-reduce)
   float* m;
   float* v;
   const int64_t* step;
   float* T;
+  const float* stats;
   Layout L;
   Hyper hp;
+  int n_tile_blocks;      // blocks [0, n_tile_blocks) take 32x32 tiles of the three H x H W2 matrices
 };
 
-__global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
-  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+constexpr int kTile = 32;
+
+// Adam bias corrections of this step, computed once by the weight-gradient kernel (stats[5..7])
+struct AdamStep {
+  float step_pi, step_q, bc2_sqrt;
+};
+
+// one element: gradient (Σ partials or the all-reduced flat gradient), torch.optim.Adam, soft update
+__device__ __forceinline__ float adam_elem(const ApplyArgs& a, const AdamStep& st, int64_t e, float* tp_out) {
   const Layout& L = a.L;
-  if (e >= L.n_params) return;
-  if (e == 0 && !a.hp.auto_ent) return;
-  const float g = a.grads[e] * a.hp.inv_world;
+  float g;
+  if (a.partials && e != 0) {
+    g = a.partials[e];
+#pragma unroll
+    for (int p = 1; p < kParts; ++p) g += a.partials[(size_t)p * L.n_params + e];
+    a.grads[e] = g;
+  } else {
+    g = a.grads[e];
+  }
+  g *= a.hp.inv_world;
   const bool is_q = e >= L.q_base[0];
-  const double lr = is_q ? a.hp.lr_q : a.hp.lr_pi;
-  const double t = (double)*a.step;
-  const double bc1 = 1.0 - pow((double)a.hp.beta1, t);
-  const double bc2 = 1.0 - pow((double)a.hp.beta2, t);
-  const float step_size = (float)(lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
   float m = a.m[e], v = a.v[e];
   m = m + (1.0f - a.hp.beta1) * (g - m);             // exp_avg.lerp_(grad, 1 - beta1)
   v = v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
-  const float denom = sqrtf(v) / bc2_sqrt + a.hp.eps;
-  const float p = a.params[e] + (-step_size) * (m / denom);
+  const float denom = sqrtf(v) / st.bc2_sqrt + a.hp.eps;
+  const float p = a.params[e] + (-(is_q ? st.step_q : st.step_pi)) * (m / denom);
   a.m[e] = m;
   a.v[e] = v;
   a.params[e] = p;
-  const int H = L.H;
-  if (e >= L.p_w2 && e < L.p_w2 + (int64_t)H * H) {
-    const int64_t l = e - L.p_w2;
-    a.T[(l % H) * H + l / H] = p;
-  }
   if (is_q) {
-    const int k = e >= L.q_base[1] ? 1 : 0;
     const int64_t qe = e - L.q_base[0];
     const float tp = a.targets[qe] * (1.0f - a.hp.tau) + p * a.hp.tau;
     a.targets[qe] = tp;
-    const int64_t l = e - L.q_base[k] - L.c_w2;
-    if (l >= 0 && l < (int64_t)H * H) {
-      a.T[(size_t)(1 + k) * H * H + (l % H) * H + l / H] = p;
-      a.T[(size_t)(3 + k) * H * H + (l % H) * H + l / H] = tp;
-    }
+    *tp_out = tp;
   }
+  return p;
+}
+
+__global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
+  __shared__ float tile[2][kTile][kTile + 1];
+  const AdamStep st{a.stats[5], a.stats[6], a.stats[7]};
+  const Layout& L = a.L;
+  const int H = L.H;
+  const int64_t HH = (int64_t)H * H;
+  const int64_t w2[3] = {L.p_w2, L.q_base[0] + L.c_w2, L.q_base[1] + L.c_w2};
+  if ((int)blockIdx.x < a.n_tile_blocks) {
+    // 32 x 32 tile of one W2: Adam on row-major elements, transposed copies written through LDS
+    const int tpm = (H / kTile) * (H / kTile);
+    const int mat = blockIdx.x / tpm, t = blockIdx.x % tpm;
+    const int r0 = (t / (H / kTile)) * kTile, c0 = (t % (H / kTile)) * kTile;
+    const int tc = threadIdx.x % kTile, tr = threadIdx.x / kTile;  // 8 rows per pass
+    for (int rr = tr; rr < kTile; rr += kThreads / kTile) {
+      float tp = 0.0f;
+      const int64_t l = (int64_t)(r0 + rr) * H + c0 + tc;
+      const float p = adam_elem(a, st, w2[mat] + l, &tp);
+      tile[0][tc][rr] = p;
+      tile[1][tc][rr] = tp;
+    }
+    __syncthreads();
+    for (int cc = tr; cc < kTile; cc += kThreads / kTile) {
+      const int64_t o = (int64_t)(c0 + cc) * H + r0 + tc;  // T[col][row]
+      if (mat == 0) {
+        a.T[o] = tile[0][cc][tc];
+      } else {
+        a.T[(size_t)mat * HH + o] = tile[0][cc][tc];
+        a.T[(size_t)(2 + mat) * HH + o] = tile[1][cc][tc];
+      }
+    }
+    return;
+  }
+  // every other element: flat index over the parameters outside the three W2 blocks
+  int64_t f = (int64_t)(blockIdx.x - a.n_tile_blocks) * kThreads + threadIdx.x;
+  int64_t e = f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (e >= w2[k]) e += HH;
+  if (e >= L.n_params) return;
+  if (e == 0 && !a.hp.auto_ent) return;
+  float tp;
+  adam_elem(a, st, e, &tp);
 }
 
 __global__ void sac_transpose_kernel(const float* params, const float* targets, float* T, Layout L) {
@@ -920,6 +1298,12 @@ int sacf_destroy(sacf_handle* h) {
   return SACF_OK;
 }
 
+#ifdef SACF_PHASE_TIMING
+int sacf_debug_stamps(unsigned long long* out16) {
+  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_sac_stamp), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -1;
+}
+#endif
+
 const char* sacf_last_error(const sacf_handle* h) { return h ? h->err : "null handle"; }
 int64_t sacf_param_count(const sacf_handle* h) { return h ? h->L.n_params : -1; }
 int64_t sacf_target_count(const sacf_handle* h) { return h ? h->L.n_targets : -1; }
@@ -1006,7 +1390,9 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   if (h->L.H / ks < 8 || (h->L.H / ks) % 8) ks = 1;
 #define ROWS(RR_, KS_) \
   hipLaunchKernelGGL((sac_rows_kernel<RR_, KS_>), dim3(h->L.B / RR_), dim3(kCols * KS_), 0, h->stream, a)
-  if (rr == 4 && ks == 1) ROWS(4, 1);
+  if (!getenv("SACF_ROWS") && h->L.H <= kCols) {  // default: the four-group one-row kernel
+    hipLaunchKernelGGL(sac_rows_g4_kernel, dim3(h->L.B), dim3(kCols * 4), 0, h->stream, a);
+  } else if (rr == 4 && ks == 1) ROWS(4, 1);
   else if (rr == 4 && ks == 2) ROWS(4, 2);
   else if (rr == 2 && ks == 2) ROWS(2, 2);
   else if (rr == 1 && ks == 4) ROWS(1, 4);
@@ -1029,8 +1415,9 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   w.stats = h->stats;
   w.hp = h->hp;
   hipLaunchKernelGGL(sac_wgrad_kernel, dim3(h->n_tasks + 1, kParts), dim3(kThreads), 0, h->stream, w);
-  hipLaunchKernelGGL(sac_gsum_kernel, dim3((unsigned)((h->L.n_params - 1 + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                     h->stream, h->partials, h->grads, h->L.n_params);
+  if (h->cfg.world_size > 1)  // the flat gradient is all-reduced before sacf_apply; single process: summed there
+    hipLaunchKernelGGL(sac_gsum_kernel, dim3((unsigned)((h->L.n_params - 1 + kThreads - 1) / kThreads)), dim3(kThreads),
+                       0, h->stream, h->partials, h->grads, h->L.n_params);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
 }
@@ -1047,9 +1434,14 @@ int sacf_apply(sacf_handle* h) {
   a.T = h->T;
   a.L = h->L;
   a.hp = h->hp;
+  a.partials = h->cfg.world_size > 1 ? nullptr : h->partials;
+  a.stats = h->stats;
+  const int64_t HH = (int64_t)h->L.H * h->L.H;
+  a.n_tile_blocks = 3 * (h->L.H / kTile) * (h->L.H / kTile);
+  const int64_t rest = h->L.n_params - 3 * HH;
   SDev g(h->device);
-  hipLaunchKernelGGL(sac_apply_kernel, dim3((unsigned)((h->L.n_params + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                     h->stream, a);
+  hipLaunchKernelGGL(sac_apply_kernel, dim3((unsigned)(a.n_tile_blocks + (rest + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, h->stream, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_apply: %s", hipGetErrorString(e));
 }
