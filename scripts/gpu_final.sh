@@ -20,5 +20,8 @@ timeout -k 10 200 python bench.py --collav none --no-cpu-baseline --sac-steps 0 
 tail -1 $O/bench_${TAG}_none.log
 cd /tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python3 $R/bench.py > $O/prof_$TAG.log 2>&1; hard $? rocprof_stats
-tail -1 $O/prof_$TAG.log
+cd $R
+python scripts/trace_summary.py $O/prof_$TAG $O/prof_$TAG.log $O/trace_vs_bench_$TAG.json; hard $? trace_summary
+find $O -name "*kernel_trace.csv" -delete
+du -sh $O
 echo DONE
