@@ -689,18 +689,34 @@ __device__ __forceinline__ double xor_shfl_d(double x, int mask) {
 }
 
 
+// Open-loop decision stream (shipsim_run_table, the C3 workload of SURVEY.md §8(d)): actions come
+// from a device table, a completed decision is followed at once by the next one and an ended
+// episode is reset in place, so an env never idles inside a launch while it has ticks left.
+struct ChainArgs {
+  const float* table;  // [n_eps][n_dec][n_envs] scoping angles
+  int32_t n_eps, n_dec;
+  int32_t* ep_idx;     // [env] episode counter (table row = ep % n_eps)
+  int32_t* dec_idx;    // [env] decision index within the episode
+  int32_t* decisions;  // [env] decisions completed in this call (may be null)
+  double* log;         // [env][log_cap][SHIPSIM_DECLOG_COLS] per-decision record (may be null)
+  int32_t* log_len;    // [env] records written (counts on past log_cap)
+  int32_t log_cap;
+};
+
 // MultiShipRLEnv.step (env.py:624-773), sliced: every env of the launch ticks (_step :563-622)
 // until its decision point (RoA + one tick, or done) or until `max_ticks` ticks have run in this
 // call; an env that paused resumes in the next call without consuming an action. Envs waiting
 // for a decision consume action[env] first (IW sampling). LPE lanes per env: lane & 1 selects the
 // ship, the LPE/2 sub-lanes of a ship hold identical state, run the control chain redundantly and
 // split the map queries (edges for the coastline distance, hull corners for grounding).
-template <bool DETAILED, int COLLAV, int LPE, bool REC>
+template <bool DETAILED, int COLLAV, int LPE, bool REC, bool CHAIN = false>
 __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K, Traj T,
                                                       const float* __restrict__ action,
                                                       const uint8_t* __restrict__ active_mask, int max_ticks,
                                                       float* obs_out, double* reward_out, uint8_t* done_out,
-                                                      uint32_t* events_out, int32_t* ticks_out, uint8_t* ready_out) {
+                                                      uint32_t* events_out, int32_t* ticks_out, uint8_t* ready_out,
+                                                      const ChainArgs CH) {
+  static_assert(!(REC && CHAIN), "trajectory recording runs the per-decision step only");
   constexpr int NSUB = LPE / 2;
   static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 64, "LPE must be a power of two in [2, 64]");
   __shared__ ShipConst lds_sc[2];
@@ -745,7 +761,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   double travel_dist = S.travel_dist()[envc], travel_time = S.travel_time()[envc], acc = S.acc()[envc];
   double n_base = S.n_base()[envc], e_base = S.e_base()[envc];
   double p_last = S.p_last()[envc], chi_last = S.chi_last()[envc];
-  const double mach_dt = S.mach_dt()[envc];
+  double mach_dt = S.mach_dt()[envc];
   float st4[4];
   for (int i = 0; i < 4; ++i) st4[i] = S.states4()[envc * 4 + i];
   uint32_t snap_bits = S.snap_bits()[envc];
@@ -771,9 +787,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     printf("[dbg] env %d lie %d start: running %d dflags %d sc %d n_base %f phase %d\n", env, lie, (int)running, dflags,
            sampling_count, n_base, phase);
 #endif
-  if (running && (dflags & DF_AWAITING)) {
-    // ---- intermediate waypoint sampling (env.py:659-696) ----
-    float sa = action[envc];
+  // ---- intermediate waypoint sampling (env.py:659-696) for an env that waits for a decision ----
+  auto decision_prologue = [&](float sa) __attribute__((always_inline)) {
     if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
     phase = 0;
     have_iw = false;
@@ -815,7 +830,70 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         acc = 0;
       }
     }
+  };
+
+  // ---- CHAIN: in-place reset (env.py:238-342, as reset_kernel) and the next decision ----
+  int ep_i = 0, dec_i = 0, n_decided = 0, log_n = 0;
+  if (CHAIN) {
+    ep_i = CH.ep_idx[envc];
+    dec_i = CH.dec_idx[envc];
+    log_n = CH.log_len ? CH.log_len[envc] : 0;
   }
+  auto table_action = [&]() __attribute__((always_inline)) -> float {
+    return CH.table[((size_t)(ep_i % CH.n_eps) * CH.n_dec + dec_i) * P.n_envs + envc];
+  };
+  auto reset_env = [&]() __attribute__((always_inline)) {
+    s.n = c.init_n; s.e = c.init_e; s.yaw = c.init_yaw; s.u = c.init_u; s.v = c.init_v; s.r = c.init_r;
+    s.omega = c.init_omega; s.time = 0.0;
+    s.e_ct = 0; s.e_ct_int = 0; s.hdg_ei = 0; s.hdg_prev = 0;
+    s.spd_a = 0; s.spd_b = DETAILED ? c.init_shaft_ei : 0.0;
+    s.next_wpt = 1; s.stop = 0; s.n_route = c.n_route;
+    for (int i = 0; i < c.n_route; ++i) {
+      rn[i] = K.cfg_route_n()[ship * kMaxRoute + i];
+      re[i] = K.cfg_route_e()[ship * kMaxRoute + i];
+    }
+    load_segment(s, rn, re);
+    mach_dt = P.mach_dt_reset;
+    control_and_integrate<DETAILED, false, (NSUB >= 2)>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false, nullptr,
+                                                         nullptr, (sub & 1) != 0);  // init_step
+    sampling_count = 0;
+    travel_dist = 0; travel_time = 0; acc = 0;
+    n_base = P.n_base0; e_base = P.e_base0;
+    for (int i = 0; i < 8; ++i) ns[i] = P.initial_states[i];
+    snap_bits = 0;
+    phase = 0;
+    have_iw = false;
+  };
+  // a decision just completed (ready): record it, reset if the episode ended (done, or n_dec decisions
+  // = the rollout's max_path_length), consume the next table action. A sampling failure completes the
+  // new decision at once, hence the (bounded) loop.
+  auto chain_next = [&]() __attribute__((always_inline)) {
+    for (int guard = 0; guard < 8 && ready; ++guard) {
+      if (CH.log && lie == 0 && log_n < CH.log_cap) {
+        double* rec = CH.log + ((size_t)env * CH.log_cap + log_n) * SHIPSIM_DECLOG_COLS;
+        rec[SHIPSIM_DL_REWARD] = out_r; rec[SHIPSIM_DL_EVENTS] = (double)out_bits;
+        rec[SHIPSIM_DL_DONE] = out_done ? 1.0 : 0.0; rec[SHIPSIM_DL_EPISODE] = (double)ep_i;
+        rec[SHIPSIM_DL_DECISION] = (double)dec_i; rec[SHIPSIM_DL_TICKS] = (double)ticks;
+        for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS + i] = (double)ns[i];
+      }
+      log_n += 1;
+      n_decided += 1;
+      if (out_done || dec_i + 1 >= CH.n_dec) {
+        reset_env();
+        ep_i += 1;
+        dec_i = 0;
+      } else {
+        dec_i += 1;
+      }
+      if (lie == 0)
+        for (int i = 0; i < 8; ++i) S.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
+      ready = false;
+      out_done = false;
+      decision_prologue(table_action());
+    }
+  };
+
+  if (running && (dflags & DF_AWAITING)) decision_prologue(CHAIN ? table_action() : action[envc]);
 
   const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
   bool going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
@@ -823,7 +901,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   unsigned long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long pt_last = wall_clock64();
 #endif
-  while (__any(going)) {
+  // CHAIN: the tick loop hands over to the (rare) chaining code below whenever a decision of the
+  // wave completes, so the loop body itself is the per-decision kernel's.
+  for (;;) {
+  while (__any(going) && !(CHAIN && __any(ready && running))) {
     // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
@@ -1049,6 +1130,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     }
     PT_MARK(3);
   }
+  if (!CHAIN) break;
+  if (ready && running) chain_next();
+  going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
+  if (!__any(going)) break;
+  }
 #ifdef SHIPSIM_PHASE_TIMING
   if ((threadIdx.x & 63) == 0)
     for (int k = 0; k < 4; ++k) atomicAdd(&g_phase_cycles[k], pt_acc[k]);
@@ -1065,6 +1151,13 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     if (sub == 0)
       for (int k = 0; k < 3; ++k) T.fuel[(size_t)qc * 3 + k] = fuel[k];
     if (lie == 0) T.len[env] = rec_t;
+  }
+  if (CHAIN && lie == 0) {
+    CH.ep_idx[env] = ep_i;
+    CH.dec_idx[env] = dec_i;
+    if (CH.decisions) CH.decisions[env] = n_decided;
+    if (CH.log_len) CH.log_len[env] = log_n;
+    S.mach_dt()[env] = mach_dt;
   }
   if (lie == 0) {
     S.sampling_count()[env] = sampling_count;
@@ -1404,7 +1497,7 @@ static void launch_step(shipsim_handle* h, int lpe, const float* action, const u
 #define L(LPE, REC)                                                                                              \
   hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, REC>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S,  \
                      h->K, h->T, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, \
-                     ready_out)
+                     ready_out, ChainArgs{})
   if (h->T.ship) {
     L(16, true);
     return;
@@ -1928,6 +2021,33 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
     hipLaunchKernelGGL(single_tick_kernel<true>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
   else
     hipLaunchKernelGGL(single_tick_kernel<false>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
+  HIPCHK(h, hipGetLastError());
+  return SHIPSIM_OK;
+}
+
+int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
+                      int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
+                      int32_t log_cap, int32_t* log_len) {
+  if (!h || !h->dev_block || !table || !ep_idx || !dec_idx || n_eps < 1 || n_dec < 1 || max_ticks < 1 ||
+      (log && (!log_len || log_cap < 1)))
+    return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "run_table: AST kind only");
+  if (h->T.ship) return fail(h, SHIPSIM_EINVAL, "run_table: trajectory recording is on (use shipsim_step)");
+  DeviceGuard g(h->device);
+  ChainArgs ch;
+  ch.table = table; ch.n_eps = n_eps; ch.n_dec = n_dec; ch.ep_idx = ep_idx; ch.dec_idx = dec_idx;
+  ch.decisions = decisions_out; ch.log = log; ch.log_len = log_len; ch.log_cap = log_cap;
+  const int threads = 64, blocks = (h->P.n_envs * 16 + threads - 1) / threads;
+#define CHAINED(D, CA)                                                                                                 \
+  hipLaunchKernelGGL((ast_step_kernel<D, CA, 16, false, true>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, \
+                     h->K, h->T, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out, nullptr, ch)
+  const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
+  switch (h->P.collav) {
+    case SHIPSIM_COLLAV_SBMPC: if (det) CHAINED(true, SHIPSIM_COLLAV_SBMPC); else CHAINED(false, SHIPSIM_COLLAV_SBMPC); break;
+    case SHIPSIM_COLLAV_SIMPLE: if (det) CHAINED(true, SHIPSIM_COLLAV_SIMPLE); else CHAINED(false, SHIPSIM_COLLAV_SIMPLE); break;
+    default: if (det) CHAINED(true, SHIPSIM_COLLAV_NONE); else CHAINED(false, SHIPSIM_COLLAV_NONE); break;
+  }
+#undef CHAINED
   HIPCHK(h, hipGetLastError());
   return SHIPSIM_OK;
 }

@@ -48,6 +48,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_set_trajectory.argtypes = [P, P, P, C.c_int32, P]
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
+    L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
     if L.shipsim_abi_version() != abi.ABI_VERSION:
         raise ShipSimError(f"ABI mismatch: library {L.shipsim_abi_version()} vs binding {abi.ABI_VERSION}")
     _lib = L
@@ -57,7 +58,7 @@ def load_library(path=LIB_PATH):
 EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_default_config", "shipsim_create",
                     "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
-                    "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step")
+                    "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table")
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
@@ -145,6 +146,27 @@ class ShipSim:
 
     def tick(self, k=1):
         self._check(self.L.shipsim_tick(self.h, int(k), None), "shipsim_tick")
+
+    def run_table(self, table, max_ticks, ep_idx, dec_idx, out=None, log=None, log_len=None):
+        """Open-loop decision stream (shipsim_run_table): table (n_eps, n_dec, N) float32 scoping angles
+        on the device; ep_idx / dec_idx (N,) int32 device counters, updated in place. Returns
+        dict(ticks=(N,) int32, decisions=(N,) int32). log: optional (N, cap, DECLOG_COLS) float64 with
+        log_len (N,) int32."""
+        t = self._dev(table, torch.float32)
+        if t.dim() != 3 or t.shape[2] != self.n_envs:
+            raise ValueError(f"table must be (n_eps, n_dec, {self.n_envs})")
+        for x in (ep_idx, dec_idx):
+            if x.dtype != torch.int32 or x.device != self.device or x.numel() != self.n_envs:
+                raise ValueError("ep_idx / dec_idx must be int32 device tensors of n_envs elements")
+        if out is None:
+            out = dict(ticks=torch.zeros(self.n_envs, dtype=torch.int32, device=self.device),
+                       decisions=torch.zeros(self.n_envs, dtype=torch.int32, device=self.device))
+        cap = int(log.shape[1]) if log is not None else 0
+        self._check(self.L.shipsim_run_table(self.h, _ptr(t), int(t.shape[0]), int(t.shape[1]), int(max_ticks),
+                                             _ptr(ep_idx), _ptr(dec_idx), _ptr(out["ticks"]), _ptr(out["decisions"]),
+                                             _ptr(log), cap, _ptr(log_len)), "shipsim_run_table")
+        self._keep_table = t
+        return out
 
     def legacy_step(self, k=1, out=None):
         """k legacy MultiShipEnv.step() ticks of every env (shipsim_legacy_step): dict(states=(N, 8) f64

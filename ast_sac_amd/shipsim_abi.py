@@ -24,6 +24,10 @@ COLLAV = {"none": COLLAV_NONE, None: COLLAV_NONE, "simple": COLLAV_SIMPLE, "sbmp
 MACH_SIMPLIFIED, MACH_DETAILED = 0, 1
 SG_GEN, SG_MOTOR, SG_OFF = 0, 1, 2
 
+# shipsim_run_table per-decision record columns
+DECLOG_COLS = 14
+DL_REWARD, DL_EVENTS, DL_DONE, DL_EPISODE, DL_DECISION, DL_TICKS, DL_OBS = 0, 1, 2, 3, 4, 5, 6
+
 # legacy MultiShipEnv termination_conditions bits (shipsim_legacy_step, termination_flags.py:66-68)
 LT_TEST_REACHED = 1 << 0
 LT_TEST_OUTSIDE = 1 << 1

@@ -1,12 +1,15 @@
 """Headline benchmark: batched two-ship AST env-steps/sec (BASELINE.json metric) on 1..8 MI355X.
 
-A "step" is one sliced batched MultiShipRLEnv.step() over every env of every rank
-(shipsim_step with max_ticks = --slice): every env runs up to `slice` ticks of its current
-decision (one decision = tick until RoA + 1 tick, or done; ≈130 env-ticks per decision at
-dt = 4 s); envs waiting for a decision first consume a scoping angle; envs whose episode ended
-are auto-reset (masked reset kernel) inside the step. Actions come from a device-resident
-synthetic table U(-1, 1) (PCG64 seeded per global env id, SURVEY.md §8(d) C3 input) mapped by
-NormalizedBoxEnv's float32 rule.
+A "step" is one launch over every env of every rank in which each env runs up to `--slice` (128)
+`_step` ticks of the C3 decision stream: decisions (tick until RoA + 1 tick,
+or done; ≈130 env-ticks per decision at dt = 4 s) with scoping angles from a device-resident
+synthetic table U(-1, 1) (PCG64 seeded per rank, NormalizedBoxEnv's float32 rule), 9 decisions per
+episode (max_path_length), auto-reset on episode end. Default --mode table runs it with
+shipsim_run_table (a completed decision is followed at once by the next, episodes reset inside
+the kernel, every decision's result written to a per-env record ring); --mode step drives the
+same stream from the host with shipsim_step slices + masked shipsim_reset between launches (the
+RL collector's call pattern, where the policy picks the next action). Both give identical
+per-decision results (tests/test_gpu_table.py).
 
 value = env-ticks (one `_step` of one env, both ships + reward/termination) summed over all ranks
         / max-over-ranks wall time of the K timed steps.
@@ -40,6 +43,10 @@ def parse():
     p.add_argument("--collav", default="sbmpc", choices=["none", "simple", "sbmpc"])
     p.add_argument("--machinery", default="detailed", choices=["detailed", "simplified"])
     p.add_argument("--slice", type=int, default=128, help="max ticks per env per step call (0 = whole decision)")
+    p.add_argument("--mode", default="table", choices=["table", "step"],
+                   help="table: shipsim_run_table, decisions chained and episodes reset inside the kernel (the "
+                        "C3 open-loop decision stream); step: shipsim_step slices + host-side table lookup and "
+                        "masked shipsim_reset between calls (the RL collector's call pattern)")
     p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library default)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -190,7 +197,29 @@ def main():
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
 
+    ep32 = torch.zeros(N, dtype=torch.int32, device=dev)
+    dec32 = torch.zeros(N, dtype=torch.int32, device=dev)
+    tout = dict(ticks=out["ticks"], decisions=torch.empty(N, dtype=torch.int32, device=dev))
+    if args.mode == "table" and args.slice <= 0:
+        raise SystemExit("--mode table needs --slice >= 1")
+    # every completed decision's result (reward, events, done, obs: what MultiShipRLEnv.step returns) is
+    # written to a per-env record ring, as shipsim_step writes its outputs
+    dlog = torch.zeros((N, 8, abi.DECLOG_COLS), dtype=torch.float64, device=dev)
+    dlog_len = torch.zeros(N, dtype=torch.int32, device=dev)
+
+    def one_step_table(timed_i=None):
+        dlog_len.zero_()
+        if timed_i is not None:
+            ev0[timed_i].record()
+        sim.run_table(table, args.slice, ep32, dec32, out=tout, log=dlog, log_len=dlog_len)
+        if timed_i is not None:
+            ev1[timed_i].record()
+        total_ticks.add_(tout["ticks"].sum())
+        total_decisions.add_(tout["decisions"].sum())
+
     def one_step(timed_i=None):
+        if args.mode == "table":
+            return one_step_table(timed_i)
         act = table[ep_idx % table_eps, dec_idx, ar]
         if timed_i is not None:
             ev0[timed_i].record()
@@ -277,6 +306,7 @@ def main():
                                    "reward_designs), dt 4 s",
                        "envs_per_gpu": N, "global_envs": N * world, "collav": args.collav,
                        "machinery": args.machinery, "slice_ticks": args.slice, "lanes_per_env": args.lpe or 16,
+                       "mode": args.mode,
                        "parallelism": f"env-shard x{world}"},
             "decisions_per_s": all_dec / elapsed,
             "env_ticks_per_decision": all_ticks / max(all_dec, 1),

@@ -332,6 +332,31 @@ int shipsim_set_trajectory(shipsim_handle* h, double* ship_rows, double* env_row
 #define SHIPSIM_SBMPC_IN 17
 int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double* out, void* stream);
 
+/* ---- open-loop decision stream (the C3 workload of SURVEY.md §8(d)) -------------------------
+ * Every env draws the scoping angle (radians, already denormalised) of decision d of its episode e from
+ * table[((e % n_eps) * n_dec + d) * n_envs + env] and runs decisions back to back inside the call: a
+ * completed decision (MultiShipRLEnv.step, env.py:624-773) is followed at once by the next one, and an
+ * episode that ends — done, or n_dec decisions (the rollout's max_path_length, rollout_functions.py:
+ * 106-160) — is reset in place (reset + init_step, env.py:238-342) before its next decision. Each env
+ * runs at most max_ticks (>= 1) _step ticks per call; an env paused mid-decision resumes in the next
+ * call. Results are those of shipsim_step / shipsim_reset driven by the same table.
+ *   ep_idx, dec_idx  N int32 (device, in/out): episode counter and decision index of every env
+ *   ticks_out        N int32: _step ticks run in this call (may be NULL)
+ *   decisions_out    N int32: decisions completed in this call (may be NULL)
+ *   log              N x log_cap x SHIPSIM_DECLOG_COLS doubles: one record per completed decision
+ *                    (may be NULL); log_len N int32 (in/out) counts records (past log_cap too). */
+#define SHIPSIM_DECLOG_COLS 14
+#define SHIPSIM_DL_REWARD 0   /* accumulated (un-scaled) reward of the decision */
+#define SHIPSIM_DL_EVENTS 1   /* SHIPSIM_EV_* bits */
+#define SHIPSIM_DL_DONE 2     /* combined_done */
+#define SHIPSIM_DL_EPISODE 3  /* ep_idx of the decision */
+#define SHIPSIM_DL_DECISION 4 /* dec_idx of the decision */
+#define SHIPSIM_DL_TICKS 5    /* ticks run in the call when the decision completed */
+#define SHIPSIM_DL_OBS 6      /* 8 columns: the observation returned */
+int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
+                      int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
+                      int32_t log_cap, int32_t* log_len);
+
 /* ---- legacy per-tick MultiShipEnv (rl_env/ship_in_transit/env.py:783-1181) ----
  * AST kind. Each of the k ticks is one MultiShipEnv.step() (:1104-1173) of every env: test_step
  * (:923-1023, SBMPC / simple collision avoidance as configured) + obs_step (:1025-1102) +

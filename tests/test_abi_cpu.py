@@ -62,7 +62,7 @@ def test_header_constants_match_binding():
              "F_NEXT_WPT": abi.F_NEXT_WPT, "F_STOP": abi.F_STOP, "N_SHIP_FIELDS": abi.N_SHIP_FIELDS,
              "E_SAMPLING_COUNT": abi.E_SAMPLING_COUNT, "E_ROUTE_EAST": abi.E_ROUTE_EAST}
     for name in dir(abi):  # trajectory record layout and SBMPC batch layout, every column
-        if name.startswith(("TS_", "TE_", "TRAJ_", "SBMPC_IN", "LT_")) and name != "LT_DONE_MASK":
+        if name.startswith(("TS_", "TE_", "TRAJ_", "SBMPC_IN", "LT_", "DL_", "DECLOG_")) and name != "LT_DONE_MASK":
             pairs[name] = getattr(abi, name)
     assert "TS_TIME_LIST" in pairs and "TE_FLAG_IMMINENT" in pairs and "LT_OBS_NAV_FAILURE" in pairs
     for k, v in pairs.items():
