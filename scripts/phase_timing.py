@@ -49,3 +49,8 @@ cyc = np.array(buf[:4], dtype=np.float64)
 print(f"{collav} lpe{lpe} N={N}: {ticks / dt / 1e6:.1f} M env-ticks/s (timing build)")
 for k, name in enumerate(["exchange+sbmpc", "control+integrate", "map queries", "reward+termination+decision"]):
     print(f"  phase {k} {name:30s} {100 * cyc[k] / cyc.sum():5.1f} %")
+sb = np.array(buf[4:8], dtype=np.float64)
+if sb.sum() > 0:  # SbTimer: per-scenario split of sbmpc_scenario_cost (summed over lanes)
+    print("  SBMPC scenario split:", ", ".join(f"{n} {100 * v / sb.sum():.1f} %" for n, v in
+                                             zip(["setup+skip", "sample0", "horizon loop", "final/fallback"], sb)))
+    print(f"  SBMPC share of phase 0 (lane-cycles / 32 per half-wave): {sb.sum() / 32 / max(cyc[0], 1):.2f}")
