@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library default)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-c2", action="store_true", help="skip the configs[1] single-ship secondary line")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round1_pmc_traffic.json"))
     p.add_argument("--sac-steps", type=int, default=300, help="timed SAC grad steps (0 = skip the SAC line)")
     p.add_argument("--sac-batch", type=int, default=256, help="SAC batch per GPU")
@@ -145,6 +146,41 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
                 ref.train_from_torch(rb.random_batch(batch))
         eager(3)
         res["reference_order_eager_grad_steps_per_s"] = eager_steps / timed(eager, eager_steps)
+    return res
+
+
+def bench_c2(dev, n_ships=4096):
+    """configs[1] (C2): 4096 single ships, SimpleShipModel + ThrustFromSpeedSetPoint +
+    HeadingByRouteController, PCG64-perturbed initial states, the whole 10,000 s
+    horizon with shipsim_tick (single_tick_kernel, one lane per ship); secondary line, ship-ticks/s."""
+    import numpy as np
+    import torch
+    from ast_sac_amd import shipsim_abi as abi
+    from ast_sac_amd.shipsim import ShipSim
+    res = {"ships": n_ships, "unit": "ship-ticks/s", "kernel": "single_tick_kernel"}
+    init = abi.c2_initial_states(n_ships)
+    for dt in (30, 4):
+        cfg = abi.c2_config(dt)
+        n_ticks = int(np.ceil(cfg.simulation_time / dt))
+        per = 64 if dt == 30 else 250
+        best = None
+        for rep in range(2):  # first pass warms up
+            sim = ShipSim(cfg, n_ships, device=dev)
+            for f, col in ((abi.F_NORTH, 0), (abi.F_EAST, 1), (abi.F_YAW, 2), (abi.F_U, 3)):
+                sim.set(f, torch.from_numpy(np.ascontiguousarray(init[:, col])))
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            done = 0
+            while done < n_ticks:
+                k = min(per, n_ticks - done)
+                sim.tick(k)
+                done += k
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - t0
+            sim.close()
+            best = el if best is None else min(best, el)
+        res[f"dt{dt}"] = n_ships * n_ticks / best
+        res[f"dt{dt}_ticks"] = n_ticks
     return res
 
 
@@ -280,6 +316,7 @@ def main():
                 traffic = pmc.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
+    c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
     sac = None
     if args.sac_steps > 0:
         sac = bench_sac(dev, world, dist.group.WORLD if world > 1 else None, args.sac_steps, args.sac_batch)
@@ -318,6 +355,7 @@ def main():
                          "launches": int(len(all_ms))},
             "cpu_baseline": cpu,
             "sac": sac,
+            "c2_single_ship": c2,
         }
         print(json.dumps(line))
     if world > 1:
