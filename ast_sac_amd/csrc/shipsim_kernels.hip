@@ -337,6 +337,12 @@ struct SbTimer {
   } while (0)
 #endif
 
+// SBMPCParams.P_ca_ = [0.4, 0.6, 0.8, 1.0] (sbmpc.py:36) by selects: a per-lane indexed constant array would be
+// a memory load on the scenario's critical path
+__device__ __forceinline__ double p_ca_of(int jp) {
+  return jp == 0 ? 0.4 : (jp == 1 ? 0.6 : (jp == 2 ? 0.8 : 1.0));
+}
+
 __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
 #ifdef SHIPSIM_PHASE_TIMING
   SbTimer sb_timer;
@@ -349,8 +355,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   const double max_d_safe = py_max(py_max(d_safe + in.obs_l / 2, 0.5 * d_safe + in.obs_l / 2),
                                    py_max(d_safe + in.obs_w / 2, d_safe + os_l / 2 + in.obs_l / 2));
   const double CHI_DEG = -30.0 + 10.0 * ichi;
-  const double P_CA[4] = {0.4, 0.6, 0.8, 1.0};
-  const double P_ca = P_CA[jp];
+  const double P_ca = p_ca_of(jp);
   const double Chi_ca = CHI_DEG * (kPi / 180.0);
   const double ud = in.u_d * P_ca;
   const double psi_d = in.chi_d + Chi_ca;
@@ -514,13 +519,12 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
     }
     int best0 = __shfl(idx, 0, 64);
     int best1 = __shfl(idx, 32, 64);
-    const double P_CA[4] = {0.4, 0.6, 0.8, 1.0};
     if (lane == src0) {
-      p_best = P_CA[best0 & 3];
+      p_best = p_ca_of(best0 & 3);
       chi_best = (-30.0 + 10.0 * (best0 >> 2)) * (kPi / 180.0);
     }
     if (src1 >= 0 && lane == src1) {
-      p_best = P_CA[best1 & 3];
+      p_best = p_ca_of(best1 & 3);
       chi_best = (-30.0 + 10.0 * (best1 >> 2)) * (kPi / 180.0);
     }
   }
