@@ -878,7 +878,10 @@ constexpr int kMaxMats = 24;
 // Row split of the weight gradients: grid.y = kParts blocks per tile each reduce B / kParts rows
 // into partial gradient p (same layout as the flat gradient); sac_gsum_kernel adds the kParts
 // partials in a fixed order (deterministic) into the gradient.
-constexpr int kParts = 8;
+#ifndef SAC_KPARTS
+#define SAC_KPARTS 8
+#endif
+constexpr int kParts = SAC_KPARTS;
 struct WgradArgs {
   GMat mats[kMaxMats];
   const GTask* tasks;
