@@ -1,0 +1,125 @@
+"""The bench workload itself at full size (BASELINE.json configs[2]: 4096 two-ship AST envs, PTI
+machinery, dt 4 s, the decision stream of shipsim_run_table in 128-tick launches, as bench.py runs
+it), checked two ways:
+  - every env: size-independent invariants of the decision log (finite records, episode / decision
+    counters in order, each episode ends on done or on the 9th decision, ticks per launch bounded);
+  - every 16th env: decision by decision against the CPU oracle replaying the same episodes
+    (reward, termination bits, done, obs), with the oracle's few-ulp initial-condition variants
+    (gpu_harness.run_oracle_variants) as the acceptance envelope.
+Needs an MI355X."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import gpu_harness as H
+from ast_sac_amd import shipsim_abi as abi
+from ast_sac_amd.shipsim import ShipSim
+from parity import rel_err
+
+pytestmark = pytest.mark.gpu
+
+N = 4096
+SLICE = 128
+LAUNCHES = 12
+N_EPS = 3
+
+
+def _run(cfg, a_norm):
+    sim = ShipSim(cfg, N)
+    sim.reset()
+    table = torch.from_numpy(abi.normalized_to_scoping(a_norm)).cuda()
+    ep = torch.zeros(N, dtype=torch.int32, device="cuda")
+    dec = torch.zeros(N, dtype=torch.int32, device="cuda")
+    cap = 64
+    log = torch.zeros((N, cap, abi.DECLOG_COLS), dtype=torch.float64, device="cuda")
+    log_len = torch.zeros(N, dtype=torch.int32, device="cuda")
+    ticks = []
+    for _ in range(LAUNCHES):
+        o = sim.run_table(table, SLICE, ep, dec, log=log, log_len=log_len)
+        ticks.append(o["ticks"].cpu().numpy())
+    torch.cuda.synchronize()
+    out = log.cpu().numpy(), log_len.cpu().numpy(), np.array(ticks), ep.cpu().numpy(), dec.cpu().numpy()
+    sim.close()
+    return out
+
+
+def _episodes(rows):
+    """decision-log rows of one env -> per episode [(obs, reward, done, bits, -1), ...] (harness tuples)"""
+    eps = []
+    for r in rows:
+        e = int(r[abi.DL_EPISODE])
+        while len(eps) <= e:
+            eps.append([])
+        eps[e].append((r[abi.DL_OBS:abi.DL_OBS + 8].astype(np.float32), r[abi.DL_REWARD], bool(r[abi.DL_DONE]),
+                       int(r[abi.DL_EVENTS]), -1))
+    return eps
+
+
+def _match(g_eps, o_rec, rtol=1e-5):
+    """g_eps (possibly ending in an unfinished episode) against the oracle's episodes; ticks are not
+    compared (the log holds ticks per launch, not per decision)."""
+    worst = 0.0
+    for k, gd in enumerate(g_eps):
+        od = o_rec[k][1]
+        if len(gd) > len(od) or (k < len(g_eps) - 1 and len(gd) != len(od)):
+            return np.inf
+        for g, o in zip(gd, od):
+            if (g[3] & 0x7FFFF) != (o[3] & 0x7FFFF) or g[2] != o[2]:
+                return np.inf
+            e = max(float(rel_err(g[0][None], o[0][None]).max()), float(abs(g[1] - o[1]) / (abs(o[1]) + 1e-6)))
+            worst = max(worst, e)
+    return worst
+
+
+@pytest.mark.parametrize("collav", ["sbmpc", "none"])
+def test_bench_workload_full_size(collav):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    cfg = abi.ast_config(collav)
+    n_dec = cfg.max_sampling_frequency
+    a_norm = np.random.Generator(np.random.PCG64(20251015)).uniform(-1, 1, (N_EPS, n_dec, N)).astype(np.float32)
+    log, log_len, ticks, ep, dec = _run(cfg, a_norm)
+
+    # invariants, every env
+    assert ticks.max() <= SLICE and (ticks == SLICE).mean() > 0.99  # the stream keeps every env busy
+    assert (log_len >= 4).all() and log_len.max() <= log.shape[1]
+    total_dec = 0
+    for i in range(N):
+        rows = log[i, :log_len[i]]
+        assert np.isfinite(rows).all(), i
+        e, d = rows[:, abi.DL_EPISODE].astype(int), rows[:, abi.DL_DECISION].astype(int)
+        # counters advance by one decision, or start a new episode at decision 0
+        nxt_same = (e[1:] == e[:-1]) & (d[1:] == d[:-1] + 1)
+        nxt_new = (e[1:] == e[:-1] + 1) & (d[1:] == 0)
+        assert (nxt_same | nxt_new).all(), i
+        # an episode ends on done or on its n_dec-th decision, never otherwise
+        ends = np.nonzero(nxt_new)[0]
+        assert ((rows[ends, abi.DL_DONE] == 1) | (d[ends] == n_dec - 1)).all(), i
+        assert (d < n_dec).all()
+        total_dec += len(rows)
+    assert total_dec == int(log_len.sum())
+
+    # oracle, every 16th env
+    idx = np.arange(0, N, 16)
+    tables = [[a_norm[k % N_EPS, :, i] for k in range(int(log[i, log_len[i] - 1, abi.DL_EPISODE]) + 1)] for i in idx]
+    g_all = [_episodes(log[i, :log_len[i]]) for i in idx]
+    orc = H.run_oracle(cfg, tables)
+    worst, bad = 0.0, []
+    for j, i in enumerate(idx):
+        w = _match(g_all[j], orc[j][0])
+        if not w <= 1e-5:
+            for eps in H.PERTURBATIONS[1:]:  # the oracle's own few-ulp envelope (gpu_harness)
+                c = copy.deepcopy(cfg)
+                c.ship[0].initial_north_position_m *= 1 + eps
+                c.ship[1].initial_east_position_m *= 1 - eps
+                w = min(w, _match(g_all[j], H.run_oracle(c, [tables[j]])[0][0]))
+                if w <= 1e-5:
+                    break
+        if not w <= 1e-5:
+            bad.append(int(i))
+        else:
+            worst = max(worst, w)
+    assert not bad, f"envs off the oracle: {bad[:20]}"
+    assert worst <= 1e-5
