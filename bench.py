@@ -1,7 +1,7 @@
 """Headline benchmark: batched two-ship AST env-steps/sec (BASELINE.json metric) on 1..8 MI355X.
 
-A "step" is one launch over every env of every rank in which each env runs up to `--slice` (128)
-`_step` ticks of the C3 decision stream: decisions (tick until RoA + 1 tick,
+A "step" is one launch over every env of every rank in which each env runs `--slice` (2048, about
+two episodes) `_step` ticks of the C3 decision stream: decisions (tick until RoA + 1 tick,
 or done; ≈130 env-ticks per decision at dt = 4 s) with scoping angles from a device-resident
 synthetic table U(-1, 1) (PCG64 seeded per rank, NormalizedBoxEnv's float32 rule), 9 decisions per
 episode (max_path_length), auto-reset on episode end. Default --mode table runs it with
@@ -9,7 +9,11 @@ shipsim_run_table (a completed decision is followed at once by the next, episode
 the kernel, every decision's result written to a per-env record ring); --mode step drives the
 same stream from the host with shipsim_step slices + masked shipsim_reset between launches (the
 RL collector's call pattern, where the policy picks the next action). Both give identical
-per-decision results (tests/test_gpu_table.py).
+per-decision results (tests/test_gpu_table.py). Launch length matters because the launch ends
+with its slowest wave: per-wave cost varies with SBMPC activity (waves whose envs are inside 2 km
+of the obstacle ship do ~2x the work), and that variance averages out over longer launches
+(sbmpc: 128 ticks 251 M, 512 369 M, 1024 446 M, 2048 483 M, 4096 511 M env-ticks/s;
+profiles/round1_sweeps.md).
 
 value = env-ticks (one `_step` of one env, both ships + reward/termination) summed over all ranks
         / max-over-ranks wall time of the K timed steps.
@@ -37,12 +41,13 @@ ALGO_BYTES_PER_ENV_TICK = 616  # C3/C5 detailed dynamics, one 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=40)
-    p.add_argument("--warmup", type=int, default=12)
+    p.add_argument("--steps", type=int, default=8)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--envs-per-gpu", type=int, default=4096)
     p.add_argument("--collav", default="sbmpc", choices=["none", "simple", "sbmpc"])
     p.add_argument("--machinery", default="detailed", choices=["detailed", "simplified"])
-    p.add_argument("--slice", type=int, default=128, help="max ticks per env per step call (0 = whole decision)")
+    p.add_argument("--slice", type=int, default=2048,
+                   help="max ticks per env per step call (0 = whole decision); table mode: ticks per env per launch")
     p.add_argument("--mode", default="table", choices=["table", "step"],
                    help="table: shipsim_run_table, decisions chained and episodes reset inside the kernel (the "
                         "C3 open-loop decision stream); step: shipsim_step slices + host-side table lookup and "
@@ -240,14 +245,19 @@ def main():
         raise SystemExit("--mode table needs --slice >= 1")
     # every completed decision's result (reward, events, done, obs: what MultiShipRLEnv.step returns) is
     # written to a per-env record ring, as shipsim_step writes its outputs
-    dlog = torch.zeros((N, 8, abi.DECLOG_COLS), dtype=torch.float64, device=dev)
+    # (sized for every decision of a launch: decisions average ~130 ticks at dt 4 s and the measured
+    # maximum is ~slice / 76; the largest per-launch count is reported as decision_log.max_per_launch)
+    dlog_cap = max(8, args.slice // 32 + 16)
+    dlog = torch.zeros((N, dlog_cap, abi.DECLOG_COLS), dtype=torch.float64, device=dev)
     dlog_len = torch.zeros(N, dtype=torch.int32, device=dev)
+    dlog_max = torch.zeros((), dtype=torch.int32, device=dev)
 
     def one_step_table(timed_i=None):
         dlog_len.zero_()
         if timed_i is not None:
             ev0[timed_i].record()
         sim.run_table(table, args.slice, ep32, dec32, out=tout, log=dlog, log_len=dlog_len)
+        torch.maximum(dlog_max, dlog_len.max(), out=dlog_max)
         if timed_i is not None:
             ev1[timed_i].record()
         total_ticks.add_(tout["ticks"].sum())
@@ -312,7 +322,7 @@ def main():
         try:
             with open(args.pmc_json) as f:
                 pmc = json.load(f)
-            if pmc.get("collav") == args.collav and pmc.get("envs") == N:
+            if pmc.get("collav") == args.collav and pmc.get("envs") == N and pmc.get("slice") == args.slice:
                 traffic = pmc.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -347,6 +357,7 @@ def main():
                        "parallelism": f"env-shard x{world}"},
             "decisions_per_s": all_dec / elapsed,
             "env_ticks_per_decision": all_ticks / max(all_dec, 1),
+            "decision_log": {"cap": dlog_cap, "max_per_launch": int(dlog_max.item())} if args.mode == "table" else None,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"ast_step_kernel (avg {kmean:.3f} ms/launch, "

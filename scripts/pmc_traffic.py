@@ -22,12 +22,12 @@ def per_dispatch(d, counter, kernel="ast_step_kernel"):
     return list(vals.values())
 
 
-def main(fetch_dir, write_dir, out, collav="sbmpc", envs=4096):
+def main(fetch_dir, write_dir, out, slice_ticks="2048", collav="sbmpc", envs=4096):
     fe = per_dispatch(fetch_dir, "FETCH_SIZE")
     wr = per_dispatch(write_dir, "WRITE_SIZE")
     fetch_b = 2 * 1024 * sum(fe) / len(fe)
     write_b = 1024 * sum(wr) / len(wr)
-    res = dict(kernel="ast_step_kernel", collav=collav, envs=envs, dispatches=[len(fe), len(wr)],
+    res = dict(kernel="ast_step_kernel", collav=collav, envs=envs, slice=int(slice_ticks), dispatches=[len(fe), len(wr)],
                fetch_size_kb_raw=sum(fe) / len(fe), write_size_kb=sum(wr) / len(wr),
                fetch_bytes_corrected=fetch_b, write_bytes=write_b, hbm_bytes_per_launch=fetch_b + write_b,
                note="FETCH_SIZE x2 (gfx950 wide-read correction, MI355X_MICROARCH.md HBM section); "
@@ -39,4 +39,4 @@ def main(fetch_dir, write_dir, out, collav="sbmpc", envs=4096):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
