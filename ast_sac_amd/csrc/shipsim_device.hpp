@@ -190,15 +190,37 @@ __device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, 
   tau[2] = tau_coeff * c_n * c.proj_area_l * c.l_ship;
 }
 
+// get_wind_force with the reference's angles eliminated algebraically (the C2 single-ship kernel):
+// sin/cos(wind_direction - yaw) by the difference formulas from (sy, cy) = sin/cos(yaw) and
+// (wsin, wcos) = sin/cos(wind_direction); with gamma_rw = -atan2(v_rw, u_rw) and V = |V_rw|,
+// cos(gamma) = u_rw / V, sin(gamma) = -v_rw / V, sin(2 gamma) = -2 u_rw v_rw / V^2, so
+//   tau = (-0.5 rho cx A_f u_rw V, -0.5 rho cy A_l v_rw V, -rho cn A_l L u_rw v_rw):
+// one sqrt instead of atan2 and three sincos; equal to wind_force up to rounding (V = 0 gives 0).
+__device__ __forceinline__ void wind_force_alg(const ShipConst& c, const Params& P, const Ship& s, double sy,
+                                               double cy, double wsin, double wcos, double tau[3]) {
+  const double cw = wcos * cy + wsin * sy;
+  const double sw = wsin * cy - wcos * sy;
+  const double u_rw = P.wind_speed * cw - s.u;
+  const double v_rw = P.wind_speed * sw - s.v;
+  const double V = sqrt(u_rw * u_rw + v_rw * v_rw);
+  const double h = 0.5 * c.rho_a;
+  tau[0] = -(h * c.cx * c.proj_area_f) * (u_rw * V);
+  tau[1] = -(h * c.cy * c.proj_area_l) * (v_rw * V);
+  tau[2] = -(c.rho_a * c.cn * c.proj_area_l * c.l_ship) * (u_rw * v_rw);
+}
+
 // update_differentials (ShipModelAST :882-888 / SimpleShipModel run_colav :399-404):
 // three_dof_kinematics :519-528, shaft_eq + thrust (ship_engine.py:403-443), three_dof_kinetics
 // :834-864 with rudder :866-880. `ctrl` is the engine throttle (detailed) or thrust force (simplified).
-template <bool PAIRED = false>
+// ALGW: wind by wind_force_alg ((wsin, wcos) = sin/cos(wind_direction)), one sincos per tick.
+template <bool PAIRED = false, bool ALGW = false>
 __device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params& P, const Ship& s, double ctrl,
-                                               double delta, bool detailed, bool odd = false) {
+                                               double delta, bool detailed, bool odd = false, double wsin = 0.0,
+                                               double wcos = 1.0) {
   Deriv d;
-  double sy, cy, sw, cw;
-  sincos2<PAIRED>(s.yaw, P.wind_dir - s.yaw, odd, sy, cy, sw, cw);
+  double sy, cy, sw = 0.0, cw = 1.0;
+  if (ALGW) sincos(s.yaw, &sy, &cy);
+  else sincos2<PAIRED>(s.yaw, P.wind_dir - s.yaw, odd, sy, cy, sw, cw);
   d.dn = cy * s.u + (-sy) * s.v + 0 * s.r;
   d.de = sy * s.u + cy * s.v + 0 * s.r;
   d.dyaw = 0 * s.u + 0 * s.v + 1 * s.r;
@@ -219,7 +241,8 @@ __device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params&
   double fv = -c.c_rudder_v * delta * (s.u - vc0);
   double fr = -c.c_rudder_r * delta * (s.u - vc0);
   double tau[3];
-  wind_force<PAIRED>(c, P, s, sw, cw, odd, tau);
+  if (ALGW) wind_force_alg(c, P, s, sy, cy, wsin, wcos, tau);
+  else wind_force<PAIRED>(c, P, s, sw, cw, odd, tau);
   double u_r = s.u - vc0;
   double v_r = s.v - vc1;
   double x_g = 0.0;

@@ -169,13 +169,14 @@ __device__ __forceinline__ const ShipConst* stage_consts(const Params& P, ShipCo
 // one controlled ship tick: autopilot -> speed control -> store -> update -> integrate -> next_time
 // (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339)
 // PAIRED: sub-lanes 2k / 2k+1 of the ship share the batched sincos calls (odd = this lane is 2k+1)
-template <bool DETAILED, bool REC = false, bool PAIRED = false>
+// ALGW: algebraic wind force (differentials), (wsin, wcos) = sin/cos(wind_direction)
+template <bool DETAILED, bool REC = false, bool PAIRED = false, bool ALGW = false>
 __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const Params& P, Ship& s,
                                                       const double* __restrict__ rn, const double* __restrict__ re,
                                                       double offset, double speed_factor, double mach_dt,
                                                       int simple_collav_flag /*0 none, 1 rl(-15deg), 2 noniw(+15)*/,
                                                       bool imminent, double* row = nullptr, double* fuel = nullptr,
-                                                      bool odd = false) {
+                                                      bool odd = false, double wsin = 0.0, double wcos = 1.0) {
   const double N = s.n, E = s.e, H = s.yaw, U = s.u;
   if (next_wpt_advance(c, s, N, E)) {
     s.next_wpt += 1;
@@ -210,7 +211,7 @@ __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const 
       row[SHIPSIM_TS_TIME_LIST] = s.time;
     }
   }
-  Deriv d = differentials<PAIRED>(c, P, s, ctrl, rudder, DETAILED, odd);
+  Deriv d = differentials<PAIRED, ALGW>(c, P, s, ctrl, rudder, DETAILED, odd, wsin, wcos);
   integrate(s, d, P.dt, mach_dt, DETAILED);
 }
 
@@ -1186,7 +1187,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   }
 }
 
-// C2 single-ship loop body, k ticks per launch (one lane per ship)
+// C2 single-ship loop body, k ticks per launch (one lane per ship; algebraic wind force)
 template <bool DETAILED>
 __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevState S, ConstBuf K, int k) {
   __shared__ ShipConst lds_sc[2];
@@ -1199,7 +1200,11 @@ __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevStat
   Ship s;
   load_ship(S, q, s);
   const double mach_dt = S.mach_dt()[q];
-  for (int i = 0; i < k; ++i) control_and_integrate<DETAILED>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false);
+  double wsin, wcos;
+  sincos(P.wind_dir, &wsin, &wcos);
+  for (int i = 0; i < k; ++i)
+    control_and_integrate<DETAILED, false, false, true>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false, nullptr, nullptr,
+                                                        false, wsin, wcos);
   store_ship(S, q, s);
 }
 
