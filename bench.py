@@ -332,7 +332,7 @@ def main():
         sac = bench_sac(dev, world, dist.group.WORLD if world > 1 else None, args.sac_steps, args.sac_batch)
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure
             nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
             nthreads = min(nthreads, 16)
             cpu = cpu_baseline(cfg, args.cpu_baseline_seconds, nthreads)
