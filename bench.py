@@ -1,7 +1,7 @@
 """Headline benchmark: batched two-ship AST env-steps/sec (BASELINE.json metric) on 1..8 MI355X.
 
-A "step" is one launch over every env of every rank in which each env runs `--slice` (2048, about
-two episodes) `_step` ticks of the C3 decision stream: decisions (tick until RoA + 1 tick,
+A "step" is one launch over every env of every rank in which each env runs `--slice` (4096, about
+four episodes) `_step` ticks of the C3 decision stream: decisions (tick until RoA + 1 tick,
 or done; ≈130 env-ticks per decision at dt = 4 s) with scoping angles from a device-resident
 synthetic table U(-1, 1) (PCG64 seeded per rank, NormalizedBoxEnv's float32 rule), 9 decisions per
 episode (max_path_length), auto-reset on episode end. Default --mode table runs it with
@@ -41,12 +41,12 @@ ALGO_BYTES_PER_ENV_TICK = 616  # C3/C5 detailed dynamics, one 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=8)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=6)
+    p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--envs-per-gpu", type=int, default=4096)
     p.add_argument("--collav", default="sbmpc", choices=["none", "simple", "sbmpc"])
     p.add_argument("--machinery", default="detailed", choices=["detailed", "simplified"])
-    p.add_argument("--slice", type=int, default=2048,
+    p.add_argument("--slice", type=int, default=4096,
                    help="max ticks per env per step call (0 = whole decision); table mode: ticks per env per launch")
     p.add_argument("--mode", default="table", choices=["table", "step"],
                    help="table: shipsim_run_table, decisions chained and episodes reset inside the kernel (the "

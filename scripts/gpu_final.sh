@@ -12,7 +12,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$TAG -o run -- python3 $R/bench.py --no-cpu-baseline --sac-steps 0 > $O/pmc_fetch_$TAG.log 2>&1; hard $? pmc_fetch
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$TAG -o run -- python3 $R/bench.py --no-cpu-baseline --sac-steps 0 > $O/pmc_write_$TAG.log 2>&1; hard $? pmc_write
 cd $R
-python scripts/pmc_traffic.py $O/pmc_fetch_$TAG $O/pmc_write_$TAG profiles/round1_pmc_traffic.json 2048 > $O/pmc_traffic_$TAG.json; hard $? pmc_json
+python scripts/pmc_traffic.py $O/pmc_fetch_$TAG $O/pmc_write_$TAG profiles/round1_pmc_traffic.json 4096 > $O/pmc_traffic_$TAG.json; hard $? pmc_json
 cp profiles/round1_pmc_traffic.json $O/round1_pmc_traffic.json
 timeout -k 10 400 python bench.py > $O/bench_${TAG}_sbmpc.log 2>&1; hard $? bench1
 tail -1 $O/bench_${TAG}_sbmpc.log

@@ -22,7 +22,7 @@ def per_dispatch(d, counter, kernel="ast_step_kernel"):
     return list(vals.values())
 
 
-def main(fetch_dir, write_dir, out, slice_ticks="2048", collav="sbmpc", envs=4096):
+def main(fetch_dir, write_dir, out, slice_ticks="4096", collav="sbmpc", envs=4096):
     fe = per_dispatch(fetch_dir, "FETCH_SIZE")
     wr = per_dispatch(write_dir, "WRITE_SIZE")
     fetch_b = 2 * 1024 * sum(fe) / len(fe)
