@@ -12,7 +12,7 @@ RL collector's call pattern, where the policy picks the next action). Both give 
 per-decision results (tests/test_gpu_table.py). Launch length matters because the launch ends
 with its slowest wave: per-wave cost varies with SBMPC activity (waves whose envs are inside 2 km
 of the obstacle ship do ~2x the work), and that variance averages out over longer launches
-(sbmpc: 128 ticks 251 M, 512 369 M, 1024 446 M, 2048 483 M, 4096 511 M env-ticks/s;
+(sbmpc: 128 ticks 251 M, 512 369 M, 1024 446 M, 2048 483 M, 4096 511-513 M env-ticks/s;
 profiles/round1_sweeps.md).
 
 value = env-ticks (one `_step` of one env, both ships + reward/termination) summed over all ranks
