@@ -1,6 +1,6 @@
 """The bench workload itself at full size (BASELINE.json configs[2]: 4096 two-ship AST envs, PTI
 machinery, dt 4 s, the decision stream of shipsim_run_table in 128-tick launches, as bench.py runs
-it), checked two ways:
+it, in 128-tick launches and in one 4096-tick launch, the bench default), checked two ways:
   - every env: size-independent invariants of the decision log (finite records, episode / decision
     counters in order, each episode ends on done or on the 9th decision, ticks per launch bounded);
   - every 16th env: decision by decision against the CPU oracle replaying the same episodes
@@ -21,18 +21,16 @@ from parity import rel_err
 pytestmark = pytest.mark.gpu
 
 N = 4096
-SLICE = 128
-LAUNCHES = 12
 N_EPS = 3
 
 
-def _run(cfg, a_norm):
+def _run(cfg, a_norm, SLICE, LAUNCHES):
     sim = ShipSim(cfg, N)
     sim.reset()
     table = torch.from_numpy(abi.normalized_to_scoping(a_norm)).cuda()
     ep = torch.zeros(N, dtype=torch.int32, device="cuda")
     dec = torch.zeros(N, dtype=torch.int32, device="cuda")
-    cap = 64
+    cap = 144
     log = torch.zeros((N, cap, abi.DECLOG_COLS), dtype=torch.float64, device="cuda")
     log_len = torch.zeros(N, dtype=torch.int32, device="cuda")
     ticks = []
@@ -73,14 +71,14 @@ def _match(g_eps, o_rec, rtol=1e-5):
     return worst
 
 
-@pytest.mark.parametrize("collav", ["sbmpc", "none"])
-def test_bench_workload_full_size(collav):
+@pytest.mark.parametrize("collav,SLICE,LAUNCHES", [("sbmpc", 128, 12), ("none", 128, 12), ("sbmpc", 4096, 1)])
+def test_bench_workload_full_size(collav, SLICE, LAUNCHES):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     cfg = abi.ast_config(collav)
     n_dec = cfg.max_sampling_frequency
     a_norm = np.random.Generator(np.random.PCG64(20251015)).uniform(-1, 1, (N_EPS, n_dec, N)).astype(np.float32)
-    log, log_len, ticks, ep, dec = _run(cfg, a_norm)
+    log, log_len, ticks, ep, dec = _run(cfg, a_norm, SLICE, LAUNCHES)
 
     # invariants, every env
     assert ticks.max() <= SLICE and (ticks == SLICE).mean() > 0.99  # the stream keeps every env busy
