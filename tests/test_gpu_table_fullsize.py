@@ -71,11 +71,14 @@ def _match(g_eps, o_rec, rtol=1e-5):
     return worst
 
 
-@pytest.mark.parametrize("collav,SLICE,LAUNCHES", [("sbmpc", 128, 12), ("none", 128, 12), ("sbmpc", 4096, 1)])
-def test_bench_workload_full_size(collav, SLICE, LAUNCHES):
+@pytest.mark.parametrize("collav,SLICE,LAUNCHES,mach", [("sbmpc", 128, 12, "detailed"), ("none", 128, 12, "detailed"),
+                                                       ("sbmpc", 4096, 1, "detailed"), ("simple", 1024, 2, "detailed"),
+                                                       ("sbmpc", 1024, 2, "simplified"),
+                                                       ("none", 1024, 2, "simplified")])
+def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    cfg = abi.ast_config(collav)
+    cfg = abi.ast_config(collav, machinery=abi.MACH_DETAILED if mach == "detailed" else abi.MACH_SIMPLIFIED)
     n_dec = cfg.max_sampling_frequency
     a_norm = np.random.Generator(np.random.PCG64(20251015)).uniform(-1, 1, (N_EPS, n_dec, N)).astype(np.float32)
     log, log_len, ticks, ep, dec = _run(cfg, a_norm, SLICE, LAUNCHES)
