@@ -96,17 +96,20 @@ class FusedSACTrainer(TorchTrainer):
         self.noise_fn = None  # callable(shape) -> ε for [obs; next_obs] rows; None = torch.randn
         self._static = None
         self._graphs = None
-        # backend "hip": the fused kernels of libsacfused.so (csrc/sac_kernels.hip); "torch": the
-        # PyTorch-op formulation above. Default: hip on a HIP device when the networks fit it.
+        # backend "hip": the fused kernels of libsacfused.so (csrc/sac_kernels.hip), the product path
+        # on a HIP device; "torch": the PyTorch-op formulation above, chosen only explicitly (or on a
+        # CPU device, where it is the test/reference path). No silent switch: networks the hip kernels
+        # do not cover raise here instead of falling back.
         if backend is None:
-            backend = "hip" if dev.type == "cuda" and self._hip_shapes_ok() else "torch"
+            backend = "hip" if dev.type == "cuda" else "torch"
         if backend not in ("hip", "torch"):
             raise ValueError(f"backend must be 'hip' or 'torch', got {backend!r}")
         self.backend = backend
         if backend == "hip":
             if not self._hip_shapes_ok():
-                raise ValueError("hip backend: needs 2 equal hidden layers (<= 256, multiple of 32), act_dim 1, "
-                                 "obs_dim <= 15 and batch_size % 4 == 0")
+                raise ValueError("FusedSACTrainer hip backend: needs 2 equal hidden layers (<= 256, multiple of 32), "
+                                 "act_dim 1, obs_dim <= 15 and batch_size % 4 == 0; pass backend='torch' to run "
+                                 "these networks with PyTorch ops")
             self._init_hip(policy_lr, qf_lr)
         self._n_train_steps_total = 0
         self._need_to_update_eval_statistics = True

@@ -150,8 +150,15 @@ def experiment_device(variant, args, device, process_group=None):
     eval_coll = BatchedPathCollector(eval_env, MakeDeterministic(policy), max_path_length=ak["max_path_length"],
                                      max_ticks=args.slice_ticks, deterministic=True)
     rb = DeviceReplayBuffer(variant["replay_buffer_size"], obs_dim, act_dim, device)
+    # --batch_size is the GLOBAL batch (the reference's 256, run/ast-sac_runner.py:55): each of the
+    # `world` ranks samples batch_size / world rows from its own buffer shard and the averaged
+    # gradient equals the single-GPU B-row gradient in expectation
+    world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+    if ak["batch_size"] % world:
+        raise ValueError(f"--batch_size {ak['batch_size']} must be a multiple of the {world} ranks")
     trainer = FusedSACTrainer(env=eval_env, policy=policy, qf1=qf1, qf2=qf2, target_qf1=tq1, target_qf2=tq2,
-                              batch_size=ak["batch_size"], process_group=process_group, **variant["trainer_kwargs"])
+                              batch_size=ak["batch_size"] // world, process_group=process_group,
+                              backend="hip", **variant["trainer_kwargs"])
     trainer.broadcast_parameters(0)
     return DeviceBatchRLAlgorithm(trainer=trainer, exploration_env=expl_env, evaluation_env=eval_env,
                                   exploration_data_collector=expl_coll, evaluation_data_collector=eval_coll,

@@ -23,7 +23,11 @@ with PTI machinery, HeadingBySampledRouteController, reward_designs, collav = sb
 default, run/ast-sac_runner.py:35), dt = 4 s. Weak scaling: envs per GPU fixed.
 
 Launch:  python bench.py                       (N = 1)
+         python bench.py --gpus N              (spawns N ranks itself: a child torch.distributed.run;
+                                                this parent process never touches the GPU)
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+One rank per GPU over RCCL ("nccl"); `--dist-backend gloo` rehearses N ranks on fewer devices, and the
+line then reports `ranks` (processes) and `n_gpus` (distinct physical devices) separately.
 """
 import argparse
 import json
@@ -58,29 +62,58 @@ def parse():
     p.add_argument("--no-c2", action="store_true", help="skip the configs[1] single-ship secondary line")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round1_pmc_traffic.json"))
     p.add_argument("--sac-steps", type=int, default=300, help="timed SAC grad steps (0 = skip the SAC line)")
-    p.add_argument("--sac-batch", type=int, default=256, help="SAC batch per GPU")
+    p.add_argument("--sac-global-batch", type=int, default=256,
+                   help="SAC batch summed over all ranks (runner: 256); each rank samples global / N rows "
+                        "(SURVEY.md §8(e))")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, one GPU per rank) | gloo (rehearsal)")
     return p.parse_args()
 
 
-def cpu_baseline(cfg, seconds, n_threads):
-    """The oracle (C restatement, OpenMP over envs) on a bounded sample of the same workload."""
+def host_threads():
+    """Threads for the CPU baseline: every core this process may run on (the box's CPU share,
+    OMP_NUM_THREADS when the launcher sets it)."""
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return (omp or avail), avail
+
+
+def cpu_baseline(cfg, seconds, n_threads, n_envs=4096):
+    """BASELINE.md CPU-baseline plan: the oracle (the fixture-pinned C restatement) compiled here
+    with -O3 -march=native, OpenMP one env per thread over every available core, on a bounded sample
+    of the same workload: C3 = batches of `n_envs` two-ship AST envs x one episode each (9 decisions
+    from the PCG64 table, as the GPU stream runs them), and C2 = `n_envs` single ships over the whole
+    10,000 s horizon at dt 30 and dt 4 (the c2_single_ship line's workload)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_ffi as O
     from ast_sac_amd import shipsim_abi as abi
-    n = max(n_threads, 8)
+    L = O.native_lib()
+    n = n_envs
     while True:
         acts = abi.normalized_to_scoping(abi.ast_action_table(n))
         t0 = time.perf_counter()
-        total, ticks, dec, ret, bits = O.ast_rollouts(cfg, acts, n_threads=n_threads)
+        total, ticks, dec, ret, bits = O.ast_rollouts(cfg, acts, n_threads=n_threads, L=L)
         dt = time.perf_counter() - t0
-        if dt >= seconds * 0.5 or n >= 1 << 16:
+        if dt >= seconds * 0.5 or n >= 64 * n_envs:
             break
-        n = int(n * min(8.0, max(2.0, seconds / max(dt, 1e-3))))
+        n = n_envs * max(2 * (n // n_envs), int(np.ceil(n / n_envs * seconds * 0.6 / max(dt, 1e-3))))
+    c2 = {}
+    init = abi.c2_initial_states(n_envs)
+    for step in (30, 4):
+        c2cfg = abi.c2_config(step)
+        n_ticks = int(np.ceil(c2cfg.simulation_time / step))
+        t0 = time.perf_counter()
+        O.c2_run(c2cfg, init, max_ticks=n_ticks, trace=False, n_threads=n_threads, L=L)
+        c2[f"dt{step}"] = n_envs * n_ticks / (time.perf_counter() - t0)
     return dict(value=total / dt, unit="env-ticks/s", cores=n_threads, kind="port",
-                sample=f"{n} two-ship AST envs x 1 episode (<=9 decisions, auto from PCG64 table), "
-                       f"{int(total)} env-ticks in {dt:.1f} s, oracle/shipsim_oracle.c -O2 OpenMP")
+                nproc=os.cpu_count(), affinity_cpus=host_threads()[1],
+                sample=f"C3: {n // n_envs} x {n_envs} two-ship AST envs x 1 episode each (<=9 decisions from the "
+                       f"PCG64 table), {int(total)} env-ticks in {dt:.1f} s; oracle/shipsim_oracle.c built -O3 "
+                       f"-march=native, OpenMP {n_threads} threads",
+                c2_ship_ticks_per_s=c2, c2_sample=f"{n_envs} single ships x whole 10,000 s horizon (dt 30, dt 4)")
 
 
 def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
@@ -189,19 +222,54 @@ def bench_c2(dev, n_ships=4096):
     return res
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` run directly: start the N ranks as ONE child process
+    (torch.distributed.run, rendezvous on 127.0.0.1) and return its exit status. Nothing here has
+    touched the GPU (no torch import), and the child is a fresh process, never an exec of this one."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def rank_layout(args, torch):
+    """(world, rank, local device index) of this process, checked against --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch with --gpus N alone "
+                         f"(it spawns the ranks) or under torch.distributed.run --nproc-per-node {args.gpus}")
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "nccl":
+        if local >= n_dev:
+            raise SystemExit(f"bench.py: rank {rank} needs device {local}, only {n_dev} visible (one GPU per rank "
+                             f"over RCCL; use --dist-backend gloo to rehearse more ranks than devices)")
+    else:  # multi-rank rehearsal on fewer GPUs than ranks
+        local = local % max(1, n_dev)
+    return world, rank, local
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import numpy as np
     import torch
     import torch.distributed as dist
     from ast_sac_amd import shipsim_abi as abi
     from ast_sac_amd.shipsim import ShipSim
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.dist_backend == "gloo":  # multi-rank rehearsal on fewer GPUs than ranks
-        local = local % max(1, torch.cuda.device_count())
+    world, rank, local = rank_layout(args, torch)
     if world > 1:
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
@@ -210,6 +278,12 @@ def main():
             dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # distinct physical devices behind the ranks (= world over RCCL; fewer under a gloo rehearsal)
+    used = torch.zeros(64, dtype=torch.float64, device=dev)
+    used[local] = 1.0
+    if world > 1:
+        dist.all_reduce(used, op=dist.ReduceOp.MAX)
+    n_devices = int(used.sum().item())
     mach = abi.MACH_DETAILED if args.machinery == "detailed" else abi.MACH_SIMPLIFIED
     cfg = abi.ast_config(args.collav, machinery=mach)
     cfg.lanes_per_env = args.lpe
@@ -329,18 +403,20 @@ def main():
     c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
     sac = None
     if args.sac_steps > 0:
-        sac = bench_sac(dev, world, dist.group.WORLD if world > 1 else None, args.sac_steps, args.sac_batch)
+        if args.sac_global_batch % world:
+            raise SystemExit(f"--sac-global-batch {args.sac_global_batch} is not a multiple of {world} ranks")
+        sac = bench_sac(dev, world, dist.group.WORLD if world > 1 else None, args.sac_steps,
+                        args.sac_global_batch // world)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure
-            nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-            nthreads = min(nthreads, 16)
-            cpu = cpu_baseline(cfg, args.cpu_baseline_seconds, nthreads)
+            cpu = cpu_baseline(cfg, args.cpu_baseline_seconds, host_threads()[0], N)
         line = {
             "metric": "batched env-steps/sec (two-ship AST)",
             "value": value,
             "unit": "env-ticks/s",
-            "n_gpus": world,
+            "n_gpus": n_devices,
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -354,7 +430,8 @@ def main():
                        "envs_per_gpu": N, "global_envs": N * world, "collav": args.collav,
                        "machinery": args.machinery, "slice_ticks": args.slice, "lanes_per_env": args.lpe or 16,
                        "mode": args.mode,
-                       "parallelism": f"env-shard x{world}"},
+                       "parallelism": f"env-shard x{world}" + (f" on {n_devices} device(s), {args.dist_backend}"
+                                                                  if n_devices != world else "")},
             "decisions_per_s": all_dec / elapsed,
             "env_ticks_per_decision": all_ticks / max(all_dec, 1),
             "decision_log": {"cap": dlog_cap, "max_per_launch": int(dlog_max.item())} if args.mode == "table" else None,

@@ -11,6 +11,23 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "liboracle.so")
 
 _lib = None
+_native = None
+
+
+def native_lib():
+    """The same oracle source compiled for the host it runs on (-O3 -march=native, OpenMP), into a
+    private temp dir: the CPU baseline of bench.py (CPU-baseline plan). The shipped
+    oracle/liboracle.so stays -O2 generic x86-64 because it is built in one container and run on
+    another machine."""
+    global _native
+    if _native is None:
+        import tempfile
+        out = os.path.join(tempfile.mkdtemp(prefix="oracle_native_"), "liboracle_native.so")
+        subprocess.check_call(["gcc", "-O3", "-march=native", "-fPIC", "-fopenmp", "-ffp-contract=off",
+                               "-fno-fast-math", "-shared", "-I" + os.path.join(ROOT, "include"), "-o", out,
+                               os.path.join(ROOT, "oracle", "shipsim_oracle.c"), "-lm"])
+        _native = _bind(C.CDLL(out))
+    return _native
 
 
 def lib():
@@ -19,7 +36,12 @@ def lib():
         src = os.path.join(ROOT, "oracle", "shipsim_oracle.c")
         if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
             subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
-        L = C.CDLL(LIB)
+        _lib = _bind(C.CDLL(LIB))
+    return _lib
+
+
+def _bind(L):
+    if True:
         P = C.c_void_p
         dp = np.ctypeslib.ndpointer(np.float64, flags="C")
         fp = np.ctypeslib.ndpointer(np.float32, flags="C")
@@ -54,8 +76,7 @@ def lib():
         L.oracle_reward_terms.argtypes = [C.c_int, dp, dp]
         L.oracle_termination_reward.restype = C.c_double
         L.oracle_termination_reward.argtypes = [C.c_double, C.c_double, ip]
-        _lib = L
-    return _lib
+    return L
 
 
 LOG_COLS = ["time", "north", "east", "yaw_deg", "rudder_deg", "u", "v", "r_deg", "shaft_rpm", "thrust", "e_ct",
@@ -145,23 +166,23 @@ class OracleEnv:
         return np.stack([north[:n], east[:n]], 1)
 
 
-def c2_run(cfg, init, max_ticks=4000, trace=True, n_threads=1):
+def c2_run(cfg, init, max_ticks=4000, trace=True, n_threads=1, L=None):
     init = np.ascontiguousarray(init, np.float64)
     n = init.shape[0]
     tr = np.zeros((n, max_ticks, 12)) if trace else None
     fin = np.zeros((n, 7))
-    T = lib().oracle_c2_run(C.byref(cfg), n, init, max_ticks, tr.ctypes.data if trace else None, fin, n_threads)
+    T = (L or lib()).oracle_c2_run(C.byref(cfg), n, init, max_ticks, tr.ctypes.data if trace else None, fin, n_threads)
     return (tr[:, :T] if trace else None), fin
 
 
-def ast_rollouts(cfg, actions, n_threads=1):
+def ast_rollouts(cfg, actions, n_threads=1, L=None):
     actions = np.ascontiguousarray(actions, np.float32)
     n, d = actions.shape
     ticks = np.zeros(n, np.int32)
     dec = np.zeros(n, np.int32)
     ret = np.zeros(n)
     bits = np.zeros(n, np.uint32)
-    total = lib().oracle_ast_rollouts(C.byref(cfg), n, d, actions, ticks, dec, ret, bits, n_threads)
+    total = (L or lib()).oracle_ast_rollouts(C.byref(cfg), n, d, actions, ticks, dec, ret, bits, n_threads)
     return total, ticks, dec, ret, bits
 
 
