@@ -1,0 +1,35 @@
+"""Content hash of the native sources: __graft_entry__.build() compiles it into each library
+(shipsim_build_info / sacf_build_info) and rebuilds whenever it changes; the ctypes bindings refuse a
+library whose embedded hash differs from the sources next to it (a stale build)."""
+import hashlib
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_HERE)
+
+SOURCES = {
+    "shipsim": ["ast_sac_amd/csrc/shipsim_kernels.hip", "ast_sac_amd/csrc/shipsim_device.hpp", "include/shipsim.h"],
+    "sacfused": ["ast_sac_amd/csrc/sac_kernels.hip", "include/sac_fused.h"],
+}
+
+
+# code-generation flags of both libraries (include paths are added by the build and not hashed, so the
+# hash is the same in every checkout of the same sources)
+HIPFLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shared", "-std=c++17"]
+
+
+def source_hash(lib):
+    h = hashlib.sha256()
+    for rel in SOURCES[lib]:
+        with open(os.path.join(_ROOT, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read() + b"\0")
+    h.update(" ".join(HIPFLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def check_library(lib, info, path, explicit):
+    """Raise if the library at `path` (build info string `info`) was not built from these sources."""
+    want = source_hash(lib)
+    if info.split()[-1] != want and not explicit:
+        raise RuntimeError(f"{path} was built from other sources ({info!r}, sources hash {want}): rebuild with "
+                           f"python -c 'import __graft_entry__ as g; g.build()'")

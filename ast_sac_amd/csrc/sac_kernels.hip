@@ -1154,6 +1154,11 @@ extern "C" {
 
 int32_t sacf_abi_version(void) { return SACF_ABI_VERSION; }
 
+#ifndef SACF_SRC_HASH
+#define SACF_SRC_HASH "unknown"
+#endif
+const char* sacf_build_info(void) { return "sacfused gfx950 HIP src " SACF_SRC_HASH; }
+
 int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** out) {
   if (!out) return SACF_EINVAL;
   *out = nullptr;

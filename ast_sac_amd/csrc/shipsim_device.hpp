@@ -69,6 +69,9 @@ struct Params {
   float action_low, action_high;
   int32_t normalize_action, pad2_;
   float initial_states[8];           // env.py:107-109
+  // host-evaluated sin/cos of uniform angles: wind_direction (algebraic wind force of the AST
+  // kernels) and the IW sampler's omega (env.py:151-161)
+  double wind_sin, wind_cos, iw_cos, iw_sin;
 };
 
 // Map edges (obstacle.py PolygonObstacle). Stored as a flat read-only device table; every lane
@@ -122,6 +125,22 @@ __device__ __forceinline__ double floor_mod(double a, double b) {
 }
 // sbmpc_misc.py:20-32
 __device__ __forceinline__ double wrap_pmpi(double x) { return -kPi + floor_mod(x - (-kPi), kPi - (-kPi)); }
+
+// DPP moves of a double / int inside a 16-lane row (an AST env at LPE 16 is exactly one row, and
+// every lane of an env shares its control flow, so every source lane is active)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) { return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false); }
+constexpr int kDppRowBcast = 0x150;  // row_newbcast:k (0x150 + k): lane k of the row to the whole row
+constexpr int kDppRowRor4 = 0x124;   // row_ror:4
+constexpr int kDppRowRor8 = 0x128;   // row_ror:8
+constexpr int kDppQuadXor2 = 0x4E;   // quad_perm [2,3,0,1]
 
 // swap a double with the partner lane (lane ^ 1) — DPP quad_perm [1,0,3,2]
 __device__ __forceinline__ double pair_swap(double x) {
@@ -211,16 +230,12 @@ __device__ __forceinline__ void wind_force_alg(const ShipConst& c, const Params&
 
 // update_differentials (ShipModelAST :882-888 / SimpleShipModel run_colav :399-404):
 // three_dof_kinematics :519-528, shaft_eq + thrust (ship_engine.py:403-443), three_dof_kinetics
-// :834-864 with rudder :866-880. `ctrl` is the engine throttle (detailed) or thrust force (simplified).
-// ALGW: wind by wind_force_alg ((wsin, wcos) = sin/cos(wind_direction)), one sincos per tick.
-template <bool PAIRED = false, bool ALGW = false>
-__device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params& P, const Ship& s, double ctrl,
-                                               double delta, bool detailed, bool odd = false, double wsin = 0.0,
-                                               double wcos = 1.0) {
+// :834-864 with rudder :866-880. `ctrl` is the engine throttle (detailed) or thrust force (simplified);
+// (sy, cy) = sin/cos(yaw), tau = get_wind_force.
+__device__ __forceinline__ Deriv differentials_body(const ShipConst& c, const Params& P, const Ship& s, double ctrl,
+                                                    double delta, bool detailed, double sy, double cy,
+                                                    const double tau[3]) {
   Deriv d;
-  double sy, cy, sw = 0.0, cw = 1.0;
-  if (ALGW) sincos(s.yaw, &sy, &cy);
-  else sincos2<PAIRED>(s.yaw, P.wind_dir - s.yaw, odd, sy, cy, sw, cw);
   d.dn = cy * s.u + (-sy) * s.v + 0 * s.r;
   d.de = sy * s.u + cy * s.v + 0 * s.r;
   d.dyaw = 0 * s.u + 0 * s.v + 1 * s.r;
@@ -240,9 +255,6 @@ __device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params&
   double vc1 = -sy * P.vc_n + cy * P.vc_e;
   double fv = -c.c_rudder_v * delta * (s.u - vc0);
   double fr = -c.c_rudder_r * delta * (s.u - vc0);
-  double tau[3];
-  if (ALGW) wind_force_alg(c, P, s, sy, cy, wsin, wcos, tau);
-  else wind_force<PAIRED>(c, P, s, sw, cw, odd, tau);
   double u_r = s.u - vc0;
   double v_r = s.v - vc1;
   double x_g = 0.0;
@@ -263,6 +275,31 @@ __device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params&
   d.dv = c.inv_m1 * f1;
   d.dr = c.inv_m2 * f2;
   return d;
+}
+
+// differentials with the reference's angle-form wind force (PAIRED: sub-lane pairs share the
+// sincos calls) or, with ALGW, the algebraic one ((wsin, wcos) = sin/cos(wind_direction)).
+template <bool PAIRED = false, bool ALGW = false>
+__device__ __forceinline__ Deriv differentials(const ShipConst& c, const Params& P, const Ship& s, double ctrl,
+                                               double delta, bool detailed, bool odd = false, double wsin = 0.0,
+                                               double wcos = 1.0) {
+  double sy, cy, sw = 0.0, cw = 1.0;
+  if (ALGW) sincos(s.yaw, &sy, &cy);
+  else sincos2<PAIRED>(s.yaw, P.wind_dir - s.yaw, odd, sy, cy, sw, cw);
+  double tau[3];
+  if (ALGW) wind_force_alg(c, P, s, sy, cy, wsin, wcos, tau);
+  else wind_force<PAIRED>(c, P, s, sw, cw, odd, tau);
+  return differentials_body(c, P, s, ctrl, delta, detailed, sy, cy, tau);
+}
+
+// differentials of the AST kernels: (sy, cy) = sin/cos(yaw) carried from the previous integration
+// step (the kernels evaluate it once per tick, after integrating, and reuse it for the encounter
+// angle of the reward), algebraic wind force with the host-evaluated sin/cos(wind_direction).
+__device__ __forceinline__ Deriv differentials_sc(const ShipConst& c, const Params& P, const Ship& s, double ctrl,
+                                                  double delta, bool detailed, double sy, double cy) {
+  double tau[3];
+  wind_force_alg(c, P, s, sy, cy, P.wind_sin, P.wind_cos, tau);
+  return differentials_body(c, P, s, ctrl, delta, detailed, sy, cy, tau);
 }
 
 // integrate_differentials :890-901 (EulerInt.integrate utils.py:50) + int.next_time :42

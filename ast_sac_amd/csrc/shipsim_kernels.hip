@@ -57,7 +57,9 @@ struct DevState {
   __host__ __device__ int32_t* dec_flags() const { return (int32_t*)ev(13); }  // DF_* (sliced stepping)
   __host__ __device__ double* legacy_states() const { return (double*)ev(14); }  // [env][4] legacy self.states
   __host__ __device__ int32_t* legacy_flags() const { return (int32_t*)ev(15); }  // 1: still the f32 initial_states
-  static constexpr int kEnvArrays = 16;
+  __host__ __device__ int32_t* dec_ticks() const { return (int32_t*)ev(16); }  // ticks of the decision in progress
+  int32_t* nonfinite;  // device counter: envs flagged SHIPSIM_EV_NONFINITE (read by shipsim_synchronize)
+  static constexpr int kEnvArrays = 17;
   static constexpr int kShipArrays = 22;
 };
 #ifdef SHIPSIM_PHASE_TIMING
@@ -166,17 +168,15 @@ __device__ __forceinline__ const ShipConst* stage_consts(const Params& P, ShipCo
   return lds;
 }
 
-// one controlled ship tick: autopilot -> speed control -> store -> update -> integrate -> next_time
-// (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339)
-// PAIRED: sub-lanes 2k / 2k+1 of the ship share the batched sincos calls (odd = this lane is 2k+1)
-// ALGW: algebraic wind force (differentials), (wsin, wcos) = sin/cos(wind_direction)
-template <bool DETAILED, bool REC = false, bool PAIRED = false, bool ALGW = false>
-__device__ __forceinline__ void control_and_integrate(const ShipConst& c, const Params& P, Ship& s,
-                                                      const double* __restrict__ rn, const double* __restrict__ re,
-                                                      double offset, double speed_factor, double mach_dt,
-                                                      int simple_collav_flag /*0 none, 1 rl(-15deg), 2 noniw(+15)*/,
-                                                      bool imminent, double* row = nullptr, double* fuel = nullptr,
-                                                      bool odd = false, double wsin = 0.0, double wcos = 1.0) {
+// control half of one ship tick: autopilot -> speed control -> (simple collav) -> store
+// (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339); returns (ctrl, rudder)
+template <bool DETAILED, bool REC>
+__device__ __forceinline__ void control_and_store(const ShipConst& c, const Params& P, Ship& s,
+                                                  const double* __restrict__ rn, const double* __restrict__ re,
+                                                  double offset, double speed_factor, double mach_dt,
+                                                  int simple_collav_flag /*0 none, 1 rl(-15deg), 2 noniw(+15)*/,
+                                                  bool imminent, double* row, double* fuel, double& ctrl_out,
+                                                  double& rudder_out) {
   const double N = s.n, E = s.e, H = s.yaw, U = s.u;
   if (next_wpt_advance(c, s, N, E)) {
     s.next_wpt += 1;
@@ -211,8 +211,44 @@ __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const 
       row[SHIPSIM_TS_TIME_LIST] = s.time;
     }
   }
+  ctrl_out = ctrl;
+  rudder_out = rudder;
+}
+
+// one controlled ship tick: autopilot -> speed control -> store -> update -> integrate -> next_time
+// with the reference's angle-form wind force (PAIRED: sub-lanes 2k / 2k+1 share the batched sincos
+// calls, odd = this lane is 2k+1) or the algebraic one (ALGW, (wsin, wcos) = sin/cos(wind_direction)).
+// The legacy per-tick kernel and the C2 single-ship kernel use this form.
+template <bool DETAILED, bool REC = false, bool PAIRED = false, bool ALGW = false>
+__device__ __forceinline__ void control_and_integrate(const ShipConst& c, const Params& P, Ship& s,
+                                                      const double* __restrict__ rn, const double* __restrict__ re,
+                                                      double offset, double speed_factor, double mach_dt,
+                                                      int simple_collav_flag, bool imminent, double* row = nullptr,
+                                                      double* fuel = nullptr, bool odd = false, double wsin = 0.0,
+                                                      double wcos = 1.0) {
+  double ctrl, rudder;
+  control_and_store<DETAILED, REC>(c, P, s, rn, re, offset, speed_factor, mach_dt, simple_collav_flag, imminent, row,
+                                   fuel, ctrl, rudder);
   Deriv d = differentials<PAIRED, ALGW>(c, P, s, ctrl, rudder, DETAILED, odd, wsin, wcos);
   integrate(s, d, P.dt, mach_dt, DETAILED);
+}
+
+// the same tick in the AST kernels (step, decision stream, reset / init_step): algebraic wind force
+// and sin/cos(yaw) carried in (sy, cy) — valid for s.yaw on entry, refreshed after the integration
+// step, so one sincos per ship-tick serves both the kinematics and the reward's encounter angle.
+template <bool DETAILED, bool REC = false>
+__device__ __forceinline__ void control_and_integrate_sc(const ShipConst& c, const Params& P, Ship& s,
+                                                         const double* __restrict__ rn,
+                                                         const double* __restrict__ re, double offset,
+                                                         double speed_factor, double mach_dt, int simple_collav_flag,
+                                                         bool imminent, double* row, double* fuel, double& sy,
+                                                         double& cy) {
+  double ctrl, rudder;
+  control_and_store<DETAILED, REC>(c, P, s, rn, re, offset, speed_factor, mach_dt, simple_collav_flag, imminent, row,
+                                   fuel, ctrl, rudder);
+  Deriv d = differentials_sc(c, P, s, ctrl, rudder, DETAILED, sy, cy);
+  integrate(s, d, P.dt, mach_dt, DETAILED);
+  sincos(s.yaw, &sy, &cy);
 }
 
 // store_last_simulation_data (ship_model.py:946-957) of a stopped ship: the previous row repeated
@@ -601,8 +637,10 @@ __global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, 
   const double mach_dt = P.mach_dt_reset;
   // init_step (env.py:307-339): one control + integrate tick, no collision avoidance
   double fuel[3] = {0.0, 0.0, 0.0};  // machinery reset restores the fuel accumulators (ship_engine.py:468-481)
-  control_and_integrate<DETAILED, REC>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false, REC ? T.ship_row(q, 0) : nullptr,
-                                       fuel);
+  double sy, cy;
+  sincos(s.yaw, &sy, &cy);
+  control_and_integrate_sc<DETAILED, REC>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false,
+                                          REC ? T.ship_row(q, 0) : nullptr, fuel, sy, cy);
   store_ship(S, q, s);
   if (REC) {
     for (int k = 0; k < 3; ++k) T.fuel[(size_t)q * 3 + k] = fuel[k];
@@ -708,12 +746,77 @@ struct ChainArgs {
   int32_t log_cap;
 };
 
+// A copy of the state table whose base pointer the compiler cannot see through: addresses derived
+// from it are recomputed where they are used (a few SALU) instead of being hoisted out of the tick
+// loop and kept alive in SGPRs for the whole launch (the big kernels are at the SGPR limit).
+__device__ __forceinline__ DevState opaque(const DevState& S) {
+  DevState o = S;
+  asm volatile("" : "+s"(o.base));
+  return o;
+}
+
+// lanes of the env: value of lane k of the env (LPE 16: the env is one DPP row)
+template <int LPE, int K>
+__device__ __forceinline__ double env_lane_d(double x, int env_lane0) {
+  if constexpr (LPE == 16) return dpp_d<kDppRowBcast + K>(x);
+  else return shfl_d(x, env_lane0 + K);
+}
+template <int LPE, int K>
+__device__ __forceinline__ int env_lane_i(int x, int env_lane0) {
+  if constexpr (LPE == 16) return dpp_i<kDppRowBcast + K>(x);
+  else return __shfl(x, env_lane0 + K, 64);
+}
+
+// min of a double / OR of an int over the sub-lanes of one ship (same lane parity) of a 16-lane env:
+// quad_perm [2,3,0,1], row_ror 4, row_ror 8 (parity-preserving) — DPP only, no LDS permute
+template <int LPE>
+__device__ __forceinline__ void ship_reduce(double& d2, int& gri) {
+  if constexpr (LPE == 16) {
+    d2 = py_min(d2, dpp_d<kDppQuadXor2>(d2));
+    gri |= dpp_i<kDppQuadXor2>(gri);
+    d2 = py_min(d2, dpp_d<kDppRowRor4>(d2));
+    gri |= dpp_i<kDppRowRor4>(gri);
+    d2 = py_min(d2, dpp_d<kDppRowRor8>(d2));
+    gri |= dpp_i<kDppRowRor8>(gri);
+  } else {
+#pragma unroll
+    for (int m = 2; m < LPE; m <<= 1) {
+      d2 = py_min(d2, xor_shfl_d(d2, m));
+      gri |= __shfl_xor(gri, m, 64);
+    }
+  }
+}
+
+// |beta| > 165° of get_distance_and_encounter_type (compute_distance.py:16-40): beta =
+// wrap(atan2(dy, dx) - heading) and cos(beta) = (dx cos h + dy sin h) / dist, so the overtaking
+// sector is c < cos(165°)·dist with c = dx·cos h + dy·sin h (sin/cos(h) carried from the test ship's
+// integration step). Within 1e-9·dist of the boundary (and at dist = 0) the reference expression
+// itself decides, so the boolean equals the reference's.
+__device__ __forceinline__ bool overtaking_sector(double dx, double dy, double dist, double sh, double ch, double h) {
+  constexpr double kCos165 = -0.96592582628906831;  // cos(165°)
+  const double c = dx * ch + dy * sh;
+  const double m = c - kCos165 * dist;
+  if (fabs(m) > 1e-9 * dist) return m < 0;
+  const double beta = floor_mod((atan2(dy, dx) - h) + kPi, 2 * kPi) - kPi;
+  return fabs(beta) > 165.0 * (kPi / 180.0);
+}
+
+// env flag bits exchanged between the two ships of an env every tick
+#define XF_GROUND 1
+#define XF_END 2
+#define XF_OUTSIDE 4
+#define XF_ROA 8
+#define XF_NONFINITE 16
+
 // MultiShipRLEnv.step (env.py:624-773), sliced: every env of the launch ticks (_step :563-622)
 // until its decision point (RoA + one tick, or done) or until `max_ticks` ticks have run in this
 // call; an env that paused resumes in the next call without consuming an action. Envs waiting
 // for a decision consume action[env] first (IW sampling). LPE lanes per env: lane & 1 selects the
 // ship, the LPE/2 sub-lanes of a ship hold identical state, run the control chain redundantly and
 // split the map queries (edges for the coastline distance, hull corners for grounding).
+// CHAIN (shipsim_run_table): decisions from the device table, chained and episodes reset in place.
+// An env whose state goes non-finite completes its decision at once, done, with
+// SHIPSIM_EV_NONFINITE | SHIPSIM_EV_TERMINAL, and is counted in S.nonfinite (shipsim_synchronize).
 template <bool DETAILED, int COLLAV, int LPE, bool REC, bool CHAIN = false>
 __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K, Traj T,
                                                       const float* __restrict__ action,
@@ -723,7 +826,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
                                                       const ChainArgs CH) {
   static_assert(!(REC && CHAIN), "trajectory recording runs the per-decision step only");
   constexpr int NSUB = LPE / 2;
-  static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 64, "LPE must be a power of two in [2, 64]");
+  static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 16, "LPE must be a power of two in [2, 16]");
+  constexpr bool SIMPLE = COLLAV == SHIPSIM_COLLAV_SIMPLE;
   __shared__ ShipConst lds_sc[2];
   __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
@@ -762,17 +866,21 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 
   Ship s;
   load_ship(S, qc, s);
+  double sy, cy;  // sin/cos(s.yaw), refreshed by every integration step
+  sincos(s.yaw, &sy, &cy);
   int sampling_count = S.sampling_count()[envc];
   double travel_dist = S.travel_dist()[envc], travel_time = S.travel_time()[envc], acc = S.acc()[envc];
   double n_base = S.n_base()[envc], e_base = S.e_base()[envc];
   double p_last = S.p_last()[envc], chi_last = S.chi_last()[envc];
   double mach_dt = S.mach_dt()[envc];
-  float st4[4];
-  for (int i = 0; i < 4; ++i) st4[i] = S.states4()[envc * 4 + i];
+  float st4[4] = {0.f, 0.f, 0.f, 0.f};  // self.states (read by the simple collision check only)
+  if (SIMPLE)
+    for (int i = 0; i < 4; ++i) st4[i] = S.states4()[envc * 4 + i];
   uint32_t snap_bits = S.snap_bits()[envc];
   int dflags = S.dec_flags()[envc];
   bool have_iw = dflags & DF_HAVE_IW;
   int phase = (dflags >> DF_PHASE_SHIFT) & 3;
+  int dec_ticks = S.dec_ticks()[envc];  // ticks of the decision in progress (across calls)
 
   float ns[8];
   for (int i = 0; i < 8; ++i) ns[i] = S.next_obs8()[envc * 8 + i];
@@ -783,9 +891,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     for (int k = 0; k < 3; ++k) fuel[k] = T.fuel[(size_t)qc * 3 + k];
   }
   double out_r = 0.0;
-  bool out_done = false, ready = false;
+  bool out_done = false, ready = false, stalled = false;
   uint32_t out_bits = 0;
+  int out_ticks = 0;
   int ticks = 0;
+  int n_nonfinite = 0;
 
 #ifdef SHIPSIM_DEBUG_ENV
   if (env == SHIPSIM_DEBUG_ENV && valid)
@@ -797,12 +907,13 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
     phase = 0;
     have_iw = false;
+    dec_ticks = 0;
     if (sampling_count < P.max_sampling) {
       sampling_count += 1;
       float tn = (float)tan((double)sa);  // np.tan on the float32 scoping angle
       double l_s = fabs(P.AB_seg * (double)tn);
-      double e_s = l_s * cos(P.omega_iw);
-      double n_s = l_s * sin(P.omega_iw);
+      double e_s = l_s * P.iw_cos;
+      double n_s = l_s * P.iw_sin;
       if (sa > 0) e_s *= -1;
       else n_s *= -1;
       double iw_n = n_base + n_s, iw_e = e_base + e_s;
@@ -830,6 +941,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
                     ~(uint32_t)(SHIPSIM_EV_TEST_STOP | SHIPSIM_EV_OBS_STOP);
         out_bits = snap_bits;
         out_done = true;
+        out_ticks = 0;
         ready = true;
       } else {
         acc = 0;
@@ -859,8 +971,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     }
     load_segment(s, rn, re);
     mach_dt = P.mach_dt_reset;
-    control_and_integrate<DETAILED, false, (NSUB >= 2)>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false, nullptr,
-                                                         nullptr, (sub & 1) != 0);  // init_step
+    sincos(s.yaw, &sy, &cy);
+    control_and_integrate_sc<DETAILED, false>(c, P, s, rn, re, 0.0, 1.0, mach_dt, 0, false, nullptr, nullptr, sy,
+                                              cy);  // init_step
     sampling_count = 0;
     travel_dist = 0; travel_time = 0; acc = 0;
     n_base = P.n_base0; e_base = P.e_base0;
@@ -869,16 +982,20 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     phase = 0;
     have_iw = false;
   };
-  // a decision just completed (ready): record it, reset if the episode ended (done, or n_dec decisions
+  // A decision just completed (ready): record it, reset if the episode ended (done, or n_dec decisions
   // = the rollout's max_path_length), consume the next table action. A sampling failure completes the
-  // new decision at once, hence the (bounded) loop.
+  // new decision at once (no tick), hence the loop; after kChainBurst such back-to-back decisions (a
+  // table whose actions all fail their sampling) the env stops for this launch with the last decision
+  // recorded and the next one pending (DF_AWAITING): the wave keeps ticking its other envs and the
+  // next launch resumes exactly there, so results do not depend on the burst bound.
+  constexpr int kChainBurst = 8;
   auto chain_next = [&]() __attribute__((always_inline)) {
-    for (int guard = 0; guard < 8 && ready; ++guard) {
+    for (int burst = 0; ready; ++burst) {
       if (CH.log && lie == 0 && log_n < CH.log_cap) {
         double* rec = CH.log + ((size_t)env * CH.log_cap + log_n) * SHIPSIM_DECLOG_COLS;
         rec[SHIPSIM_DL_REWARD] = out_r; rec[SHIPSIM_DL_EVENTS] = (double)out_bits;
         rec[SHIPSIM_DL_DONE] = out_done ? 1.0 : 0.0; rec[SHIPSIM_DL_EPISODE] = (double)ep_i;
-        rec[SHIPSIM_DL_DECISION] = (double)dec_i; rec[SHIPSIM_DL_TICKS] = (double)ticks;
+        rec[SHIPSIM_DL_DECISION] = (double)dec_i; rec[SHIPSIM_DL_TICKS] = (double)out_ticks;
         for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS + i] = (double)ns[i];
       }
       log_n += 1;
@@ -890,10 +1007,17 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       } else {
         dec_i += 1;
       }
-      if (lie == 0)
-        for (int i = 0; i < 8; ++i) S.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
+      if (lie == 0) {
+        const DevState So = opaque(S);
+        for (int i = 0; i < 8; ++i) So.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
+      }
       ready = false;
       out_done = false;
+      if (burst + 1 >= kChainBurst) {
+        stalled = true;  // next decision pending: resumed by the next launch
+        running = false;
+        break;
+      }
       decision_prologue(table_action());
     }
   };
@@ -933,9 +1057,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       }
       double pb = 1.0, cb = 0.0;
       sbmpc_cooperative(need && sub == 0, in, n_samp, P.sbmpc_dt, pb, cb);
-      pb = shfl_d(pb, env_lane0);
-      cb = shfl_d(cb, env_lane0);
-      const int need0 = __shfl((int)need, env_lane0, 64);
+      pb = env_lane_d<LPE, 0>(pb, env_lane0);
+      cb = env_lane_d<LPE, 0>(cb, env_lane0);
+      const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
       sb_active = need0;
       if (going) {
         if (need0) { p_last = pb; chi_last = cb; }
@@ -957,14 +1081,13 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         const double prev_log_n = s.log_n, prev_log_e = s.log_e;
         const double U = s.u;
         bool imminent = false;
-        if (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) {  // check_condition.py:130 on float32 self.states
+        if (SIMPLE && is_test) {  // check_condition.py:130 on float32 self.states
           float dn = st4[0] - st4[2], de = st4[1] - st4[3];
           imminent = (dn * dn + de * de) < 9000000.0f;
         }
-        control_and_integrate<DETAILED, REC, (NSUB >= 2)>(c, P, s, rn, re, -off, sf, mach_dt,
-                                                          (COLLAV == SHIPSIM_COLLAV_SIMPLE && is_test) ? 1 : 0,
-                                                          imminent, (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr,
-                                                          fuel, (sub & 1) != 0);
+        control_and_integrate_sc<DETAILED, REC>(c, P, s, rn, re, -off, sf, mach_dt, (SIMPLE && is_test) ? 1 : 0,
+                                                imminent, (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel,
+                                                sy, cy);
         my_speed_out = U;
         if (!is_test) {  // travel tracker (env.py:527-534, Q6)
           double tn = s.log_n - prev_log_n, te = s.log_e - prev_log_e;
@@ -990,15 +1113,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       }
 #endif
     }
-    int gri = gr ? 1 : 0;
-#pragma unroll
-    for (int m = 2; m < LPE; m <<= 1) {
-      d2 = py_min(d2, xor_shfl_d(d2, m));
-      gri |= __shfl_xor(gri, m, 64);
-    }
+    int gri = gr ? XF_GROUND : 0;
+    ship_reduce<LPE>(d2, gri);
     const double my_ground = sqrt(d2);
     PT_MARK(2);
-    bool my_end = false, my_outside = false, my_roa = false;
+    bool my_end = false, my_outside = false, my_roa = false, my_nf = false;
     if (going) {
       my_end = sqrt((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e)) <= 200;
       double margin = c.l_ship / 2;
@@ -1006,15 +1125,20 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
                    (s.e < P.min_east + margin || s.e > P.max_east - margin);
       double rdn = s.n - s.wp_n, rde = s.e - s.wp_e;  // is_reach_radius_of_acceptance (obstacle ship)
       my_roa = (rdn * rdn + rde * rde) < P.roa2;
+      // a NaN / Inf anywhere in the dynamic state poisons this sum (boundary error contract)
+      my_nf = !isfinite(((s.n + s.e) + (s.yaw + s.u)) + ((s.v + s.r) + (s.omega + s.e_ct_int)));
     }
-    const int my_flags = gri | (my_end ? 2 : 0) | (my_outside ? 4 : 0) | (my_roa ? 8 : 0);
+    const int my_flags = gri | (my_end ? XF_END : 0) | (my_outside ? XF_OUTSIDE : 0) | (my_roa ? XF_ROA : 0) |
+                         (my_nf ? XF_NONFINITE : 0);
     const int o_flags = pair_swap_i(my_flags);
     const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
     const double o_ect = pair_swap(s.log_ect), o_ground = pair_swap(my_ground);
     const double o_speed = pair_swap(my_speed_out), o_dtravel = pair_swap(dtravel), o_dtime = pair_swap(dtime);
     const double o_time = pair_swap(s.time);
+    const double o_sy = pair_swap(sy), o_cy = pair_swap(cy);
     if (going) {
       const double Tn = is_test ? s.n : o_n, Te = is_test ? s.e : o_e, Th = is_test ? s.yaw : o_yaw;
+      const double Tsh = is_test ? sy : o_sy, Tch = is_test ? cy : o_cy;
       const double On = is_test ? o_n : s.n, Oe = is_test ? o_e : s.e, Oyaw = is_test ? o_yaw : s.yaw;
       const double Tect = is_test ? s.log_ect : o_ect, Oect = is_test ? o_ect : s.log_ect;
       const double Tground = is_test ? my_ground : o_ground, Oground = is_test ? o_ground : my_ground;
@@ -1026,16 +1150,15 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       // next_states (env.py:582-591) and self.states
       ns[0] = (float)Tn; ns[1] = (float)Te; ns[2] = (float)Tect;
       ns[3] = (float)On; ns[4] = (float)Oe; ns[5] = (float)Oyaw; ns[6] = (float)Ospeed; ns[7] = (float)Oect;
-      st4[0] = ns[0]; st4[1] = ns[1]; st4[2] = ns[3]; st4[3] = ns[4];
+      if (SIMPLE) { st4[0] = ns[0]; st4[1] = ns[1]; st4[2] = ns[3]; st4[3] = ns[4]; }
       // get_reward_and_env_info (reward_function.py:59-270)
       const bool is_collision = ((Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe)) < 2500.0;
-      const bool is_tg = Tf & 1, is_og = Of & 1;
+      const bool is_tg = Tf & XF_GROUND, is_og = Of & XF_GROUND;
       const bool is_tnav = fabs(Tect) > 3000;
       const bool is_onav = (travel_dist > P.AB_seg * 2) || (travel_time > INFINITY) || (fabs(Oect) > 500);
       double dx = On - Tn, dy = Oe - Te;
       double dist = sqrt(dx * dx + dy * dy);
-      double beta = floor_mod((atan2(dy, dx) - Th) + kPi, 2 * kPi) - kPi;
-      const bool enc_ok = !(fabs(beta) > 165.0 * (kPi / 180.0));  // head-on or crossing (Q5)
+      const bool enc_ok = !overtaking_sector(dx, dy, dist, Tsh, Tch, Th);  // head-on or crossing (Q5)
       // the five shaped terms of reward_designs.py:33-55 (RewardDesign4 / 3): one exp each,
       // evaluated by five lanes of the env in one call when LPE >= 8, then gathered
       const double xv[5] = {dist, Tground, fabs(Tect), Oground, fabs(Oect)};
@@ -1048,8 +1171,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         const double tj = (j == 2) ? tg[2] : (j == 4) ? tg[4] : 0.0;
         const double oj = (j == 0) ? of[0] : (j == 1) ? of[1] : (j == 2) ? of[2] : (j == 3) ? of[3] : of[4];
         const double ej = exp(-((xj - tj) * (xj - tj)) / oj);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) ex[k] = shfl_d(ej, env_lane0 + k);
+        ex[0] = env_lane_d<LPE, 0>(ej, env_lane0);
+        ex[1] = env_lane_d<LPE, 1>(ej, env_lane0);
+        ex[2] = env_lane_d<LPE, 2>(ej, env_lane0);
+        ex[3] = env_lane_d<LPE, 3>(ej, env_lane0);
+        ex[4] = env_lane_d<LPE, 4>(ej, env_lane0);
       } else {
 #pragma unroll
         for (int k = 0; k < 5; ++k) ex[k] = exp(-((xv[k] - tg[k]) * (xv[k] - tg[k])) / of[k]);
@@ -1072,7 +1198,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         }
         r = o;
       }
-      const bool t6 = Tf & 2, t7 = Tf & 4, t8 = Of & 2, t9 = Of & 4;
+      const bool t6 = Tf & XF_END, t7 = Tf & XF_OUTSIDE, t8 = Of & XF_END, t9 = Of & XF_OUTSIDE;
       const bool t10 = Ttime > P.sim_time;
       uint32_t bits = (is_collision ? SHIPSIM_EV_COLLISION : 0) | (is_tg ? SHIPSIM_EV_TEST_GROUNDING : 0) |
                       (is_tnav ? SHIPSIM_EV_TEST_NAV_FAILURE : 0) | (is_og ? SHIPSIM_EV_OBS_GROUNDING : 0) |
@@ -1086,7 +1212,13 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       if (test_stop) bits |= SHIPSIM_EV_TEST_STOP;
       if (obs_stop) bits |= SHIPSIM_EV_OBS_STOP;
       if (obs_stop && !terminal && !is_test) s.stop = 1;
-      const bool combined_done = terminal || (test_stop && !terminal);
+      bool combined_done = terminal || (test_stop && !terminal);
+      const bool nonfinite = (my_flags | o_flags) & XF_NONFINITE;
+      if (nonfinite) {  // not a reference outcome: the env ends its episode here, flagged
+        bits |= SHIPSIM_EV_NONFINITE | SHIPSIM_EV_TERMINAL;
+        combined_done = true;
+        n_nonfinite += 1;
+      }
       if (REC) {  // RewardTracker.update (reward_function.py:181-186) + env.py:613-620 animation lists
         double* er = (lie == 0) ? T.env_row(env, rec_t - 1) : nullptr;
         if (er) {
@@ -1104,9 +1236,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       // ---- env.py:700-771 decision logic ----
       acc += r;
       ticks += 1;
-      bool finish = false;
+      dec_ticks += 1;
+      bool finish = nonfinite;
       if (phase == 0) {
-        const bool roa = Of & 8;
+        const bool roa = Of & XF_ROA;
         if (combined_done) finish = true;
         else if (roa) {
           if (have_iw) phase = 1;
@@ -1128,6 +1261,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         out_r = acc;
         out_done = combined_done;
         out_bits = bits;
+        out_ticks = dec_ticks;
         snap_bits = bits;
         ready = true;
       }
@@ -1151,7 +1285,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     printf("[dbg] env %d lie %d end: ready %d ticks %d sc %d n_base %f phase %d have_iw %d\n", env, lie, (int)ready,
            ticks, sampling_count, n_base, phase, (int)have_iw);
 #endif
-  if (sub == 0) store_ship(S, qc, s);
+  const DevState So = opaque(S);  // addresses recomputed here, not carried through the loop
+  if (sub == 0) store_ship(So, qc, s);
   if (REC) {
     if (sub == 0)
       for (int k = 0; k < 3; ++k) T.fuel[(size_t)qc * 3 + k] = fuel[k];
@@ -1162,18 +1297,22 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     CH.dec_idx[env] = dec_i;
     if (CH.decisions) CH.decisions[env] = n_decided;
     if (CH.log_len) CH.log_len[env] = log_n;
-    S.mach_dt()[env] = mach_dt;
+    So.mach_dt()[env] = mach_dt;
   }
   if (lie == 0) {
-    S.sampling_count()[env] = sampling_count;
-    S.travel_dist()[env] = travel_dist; S.travel_time()[env] = travel_time; S.acc()[env] = acc;
-    S.n_base()[env] = n_base; S.e_base()[env] = e_base;
-    S.p_last()[env] = p_last; S.chi_last()[env] = chi_last;
-    for (int i = 0; i < 4; ++i) S.states4()[env * 4 + i] = st4[i];
+    So.sampling_count()[env] = sampling_count;
+    So.travel_dist()[env] = travel_dist; So.travel_time()[env] = travel_time; So.acc()[env] = acc;
+    So.n_base()[env] = n_base; So.e_base()[env] = e_base;
+    So.p_last()[env] = p_last; So.chi_last()[env] = chi_last;
+    if (SIMPLE)
+      for (int i = 0; i < 4; ++i) So.states4()[env * 4 + i] = st4[i];
     if (ready)
-      for (int i = 0; i < 8; ++i) S.next_obs8()[env * 8 + i] = ns[i];
-    S.snap_bits()[env] = snap_bits;
-    S.dec_flags()[env] = (ready ? DF_AWAITING : 0) | (have_iw ? DF_HAVE_IW : 0) | (phase << DF_PHASE_SHIFT);
+      for (int i = 0; i < 8; ++i) So.next_obs8()[env * 8 + i] = ns[i];
+    So.snap_bits()[env] = snap_bits;
+    So.dec_flags()[env] = ((ready || stalled) ? DF_AWAITING : 0) | (have_iw ? DF_HAVE_IW : 0) |
+                          (phase << DF_PHASE_SHIFT);
+    So.dec_ticks()[env] = dec_ticks;
+    if (n_nonfinite) atomicAdd(So.nonfinite, n_nonfinite);
     if (ready) {
       if (reward_out) reward_out[env] = out_r;
       if (done_out) done_out[env] = out_done ? 1 : 0;
@@ -1383,6 +1522,8 @@ struct shipsim_handle {
   void* dev_block;
   void* const_block;
   void* fuel_block;  // trajectory fuel accumulators
+  int32_t* nonfinite_dev;   // device counter (DevState::nonfinite)
+  int32_t nonfinite_seen;   // its value at the last shipsim_synchronize
   Traj T;
   size_t dev_bytes;
   int ever_reset;
@@ -1533,8 +1674,11 @@ int shipsim_debug_phase_cycles(unsigned long long* out8) {
 }
 #endif
 
+#ifndef SHIPSIM_SRC_HASH
+#define SHIPSIM_SRC_HASH "unknown"
+#endif
 const char* shipsim_build_info(void) {
-  return "shipsim gfx950 HIP (fp64, lane-pair AST kernel, wave-cooperative SBMPC) built " __DATE__ " " __TIME__;
+  return "shipsim gfx950 HIP (fp64, lane-pair AST kernel, wave-cooperative SBMPC) src " SHIPSIM_SRC_HASH;
 }
 
 static void fill_ship_common(shipsim_ship_config* s, double n, double e, double yaw, double u) {
@@ -1833,6 +1977,8 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
   P.roa2 = cfg->env_radius_of_acceptance * cfg->env_radius_of_acceptance;
   P.sbmpc_tf = cfg->sbmpc_tf;
   P.sbmpc_dt = cfg->sbmpc_dt;
+  P.wind_sin = sin(cfg->wind_direction);
+  P.wind_cos = cos(cfg->wind_direction);
   P.action_low = cfg->action_low;
   P.action_high = cfg->action_high;
   P.normalize_action = cfg->normalize_action;
@@ -1848,6 +1994,8 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
     double AB_alpha = atan2(ABe, ABn);
     double AB_beta = M_PI / 2 - AB_alpha;
     P.omega_iw = M_PI / 2 - AB_beta;
+    P.iw_cos = cos(P.omega_iw);  // np.cos / np.sin of the scalar omega (env.py:226-227): glibc, as NumPy
+    P.iw_sin = sin(P.omega_iw);
     P.n_base0 = P.AB_seg_n + o->route_north[0];
     P.e_base0 = P.AB_seg_e + o->route_east[0];
     P.initial_states[0] = (float)cfg->ship[0].initial_north_position_m;
@@ -1947,6 +2095,13 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
   }
   h->dev_bytes = bytes;
   h->S.base = (char*)h->dev_block;
+  e = hipMalloc(&h->nonfinite_dev, sizeof(int32_t));
+  if (e != hipSuccess) {
+    *out = h;
+    return fail(h, SHIPSIM_EHIP, "hipMalloc(counter): %s", hipGetErrorString(e));
+  }
+  h->S.nonfinite = h->nonfinite_dev;
+  (void)hipMemsetAsync(h->nonfinite_dev, 0, sizeof(int32_t), h->stream);
   e = hipMemsetAsync(h->dev_block, 0, bytes, h->stream);
   if (e != hipSuccess) {
     *out = h;
@@ -1969,6 +2124,7 @@ int shipsim_destroy(shipsim_handle* h) {
     if (h->dev_block) (void)hipFree(h->dev_block);
     if (h->const_block) (void)hipFree(h->const_block);
     if (h->fuel_block) (void)hipFree(h->fuel_block);
+    if (h->nonfinite_dev) (void)hipFree(h->nonfinite_dev);
   }
   delete h;
   return SHIPSIM_OK;
@@ -2159,7 +2315,20 @@ int shipsim_synchronize(shipsim_handle* h) {
   DeviceGuard g(h->device);
   if (h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
   else HIPCHK(h, hipDeviceSynchronize());
+  if (h->nonfinite_dev) {
+    int32_t n = 0;
+    HIPCHK(h, hipMemcpy(&n, h->nonfinite_dev, sizeof(n), hipMemcpyDeviceToHost));
+    if (n > h->nonfinite_seen) {
+      const int32_t fresh = n - h->nonfinite_seen;
+      h->nonfinite_seen = n;
+      return fail(h, SHIPSIM_ENONFINITE,
+                  "%d env decision(s) ended on a non-finite ship state since the last synchronize (%d in all): "
+                  "flagged SHIPSIM_EV_NONFINITE, done", fresh, n);
+    }
+  }
   return SHIPSIM_OK;
 }
+
+int32_t shipsim_nonfinite_count(const shipsim_handle* h) { return h ? h->nonfinite_seen : -1; }
 
 }  // extern "C"

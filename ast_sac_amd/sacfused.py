@@ -10,7 +10,7 @@ import torch  # noqa: F401  (HIP runtime first)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACFUSED_LIB") or os.path.join(_HERE, "lib", "libsacfused.so")
 ABI_VERSION = 1
-EXPORTED_SYMBOLS = ("sacf_abi_version", "sacf_create", "sacf_destroy", "sacf_last_error", "sacf_set_stream",
+EXPORTED_SYMBOLS = ("sacf_abi_version", "sacf_build_info", "sacf_create", "sacf_destroy", "sacf_last_error", "sacf_set_stream",
                     "sacf_param_count", "sacf_target_count", "sacf_stats_count", "sacf_bind", "sacf_sync_params",
                     "sacf_set_replay", "sacf_grads", "sacf_apply")
 _lib = None
@@ -53,6 +53,12 @@ def load_library(path=LIB_PATH):
     L.sacf_apply.argtypes = [P]
     if L.sacf_abi_version() != ABI_VERSION:
         raise SacFusedError("libsacfused ABI mismatch")
+    L.sacf_build_info.restype = C.c_char_p
+    from .build_hash import check_library
+    try:
+        check_library("sacfused", L.sacf_build_info().decode(), path, explicit="SACFUSED_LIB" in os.environ)
+    except RuntimeError as e:
+        raise SacFusedError(str(e)) from None
     _lib = L
     return L
 

@@ -21,6 +21,10 @@ class ShipSimError(RuntimeError):
     pass
 
 
+class ShipSimNonFiniteError(ShipSimError):
+    """shipsim_synchronize: env decisions ended on a NaN/Inf ship state (SHIPSIM_EV_NONFINITE)."""
+
+
 def load_library(path=LIB_PATH):
     global _lib
     if _lib is not None:
@@ -45,12 +49,19 @@ def load_library(path=LIB_PATH):
     L.shipsim_get_state.argtypes = [P, C.c_int32, P]
     L.shipsim_set_state.argtypes = [P, C.c_int32, P]
     L.shipsim_synchronize.argtypes = [P]
+    L.shipsim_nonfinite_count.argtypes = [P]
+    L.shipsim_nonfinite_count.restype = C.c_int32
     L.shipsim_set_trajectory.argtypes = [P, P, P, C.c_int32, P]
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
     if L.shipsim_abi_version() != abi.ABI_VERSION:
         raise ShipSimError(f"ABI mismatch: library {L.shipsim_abi_version()} vs binding {abi.ABI_VERSION}")
+    from .build_hash import check_library
+    try:
+        check_library("shipsim", L.shipsim_build_info().decode(), path, explicit="SHIPSIM_LIB" in os.environ)
+    except RuntimeError as e:
+        raise ShipSimError(str(e)) from None
     _lib = L
     return L
 
@@ -58,7 +69,8 @@ def load_library(path=LIB_PATH):
 EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_default_config", "shipsim_create",
                     "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
-                    "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table")
+                    "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
+                    "shipsim_nonfinite_count")
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
@@ -223,7 +235,16 @@ class ShipSim:
         self.traj = None
 
     def synchronize(self):
-        self._check(self.L.shipsim_synchronize(self.h), "shipsim_synchronize")
+        """Wait for the handle's stream; raises ShipSimNonFiniteError when env decisions ended on a
+        non-finite ship state since the previous call (those envs report SHIPSIM_EV_NONFINITE, done)."""
+        rc = self.L.shipsim_synchronize(self.h)
+        if rc == abi.ENONFINITE:
+            raise ShipSimNonFiniteError(self.L.shipsim_last_error(self.h).decode())
+        self._check(rc, "shipsim_synchronize")
+
+    def nonfinite_count(self):
+        """Decisions flagged SHIPSIM_EV_NONFINITE since create (as of the last synchronize)."""
+        return int(self.L.shipsim_nonfinite_count(self.h))
 
 
 def sbmpc_eval(requests, tf=1000.0, dt=20.0, device="cuda"):

@@ -13,7 +13,8 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
+ENONFINITE = -5  # shipsim_synchronize status (include/shipsim.h)
 MAX_ROUTE = 16
 MAX_POLYS = 16
 MAX_VERTS = 128

@@ -63,6 +63,8 @@ typedef struct sacf_config {
 typedef struct sacf_handle sacf_handle;
 
 int32_t sacf_abi_version(void);
+/* "sacfused gfx950 HIP src <hash>": the content hash of the sources this library was built from */
+const char* sacf_build_info(void);
 int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** out);
 int sacf_destroy(sacf_handle* h);
 const char* sacf_last_error(const sacf_handle* h);

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 3
+#define SHIPSIM_ABI_VERSION 4
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -39,6 +39,7 @@ extern "C" {
 #define SHIPSIM_EHIP -2     /* HIP runtime failure */
 #define SHIPSIM_ESTATE -3   /* call not valid in the current state (e.g. step before reset) */
 #define SHIPSIM_ENOMEM -4
+#define SHIPSIM_ENONFINITE -5 /* shipsim_synchronize: an env's ship state went NaN/Inf (see SHIPSIM_EV_NONFINITE) */
 
 /* environment kinds */
 #define SHIPSIM_KIND_SINGLE 0  /* one ship per env, no termination (config C2; run_simplified_model loop) */
@@ -74,7 +75,9 @@ extern "C" {
 #define SHIPSIM_EV_TERMINAL (1u << 16)          /* env_info['terminal'] */
 #define SHIPSIM_EV_TEST_STOP (1u << 17)         /* env_info['test_ship_stop'] */
 #define SHIPSIM_EV_OBS_STOP (1u << 18)          /* env_info['obs_ship_stop'] */
-#define SHIPSIM_EV_NONFINITE (1u << 24)         /* build-only: a state went NaN/Inf */
+#define SHIPSIM_EV_NONFINITE (1u << 24)         /* build-only, not a reference outcome: a ship state went
+                                                   NaN/Inf in this decision; the decision ends at once with
+                                                   done = 1 and SHIPSIM_EV_TERMINAL (boundary error contract) */
 
 /* One ship: ShipConfiguration (ship_model.py:20), SimulationConfiguration (:45), rudder / machinery
  * (ship_engine.py:121,160), controller gains (controllers.py:16-38), LOS (LOS_guidance.py:15) and
@@ -351,7 +354,7 @@ int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double
 #define SHIPSIM_DL_DONE 2     /* combined_done */
 #define SHIPSIM_DL_EPISODE 3  /* ep_idx of the decision */
 #define SHIPSIM_DL_DECISION 4 /* dec_idx of the decision */
-#define SHIPSIM_DL_TICKS 5    /* ticks run in the call when the decision completed */
+#define SHIPSIM_DL_TICKS 5    /* _step ticks of the decision (across launches; 0 for a sampling failure) */
 #define SHIPSIM_DL_OBS 6      /* 8 columns: the observation returned */
 int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
                       int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
@@ -381,8 +384,11 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
 #define SHIPSIM_LT_OBS_NAV_FAILURE (1u << 9)
 int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_t* done_out, uint32_t* status_out);
 
-/* Block until all work queued on the handle's stream is done. */
+/* Block until all work queued on the handle's stream is done. Returns SHIPSIM_ENONFINITE (message in
+ * shipsim_last_error) when env decisions ended on a non-finite ship state since the previous call. */
 int shipsim_synchronize(shipsim_handle* h);
+/* Decisions flagged SHIPSIM_EV_NONFINITE since create, as of the last shipsim_synchronize. */
+int32_t shipsim_nonfinite_count(const shipsim_handle* h);
 
 #ifdef __cplusplus
 }

@@ -3,9 +3,11 @@ machinery, dt 4 s, the decision stream of shipsim_run_table in 128-tick launches
 it, in 128-tick launches and in one 4096-tick launch, the bench default), checked two ways:
   - every env: size-independent invariants of the decision log (finite records, episode / decision
     counters in order, each episode ends on done or on the 9th decision, ticks per launch bounded);
-  - every 16th env: decision by decision against the CPU oracle replaying the same episodes
-    (reward, termination bits, done, obs), with the oracle's few-ulp initial-condition variants
-    (gpu_harness.run_oracle_variants) as the acceptance envelope.
+  - every 4th env: decision by decision against the CPU oracle replaying the same episodes
+    (reward, termination bits, done, obs, and the decision's tick count exactly), with the oracle's
+    few-ulp initial-condition variants (gpu_harness.run_oracle_variants) as the acceptance
+    envelope; at most 10 % of the checked envs may need a perturbed variant (the fraction is
+    printed).
 Needs an MI355X."""
 import copy
 
@@ -51,22 +53,24 @@ def _episodes(rows):
         while len(eps) <= e:
             eps.append([])
         eps[e].append((r[abi.DL_OBS:abi.DL_OBS + 8].astype(np.float32), r[abi.DL_REWARD], bool(r[abi.DL_DONE]),
-                       int(r[abi.DL_EVENTS]), -1))
+                       int(r[abi.DL_EVENTS]), int(r[abi.DL_TICKS])))
     return eps
 
 
 def _match(g_eps, o_rec, rtol=1e-5):
-    """g_eps (possibly ending in an unfinished episode) against the oracle's episodes; ticks are not
-    compared (the log holds ticks per launch, not per decision)."""
+    """g_eps (possibly ending in an unfinished episode) against the oracle's episodes: bits, done and
+    the decision's tick count exactly, obs and reward within rtol."""
     worst = 0.0
     for k, gd in enumerate(g_eps):
         od = o_rec[k][1]
         if len(gd) > len(od) or (k < len(g_eps) - 1 and len(gd) != len(od)):
             return np.inf
         for g, o in zip(gd, od):
-            if (g[3] & 0x7FFFF) != (o[3] & 0x7FFFF) or g[2] != o[2]:
+            if (g[3] & 0x7FFFF) != (o[3] & 0x7FFFF) or g[2] != o[2] or g[4] != o[4]:
                 return np.inf
             e = max(float(rel_err(g[0][None], o[0][None]).max()), float(abs(g[1] - o[1]) / (abs(o[1]) + 1e-6)))
+            if e > rtol:
+                return e
             worst = max(worst, e)
     return worst
 
@@ -102,15 +106,16 @@ def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach):
         total_dec += len(rows)
     assert total_dec == int(log_len.sum())
 
-    # oracle, every 16th env
-    idx = np.arange(0, N, 16)
+    # oracle, every 4th env
+    idx = np.arange(0, N, 4)
     tables = [[a_norm[k % N_EPS, :, i] for k in range(int(log[i, log_len[i] - 1, abi.DL_EPISODE]) + 1)] for i in idx]
     g_all = [_episodes(log[i, :log_len[i]]) for i in idx]
     orc = H.run_oracle(cfg, tables)
-    worst, bad = 0.0, []
+    worst, bad, perturbed = 0.0, [], 0
     for j, i in enumerate(idx):
         w = _match(g_all[j], orc[j][0])
         if not w <= 1e-5:
+            perturbed += 1
             for eps in H.PERTURBATIONS[1:]:  # the oracle's own few-ulp envelope (gpu_harness)
                 c = copy.deepcopy(cfg)
                 c.ship[0].initial_north_position_m *= 1 + eps
@@ -122,5 +127,10 @@ def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach):
             bad.append(int(i))
         else:
             worst = max(worst, w)
+    frac = perturbed / len(idx)
+    print(f"\n[{collav} {mach} slice {SLICE}] {len(idx)} envs vs oracle, {sum(len(e) for e in g_all)} decisions; "
+          f"matched only by a perturbed oracle run: {perturbed} ({100 * frac:.2f} %); off the oracle: {len(bad)}; "
+          f"worst rel err {worst:.2e}")
     assert not bad, f"envs off the oracle: {bad[:20]}"
+    assert frac <= 0.10, f"{perturbed} of {len(idx)} envs matched only by a perturbed oracle run"
     assert worst <= 1e-5
