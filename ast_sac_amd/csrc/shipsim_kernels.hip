@@ -1527,6 +1527,7 @@ struct shipsim_handle {
   Traj T;
   size_t dev_bytes;
   int ever_reset;
+  int lpe;  // lanes per AST env of the step / stream kernels (lanes_per_env)
   char err[512];
 };
 
@@ -1627,13 +1628,23 @@ struct DeviceGuard {
   }
 };
 
-static int lanes_per_env(const shipsim_config* cfg) {
+// Lanes per AST env. The kernels hold ~350-450 registers per lane, so a SIMD runs one wave and the
+// throughput is (envs per wave) / (per-tick wave latency): pick the fewest lanes per env that still
+// put a wave on every SIMD of the device (n_envs * LPE / 64 >= SIMDs), in [4, 16]. Measured on
+// MI355X (profiles/round2_lpe_sweep.md): 4096 envs -> 16, 8192 -> 8 (1.5-1.8x over 16), 65536 -> 4
+// (2.2-3.1x). cfg->lanes_per_env (or $SHIPSIM_LPE) overrides; results are identical at every LPE.
+static int lanes_per_env(const shipsim_config* cfg, int n_envs, int device) {
   int lpe = cfg->lanes_per_env;
   if (lpe <= 0) {
     const char* e = getenv("SHIPSIM_LPE");
-    lpe = e ? atoi(e) : 16;
+    lpe = e ? atoi(e) : 0;
   }
-  if (lpe != 2 && lpe != 4 && lpe != 8 && lpe != 16) lpe = 16;
+  if (lpe == 2 || lpe == 4 || lpe == 8 || lpe == 16) return lpe;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  const long simds = 4L * cus;
+  lpe = 4;
+  while (lpe < 16 && (long)n_envs * lpe < 64L * simds) lpe *= 2;
   return lpe;
 }
 
@@ -1952,6 +1963,7 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
   h->device = device;
   h->stream = (hipStream_t)stream;
   DeviceGuard g(device);
+  h->lpe = lanes_per_env(cfg, n_envs, device);
   Params& P = h->P;
   memset(&P, 0, sizeof(P));
   const int ns = cfg->n_ships;
@@ -2132,6 +2144,7 @@ int shipsim_destroy(shipsim_handle* h) {
 
 const char* shipsim_last_error(const shipsim_handle* h) { return h ? h->err : "null handle"; }
 int32_t shipsim_num_envs(const shipsim_handle* h) { return h ? h->P.n_envs : -1; }
+int32_t shipsim_lanes_per_env(const shipsim_handle* h) { return h ? h->lpe : -1; }
 
 int shipsim_reset(shipsim_handle* h, const uint8_t* env_mask, float* obs_out) {
   if (!h || !h->dev_block) return SHIPSIM_EINVAL;
@@ -2161,7 +2174,7 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
   if (!action) return fail(h, SHIPSIM_EINVAL, "step: action is NULL");
   if (!h->ever_reset) return fail(h, SHIPSIM_ESTATE, "step before reset");
   DeviceGuard g(h->device);
-  const int lpe = lanes_per_env(&h->cfg);
+  const int lpe = h->lpe;
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
 #define LAUNCH(D, CA) launch_step<D, CA>(h, lpe, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, ready_out)
   switch (h->P.collav) {
@@ -2202,10 +2215,20 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
   ChainArgs ch;
   ch.table = table; ch.n_eps = n_eps; ch.n_dec = n_dec; ch.ep_idx = ep_idx; ch.dec_idx = dec_idx;
   ch.decisions = decisions_out; ch.log = log; ch.log_len = log_len; ch.log_cap = log_cap;
-  const int threads = 64, blocks = (h->P.n_envs * 16 + threads - 1) / threads;
-#define CHAINED(D, CA)                                                                                                 \
-  hipLaunchKernelGGL((ast_step_kernel<D, CA, 16, false, true>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, \
-                     h->K, h->T, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out, nullptr, ch)
+  // lanes per env: 16 (default) or 8 / 4 (more envs per wave when the handle holds more envs than
+  // the chip has SIMD slots at 16; identical results)
+  const int lpe = (h->lpe == 8 || h->lpe == 4) ? h->lpe : (h->lpe == 2 ? 4 : 16);
+  const int threads = 64, blocks = (h->P.n_envs * lpe + threads - 1) / threads;
+#define CHAINED_L(D, CA, LPE)                                                                                          \
+  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, true>), dim3(blocks), dim3(threads), 0, h->stream, h->P,      \
+                     h->S, h->K, h->T, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out,    \
+                     nullptr, ch)
+#define CHAINED(D, CA)                              \
+  do {                                              \
+    if (lpe == 8) CHAINED_L(D, CA, 8);              \
+    else if (lpe == 4) CHAINED_L(D, CA, 4);         \
+    else CHAINED_L(D, CA, 16);                      \
+  } while (0)
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
   switch (h->P.collav) {
     case SHIPSIM_COLLAV_SBMPC: if (det) CHAINED(true, SHIPSIM_COLLAV_SBMPC); else CHAINED(false, SHIPSIM_COLLAV_SBMPC); break;
@@ -2213,6 +2236,7 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
     default: if (det) CHAINED(true, SHIPSIM_COLLAV_NONE); else CHAINED(false, SHIPSIM_COLLAV_NONE); break;
   }
 #undef CHAINED
+#undef CHAINED_L
   HIPCHK(h, hipGetLastError());
   return SHIPSIM_OK;
 }

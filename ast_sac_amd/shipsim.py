@@ -43,6 +43,8 @@ def load_library(path=LIB_PATH):
     L.shipsim_last_error.restype = C.c_char_p
     L.shipsim_num_envs.argtypes = [P]
     L.shipsim_num_envs.restype = C.c_int32
+    L.shipsim_lanes_per_env.argtypes = [P]
+    L.shipsim_lanes_per_env.restype = C.c_int32
     L.shipsim_reset.argtypes = [P, P, P]
     L.shipsim_step.argtypes = [P, P, P, C.c_int32, P, P, P, P, P, P]
     L.shipsim_tick.argtypes = [P, C.c_int32, P]
@@ -70,7 +72,7 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
                     "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
                     "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
-                    "shipsim_nonfinite_count")
+                    "shipsim_nonfinite_count", "shipsim_lanes_per_env")
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
@@ -107,6 +109,7 @@ class ShipSim:
                     self.L.shipsim_destroy(h)
                 raise ShipSimError(f"shipsim_create failed ({rc}): {msg}")
         self.h = h
+        self.lanes_per_env = int(self.L.shipsim_lanes_per_env(h))
 
     def _check(self, rc, what):
         if rc:

@@ -56,7 +56,7 @@ def parse():
                    help="table: shipsim_run_table, decisions chained and episodes reset inside the kernel (the "
                         "C3 open-loop decision stream); step: shipsim_step slices + host-side table lookup and "
                         "masked shipsim_reset between calls (the RL collector's call pattern)")
-    p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library default)")
+    p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library choice from envs per GPU)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c2", action="store_true", help="skip the configs[1] single-ship secondary line")
@@ -428,7 +428,7 @@ def main():
             "config": {"workload": "C3: two-ship AST envs (ShipModelAST PTI machinery, sampled-route LOS, "
                                    "reward_designs), dt 4 s",
                        "envs_per_gpu": N, "global_envs": N * world, "collav": args.collav,
-                       "machinery": args.machinery, "slice_ticks": args.slice, "lanes_per_env": args.lpe or 16,
+                       "machinery": args.machinery, "slice_ticks": args.slice, "lanes_per_env": sim.lanes_per_env,
                        "mode": args.mode,
                        "parallelism": f"env-shard x{world}" + (f" on {n_devices} device(s), {args.dist_backend}"
                                                                   if n_devices != world else "")},

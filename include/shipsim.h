@@ -179,8 +179,8 @@ typedef struct shipsim_config {
   int32_t poly_start[SHIPSIM_MAX_POLYS + 1];
   double poly_east[SHIPSIM_MAX_VERTS];
   double poly_north[SHIPSIM_MAX_VERTS];
-  /* performance knob (no effect on results): device lanes per AST env, 2/4/8/16; 0 = default 16
-   * (or $SHIPSIM_LPE) */
+  /* performance knob (no effect on results): device lanes per AST env, 2/4/8/16 (the decision
+   * stream runs 4/8/16); 0 = $SHIPSIM_LPE or automatic (shipsim_lanes_per_env) */
   int32_t lanes_per_env;
   int32_t reserved[7];
 } shipsim_config;
@@ -242,6 +242,9 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
 int shipsim_destroy(shipsim_handle* h);
 const char* shipsim_last_error(const shipsim_handle* h);
 int32_t shipsim_num_envs(const shipsim_handle* h);
+/* Lanes per AST env the step / stream kernels run at (config lanes_per_env, or chosen at create from
+ * n_envs and the device's SIMD count; a performance knob only, results are identical). */
+int32_t shipsim_lanes_per_env(const shipsim_handle* h);
 
 /* MultiShipRLEnv.reset(): every env with env_mask[i] != 0 (NULL = all) is reset and placed with
  * init_step (one control + integrate tick, env.py:297); obs_out (N x 8 float32, device, may be NULL)

@@ -86,3 +86,20 @@ def test_chained_decisions_equal_host_driven_loop(collav, mach):
     # episodes ended by done and by the 9-decision cap both occur
     eps = np.concatenate([c[:, 3] for c in chain])
     assert eps.max() >= 2
+
+
+@pytest.mark.parametrize("collav,lpe", [("sbmpc", 8), ("none", 8), ("sbmpc", 4), ("simple", 4)])
+def test_stream_lanes_per_env_bitwise(collav, lpe):
+    """The decision stream at 8 / 4 lanes per env (more envs per wave) equals the 16-lane kernel bit
+    for bit: same per-lane arithmetic, only the split of the map queries / exps over sub-lanes moves."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    cfg = abi.ast_config(collav)
+    N = 160
+    table = _table(2, cfg.max_sampling_frequency, N, seed=99)
+    ref, t_ref = _chained(cfg, N, table, 200, 6)
+    cfg.lanes_per_env = lpe
+    got, t_got = _chained(cfg, N, table, 200, 6)
+    assert t_got == t_ref
+    for i in range(N):
+        np.testing.assert_array_equal(got[i], ref[i], err_msg=f"{collav} lpe {lpe} env {i}")
