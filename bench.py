@@ -39,6 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector spec (the resource the env kernel actually spends)
 ALGO_BYTES_PER_ENV_TICK = 616  # C3/C5 detailed dynamics, one obstacle ship
 
 
@@ -60,7 +61,8 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c2", action="store_true", help="skip the configs[1] single-ship secondary line")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round1_pmc_traffic.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round2_pmc_traffic.json"))
+    p.add_argument("--pmc-fp64-json", default=os.path.join(ROOT, "profiles", "round2_pmc_fp64.json"))
     p.add_argument("--sac-steps", type=int, default=300, help="timed SAC grad steps (0 = skip the SAC line)")
     p.add_argument("--sac-global-batch", type=int, default=256,
                    help="SAC batch summed over all ranks (runner: 256); each rank samples global / N rows "
@@ -392,14 +394,33 @@ def main():
         value = all_ticks / elapsed
         ticks_per_launch = local_ticks / args.steps
         achieved = ALGO_BYTES_PER_ENV_TICK * ticks_per_launch / (kmean * 1e-3) / 1e9
-        traffic = None
-        try:
-            with open(args.pmc_json) as f:
-                pmc = json.load(f)
-            if pmc.get("collav") == args.collav and pmc.get("envs") == N and pmc.get("slice") == args.slice:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
+        def pmc_record(path):
+            # a separate rocprofv3 --pmc pass of this same bench command (profiles/), used only when it was
+            # taken on this workload
+            try:
+                with open(path) as f:
+                    rec = json.load(f)
+            except (OSError, ValueError):
+                return None
+            same = rec.get("collav") == args.collav and rec.get("envs") == N and rec.get("slice") == args.slice
+            return rec if same else None
+        pmc = pmc_record(args.pmc_json)
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        fp64 = pmc_record(args.pmc_fp64_json)
+        fp64_valu = None
+        if fp64:
+            flops = fp64["fp64_flops_per_launch"]
+            tflops = flops / (kmean * 1e-3) / 1e12
+            fp64_valu = {"flops_per_launch": flops, "achieved_tflops": tflops, "peak_tflops": FP64_VALU_PEAK_TFLOPS,
+                         "frac": tflops / FP64_VALU_PEAK_TFLOPS,
+                         "flops_per_env_tick_all_lanes": flops / ticks_per_launch,
+                         "flops_per_env_tick_distinct": flops / ticks_per_launch * 2 / sim.lanes_per_env,
+                         "fp64_wave_instructions_per_env_tick": fp64["fp64_wave_instructions_per_launch"]
+                         / ticks_per_launch,
+                         "source": os.path.relpath(args.pmc_fp64_json, ROOT),
+                         "note": "SQ_INSTS_VALU_FLOPS_FP64(+_TRANS) per launch / this run's mean launch time; "
+                                 "'distinct' counts each ship's control chain once (the LPE/2 sub-lanes of a "
+                                 "ship repeat it)"}
     c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
     sac = None
     if args.sac_steps > 0:
@@ -440,7 +461,7 @@ def main():
                          "kernel": f"ast_step_kernel (avg {kmean:.3f} ms/launch, "
                                    f"{ticks_per_launch:.0f} env-ticks x {ALGO_BYTES_PER_ENV_TICK} B)",
                          "kernel_ms_timed": kmean, "kernel_ms_all_launches": float(all_ms.mean()),
-                         "launches": int(len(all_ms))},
+                         "launches": int(len(all_ms)), "fp64_valu": fp64_valu},
             "cpu_baseline": cpu,
             "sac": sac,
             "c2_single_ship": c2,
