@@ -418,9 +418,10 @@ def main():
                          "fp64_wave_instructions_per_env_tick": fp64["fp64_wave_instructions_per_launch"]
                          / ticks_per_launch,
                          "source": os.path.relpath(args.pmc_fp64_json, ROOT),
-                         "note": "SQ_INSTS_VALU_FLOPS_FP64(+_TRANS) per launch / this run's mean launch time; "
-                                 "'distinct' counts each ship's control chain once (the LPE/2 sub-lanes of a "
-                                 "ship repeat it)"}
+                         "note": "64 lanes x SQ_INSTS_VALU_FLOPS_FP64 (= 2 FMA + ADD + MUL + TRANS f64 wave-"
+                                 "instructions) per launch / this run's mean launch time: the FP64 VALU rate the "
+                                 "kernel issues; 'distinct' counts each ship's chain once (its LPE/2 sub-lanes "
+                                 "repeat it)"}
     c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
     sac = None
     if args.sac_steps > 0:
