@@ -56,7 +56,6 @@ struct ShipConst {
 };
 
 struct Params {
-  ShipConst sc[2];
   int32_t kind, machinery, collav, n_ships;
   int32_t max_sampling, n_envs, n_polys, pad_;
   double dt, sim_time, mach_dt_reset, mach_dt_init;

@@ -85,8 +85,8 @@ enum { SF_N = 0, SF_E, SF_YAW, SF_U, SF_V, SF_R, SF_OMEGA, SF_TIME, SF_ECT, SF_E
        SF_SPD_A, SF_SPD_B, SF_RUDDER, SF_THRUST, SF_LOG_ECT, SF_LOG_N, SF_LOG_E };
 
 struct ConstBuf {
-  // edges [SHIPSIM_MAX_VERTS] | boxes [SHIPSIM_MAX_POLYS] | config routes n/e [2][kMaxRoute] each
-  // | map grid: cell edge masks [gny][gnx] uint64 | cell containment flags [gny][gnx] uint8
+  // edges [SHIPSIM_MAX_VERTS] | boxes [SHIPSIM_MAX_POLYS] | config routes n/e [MAX_SHIPS][kMaxRoute] each
+  // | ShipConst [MAX_SHIPS] | map grid: cell edge masks [gny][gnx] uint64 | cell containment flags [gny][gnx] uint8
   const char* base;
   int32_t n_edges;
   int32_t gnx, gny;            // grid cells (0 = no grid: every query runs over the full map)
@@ -98,9 +98,12 @@ struct ConstBuf {
   __host__ __device__ const double* cfg_route_n() const {
     return (const double*)(base + sizeof(Edge) * SHIPSIM_MAX_VERTS + sizeof(PolyBox) * SHIPSIM_MAX_POLYS);
   }
-  __host__ __device__ const double* cfg_route_e() const { return cfg_route_n() + 2 * kMaxRoute; }
-  static constexpr size_t kBytes = sizeof(Edge) * SHIPSIM_MAX_VERTS + sizeof(PolyBox) * SHIPSIM_MAX_POLYS +
-                                   sizeof(double) * 4 * kMaxRoute;
+  __host__ __device__ const double* cfg_route_e() const { return cfg_route_n() + SHIPSIM_MAX_SHIPS * kMaxRoute; }
+  // per-ship constants (host make_ship_const), [ship] for the 1 + K ships of an env
+  static constexpr size_t kShipsOff = sizeof(Edge) * SHIPSIM_MAX_VERTS + sizeof(PolyBox) * SHIPSIM_MAX_POLYS +
+                                      sizeof(double) * 2 * SHIPSIM_MAX_SHIPS * kMaxRoute;
+  __host__ __device__ const ShipConst* ships() const { return (const ShipConst*)(base + kShipsOff); }
+  static constexpr size_t kBytes = kShipsOff + sizeof(ShipConst) * SHIPSIM_MAX_SHIPS;
   // grid cell of (north, east), or -1 outside the grid / no grid / non-finite position
   __device__ __forceinline__ int cell(double n, double e) const {
     const double fx = floor((e - gx0) * ginv), fy = floor((n - gy0) * ginv);
@@ -158,10 +161,10 @@ __device__ __forceinline__ void store_ship(const DevState& S, int q, const Ship&
   S.next_wpt()[q] = s.next_wpt; S.stop()[q] = s.stop; S.n_route()[q] = s.n_route;
 }
 
-// per-block LDS copy of the two ShipConst (lanes of either parity read one of two addresses)
-__device__ __forceinline__ const ShipConst* stage_consts(const Params& P, ShipConst* lds) {
-  const int nwords = (int)(sizeof(ShipConst) * 2 / sizeof(double));
-  const double* src = reinterpret_cast<const double*>(&P.sc[0]);
+// per-block LDS copy of the ships' ShipConst (lanes of one ship read one address)
+__device__ __forceinline__ const ShipConst* stage_consts(const ConstBuf& K, ShipConst* lds, int n_ships) {
+  const int nwords = (int)(sizeof(ShipConst) * n_ships / sizeof(double));
+  const double* src = reinterpret_cast<const double*>(K.ships());
   double* dst = reinterpret_cast<double*>(lds);
   for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = src[i];
   __syncthreads();
@@ -567,6 +570,73 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
   }
 }
 
+// SBMPC over a do_list of NOB obstacles (sbmpc.py:150-183; env.py:366-370 passes every obstacle ship):
+// per scenario the worst obstacle's cost (cost_i = -1, then every strictly larger cost_k), the scenario
+// with the least worst cost wins (lowest index on ties). Same wave-cooperative layout as
+// sbmpc_cooperative; slots of an env that duplicate its last ship repeat an obstacle, which changes
+// neither the max nor the D_INIT test.
+template <int NOB>
+struct SbMulti {
+  double u_d, chi_d, os_x, os_y, os_v, p_last, chi_last;
+  double ob_x[NOB], ob_y[NOB], ob_psi[NOB], ob_u[NOB], ob_v[NOB], obs_l[NOB], obs_w[NOB];
+};
+
+template <int NOB>
+__device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n_samp, double DT, double& p_best,
+                                        double& chi_best) {
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int scen = lane & 31;
+  uint64_t req = __ballot(need);
+  while (req) {
+    int src0 = __ffsll((unsigned long long)req) - 1;
+    req &= req - 1;
+    int src1 = -1;
+    if (req) {
+      src1 = __ffsll((unsigned long long)req) - 1;
+      req &= req - 1;
+    }
+    int src = half ? src1 : src0;
+    int srcc = src < 0 ? src0 : src;
+    SbIn g;
+    g.u_d = shfl_d(in.u_d, srcc); g.chi_d = shfl_d(in.chi_d, srcc);
+    g.os_x = shfl_d(in.os_x, srcc); g.os_y = shfl_d(in.os_y, srcc); g.os_v = shfl_d(in.os_v, srcc);
+    g.p_last = shfl_d(in.p_last, srcc); g.chi_last = shfl_d(in.chi_last, srcc);
+    double cost = INFINITY;
+    int idx = 64;
+    double worst = -1.0;
+#pragma unroll
+    for (int k = 0; k < NOB; ++k) {
+      g.ob_x = shfl_d(in.ob_x[k], srcc); g.ob_y = shfl_d(in.ob_y[k], srcc); g.ob_psi = shfl_d(in.ob_psi[k], srcc);
+      g.ob_u = shfl_d(in.ob_u[k], srcc); g.ob_v = shfl_d(in.ob_v[k], srcc);
+      g.obs_l = shfl_d(in.obs_l[k], srcc); g.obs_w = shfl_d(in.obs_w[k], srcc);
+      if (src >= 0 && scen < 28) {
+        const double ck = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3);
+        if (ck > worst) worst = ck;
+      }
+    }
+    if (src >= 0 && scen < 28) {
+      cost = worst;
+      idx = scen;
+    }
+    for (int off = 16; off >= 1; off >>= 1) {
+      double oc = shfl_d(cost, lane ^ off);
+      int oi = __shfl(idx, lane ^ off, 64);
+      if (oc < cost || (oc == cost && oi < idx)) { cost = oc; idx = oi; }
+    }
+    int best0 = __shfl(idx, 0, 64);
+    int best1 = __shfl(idx, 32, 64);
+    if (lane == src0) {
+      p_best = p_ca_of(best0 & 3);
+      chi_best = (-30.0 + 10.0 * (best0 >> 2)) * (kPi / 180.0);
+    }
+    if (src1 >= 0 && lane == src1) {
+      p_best = p_ca_of(best1 & 3);
+      chi_best = (-30.0 + 10.0 * (best1 >> 2)) * (kPi / 180.0);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------------------------
@@ -577,7 +647,7 @@ __global__ void init_kernel(const Params P, DevState S, ConstBuf K) {
   if (q >= nq) return;
   const int ship = q % P.n_ships;
   const int env = q / P.n_ships;
-  const ShipConst& c = P.sc[ship];
+  const ShipConst& c = K.ships()[ship];
   Ship s;
   s.n = c.init_n; s.e = c.init_e; s.yaw = c.init_yaw; s.u = c.init_u; s.v = c.init_v; s.r = c.init_r;
   s.omega = c.init_omega; s.time = 0.0;
@@ -612,8 +682,8 @@ __global__ void init_kernel(const Params P, DevState S, ConstBuf K) {
 template <bool DETAILED, bool REC>
 __global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, ConstBuf K, Traj T,
                                                    const uint8_t* mask, float* obs_out) {
-  __shared__ ShipConst lds_sc[2];
-  const ShipConst* SC = stage_consts(P, lds_sc);
+  __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   const int nq = P.n_envs * P.n_ships;
   if (q >= nq) return;
@@ -769,18 +839,22 @@ __device__ __forceinline__ int env_lane_i(int x, int env_lane0) {
 
 // min of a double / OR of an int over the sub-lanes of one ship (same lane parity) of a 16-lane env:
 // quad_perm [2,3,0,1], row_ror 4, row_ror 8 (parity-preserving) — DPP only, no LDS permute
-template <int LPE>
+template <int LPE, int SLOTS = 2>
 __device__ __forceinline__ void ship_reduce(double& d2, int& gri) {
-  if constexpr (LPE == 16) {
-    d2 = py_min(d2, dpp_d<kDppQuadXor2>(d2));
-    gri |= dpp_i<kDppQuadXor2>(gri);
-    d2 = py_min(d2, dpp_d<kDppRowRor4>(d2));
-    gri |= dpp_i<kDppRowRor4>(gri);
+  if constexpr (LPE == 16) {  // sub-lanes of a ship are the lanes of equal index mod SLOTS
+    if constexpr (SLOTS == 2) {
+      d2 = py_min(d2, dpp_d<kDppQuadXor2>(d2));
+      gri |= dpp_i<kDppQuadXor2>(gri);
+    }
+    if constexpr (SLOTS <= 4) {
+      d2 = py_min(d2, dpp_d<kDppRowRor4>(d2));
+      gri |= dpp_i<kDppRowRor4>(gri);
+    }
     d2 = py_min(d2, dpp_d<kDppRowRor8>(d2));
     gri |= dpp_i<kDppRowRor8>(gri);
   } else {
 #pragma unroll
-    for (int m = 2; m < LPE; m <<= 1) {
+    for (int m = SLOTS; m < LPE; m <<= 1) {
       d2 = py_min(d2, xor_shfl_d(d2, m));
       gri |= __shfl_xor(gri, m, 64);
     }
@@ -817,7 +891,10 @@ __device__ __forceinline__ bool overtaking_sector(double dx, double dy, double d
 // CHAIN (shipsim_run_table): decisions from the device table, chained and episodes reset in place.
 // An env whose state goes non-finite completes its decision at once, done, with
 // SHIPSIM_EV_NONFINITE | SHIPSIM_EV_TERMINAL, and is counted in S.nonfinite (shipsim_synchronize).
-template <bool DETAILED, int COLLAV, int LPE, bool REC, bool CHAIN = false>
+// SLOTS (2, 4, 8): ship slots per env. 2 is the reference's two-ship env (lane & 1 = ship); with
+// K > 1 obstacle ships (shipsim_create) ship k sits on the lanes of index k mod SLOTS, and slots past
+// the env's last ship repeat that ship (ghost lanes: same state and arithmetic, never stored).
+template <bool DETAILED, int COLLAV, int LPE, bool REC, bool CHAIN = false, int SLOTS = 2>
 __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K, Traj T,
                                                       const float* __restrict__ action,
                                                       const uint8_t* __restrict__ active_mask, int max_ticks,
@@ -825,14 +902,15 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
                                                       uint32_t* events_out, int32_t* ticks_out, uint8_t* ready_out,
                                                       const ChainArgs CH) {
   static_assert(!(REC && CHAIN), "trajectory recording runs the per-decision step only");
-  constexpr int NSUB = LPE / 2;
+  static_assert(SLOTS == 2 || (LPE == 16 && !REC && COLLAV != SHIPSIM_COLLAV_SIMPLE), "multi-obstacle layout");
+  constexpr int NSUB = LPE / SLOTS;
   static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 16, "LPE must be a power of two in [2, 16]");
   constexpr bool SIMPLE = COLLAV == SHIPSIM_COLLAV_SIMPLE;
-  __shared__ ShipConst lds_sc[2];
+  __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
   __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
-  const ShipConst* SC = stage_consts(P, lds_sc);
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
   for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) {
     const Edge ed = K.edges()[i];
     EdgeX x;
@@ -849,15 +927,19 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const int env = gl / LPE;
   const int lie = gl % LPE;
-  const int ship = lie & 1;
-  const int sub = lie >> 1;
+  const int ship = lie % SLOTS;
+  const int sub = lie / SLOTS;
   const bool is_test = ship == 0;
+  const int nsh = (SLOTS == 2) ? 2 : P.n_ships;
+  const bool ghost = (SLOTS > 2) && ship >= nsh;
+  const int shipc = ghost ? nsh - 1 : ship;  // the ship this lane simulates
+  const bool is_obs1 = shipc == 1;            // "the" obstacle ship (sampling, decisions, observation)
   const int lane = threadIdx.x & 63;
   const int env_lane0 = lane - lie;
   const bool valid = env < P.n_envs;
   const int envc = valid ? env : 0;
-  const int qc = envc * 2 + ship;
-  const ShipConst& c = SC[ship];
+  const int qc = envc * nsh + shipc;
+  const ShipConst& c = SC[shipc];
   double* rn = S.route_n() + (size_t)qc * kMaxRoute;
   double* re = S.route_e() + (size_t)qc * kMaxRoute;
 
@@ -919,7 +1001,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       double iw_n = n_base + n_s, iw_e = e_base + e_s;
       n_base = iw_n + P.AB_seg_n;
       e_base = iw_e + P.AB_seg_e;
-      if (!is_test) {  // auto_pilot.update_route: list.insert(-1, IW); every sub-lane writes the same bytes
+      if (is_obs1) {  // auto_pilot.update_route: list.insert(-1, IW); every sub-lane writes the same bytes
         int L = s.n_route;
         rn[L] = s.end_n; re[L] = s.end_e;
         rn[L - 1] = iw_n; re[L - 1] = iw_e;
@@ -966,8 +1048,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     s.spd_a = 0; s.spd_b = DETAILED ? c.init_shaft_ei : 0.0;
     s.next_wpt = 1; s.stop = 0; s.n_route = c.n_route;
     for (int i = 0; i < c.n_route; ++i) {
-      rn[i] = K.cfg_route_n()[ship * kMaxRoute + i];
-      re[i] = K.cfg_route_e()[ship * kMaxRoute + i];
+      rn[i] = K.cfg_route_n()[shipc * kMaxRoute + i];
+      re[i] = K.cfg_route_e()[shipc * kMaxRoute + i];
     }
     load_segment(s, rn, re);
     mach_dt = P.mach_dt_reset;
@@ -1039,7 +1121,59 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
     double sf = 1.0, off = 0.0;
     bool sb_active = false;
-    if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
+    if (COLLAV == SHIPSIM_COLLAV_SBMPC && SLOTS > 2) {  // do_list of every obstacle ship (env.py:366-370)
+      constexpr int NOB = SLOTS - 1;
+      SbMulti<NOB> in;
+      double obn[NOB], obe[NOB];
+#pragma unroll
+      for (int k = 0; k < NOB; ++k) {
+        double x = 0, y = 0, psi = 0, u = 0, v = 0;
+        switch (k + 1) {  // slot k + 1's first lane of the env row (row broadcast)
+#define SB_GATHER(M)                              \
+  case M:                                         \
+    if constexpr (M < SLOTS) {                    \
+      x = env_lane_d<LPE, M>(s.e, env_lane0);     \
+      y = env_lane_d<LPE, M>(s.n, env_lane0);     \
+      psi = env_lane_d<LPE, M>(s.yaw, env_lane0); \
+      u = env_lane_d<LPE, M>(s.u, env_lane0);     \
+      v = env_lane_d<LPE, M>(s.v, env_lane0);     \
+    }                                             \
+    break;
+          SB_GATHER(1) SB_GATHER(2) SB_GATHER(3) SB_GATHER(4) SB_GATHER(5) SB_GATHER(6) SB_GATHER(7)
+#undef SB_GATHER
+          default: break;
+        }
+        const ShipConst& ck = SC[(k + 1 < nsh) ? k + 1 : nsh - 1];
+        in.ob_x[k] = x; in.ob_y[k] = y; in.ob_psi[k] = -psi; in.ob_u[k] = u; in.ob_v[k] = v;
+        in.obs_l[k] = ck.obs_l_cfg; in.obs_w[k] = ck.obs_w_cfg;
+        obn[k] = y; obe[k] = x;
+      }
+      bool need = false;
+      in.u_d = 0; in.chi_d = 0; in.os_x = 0; in.os_y = 0; in.os_v = 0; in.p_last = 0; in.chi_last = 0;
+      if (going && is_test) {
+        const double los_arg = los_update(c, s, s.n, s.e);
+#pragma unroll
+        for (int k = 0; k < NOB; ++k) {  // sbmpc.py:150-156: active when any obstacle is within D_INIT
+          const double d0 = obe[k] - s.e, d1 = obn[k] - s.n;
+          need = need || sqrt(d0 * d0 + d1 * d1) < 2000.0;
+        }
+        if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
+        in.u_d = c.desired_speed;
+        in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
+        in.p_last = p_last; in.chi_last = chi_last;
+      }
+      double pb = 1.0, cb = 0.0;
+      sbmpc_cooperative_multi<NOB>(need && sub == 0, in, n_samp, P.sbmpc_dt, pb, cb);
+      pb = env_lane_d<LPE, 0>(pb, env_lane0);
+      cb = env_lane_d<LPE, 0>(cb, env_lane0);
+      const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
+      sb_active = need0;
+      if (going) {
+        if (need0) { p_last = pb; chi_last = cb; }
+        else { p_last = 1; chi_last = 0; }
+        if (is_test && need0) { sf = pb; off = cb; }
+      }
+    } else if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
       bool need = false;
       SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       if (going && is_test) {
@@ -1089,7 +1223,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
                                                 imminent, (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel,
                                                 sy, cy);
         my_speed_out = U;
-        if (!is_test) {  // travel tracker (env.py:527-534, Q6)
+        if (is_obs1) {  // travel tracker (env.py:527-534, Q6)
           double tn = s.log_n - prev_log_n, te = s.log_e - prev_log_e;
           dtravel = sqrt(tn * tn + te * te);
           dtime = P.dt;
@@ -1114,7 +1248,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 #endif
     }
     int gri = gr ? XF_GROUND : 0;
-    ship_reduce<LPE>(d2, gri);
+    ship_reduce<LPE, SLOTS>(d2, gri);
     const double my_ground = sqrt(d2);
     PT_MARK(2);
     bool my_end = false, my_outside = false, my_roa = false, my_nf = false;
@@ -1130,33 +1264,68 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     }
     const int my_flags = gri | (my_end ? XF_END : 0) | (my_outside ? XF_OUTSIDE : 0) | (my_roa ? XF_ROA : 0) |
                          (my_nf ? XF_NONFINITE : 0);
-    const int o_flags = pair_swap_i(my_flags);
-    const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
-    const double o_ect = pair_swap(s.log_ect), o_ground = pair_swap(my_ground);
-    const double o_speed = pair_swap(my_speed_out), o_dtravel = pair_swap(dtravel), o_dtime = pair_swap(dtime);
-    const double o_time = pair_swap(s.time);
-    const double o_sy = pair_swap(sy), o_cy = pair_swap(cy);
+    // env-level view of the tick: the ship under test (T), the obstacle ship (O) and the nearest
+    // obstacle ship (C; = O with one obstacle ship)
+    double Tn, Te, Th, Tsh, Tch, Tect, Tground, Ttime, On, Oe, Oyaw, Oect, Oground, Ospeed, Odtravel, Odtime, Cn, Ce;
+    int Tf, Of;
+    bool any_nf;
+    if constexpr (SLOTS == 2) {  // the partner lane (lane ^ 1) holds the other ship
+      const int o_flags = pair_swap_i(my_flags);
+      const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
+      const double o_ect = pair_swap(s.log_ect), o_ground = pair_swap(my_ground);
+      const double o_speed = pair_swap(my_speed_out), o_dtravel = pair_swap(dtravel), o_dtime = pair_swap(dtime);
+      const double o_time = pair_swap(s.time);
+      const double o_sy = pair_swap(sy), o_cy = pair_swap(cy);
+      Tn = is_test ? s.n : o_n; Te = is_test ? s.e : o_e; Th = is_test ? s.yaw : o_yaw;
+      Tsh = is_test ? sy : o_sy; Tch = is_test ? cy : o_cy;
+      On = is_test ? o_n : s.n; Oe = is_test ? o_e : s.e; Oyaw = is_test ? o_yaw : s.yaw;
+      Tect = is_test ? s.log_ect : o_ect; Oect = is_test ? o_ect : s.log_ect;
+      Tground = is_test ? my_ground : o_ground; Oground = is_test ? o_ground : my_ground;
+      Tf = is_test ? my_flags : o_flags; Of = is_test ? o_flags : my_flags;
+      Ospeed = is_test ? o_speed : my_speed_out;
+      Ttime = is_test ? s.time : o_time;
+      Odtravel = is_test ? o_dtravel : dtravel;
+      Odtime = is_test ? o_dtime : dtime;
+      Cn = On; Ce = Oe;
+      any_nf = (my_flags | o_flags) & XF_NONFINITE;
+    } else {  // slot k's first lane of the env row holds ship k
+      Tn = env_lane_d<LPE, 0>(s.n, env_lane0); Te = env_lane_d<LPE, 0>(s.e, env_lane0);
+      Th = env_lane_d<LPE, 0>(s.yaw, env_lane0); Tsh = env_lane_d<LPE, 0>(sy, env_lane0);
+      Tch = env_lane_d<LPE, 0>(cy, env_lane0); Tect = env_lane_d<LPE, 0>(s.log_ect, env_lane0);
+      Tground = env_lane_d<LPE, 0>(my_ground, env_lane0); Ttime = env_lane_d<LPE, 0>(s.time, env_lane0);
+      Tf = env_lane_i<LPE, 0>(my_flags, env_lane0);
+      On = env_lane_d<LPE, 1>(s.n, env_lane0); Oe = env_lane_d<LPE, 1>(s.e, env_lane0);
+      Oyaw = env_lane_d<LPE, 1>(s.yaw, env_lane0); Oect = env_lane_d<LPE, 1>(s.log_ect, env_lane0);
+      Oground = env_lane_d<LPE, 1>(my_ground, env_lane0); Ospeed = env_lane_d<LPE, 1>(my_speed_out, env_lane0);
+      Odtravel = env_lane_d<LPE, 1>(dtravel, env_lane0); Odtime = env_lane_d<LPE, 1>(dtime, env_lane0);
+      Of = env_lane_i<LPE, 1>(my_flags, env_lane0);
+      int nf = Tf | Of;
+      Cn = On; Ce = Oe;
+      double cd = (Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe);
+#define NEAREST(M)                                                                                  \
+  if constexpr (M < SLOTS) {                                                                        \
+    const double kn = env_lane_d<LPE, M>(s.n, env_lane0), ke = env_lane_d<LPE, M>(s.e, env_lane0); \
+    nf |= env_lane_i<LPE, M>(my_flags, env_lane0);                                                  \
+    const double kd = (Tn - kn) * (Tn - kn) + (Te - ke) * (Te - ke);                                \
+    if (kd < cd) { cd = kd; Cn = kn; Ce = ke; }                                                     \
+  }
+      NEAREST(2) NEAREST(3) NEAREST(4) NEAREST(5) NEAREST(6) NEAREST(7)
+#undef NEAREST
+      any_nf = nf & XF_NONFINITE;
+    }
     if (going) {
-      const double Tn = is_test ? s.n : o_n, Te = is_test ? s.e : o_e, Th = is_test ? s.yaw : o_yaw;
-      const double Tsh = is_test ? sy : o_sy, Tch = is_test ? cy : o_cy;
-      const double On = is_test ? o_n : s.n, Oe = is_test ? o_e : s.e, Oyaw = is_test ? o_yaw : s.yaw;
-      const double Tect = is_test ? s.log_ect : o_ect, Oect = is_test ? o_ect : s.log_ect;
-      const double Tground = is_test ? my_ground : o_ground, Oground = is_test ? o_ground : my_ground;
-      const int Tf = is_test ? my_flags : o_flags, Of = is_test ? o_flags : my_flags;
-      const double Ospeed = is_test ? o_speed : my_speed_out;
-      const double Ttime = is_test ? s.time : o_time;
-      travel_dist += is_test ? o_dtravel : dtravel;
-      travel_time += is_test ? o_dtime : dtime;
+      travel_dist += Odtravel;
+      travel_time += Odtime;
       // next_states (env.py:582-591) and self.states
       ns[0] = (float)Tn; ns[1] = (float)Te; ns[2] = (float)Tect;
       ns[3] = (float)On; ns[4] = (float)Oe; ns[5] = (float)Oyaw; ns[6] = (float)Ospeed; ns[7] = (float)Oect;
       if (SIMPLE) { st4[0] = ns[0]; st4[1] = ns[1]; st4[2] = ns[3]; st4[3] = ns[4]; }
       // get_reward_and_env_info (reward_function.py:59-270)
-      const bool is_collision = ((Tn - On) * (Tn - On) + (Te - Oe) * (Te - Oe)) < 2500.0;
+      const bool is_collision = ((Tn - Cn) * (Tn - Cn) + (Te - Ce) * (Te - Ce)) < 2500.0;
       const bool is_tg = Tf & XF_GROUND, is_og = Of & XF_GROUND;
       const bool is_tnav = fabs(Tect) > 3000;
       const bool is_onav = (travel_dist > P.AB_seg * 2) || (travel_time > INFINITY) || (fabs(Oect) > 500);
-      double dx = On - Tn, dy = Oe - Te;
+      double dx = Cn - Tn, dy = Ce - Te;
       double dist = sqrt(dx * dx + dy * dy);
       const bool enc_ok = !overtaking_sector(dx, dy, dist, Tsh, Tch, Th);  // head-on or crossing (Q5)
       // the five shaped terms of reward_designs.py:33-55 (RewardDesign4 / 3): one exp each,
@@ -1211,9 +1380,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       if (terminal) bits |= SHIPSIM_EV_TERMINAL;
       if (test_stop) bits |= SHIPSIM_EV_TEST_STOP;
       if (obs_stop) bits |= SHIPSIM_EV_OBS_STOP;
-      if (obs_stop && !terminal && !is_test) s.stop = 1;
+      if (obs_stop && !terminal && is_obs1) s.stop = 1;
+      if (SLOTS > 2 && shipc >= 2 && (my_flags & (XF_END | XF_OUTSIDE | XF_GROUND)))
+        s.stop = 1;  // further obstacle ships freeze at their last waypoint / off the map / aground
       bool combined_done = terminal || (test_stop && !terminal);
-      const bool nonfinite = (my_flags | o_flags) & XF_NONFINITE;
+      const bool nonfinite = any_nf;
       if (nonfinite) {  // not a reference outcome: the env ends its episode here, flagged
         bits |= SHIPSIM_EV_NONFINITE | SHIPSIM_EV_TERMINAL;
         combined_done = true;
@@ -1286,7 +1457,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
            ticks, sampling_count, n_base, phase, (int)have_iw);
 #endif
   const DevState So = opaque(S);  // addresses recomputed here, not carried through the loop
-  if (sub == 0) store_ship(So, qc, s);
+  if (sub == 0 && !ghost) store_ship(So, qc, s);
   if (REC) {
     if (sub == 0)
       for (int k = 0; k < 3; ++k) T.fuel[(size_t)qc * 3 + k] = fuel[k];
@@ -1321,7 +1492,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     if (ticks_out) ticks_out[env] = ticks;
     if (ready_out) ready_out[env] = ready ? 1 : 0;
   }
-  if (ready && obs_out && sub == 0) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
+  if (ready && obs_out && sub == 0 && ship < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
     for (int i = 0; i < 4; ++i) obs_out[env * 8 + ship * 4 + i] = ns[ship * 4 + i];
   }
 }
@@ -1329,8 +1500,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 // C2 single-ship loop body, k ticks per launch (one lane per ship; algebraic wind force)
 template <bool DETAILED>
 __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevState S, ConstBuf K, int k) {
-  __shared__ ShipConst lds_sc[2];
-  const ShipConst* SC = stage_consts(P, lds_sc);
+  __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P.n_envs) return;
   const ShipConst& c = SC[0];
@@ -1355,10 +1526,10 @@ template <bool DETAILED, int COLLAV>
 __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevState S, ConstBuf K, int k,
                                                          double* __restrict__ states_out, uint8_t* __restrict__ done_out,
                                                          uint32_t* __restrict__ status_out) {
-  __shared__ ShipConst lds_sc[2];
+  __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
-  const ShipConst* SC = stage_consts(P, lds_sc);
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
   for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) lds_edges_raw[i] = K.edges()[i];
   for (int i = threadIdx.x; i < P.n_polys; i += blockDim.x) lds_boxes[i] = K.boxes()[i];
   __syncthreads();
@@ -1672,6 +1843,23 @@ static void launch_step(shipsim_handle* h, int lpe, const float* action, const u
 #undef L
 }
 
+// K > 1 obstacle ships (detailed machinery, collav none / sbmpc): 16 lanes per env in 4 or 8 ship slots
+static int ship_slots(const shipsim_handle* h) { return h->P.n_ships <= 2 ? 2 : (h->P.n_ships <= 4 ? 4 : 8); }
+
+template <int CA, bool CHAIN>
+static void launch_multi(shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks,
+                         float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
+                         int32_t* ticks_out, uint8_t* ready_out, const ChainArgs& ch) {
+  const int threads = 64, blocks = (h->P.n_envs * 16 + threads - 1) / threads;
+#define LM(SL)                                                                                                         \
+  hipLaunchKernelGGL((ast_step_kernel<true, CA, 16, false, CHAIN, SL>), dim3(blocks), dim3(threads), 0, h->stream,  \
+                     h->P, h->S, h->K, h->T, action, active, max_ticks, obs_out, reward_out, done_out, events_out,    \
+                     ticks_out, ready_out, ch)
+  if (ship_slots(h) == 4) LM(4);
+  else LM(8);
+#undef LM
+}
+
 extern "C" {
 
 int32_t shipsim_abi_version(void) { return SHIPSIM_ABI_VERSION; }
@@ -1927,6 +2115,13 @@ static int validate(const shipsim_config* cfg, char* err, size_t n) {
   if (cfg->machinery < 0 || cfg->machinery > 1) return snprintf(err, n, "bad machinery %d", cfg->machinery), 1;
   if (cfg->collav < 0 || cfg->collav > 2) return snprintf(err, n, "bad collav %d", cfg->collav), 1;
   int ns = cfg->kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
+  if (cfg->kind == SHIPSIM_KIND_AST) {
+    ns = cfg->n_ships;
+    if (ns < 2 || ns > SHIPSIM_MAX_SHIPS)
+      return snprintf(err, n, "n_ships %d: 1 ship under test + 1..%d obstacle ships", ns, SHIPSIM_MAX_OBS), 1;
+    if (ns > 2 && (cfg->machinery != SHIPSIM_MACH_DETAILED || cfg->collav == SHIPSIM_COLLAV_SIMPLE))
+      return snprintf(err, n, "%d obstacle ships: detailed machinery and collav none / sbmpc only", ns - 1), 1;
+  }
   if (cfg->n_ships != ns) return snprintf(err, n, "n_ships %d != %d for kind %d", cfg->n_ships, ns, cfg->kind), 1;
   if (!(cfg->time_step > 0)) return snprintf(err, n, "time_step must be > 0"), 1;
   if (cfg->max_sampling_frequency < 0 || cfg->max_sampling_frequency + 2 > SHIPSIM_MAX_ROUTE)
@@ -1946,31 +2141,33 @@ static int validate(const shipsim_config* cfg, char* err, size_t n) {
   return 0;
 }
 
-int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, void* stream, shipsim_handle** out) {
-  if (!cfg || !out || n_envs <= 0) return SHIPSIM_EINVAL;
+static char g_create_err[512];  // message of the last failed shipsim_create (shipsim_last_error(NULL))
+
+int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_ships, int32_t device, void* stream,
+                   shipsim_handle** out) {
+  if (!cfg_in || !out || n_envs <= 0) return SHIPSIM_EINVAL;
   *out = nullptr;
   shipsim_handle* h = new (std::nothrow) shipsim_handle();
   if (!h) return SHIPSIM_ENOMEM;
   memset(h, 0, sizeof(*h));
+  h->cfg = *cfg_in;
+  if (n_obs_ships > 0 && h->cfg.kind == SHIPSIM_KIND_AST) h->cfg.n_ships = 1 + n_obs_ships;
+  const shipsim_config* cfg = &h->cfg;
   if (validate(cfg, h->err, sizeof(h->err))) {
-    // keep the message reachable for the caller through a static buffer
-    static char last[512];
-    snprintf(last, sizeof(last), "%s", h->err);
+    snprintf(g_create_err, sizeof(g_create_err), "%s", h->err);
     delete h;
     return SHIPSIM_EINVAL;
   }
-  h->cfg = *cfg;
   h->device = device;
   h->stream = (hipStream_t)stream;
   DeviceGuard g(device);
-  h->lpe = lanes_per_env(cfg, n_envs, device);
+  h->lpe = cfg->n_ships > 2 ? 16 : lanes_per_env(cfg, n_envs, device);  // K > 1: 16 lanes in ship slots
   Params& P = h->P;
   memset(&P, 0, sizeof(P));
   const int ns = cfg->n_ships;
-  for (int i = 0; i < ns; ++i) make_ship_const(cfg, &cfg->ship[i], &P.sc[i]);
-  if (ns == 1) P.sc[1] = P.sc[0];
-  P.sc[1].obs_l_cfg = cfg->ship[ns - 1].length_of_ship;
-  P.sc[1].obs_w_cfg = cfg->ship[ns - 1].width_of_ship;
+  ShipConst sc[SHIPSIM_MAX_SHIPS];
+  memset(sc, 0, sizeof(sc));
+  for (int i = 0; i < ns; ++i) make_ship_const(cfg, &cfg->ship[i], &sc[i]);
   P.kind = cfg->kind;
   P.machinery = cfg->machinery;
   P.collav = cfg->collav;
@@ -2063,8 +2260,9 @@ int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, vo
   for (int s = 0; s < ns; ++s)
     for (int i = 0; i < cfg->ship[s].n_route; ++i) {
       R[s * kMaxRoute + i] = cfg->ship[s].route_north[i];
-      R[2 * kMaxRoute + s * kMaxRoute + i] = cfg->ship[s].route_east[i];
+      R[SHIPSIM_MAX_SHIPS * kMaxRoute + s * kMaxRoute + i] = cfg->ship[s].route_east[i];
     }
+  memcpy(hostc + ConstBuf::kShipsOff, sc, sizeof(ShipConst) * SHIPSIM_MAX_SHIPS);
   if (use_grid)
     build_grid(E, nv, B, cfg->n_polys, mn_e - kGridPad, mn_n - kGridPad, gnx, gny, (uint64_t*)(hostc + grid_off),
                (uint8_t*)(hostc + grid_off + gcells * sizeof(uint64_t)));
@@ -2142,7 +2340,7 @@ int shipsim_destroy(shipsim_handle* h) {
   return SHIPSIM_OK;
 }
 
-const char* shipsim_last_error(const shipsim_handle* h) { return h ? h->err : "null handle"; }
+const char* shipsim_last_error(const shipsim_handle* h) { return h ? h->err : g_create_err; }
 int32_t shipsim_num_envs(const shipsim_handle* h) { return h ? h->P.n_envs : -1; }
 int32_t shipsim_lanes_per_env(const shipsim_handle* h) { return h ? h->lpe : -1; }
 
@@ -2177,6 +2375,16 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
   const int lpe = h->lpe;
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
 #define LAUNCH(D, CA) launch_step<D, CA>(h, lpe, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, ready_out)
+  if (ship_slots(h) > 2) {
+    if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
+      launch_multi<SHIPSIM_COLLAV_SBMPC, false>(h, action, active, max_ticks, obs_out, reward_out, done_out,
+                                                events_out, ticks_out, ready_out, ChainArgs{});
+    else
+      launch_multi<SHIPSIM_COLLAV_NONE, false>(h, action, active, max_ticks, obs_out, reward_out, done_out,
+                                               events_out, ticks_out, ready_out, ChainArgs{});
+    HIPCHK(h, hipGetLastError());
+    return SHIPSIM_OK;
+  }
   switch (h->P.collav) {
     case SHIPSIM_COLLAV_NONE: if (det) LAUNCH(true, 0); else LAUNCH(false, 0); break;
     case SHIPSIM_COLLAV_SIMPLE: if (det) LAUNCH(true, 1); else LAUNCH(false, 1); break;
@@ -2230,6 +2438,16 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
     else CHAINED_L(D, CA, 16);                      \
   } while (0)
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
+  if (ship_slots(h) > 2) {
+    if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
+      launch_multi<SHIPSIM_COLLAV_SBMPC, true>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr,
+                                               ticks_out, nullptr, ch);
+    else
+      launch_multi<SHIPSIM_COLLAV_NONE, true>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr,
+                                              ticks_out, nullptr, ch);
+    HIPCHK(h, hipGetLastError());
+    return SHIPSIM_OK;
+  }
   switch (h->P.collav) {
     case SHIPSIM_COLLAV_SBMPC: if (det) CHAINED(true, SHIPSIM_COLLAV_SBMPC); else CHAINED(false, SHIPSIM_COLLAV_SBMPC); break;
     case SHIPSIM_COLLAV_SIMPLE: if (det) CHAINED(true, SHIPSIM_COLLAV_SIMPLE); else CHAINED(false, SHIPSIM_COLLAV_SIMPLE); break;
@@ -2244,6 +2462,7 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
 int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_t* done_out, uint32_t* status_out) {
   if (!h || !h->dev_block || k < 0) return SHIPSIM_EINVAL;
   if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "legacy_step: AST kind only");
+  if (h->P.n_ships != 2) return fail(h, SHIPSIM_EINVAL, "legacy_step: the legacy MultiShipEnv has one obstacle ship");
   if (k == 0) return SHIPSIM_OK;
   DeviceGuard g(h->device);
   const int threads = 64, blocks = (2 * h->P.n_envs + threads - 1) / threads;
@@ -2309,6 +2528,7 @@ int shipsim_set_trajectory(shipsim_handle* h, double* ship_rows, double* env_row
                            int32_t* lengths) {
   if (!h || !h->dev_block) return SHIPSIM_EINVAL;
   if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "set_trajectory: SHIPSIM_KIND_AST only");
+  if (h->P.n_ships != 2 && ship_rows) return fail(h, SHIPSIM_EINVAL, "set_trajectory: one obstacle ship only");
   if (!ship_rows) {
     memset(&h->T, 0, sizeof(h->T));
     return SHIPSIM_OK;

@@ -37,7 +37,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_abi_version.restype = C.c_int32
     L.shipsim_build_info.restype = C.c_char_p
     L.shipsim_default_config.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_double, cfgp]
-    L.shipsim_create.argtypes = [cfgp, C.c_int32, C.c_int32, P, C.POINTER(P)]
+    L.shipsim_create.argtypes = [cfgp, C.c_int32, C.c_int32, C.c_int32, P, C.POINTER(P)]
     L.shipsim_destroy.argtypes = [P]
     L.shipsim_last_error.argtypes = [P]
     L.shipsim_last_error.restype = C.c_char_p
@@ -90,21 +90,24 @@ def _ptr(t):
 class ShipSim:
     """N independent environments on one device, state resident in HBM."""
 
-    def __init__(self, cfg, n_envs, device=None):
+    def __init__(self, cfg, n_envs, device=None, n_obs_ships=0):
+        """n_obs_ships: obstacle ships per env (AST; 0 = cfg.n_ships - 1, see shipsim_create)."""
         if not torch.cuda.is_available():
             raise ShipSimError("ShipSim needs a HIP device (torch.cuda.is_available() is False)")
         self.L = load_library()
         self.cfg = cfg
         self.n_envs = int(n_envs)
+        if n_obs_ships > 0 and cfg.kind == abi.KIND_AST:
+            cfg.n_ships = 1 + int(n_obs_ships)
         self.n_ships = int(cfg.n_ships)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
         with torch.cuda.device(self.device):
             self.stream = torch.cuda.current_stream(self.device)
             h = C.c_void_p()
-            rc = self.L.shipsim_create(C.byref(cfg), self.n_envs, self.device.index, C.c_void_p(self.stream.cuda_stream),
-                                       C.byref(h))
+            rc = self.L.shipsim_create(C.byref(cfg), self.n_envs, int(n_obs_ships), self.device.index,
+                                       C.c_void_p(self.stream.cuda_stream), C.byref(h))
             if rc:
-                msg = self.L.shipsim_last_error(h).decode() if h.value else "invalid config"
+                msg = self.L.shipsim_last_error(h if h.value else None).decode()
                 if h.value:
                     self.L.shipsim_destroy(h)
                 raise ShipSimError(f"shipsim_create failed ({rc}): {msg}")

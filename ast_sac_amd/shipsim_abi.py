@@ -13,11 +13,13 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 ENONFINITE = -5  # shipsim_synchronize status (include/shipsim.h)
 MAX_ROUTE = 16
 MAX_POLYS = 16
 MAX_VERTS = 128
+MAX_OBS = 4
+MAX_SHIPS = 1 + MAX_OBS
 
 KIND_SINGLE, KIND_NONIW, KIND_AST = 0, 1, 2
 COLLAV_NONE, COLLAV_SIMPLE, COLLAV_SBMPC = 0, 1, 2
@@ -131,7 +133,7 @@ class Config(C.Structure):
         ("env_radius_of_acceptance", C.c_double), ("current_velocity_component_from_north", C.c_double),
         ("current_velocity_component_from_east", C.c_double), ("wind_speed", C.c_double),
         ("wind_direction", C.c_double), ("sbmpc_tf", C.c_double), ("sbmpc_dt", C.c_double),
-        ("action_low", C.c_float), ("action_high", C.c_float), ("ship", ShipConfig * 2),
+        ("action_low", C.c_float), ("action_high", C.c_float), ("ship", ShipConfig * MAX_SHIPS),
         ("n_polys", C.c_int32), ("poly_start", C.c_int32 * (MAX_POLYS + 1)),
         ("poly_east", C.c_double * MAX_VERTS), ("poly_north", C.c_double * MAX_VERTS),
         ("lanes_per_env", C.c_int32), ("reserved", C.c_int32 * 7)]
@@ -257,10 +259,36 @@ def _base(kind, collav, time_step, machinery):
     return cfg
 
 
-def ast_config(collav="sbmpc", time_step=4, machinery=MACH_DETAILED):
+# Further obstacle ships of the multi-obstacle scenarios (configs[4] C5, K > 1; beyond the reference,
+# which builds one obstacle ship): (initial north, east, yaw [deg], speed, desired speed, route (north, east)).
+# Routes run over water of the reference map: ship 2 sails the obstacle route in the opposite
+# direction, ship 3 the test ship's route from its far end (head-on traffic), ship 4 the obstacle
+# route from half way along it.
+TRAFFIC_SHIPS = (
+    (100.0, 5100.0, 45.0, 3.5, 4.0, ((0, 5000), (10000, 15000))),
+    (3000.0, 17500.0, -23.2, 4.0, 4.0, ((3000, 17500), (6500, 16000), (7000, 12000), (2500, 7500), (2000, 4500),
+                                        (0, 0))),
+    (5000.0, 10000.0, -135.0, 3.5, 4.0, ((5000, 10000), (0, 5000))),
+)
+
+
+def ast_config(collav="sbmpc", time_step=4, machinery=MACH_DETAILED, n_obs_ships=1):
     """run/env_setup.py:prepare_multiship_rl_env (runner defaults). With machinery=MACH_SIMPLIFIED
-    the ships become run_colav SimpleShipModel + ThrustFromSpeedSetPoint(150, 150, 75)."""
+    the ships become run_colav SimpleShipModel + ThrustFromSpeedSetPoint(150, 150, 75).
+    n_obs_ships > 1 adds TRAFFIC_SHIPS[:K-1] as ships 2..K (include/shipsim.h shipsim_create)."""
+    if not 1 <= n_obs_ships <= MAX_OBS:
+        raise ValueError(f"n_obs_ships must be in 1..{MAX_OBS}")
     cfg = _base(KIND_AST, collav, time_step, machinery)
+    cfg.n_ships = 1 + n_obs_ships
+    for k in range(n_obs_ships - 1):
+        north, east, yaw, u, ud, route = TRAFFIC_SHIPS[k]
+        s = cfg.ship[2 + k]
+        _ship_common(s, north, east, np.deg2rad(yaw), u)
+        s.initial_propeller_shaft_speed_rad_per_s = 200 * np.pi / 30
+        s.heading_kp, s.heading_kd, s.heading_ki = 1.65, 75, 0.001
+        s.speed_kp, s.speed_ki, s.speed_kd = 150, 150, 75
+        s.desired_forward_speed = ud
+        _set_route(s, route)
     t, o = cfg.ship[0], cfg.ship[1]
     _ship_common(t, 100, 100, 60 * np.pi / 180, 4.25)
     _ship_common(o, 9900, 14900, -135 * np.pi / 180, 3.5)

@@ -27,11 +27,13 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 4
+#define SHIPSIM_ABI_VERSION 5
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
 #define SHIPSIM_MAX_VERTS 128  /* total polygon vertices */
+#define SHIPSIM_MAX_OBS 4      /* obstacle ships per AST env (configs[4] C5: K in {1, 2, 4}) */
+#define SHIPSIM_MAX_SHIPS (1 + SHIPSIM_MAX_OBS)
 
 /* status codes */
 #define SHIPSIM_OK 0
@@ -158,7 +160,7 @@ typedef struct shipsim_config {
   int32_t max_sampling_frequency; /* args.max_sampling_frequency (9) */
   int32_t machinery_dt_quirk;     /* 1: machinery integrates with dt 0.01 after reset */
   int32_t normalize_action;       /* args.normalize_action: env denormalizes [-1,1] itself */
-  int32_t n_ships;                /* 1 (SINGLE) or 2 */
+  int32_t n_ships;                /* 1 (SINGLE), 2 (NONIW), 1 + K obstacle ships (AST, K <= SHIPSIM_MAX_OBS) */
   double time_step;               /* args.time_step */
   double simulation_time;         /* SimulationConfiguration.simulation_time */
   double env_radius_of_acceptance;/* args.radius_of_acceptance used by is_reach_radius_of_acceptance */
@@ -173,7 +175,9 @@ typedef struct shipsim_config {
   /* action box of the wrapped env (env.py:93-104), float32 as in the reference */
   float action_low;
   float action_high;
-  shipsim_ship_config ship[2]; /* [0] ship under test, [1] obstacle ship */
+  /* [0] ship under test, [1] the obstacle ship (intermediate-waypoint sampling, the decisions, the
+   * observation), [2..K] further obstacle ships (AST with K > 1, see shipsim_create) */
+  shipsim_ship_config ship[SHIPSIM_MAX_SHIPS];
   /* PolygonObstacle map: polygon p owns vertices [poly_start[p], poly_start[p+1]), (east, north) */
   int32_t n_polys;
   int32_t poly_start[SHIPSIM_MAX_POLYS + 1];
@@ -185,7 +189,7 @@ typedef struct shipsim_config {
   int32_t reserved[7];
 } shipsim_config;
 
-/* Per-ship state fields for get/set_state (SoA, double unless noted) */
+/* Per-ship state fields for get/set_state (SoA, double unless noted; [env][ship], n_ships = 1 + K) */
 #define SHIPSIM_F_NORTH 0
 #define SHIPSIM_F_EAST 1
 #define SHIPSIM_F_YAW 2
@@ -236,10 +240,24 @@ int shipsim_default_config(int32_t kind, int32_t machinery, int32_t collav, doub
                            shipsim_config* cfg);
 
 /* Allocate device state for n_envs environments on `device`, bound to `stream` (hipStream_t;
- * NULL = default stream). The handle starts un-reset. */
-int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t device, void* stream,
+ * NULL = default stream). The handle starts un-reset.
+ * n_obs_ships (AST kind): obstacle ships per env, 1..SHIPSIM_MAX_OBS (<= 0: cfg->n_ships - 1), configured
+ * in cfg->ship[1..K]. K = 1 is the reference env (rl_env/ship_in_transit/env.py:76 unpacks [test, obs]).
+ * K > 1 generalises it the way the reference's own pieces already do — parity unpinned beyond them:
+ *   - SBMPC of the ship under test sees every obstacle ship (env.py:366-370 builds do_list from
+ *     assets[1::]; sbmpc.py:150-176: active when any is within D_INIT, worst obstacle per scenario);
+ *   - ship 1 is "the" obstacle ship: it samples the intermediate waypoints from the action, its radius
+ *     of acceptance ends a decision, its grounding / navigation failure terms enter the reward and the
+ *     observation reports it (env.py:538-773, reward_function.py:59-270);
+ *   - ships 2..K follow their own routes with the same autopilot / throttle controllers (obs_step
+ *     without sampling) and freeze (obs_step's stop branch) once they reach their last waypoint, leave
+ *     the map or ground;
+ *   - the collision reward / termination and the encounter angle use the nearest obstacle ship.
+ * K > 1 needs detailed machinery and collav none or sbmpc. */
+int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t n_obs_ships, int32_t device, void* stream,
                    shipsim_handle** out);
 int shipsim_destroy(shipsim_handle* h);
+/* Message of the last failed call on h; with h == NULL, of the last failed shipsim_create. */
 const char* shipsim_last_error(const shipsim_handle* h);
 int32_t shipsim_num_envs(const shipsim_handle* h);
 /* Lanes per AST env the step / stream kernels run at (config lanes_per_env, or chosen at create from

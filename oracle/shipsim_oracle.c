@@ -707,25 +707,31 @@ static double sb_cost(const o_sbmpc* sb, int n_samp, double DT, double P_ca, dou
   return H1 + H2;
 }
 
-/* get_optimal_ctrl_offset :113-185 for one dynamic obstacle */
-static void sbmpc_offset(o_sbmpc* sb, double T, double DT, double u_d, double chi_d, const double os[6],
-                         const double ob[5], double obs_l, double obs_w, double* P_best, double* Chi_best) {
+/* get_optimal_ctrl_offset :113-185 over the do_list of n_obst dynamic obstacles (ob[k][5] =
+ * [x, y, psi, u, v], obs_l[k], obs_w[k]): active when any obstacle is within D_INIT (:150-156); per
+ * scenario the worst obstacle's cost counts (:170-176), the scenario with the least worst cost wins */
+static void sbmpc_offset_multi(o_sbmpc* sb, double T, double DT, double u_d, double chi_d, const double os[6],
+                               int n_obst, const double (*ob)[5], const double* obs_l, const double* obs_w,
+                               double* P_best, double* Chi_best) {
   int n = (int)(T / DT);
   if (n > SB_MAXN) n = SB_MAXN;
-  double ox[SB_MAXN], oy[SB_MAXN], ou[SB_MAXN], ov[SB_MAXN];
-  /* Obstacle.__init__ / calculate_trajectory sbmpc_misc.py:35-83 */
-  double opsi = ob[2];
-  double r11 = -sin(opsi), r12 = cos(opsi), r21 = cos(opsi), r22 = sin(opsi);
-  ox[0] = ob[0]; oy[0] = ob[1]; ou[0] = ob[3]; ov[0] = ob[4];
-  for (int i = 1; i < n; ++i) {
-    ox[i] = ox[i - 1] + (r11 * ou[i - 1] + r12 * ov[i - 1]) * DT;
-    oy[i] = oy[i - 1] + (r21 * ou[i - 1] + r22 * ov[i - 1]) * DT;
-    ou[i] = ou[i - 1];
-    ov[i] = ov[i - 1];
-  }
+  double ox[SHIPSIM_MAX_OBS][SB_MAXN], oy[SHIPSIM_MAX_OBS][SB_MAXN];
+  double ou0[SHIPSIM_MAX_OBS], ov0[SHIPSIM_MAX_OBS], opsi_k[SHIPSIM_MAX_OBS];
   sb->active = 0;
-  double d0 = ox[0] - os[0], d1 = oy[0] - os[1];
-  if (sqrt(d0 * d0 + d1 * d1) < 2000.0) sb->active = 1;
+  for (int k = 0; k < n_obst; ++k) {
+    /* Obstacle.__init__ / calculate_trajectory sbmpc_misc.py:35-83 */
+    double opsi = ob[k][2];
+    double r11 = -sin(opsi), r12 = cos(opsi), r21 = cos(opsi), r22 = sin(opsi);
+    double ou = ob[k][3], ov = ob[k][4];
+    ox[k][0] = ob[k][0]; oy[k][0] = ob[k][1];
+    for (int i = 1; i < n; ++i) {
+      ox[k][i] = ox[k][i - 1] + (r11 * ou + r12 * ov) * DT;
+      oy[k][i] = oy[k][i - 1] + (r21 * ou + r22 * ov) * DT;
+    }
+    ou0[k] = ou; ov0[k] = ov; opsi_k[k] = opsi;
+    double d0 = ox[k][0] - os[0], d1 = oy[k][0] - os[1];
+    if (sqrt(d0 * d0 + d1 * d1) < 2000.0) sb->active = 1;
+  }
   if (!sb->active) {
     *P_best = 1; *Chi_best = 0;
     sb->P_last = 1; sb->Chi_last = 0;
@@ -751,8 +757,11 @@ static void sbmpc_offset(o_sbmpc* sb, double T, double DT, double u_d, double ch
         sv[k] = 0;
       }
       double cost_i = -1;
-      double ck = sb_cost(sb, n, DT, P_CA[j], chi_ca, ox, oy, opsi, ou[0], ov[0], obs_l, obs_w, sx, sy, spsi, su, sv);
-      if (ck > cost_i) cost_i = ck;
+      for (int k = 0; k < n_obst; ++k) {
+        double ck = sb_cost(sb, n, DT, P_CA[j], chi_ca, ox[k], oy[k], opsi_k[k], ou0[k], ov0[k], obs_l[k], obs_w[k],
+                            sx, sy, spsi, su, sv);
+        if (ck > cost_i) cost_i = ck;
+      }
       if (cost_i < cost) { cost = cost_i; pb = P_CA[j]; cb = chi_ca; }
     }
   }
@@ -760,12 +769,20 @@ static void sbmpc_offset(o_sbmpc* sb, double T, double DT, double u_d, double ch
   *P_best = pb; *Chi_best = cb;
 }
 
+/* the reference's single-obstacle call */
+static void sbmpc_offset(o_sbmpc* sb, double T, double DT, double u_d, double chi_d, const double os[6],
+                         const double ob[5], double obs_l, double obs_w, double* P_best, double* Chi_best) {
+  const double (*obl)[5] = (const double (*)[5])ob;
+  sbmpc_offset_multi(sb, T, DT, u_d, chi_d, os, 1, obl, &obs_l, &obs_w, P_best, Chi_best);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* environments                                                                               */
 /* ------------------------------------------------------------------------------------------ */
 typedef struct {
   shipsim_config cfg;
-  o_asset a[2]; /* [test, obs] */
+  o_asset a[SHIPSIM_MAX_SHIPS]; /* [test, obs, further obstacle ships (K > 1)] */
+  int n_ships;                   /* 1 (SINGLE), 2, or 1 + K (AST) */
   o_map map;
   o_sbmpc sb;
   /* intermediate waypoint sampler env.py:143-169 */
@@ -807,12 +824,14 @@ static void env_init_iw(o_env* env) { /* init_get_intermediate_waypoints env.py:
 o_env* oracle_env_create(const shipsim_config* cfg) {
   o_env* env = (o_env*)calloc(1, sizeof(o_env));
   env->cfg = *cfg;
-  int ns = cfg->kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
+  int ns = cfg->kind == SHIPSIM_KIND_SINGLE ? 1 : (cfg->kind == SHIPSIM_KIND_AST ? cfg->n_ships : 2);
+  if (ns < 1 || ns > SHIPSIM_MAX_SHIPS) ns = 2;
+  env->n_ships = ns;
   for (int i = 0; i < ns; ++i) asset_init(&env->a[i], cfg, i);
   map_init(&env->map, cfg);
   env->sb.P_last = 1.0;
   env->sb.Chi_last = 0.0;
-  if (ns == 2) {
+  if (ns >= 2) {
     env_init_iw(env);
     /* env.py:107-113 initial_states */
     float* s = env->initial_states;
@@ -847,8 +866,7 @@ static void ship_tick(o_asset* a, double rudder, double ctrl) {
 }
 
 static void env_init_step(o_env* env) { /* init_step env.py:297-342 (run_colav/env.py:279-323) */
-  int ns = env->cfg.kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
-  for (int i = 0; i < ns; ++i) {
+  for (int i = 0; i < env->n_ships; ++i) {
     o_asset* a = &env->a[i];
     double n = a->m.north, e = a->m.east, h = a->m.yaw, u = a->m.u;
     double rudder = ap_rudder(&a->ap, n, e, h, 0.0);
@@ -866,10 +884,17 @@ static void sbmpc_block(o_env* env, o_asset* self, double n, double e, double* s
   double u_d = self->desired_speed;
   const o_ship* o = &env->a[0].m;
   double os[6] = {o->east, o->north, -o->yaw, o->u, o->v, o->r};
-  const o_ship* b = &env->a[1].m;
-  double ob[5] = {b->east, b->north, -b->yaw, b->u, b->v};
-  sbmpc_offset(&env->sb, env->cfg.sbmpc_tf, env->cfg.sbmpc_dt, u_d, -chi_d, os, ob, env->a[1].length_cfg,
-               env->a[1].width_cfg, sf, off);
+  /* do_list: every obstacle ship, assets[1::] (env.py:366-370) */
+  double ob[SHIPSIM_MAX_OBS][5], ol[SHIPSIM_MAX_OBS], ow[SHIPSIM_MAX_OBS];
+  const int K = env->n_ships - 1;
+  for (int k = 0; k < K; ++k) {
+    const o_ship* b = &env->a[1 + k].m;
+    ob[k][0] = b->east; ob[k][1] = b->north; ob[k][2] = -b->yaw; ob[k][3] = b->u; ob[k][4] = b->v;
+    ol[k] = env->a[1 + k].length_cfg;
+    ow[k] = env->a[1 + k].width_cfg;
+  }
+  sbmpc_offset_multi(&env->sb, env->cfg.sbmpc_tf, env->cfg.sbmpc_dt, u_d, -chi_d, os, K, (const double (*)[5])ob, ol,
+                     ow, sf, off);
 }
 
 /* float32 is_collision_imminent on self.states (check_condition.py:130-140) */
@@ -924,17 +949,41 @@ static void ast_obs_step(o_env* env, float out5[5]) {
   }
 }
 
+/* further obstacle ship (K > 1, include/shipsim.h shipsim_create): obs_step :447-536 without the
+ * intermediate-waypoint sampling and the travel trackers; frozen once it reached its last waypoint,
+ * left the map or grounded (the stop branch :452-479) */
+static void ast_traffic_step(o_env* env, int which) {
+  o_asset* a = &env->a[which];
+  if (a->stop_flag) {
+    asset_store_last(a);
+    next_time(&a->m);
+    next_time(&a->m);
+    return;
+  }
+  double n = a->m.north, e = a->m.east, h = a->m.yaw, u = a->m.u;
+  double rudder = ap_rudder(&a->ap, n, e, h, 0.0);
+  double thr = speed_ctrl(a, a->desired_speed, u);
+  ship_tick(a, rudder, thr);
+}
+
 /* get_reward_and_env_info reward_function.py:59-270 (+ get_env_info run_colav :53-225 when
- * with_reward == 0). Returns r_total, fills event bits. */
+ * with_reward == 0). Returns r_total, fills event bits. With K > 1 obstacle ships the collision
+ * terms use the nearest one (lowest index on ties); the obstacle-ship terms stay with ship 1. */
 static double reward_and_info(o_env* env, uint32_t* bits_out, int with_reward) {
   o_asset* T = &env->a[0];
   o_asset* O = &env->a[1];
   const o_map* mp = &env->map;
   double tn = T->m.north, te = T->m.east, th = T->m.yaw, tect = T->log_ect, tL = T->m.l_ship;
   double on = O->m.north, oe = O->m.east, oect = O->log_ect, oL = O->m.l_ship;
-  double dist;
-  int enc = encounter(tn, te, th, on, oe, &dist);
+  double cn = on, ce = oe;  /* nearest obstacle ship */
   double cd = (tn - on) * (tn - on) + (te - oe) * (te - oe);
+  for (int k = 2; k < env->n_ships; ++k) {
+    const o_ship* b = &env->a[k].m;
+    double d2 = (tn - b->north) * (tn - b->north) + (te - b->east) * (te - b->east);
+    if (d2 < cd) { cd = d2; cn = b->north; ce = b->east; }
+  }
+  double dist;
+  int enc = encounter(tn, te, th, cn, ce, &dist);
   int is_collision = cd < 50.0 * 50.0;
   double t_ground = map_distance(mp, tn, te);
   int is_tg = is_pos_inside_obstacles(mp, tn, te, tL);
@@ -980,6 +1029,7 @@ static double ast_underscore_step(o_env* env, float obs8[8], int* combined_done,
   float t3[3], o5[5];
   ast_test_step(env, t3);
   ast_obs_step(env, o5);
+  for (int k = 2; k < env->n_ships; ++k) ast_traffic_step(env, k);
   float ns[8] = {t3[0], t3[1], t3[2], o5[0], o5[1], o5[2], o5[3], o5[4]};
   memcpy(env->states, ns, sizeof(ns));
   memcpy(obs8, ns, sizeof(ns));
@@ -988,6 +1038,14 @@ static double ast_underscore_step(o_env* env, float obs8[8], int* combined_done,
   int done = ((*bits & SHIPSIM_EV_TEST_STOP) != 0) && !terminal;
   int obs_stop = ((*bits & SHIPSIM_EV_OBS_STOP) != 0) && !terminal;
   if (obs_stop) env->a[1].stop_flag = 1;
+  for (int k = 2; k < env->n_ships; ++k) { /* further obstacle ships freeze at their end / off the map / aground */
+    o_asset* a = &env->a[k];
+    const o_nav* nv = &a->ap.nav;
+    if (is_reaches_endpoint(nv->north[nv->n - 1], nv->east[nv->n - 1], a->m.north, a->m.east) ||
+        is_pos_outside_horizon(&env->map, a->m.north, a->m.east, a->m.l_ship) ||
+        is_pos_inside_obstacles(&env->map, a->m.north, a->m.east, a->m.l_ship))
+      a->stop_flag = 1;
+  }
   *combined_done = terminal || done;
   env->ticks_total++;
   if (env->rtick_buf && env->rtick_len < env->rtick_cap) env->rtick_buf[env->rtick_len++] = r;
@@ -1000,7 +1058,7 @@ void oracle_env_reset(o_env* env, float obs8[8]) {
     asset_reset(&env->a[0], env->cfg.machinery_dt_quirk);
     return;
   }
-  for (int i = 0; i < 2; ++i) asset_reset(&env->a[i], env->cfg.machinery_dt_quirk);
+  for (int i = 0; i < env->n_ships; ++i) asset_reset(&env->a[i], env->cfg.machinery_dt_quirk);
   env_init_iw(env);
   memcpy(env->next_observations, env->initial_states, sizeof(env->initial_states));
   env->accumulated_rewards = 0;

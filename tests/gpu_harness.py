@@ -35,7 +35,7 @@ def run_oracle(cfg, tables):
                 if d:
                     break
             rec.append((o0, decs))
-        ships = np.array([env.ship_state(s) for s in range(2)])
+        ships = np.array([env.ship_state(s) for s in range(cfg.n_ships)])
         out.append((rec, ships, env.env_state()))
     return out
 

@@ -98,8 +98,21 @@ def test_create_rejects_bad_config_without_touching_a_device(lib):
     cfg = abi.ast_config("none")
     cfg.abi_version = 99
     h = C.c_void_p()
-    rc = lib.shipsim_create(C.byref(cfg), 4, 0, None, C.byref(h))
+    rc = lib.shipsim_create(C.byref(cfg), 4, 0, 0, None, C.byref(h))
     assert rc == -1  # SHIPSIM_EINVAL
+    assert b"abi_version" in lib.shipsim_last_error(None)
     cfg = abi.ast_config("none")
-    rc = lib.shipsim_create(C.byref(cfg), 0, 0, None, C.byref(h))
+    rc = lib.shipsim_create(C.byref(cfg), 0, 0, 0, None, C.byref(h))
     assert rc == -1
+
+
+@pytest.mark.parametrize("k,collav,mach,msg", [(5, "none", abi.MACH_DETAILED, b"obstacle ships"),
+                                               (2, "simple", abi.MACH_DETAILED, b"collav none / sbmpc"),
+                                               (4, "sbmpc", abi.MACH_SIMPLIFIED, b"detailed machinery")])
+def test_create_rejects_unsupported_obstacle_counts(lib, k, collav, mach, msg):
+    """C5 K obstacle ships: 1..SHIPSIM_MAX_OBS, K > 1 with detailed machinery and collav none / sbmpc."""
+    cfg = abi.ast_config(collav, machinery=mach)
+    h = C.c_void_p()
+    rc = lib.shipsim_create(C.byref(cfg), 4, k, 0, None, C.byref(h))
+    assert rc == -1 and not h.value
+    assert msg in lib.shipsim_last_error(None)
