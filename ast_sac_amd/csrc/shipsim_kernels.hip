@@ -2191,7 +2191,7 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
   P.action_low = cfg->action_low;
   P.action_high = cfg->action_high;
   P.normalize_action = cfg->normalize_action;
-  if (ns == 2) {  // init_get_intermediate_waypoints env.py:143-161
+  if (ns >= 2) {  // init_get_intermediate_waypoints env.py:143-161 (ship 1 samples)
     const shipsim_ship_config* o = &cfg->ship[1];
     double ABn = o->route_north[o->n_route - 1] - o->route_north[0];
     double ABe = o->route_east[o->n_route - 1] - o->route_east[0];
