@@ -108,7 +108,7 @@ class FusedSACTrainer(TorchTrainer):
         if backend == "hip":
             if not self._hip_shapes_ok():
                 raise ValueError("FusedSACTrainer hip backend: needs 2 equal hidden layers (<= 256, multiple of 32), "
-                                 "act_dim 1, obs_dim <= 15 and batch_size % 4 == 0; pass backend='torch' to run "
+                                 "act_dim 1, obs_dim <= 15 and a per-rank batch_size that is a multiple of 32 and <= 1024; pass backend='torch' to run "
                                  "these networks with PyTorch ops")
             self._init_hip(policy_lr, qf_lr)
         self._n_train_steps_total = 0
@@ -123,7 +123,7 @@ class FusedSACTrainer(TorchTrainer):
             obs = pol.fcs[0].weight.shape[1]
             ok = (len(pol.fcs) == 2 and pol.fcs[1].weight.shape == (H, H) and pol.last_fc.weight.shape == (1, H)
                   and getattr(pol, "last_fc_log_std", None) is not None and H % 32 == 0 and H <= 256
-                  and obs <= 15 and self.batch_size % 4 == 0)
+                  and obs <= 15 and self.batch_size % 32 == 0 and 32 <= self.batch_size <= 1024)
             for n in nets:
                 ok = ok and len(n.fcs) == 2 and n.fcs[0].weight.shape == (H, obs + 1) \
                     and n.fcs[1].weight.shape == (H, H) and n.last_fc.weight.shape == (1, H)

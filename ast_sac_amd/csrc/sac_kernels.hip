@@ -2,23 +2,20 @@
 //
 // One grad step of ast_sac/torch/sac/sac.py (compute_loss :156-270, train_from_torch :102-154,
 // update_target_networks :160-166) for TanhGaussianPolicy + twin ConcatMlp critics with two hidden
-// layers of width H and act_dim 1, in three kernels:
+// layers of width H and act_dim 1, as batched GEMMs on the matrix cores (v_mfma_f32_32x32x2_f32,
+// exact fp32) in six launches:
 //
-//   sac_rows_g4_kernel: one batch row per block (default; sac_rows_kernel<RR, KS> is the general
-//                      shape). Gathers the batch (or samples it from the replay ring with Philox),
-//                      runs actor(obs), actor(next_obs), Q1/Q2 on (obs, ã) and (obs, a), target
-//                      Q1/Q2 on (next_obs, ã'), the per-row losses, and the whole per-row backward.
-//                      Everything in one SAC update is row-local except the batch means, whose 1/B
-//                      factors are constants, so no grid-wide step is needed until the weight
-//                      gradients. Bound: every block streams 8 H x H fp32 matrices (2 MB at H = 256)
-//                      from L2; scripts/mb_weight_read.hip measures that alone at ≈19 µs on MI355X.
-//   sac_wgrad_kernel : every weight/bias gradient = Σ_rows dY[r]ᵀ X[r] (64×64 tiles, 4×4 per thread,
-//                      LDS-staged row chunks, rows split kParts ways into partial gradients) + the loss
-//                      scalars, d(log α) and this step's Adam bias corrections.
-//   sac_gsum_kernel  : (data parallel only) Σ of the partials into the flat gradient before the all-reduce.
-//   sac_apply_kernel : Σ partials (single process), torch.optim.Adam on every element (two lr groups),
-//                      soft target update θ' ← θ'(1−τ) + θτ, and the transposed H×H copies the rows
-//                      kernel reads (32×32 tiles through LDS).
+//   sac_actor_fwd_kernel / sac_critic_fwd_kernel / sac_critic_bwd_kernel / sac_actor_bwd_kernel:
+//       the forward and backward passes over the batch (2B actor rows [obs; next_obs], 2B critic
+//       rows [(obs, ã); (obs, a)] per critic, B target rows), each a 32 x 32-tiled GEMM with the
+//       elementwise work (input layer, bias, ReLU, heads, TanhNormal, losses, masks) fused into
+//       the operand fetch or the epilogue; see the MFMA-path section below.
+//   sac_wgrad_mfma_kernel: every weight/bias gradient = Σ_rows dY[r]ᵀ X[r] (the H x H ones on MFMA,
+//       the rest on the VALU) straight into the flat gradient, plus the loss scalars, d(log α) and
+//       this step's Adam bias corrections.
+//   sac_apply_kernel : torch.optim.Adam on every element (two lr groups; the gradient divided by the
+//       world size after the caller's all-reduce), soft target update θ' ← θ'(1−τ) + θτ, and the
+//       transposed H×H copies the forward kernels read (32×32 tiles through LDS).
 //
 // Only the four gradients the reference keeps are formed: the π-loss gradient w.r.t. the critics
 // (which sac.py:123-133 discards with qf*_optimizer.zero_grad()) is never computed; α is treated as a
@@ -136,734 +133,7 @@ __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.0f); }
 __device__ __forceinline__ float softplus(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
 // ---------------------------------------------------------------------------------------------
-// rows kernel: RR batch rows per block, KS k-groups of kCols threads (split-K matvecs)
-// ---------------------------------------------------------------------------------------------
-constexpr int kCols = 256;  // column threads per k-group (>= H)
-
-// acc[i] += Σ_{k in this k-group's slice} WT[k*H + j] · in[i][k]. With W row-major (out, in) the
-// same indexing computes the backward product Σ_jj W[jj][m] · d[i][jj] for column m.
-template <int NR, int KS>
-__device__ __forceinline__ void mv_part(const float* __restrict__ WT, int H, const float* in, int ld, int j, int kg,
-                                        float (&acc)[NR]) {
-  const int len = H / KS, k0 = kg * len, k1 = k0 + len;
-#pragma unroll 2
-  for (int k = k0; k < k1; k += 8) {
-    float w[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) w[u] = WT[(size_t)(k + u) * H + j];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const float4 x0 = *reinterpret_cast<const float4*>(in + i * ld + k);
-      const float4 x1 = *reinterpret_cast<const float4*>(in + i * ld + k + 4);
-      acc[i] = fmaf(w[0], x0.x, acc[i]);
-      acc[i] = fmaf(w[1], x0.y, acc[i]);
-      acc[i] = fmaf(w[2], x0.z, acc[i]);
-      acc[i] = fmaf(w[3], x0.w, acc[i]);
-      acc[i] = fmaf(w[4], x1.x, acc[i]);
-      acc[i] = fmaf(w[5], x1.y, acc[i]);
-      acc[i] = fmaf(w[6], x1.z, acc[i]);
-      acc[i] = fmaf(w[7], x1.w, acc[i]);
-    }
-  }
-}
-
-// sum the k-groups' partials into the kg == 0 threads (every thread of the block must call this)
-template <int NR, int KS>
-__device__ __forceinline__ void kreduce(float (&acc)[NR], float* part, int j, int kg) {
-  if (KS == 1) return;
-  if (kg > 0)
-#pragma unroll
-    for (int i = 0; i < NR; ++i) part[((kg - 1) * NR + i) * kCols + j] = acc[i];
-  __syncthreads();
-  if (kg == 0)
-    for (int g = 1; g < KS; ++g)
-#pragma unroll
-      for (int i = 0; i < NR; ++i) acc[i] += part[((g - 1) * NR + i) * kCols + j];
-  __syncthreads();
-}
-
-// block-wide sum over NW waves of N (<= 32) per-thread partials -> out[0..N)
-template <int N, int NW>
-__device__ inline void block_sum_w(float (&v)[N], float (*red)[32], float* out) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    float x = v[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
-    if (lane == 0) red[wave][i] = x;
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < N) {
-    float t = 0.0f;
-    for (int w = 0; w < NW; ++w) t += red[w][threadIdx.x];
-    out[threadIdx.x] = t;
-  }
-  __syncthreads();
-}
-
-// per-row scalar slots in LDS
-enum { S_MEAN, S_LSRAW, S_STD, S_Z, S_A, S_LOGP, S_Q1, S_Q2, S_T1, S_T2, S_DQ1, S_DQ2, S_DMEAN, S_DLS, S_NSLOT };
-
-template <int RR, int KS>
-__global__ __launch_bounds__(kCols* KS) void sac_rows_kernel(RowsArgs a) {
-  constexpr int NW = kCols * KS / 64;
-  const Layout& L = a.L;
-  const int H = L.H, O = L.O, B = L.B;
-  const int tid = threadIdx.x;
-  const int j = tid % kCols, kg = tid / kCols;
-  const bool col = j < H;
-  const bool lead = kg == 0 && col;  // finalises column j
-  const int r0 = blockIdx.x * RR;
-  const float* P = a.params;
-  const float* TG = a.targets;
-
-  __shared__ float s_x[2 * RR][kXLd];  // actor inputs: obs rows | next_obs rows
-  __shared__ float s_act[RR], s_rew[RR], s_term[RR], s_eps[2 * RR];
-  __shared__ __attribute__((aligned(16))) float s_h1[2 * RR][SACF_MAX_HIDDEN];
-  __shared__ __attribute__((aligned(16))) float s_h2[2 * RR][SACF_MAX_HIDDEN];
-  __shared__ __attribute__((aligned(16))) float s_g1[2][2 * RR][SACF_MAX_HIDDEN];  // critic rows: (obs, ã) | (obs, a)
-  __shared__ __attribute__((aligned(16))) float s_g2[2][2 * RR][SACF_MAX_HIDDEN];
-  __shared__ float s_part[(KS > 1 ? KS - 1 : 1) * 2 * RR * kCols];
-  __shared__ float s_red[NW][32];
-  __shared__ float s_sum[32];
-  __shared__ float s_row[S_NSLOT][2 * RR];
-
-  // ---- batch rows + reparameterisation noise ----
-  if (tid < RR) {
-    const int r = r0 + tid;
-    int64_t idx = r;
-    uint32_t c[4] = {(uint32_t)r, (uint32_t)*a.step, (uint32_t)((uint64_t)*a.step >> 32), 0x5AC0u};
-    if (a.sampled || !a.eps) philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-    if (a.sampled) {
-      const int64_t size = *a.size_dev > 0 ? *a.size_dev : 1;
-      const double u = ((double)c[0] + 0.5) * (1.0 / 4294967296.0);
-      idx = (int64_t)(u * (double)size);
-      if (idx >= a.capacity) idx = a.capacity - 1;
-    }
-    float e0, e1;
-    if (a.eps) {
-      e0 = a.eps[r];
-      e1 = a.eps[B + r];
-    } else {  // Box-Muller on two 32-bit uniforms
-      const float u1 = ((float)c[1] + 1.0f) * 2.3283064365386963e-10f;
-      const float u2 = (float)c[2] * 2.3283064365386963e-10f;
-      const float rad = sqrtf(-2.0f * logf(u1));
-      e0 = rad * cosf(6.283185307179586f * u2);
-      e1 = rad * sinf(6.283185307179586f * u2);
-    }
-    for (int m = 0; m < O; ++m) {
-      s_x[tid][m] = a.obs[idx * O + m];
-      s_x[RR + tid][m] = a.nobs[idx * O + m];
-    }
-    s_act[tid] = a.act[idx];
-    s_rew[tid] = a.rew[idx];
-    s_term[tid] = a.term[idx];
-    s_eps[tid] = e0;
-    s_eps[RR + tid] = e1;
-  }
-  __syncthreads();
-
-  // ---- actor forward on 2RR rows (gaussian_policy.py:105-118) ----
-  if (lead) {
-    float acc[2 * RR];
-    const float b = P[L.p_b1 + j];
-#pragma unroll
-    for (int i = 0; i < 2 * RR; ++i) acc[i] = b;
-    for (int m = 0; m < O; ++m) {
-      const float w = P[L.p_w1 + (int64_t)j * O + m];
-#pragma unroll
-      for (int i = 0; i < 2 * RR; ++i) acc[i] = fmaf(w, s_x[i][m], acc[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 2 * RR; ++i) s_h1[i][j] = relu(acc[i]);
-  }
-  __syncthreads();
-  {
-    float acc[2 * RR];
-    const float b = lead ? P[L.p_b2 + j] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 2 * RR; ++i) acc[i] = b;
-    if (col) mv_part<2 * RR, KS>(a.T, H, &s_h1[0][0], SACF_MAX_HIDDEN, j, kg, acc);
-    kreduce<2 * RR, KS>(acc, s_part, j, kg);
-    if (lead)
-#pragma unroll
-      for (int i = 0; i < 2 * RR; ++i) s_h2[i][j] = relu(acc[i]);
-  }
-  __syncthreads();
-  {
-    float v[4 * RR];
-    const float wm = lead ? P[L.p_wm + j] : 0.0f, ws = lead ? P[L.p_ws + j] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 2 * RR; ++i) {
-      const float h = lead ? s_h2[i][j] : 0.0f;
-      v[i] = wm * h;
-      v[2 * RR + i] = ws * h;
-    }
-    block_sum_w<4 * RR, NW>(v, s_red, s_sum);
-  }
-  if (tid < 2 * RR) {  // TanhNormal.rsample_and_logprob (distributions.py:346-392)
-    const int i = tid;
-    const float mean = s_sum[i] + P[L.p_bm];
-    const float ls_raw = s_sum[2 * RR + i] + P[L.p_bs];
-    const float log_std = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
-    const float std = expf(log_std);
-    const float z = mean + std * s_eps[i];
-    const float act = tanhf(z);
-    const float var = std * std;
-    const float d = z - mean;
-    const float lp = -(d * d) / (2.0f * var) - logf(std) - kLogSqrt2Pi;
-    const float corr = -2.0f * (kLog2 - z - softplus(-2.0f * z));
-    s_row[S_MEAN][i] = mean;
-    s_row[S_LSRAW][i] = ls_raw;
-    s_row[S_STD][i] = std;
-    s_row[S_Z][i] = z;
-    s_row[S_A][i] = act;
-    s_row[S_LOGP][i] = lp + corr;
-  }
-  __syncthreads();
-
-  // ---- critics on (obs, ã) rows 0..RR-1 and (obs, a) rows RR..2RR-1 ----
-  if (lead) {
-    for (int k = 0; k < 2; ++k) {
-      const float* C = P + L.q_base[k];
-      float base[RR];
-      const float b = C[L.c_b1 + j];
-#pragma unroll
-      for (int i = 0; i < RR; ++i) base[i] = b;
-      for (int m = 0; m < O; ++m) {
-        const float w = C[L.c_w1 + (int64_t)j * (O + 1) + m];
-#pragma unroll
-        for (int i = 0; i < RR; ++i) base[i] = fmaf(w, s_x[i][m], base[i]);
-      }
-      const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
-#pragma unroll
-      for (int i = 0; i < RR; ++i) {
-        s_g1[k][i][j] = relu(fmaf(wa, s_row[S_A][i], base[i]));
-        s_g1[k][RR + i][j] = relu(fmaf(wa, s_act[i], base[i]));
-      }
-    }
-  }
-  __syncthreads();
-  for (int k = 0; k < 2; ++k) {
-    const float* C = P + L.q_base[k];
-    float acc[2 * RR];
-    const float b = lead ? C[L.c_b2 + j] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 2 * RR; ++i) acc[i] = b;
-    if (col) mv_part<2 * RR, KS>(a.T + (size_t)(1 + k) * H * H, H, &s_g1[k][0][0], SACF_MAX_HIDDEN, j, kg, acc);
-    kreduce<2 * RR, KS>(acc, s_part, j, kg);
-    if (lead)
-#pragma unroll
-      for (int i = 0; i < 2 * RR; ++i) s_g2[k][i][j] = relu(acc[i]);
-  }
-  __syncthreads();
-  {
-    float v[4 * RR];
-    const float w0 = lead ? P[L.q_base[0] + L.c_w3 + j] : 0.0f, w1 = lead ? P[L.q_base[1] + L.c_w3 + j] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 2 * RR; ++i) {
-      v[i] = lead ? w0 * s_g2[0][i][j] : 0.0f;
-      v[2 * RR + i] = lead ? w1 * s_g2[1][i][j] : 0.0f;
-    }
-    block_sum_w<4 * RR, NW>(v, s_red, s_sum);
-  }
-  if (tid < 2 * RR) {
-    s_row[S_Q1][tid] = s_sum[tid] + P[L.q_base[0] + L.c_b3];
-    s_row[S_Q2][tid] = s_sum[2 * RR + tid] + P[L.q_base[1] + L.c_b3];
-  }
-  __syncthreads();
-
-  // ---- target critics on (next_obs, ã') (rows RR..2RR-1 of s_h1/s_h2 are free now) ----
-  for (int k = 0; k < 2; ++k) {
-    const float* C = TG + (int64_t)k * L.q_size;
-    if (lead) {
-      float acc[RR];
-      const float b = C[L.c_b1 + j];
-#pragma unroll
-      for (int i = 0; i < RR; ++i) acc[i] = b;
-      for (int m = 0; m < O; ++m) {
-        const float w = C[L.c_w1 + (int64_t)j * (O + 1) + m];
-#pragma unroll
-        for (int i = 0; i < RR; ++i) acc[i] = fmaf(w, s_x[RR + i][m], acc[i]);
-      }
-      const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
-#pragma unroll
-      for (int i = 0; i < RR; ++i) s_h1[RR + i][j] = relu(fmaf(wa, s_row[S_A][RR + i], acc[i]));
-    }
-    __syncthreads();
-    {
-      float acc[RR];
-      const float b = lead ? C[L.c_b2 + j] : 0.0f;
-#pragma unroll
-      for (int i = 0; i < RR; ++i) acc[i] = b;
-      if (col) mv_part<RR, KS>(a.T + (size_t)(3 + k) * H * H, H, &s_h1[RR][0], SACF_MAX_HIDDEN, j, kg, acc);
-      kreduce<RR, KS>(acc, s_part, j, kg);
-      if (lead)
-#pragma unroll
-        for (int i = 0; i < RR; ++i) s_h2[RR + i][j] = relu(acc[i]);
-    }
-    __syncthreads();
-    float v[RR];
-    const float w3 = lead ? C[L.c_w3 + j] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < RR; ++i) v[i] = lead ? w3 * s_h2[RR + i][j] : 0.0f;
-    block_sum_w<RR, NW>(v, s_red, s_sum);
-    if (tid < RR) s_row[k == 0 ? S_T1 : S_T2][tid] = s_sum[tid] + C[L.c_b3];
-    __syncthreads();
-  }
-
-  // ---- losses and output gradients per row (sac.py:170-247) ----
-  const float log_alpha = P[0];
-  const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
-  const float invB = 1.0f / (float)B;
-  if (tid < RR) {
-    const int i = tid, r = r0 + i;
-    const float q1a = s_row[S_Q1][i], q2a = s_row[S_Q2][i];
-    const float q1b = s_row[S_Q1][RR + i], q2b = s_row[S_Q2][RR + i];
-    const float tq = fminf(s_row[S_T1][i], s_row[S_T2][i]) - alpha * s_row[S_LOGP][RR + i];
-    float qt = a.hp.rscale * s_rew[i] + ((1.0f - s_term[i]) * a.hp.gamma) * tq;
-    qt = fminf(fmaxf(qt, -a.hp.clip), a.hp.clip);
-    const float qmin = fminf(q1a, q2a);
-    // torch.minimum backward: the smaller input takes the gradient, ties split it in half
-    const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
-    const float w2 = 1.0f - w1;
-    s_row[S_DQ1][i] = -w1 * invB;
-    s_row[S_DQ2][i] = -w2 * invB;
-    const float dq1b = (2.0f * invB) * (q1b - qt), dq2b = (2.0f * invB) * (q2b - qt);
-    s_row[S_DQ1][RR + i] = dq1b;
-    s_row[S_DQ2][RR + i] = dq2b;
-    a.sc.q_dq[0][r] = dq1b;
-    a.sc.q_dq[1][r] = dq2b;
-    const float logp = s_row[S_LOGP][i], act = s_row[S_A][i];
-    a.sc.p_pl[r] = alpha * logp - qmin + (a.hp.areg != 0.0f ? a.hp.areg * (act * act) : 0.0f);
-    a.sc.p_q1l[r] = (q1b - qt) * (q1b - qt);
-    a.sc.p_q2l[r] = (q2b - qt) * (q2b - qt);
-    a.sc.p_la[r] = -(log_alpha * (logp + a.hp.tent));
-    a.sc.p_ga[r] = -(logp + a.hp.tent);
-    float* st = a.stats + 8;
-    st[r] = q1b;
-    st[B + r] = q2b;
-    st[2 * B + r] = qt;
-    st[3 * B + r] = logp;
-    st[4 * B + r] = tanhf(s_row[S_MEAN][i]);
-    st[5 * B + r] = s_row[S_STD][i];
-    for (int m = 0; m < kXLd; ++m) {
-      const float x = m < O ? s_x[i][m] : (m == O ? s_act[i] : 0.0f);
-      a.sc.q_x[0][(int64_t)r * kXLd + m] = x;
-      a.sc.q_x[1][(int64_t)r * kXLd + m] = x;
-      a.sc.a_x[(int64_t)r * kXLd + m] = m < O ? s_x[i][m] : 0.0f;
-    }
-  }
-  __syncthreads();
-
-  // ---- critic backward: dg2 = dq·w3 ⊙ [g2 > 0], dg1 = (W2ᵀ dg2) ⊙ [g1 > 0] ----
-  if (lead) {
-    for (int k = 0; k < 2; ++k) {
-      const float* C = P + L.q_base[k];
-      const float* dq = s_row[k == 0 ? S_DQ1 : S_DQ2];
-      const float w3 = C[L.c_w3 + j];
-#pragma unroll
-      for (int i = 0; i < 2 * RR; ++i) {
-        const float g2 = s_g2[k][i][j];
-        const float dg2 = g2 > 0.0f ? dq[i] * w3 : 0.0f;
-        if (i >= RR) {
-          const int64_t o = (int64_t)(r0 + i - RR) * H + j;
-          a.sc.q_g2[k][o] = g2;
-          a.sc.q_dg2[k][o] = dg2;
-        }
-        s_g2[k][i][j] = dg2;
-      }
-    }
-  }
-  __syncthreads();
-  {
-    float v[2 * RR];  // d(ã) partials for the policy rows, both critics
-    for (int k = 0; k < 2; ++k) {
-      const float* C = P + L.q_base[k];
-      float acc[2 * RR];
-#pragma unroll
-      for (int i = 0; i < 2 * RR; ++i) acc[i] = 0.0f;
-      // Σ_jj W2[jj][m]·dg2[i][jj] with m = this column: W2 row-major reads are coalesced over m
-      if (col) mv_part<2 * RR, KS>(C + L.c_w2, H, &s_g2[k][0][0], SACF_MAX_HIDDEN, j, kg, acc);
-      kreduce<2 * RR, KS>(acc, s_part, j, kg);
-      const float wa = lead ? C[L.c_w1 + (int64_t)j * (O + 1) + O] : 0.0f;
-#pragma unroll
-      for (int i = 0; i < 2 * RR; ++i) {
-        const float g1 = lead ? s_g1[k][i][j] : 0.0f;
-        const float dg1 = g1 > 0.0f ? acc[i] : 0.0f;
-        if (i < RR) {
-          v[k * RR + i] = wa * dg1;
-        } else if (lead) {
-          const int64_t o = (int64_t)(r0 + i - RR) * H + j;
-          a.sc.q_g1[k][o] = g1;  // (obs, a) rows feed the weight gradients
-          a.sc.q_dg1[k][o] = dg1;
-        }
-      }
-    }
-    block_sum_w<2 * RR, NW>(v, s_red, s_sum);
-  }
-
-  // ---- actor backward on the obs rows ----
-  if (tid < RR) {
-    const int i = tid, r = r0 + i;
-    const float act = s_row[S_A][i], z = s_row[S_Z][i], mean = s_row[S_MEAN][i], std = s_row[S_STD][i];
-    const float ls_raw = s_row[S_LSRAW][i];
-    float dA = s_sum[i] + s_sum[RR + i];
-    if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
-    const float ainv = alpha * invB;
-    const float d = z - mean, var = std * std;
-    const float sig = 1.0f / (1.0f + expf(2.0f * z));  // sigmoid(-2z)
-    const float gz = dA * (1.0f - act * act) + ainv * (-(d / var) + (2.0f - 4.0f * sig));
-    const float dmean = gz + ainv * (d / var);
-    const float dstd = gz * s_eps[i] + ainv * ((d * d) / (var * std) - 1.0f / std);
-    const float dls = (ls_raw >= -20.0f && ls_raw <= 2.0f) ? dstd * std : 0.0f;
-    s_row[S_DMEAN][i] = dmean;
-    s_row[S_DLS][i] = dls;
-    a.sc.a_dhead[(int64_t)r * 2] = dmean;
-    a.sc.a_dhead[(int64_t)r * 2 + 1] = dls;
-  }
-  __syncthreads();
-  if (lead) {
-    const float wm = P[L.p_wm + j], ws = P[L.p_ws + j];
-#pragma unroll
-    for (int i = 0; i < RR; ++i) {
-      const float h2 = s_h2[i][j];
-      const float dh2 = h2 > 0.0f ? (wm * s_row[S_DMEAN][i] + ws * s_row[S_DLS][i]) : 0.0f;
-      const int64_t o = (int64_t)(r0 + i) * H + j;
-      a.sc.a_h2[o] = h2;
-      a.sc.a_dh2[o] = dh2;
-      s_h2[i][j] = dh2;
-    }
-  }
-  __syncthreads();
-  {
-    float acc[RR];
-#pragma unroll
-    for (int i = 0; i < RR; ++i) acc[i] = 0.0f;
-    if (col) mv_part<RR, KS>(P + L.p_w2, H, &s_h2[0][0], SACF_MAX_HIDDEN, j, kg, acc);
-    kreduce<RR, KS>(acc, s_part, j, kg);
-    if (lead) {
-#pragma unroll
-      for (int i = 0; i < RR; ++i) {
-        const float h1 = s_h1[i][j];
-        const int64_t o = (int64_t)(r0 + i) * H + j;
-        a.sc.a_h1[o] = h1;
-        a.sc.a_dh1[o] = h1 > 0.0f ? acc[i] : 0.0f;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// rows kernel, one batch row per block, four 256-thread groups working on independent matrices:
-// the six critic / target-critic rows of the forward pass are one phase (group g = Q1, Q2, T1, T2,
-// each over the full K), the twin-critic backward is one phase (two groups per critic, split-K 2).
-// Same math as sac_rows_kernel<1, 4>; 4 H x H matvec phases per block instead of 8.
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kCols * 4) void sac_rows_g4_kernel(RowsArgs a) {
-  constexpr int NW = kCols * 4 / 64;
-  const Layout& L = a.L;
-  const int H = L.H, O = L.O, B = L.B;
-  const int tid = threadIdx.x;
-  const int j = tid % kCols, kg = tid / kCols;
-  const bool col = j < H;
-  const bool lead = kg == 0 && col;
-  const int r = blockIdx.x;
-  const float* P = a.params;
-  const float* TG = a.targets;
-  SAC_MARK(0);
-
-  __shared__ float s_x[2][kXLd];  // obs row | next_obs row
-  __shared__ float s_act, s_rew, s_term, s_eps[2];
-  __shared__ __attribute__((aligned(16))) float s_h1[2][SACF_MAX_HIDDEN];     // actor: obs | next_obs
-  __shared__ __attribute__((aligned(16))) float s_h2[2][SACF_MAX_HIDDEN];
-  __shared__ __attribute__((aligned(16))) float s_g1[4][2][SACF_MAX_HIDDEN];  // Q1, Q2: (obs, ã) | (obs, a); T1, T2: row 0
-  __shared__ __attribute__((aligned(16))) float s_g2[4][2][SACF_MAX_HIDDEN];
-  __shared__ float s_part[3 * 2 * kCols];
-  __shared__ float s_red[NW][32];
-  __shared__ float s_sum[32];
-  __shared__ float s_row[S_NSLOT][2];
-
-  // ---- batch row + reparameterisation noise ----
-  if (tid == 0) {
-    int64_t idx = r;
-    uint32_t c[4] = {(uint32_t)r, (uint32_t)*a.step, (uint32_t)((uint64_t)*a.step >> 32), 0x5AC0u};
-    if (a.sampled || !a.eps) philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-    if (a.sampled) {
-      const int64_t size = *a.size_dev > 0 ? *a.size_dev : 1;
-      const double u = ((double)c[0] + 0.5) * (1.0 / 4294967296.0);
-      idx = (int64_t)(u * (double)size);
-      if (idx >= a.capacity) idx = a.capacity - 1;
-    }
-    float e0, e1;
-    if (a.eps) {
-      e0 = a.eps[r];
-      e1 = a.eps[B + r];
-    } else {
-      const float u1 = ((float)c[1] + 1.0f) * 2.3283064365386963e-10f;
-      const float u2 = (float)c[2] * 2.3283064365386963e-10f;
-      const float rad = sqrtf(-2.0f * logf(u1));
-      e0 = rad * cosf(6.283185307179586f * u2);
-      e1 = rad * sinf(6.283185307179586f * u2);
-    }
-    for (int m = 0; m < O; ++m) {
-      s_x[0][m] = a.obs[idx * O + m];
-      s_x[1][m] = a.nobs[idx * O + m];
-    }
-    s_act = a.act[idx];
-    s_rew = a.rew[idx];
-    s_term = a.term[idx];
-    s_eps[0] = e0;
-    s_eps[1] = e1;
-  }
-  __syncthreads();
-  SAC_MARK(1);
-
-  // ---- actor forward on obs and next_obs ----
-  if (lead) {
-    float acc[2];
-    const float b = P[L.p_b1 + j];
-    acc[0] = b;
-    acc[1] = b;
-    for (int m = 0; m < O; ++m) {
-      const float w = P[L.p_w1 + (int64_t)j * O + m];
-      acc[0] = fmaf(w, s_x[0][m], acc[0]);
-      acc[1] = fmaf(w, s_x[1][m], acc[1]);
-    }
-    s_h1[0][j] = relu(acc[0]);
-    s_h1[1][j] = relu(acc[1]);
-  }
-  __syncthreads();
-  SAC_MARK(2);
-  {
-    float acc[2];
-    const float b = lead ? P[L.p_b2 + j] : 0.0f;
-    acc[0] = b;
-    acc[1] = b;
-    if (col) mv_part<2, 4>(a.T, H, &s_h1[0][0], SACF_MAX_HIDDEN, j, kg, acc);
-    kreduce<2, 4>(acc, s_part, j, kg);
-    if (lead) {
-      s_h2[0][j] = relu(acc[0]);
-      s_h2[1][j] = relu(acc[1]);
-    }
-  }
-  __syncthreads();
-  SAC_MARK(3);
-  {
-    float v[4];
-    const float wm = lead ? P[L.p_wm + j] : 0.0f, ws = lead ? P[L.p_ws + j] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float h = lead ? s_h2[i][j] : 0.0f;
-      v[i] = wm * h;
-      v[2 + i] = ws * h;
-    }
-    block_sum_w<4, NW>(v, s_red, s_sum);
-  }
-  if (tid < 2) {  // TanhNormal.rsample_and_logprob (distributions.py:346-392)
-    const int i = tid;
-    const float mean = s_sum[i] + P[L.p_bm];
-    const float ls_raw = s_sum[2 + i] + P[L.p_bs];
-    const float log_std = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
-    const float std = expf(log_std);
-    const float z = mean + std * s_eps[i];
-    const float act = tanhf(z);
-    const float var = std * std;
-    const float d = z - mean;
-    const float lp = -(d * d) / (2.0f * var) - logf(std) - kLogSqrt2Pi;
-    const float corr = -2.0f * (kLog2 - z - softplus(-2.0f * z));
-    s_row[S_MEAN][i] = mean;
-    s_row[S_LSRAW][i] = ls_raw;
-    s_row[S_STD][i] = std;
-    s_row[S_Z][i] = z;
-    s_row[S_A][i] = act;
-    s_row[S_LOGP][i] = lp + corr;
-  }
-  __syncthreads();
-  SAC_MARK(4);
-
-  // ---- first layers: group g = Q1, Q2 on (obs, ã) | (obs, a); T1, T2 on (next_obs, ã') ----
-  const bool is_t = kg >= 2;
-  const float* C = is_t ? TG + (int64_t)(kg - 2) * L.q_size : P + L.q_base[kg];
-  if (col) {
-    const float* xin = s_x[is_t ? 1 : 0];
-    float base = C[L.c_b1 + j];
-    for (int m = 0; m < O; ++m) base = fmaf(C[L.c_w1 + (int64_t)j * (O + 1) + m], xin[m], base);
-    const float wa = C[L.c_w1 + (int64_t)j * (O + 1) + O];
-    if (is_t) {
-      s_g1[kg][0][j] = relu(fmaf(wa, s_row[S_A][1], base));
-    } else {
-      s_g1[kg][0][j] = relu(fmaf(wa, s_row[S_A][0], base));
-      s_g1[kg][1][j] = relu(fmaf(wa, s_act, base));
-    }
-  }
-  __syncthreads();
-  SAC_MARK(5);
-  // ---- second layers, all four at once (full K per group) ----
-  if (col) {
-    const float b = C[L.c_b2 + j];
-    float acc[2] = {b, b};
-    const float* WT = a.T + (size_t)(1 + kg) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
-    if (is_t) {
-      float a1[1] = {b};
-      mv_part<1, 1>(WT, H, &s_g1[kg][0][0], SACF_MAX_HIDDEN, j, 0, a1);
-      acc[0] = a1[0];
-    } else {
-      mv_part<2, 1>(WT, H, &s_g1[kg][0][0], SACF_MAX_HIDDEN, j, 0, acc);
-    }
-    s_g2[kg][0][j] = relu(acc[0]);
-    if (!is_t) s_g2[kg][1][j] = relu(acc[1]);
-  }
-  __syncthreads();
-  SAC_MARK(6);
-  {
-    // heads: Q1 (2 rows), Q2 (2 rows), T1, T2 -> v[0..5]
-    float v[6] = {0, 0, 0, 0, 0, 0};
-    if (col) {
-      const float w3 = C[L.c_w3 + j];
-      if (is_t) {
-        v[4 + (kg - 2)] = w3 * s_g2[kg][0][j];
-      } else {
-        v[2 * kg] = w3 * s_g2[kg][0][j];
-        v[2 * kg + 1] = w3 * s_g2[kg][1][j];
-      }
-    }
-    block_sum_w<6, NW>(v, s_red, s_sum);
-  }
-  const float log_alpha = P[0];
-  const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
-  const float invB = 1.0f / (float)B;
-  if (tid == 0) {  // losses and output gradients (sac.py:170-247)
-    const float q1a = s_sum[0] + P[L.q_base[0] + L.c_b3], q1b = s_sum[1] + P[L.q_base[0] + L.c_b3];
-    const float q2a = s_sum[2] + P[L.q_base[1] + L.c_b3], q2b = s_sum[3] + P[L.q_base[1] + L.c_b3];
-    const float t1 = s_sum[4] + TG[L.c_b3], t2 = s_sum[5] + TG[L.q_size + L.c_b3];
-    const float tq = fminf(t1, t2) - alpha * s_row[S_LOGP][1];
-    float qt = a.hp.rscale * s_rew + ((1.0f - s_term) * a.hp.gamma) * tq;
-    qt = fminf(fmaxf(qt, -a.hp.clip), a.hp.clip);
-    const float qmin = fminf(q1a, q2a);
-    const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
-    const float w2 = 1.0f - w1;
-    s_row[S_DQ1][0] = -w1 * invB;
-    s_row[S_DQ2][0] = -w2 * invB;
-    const float dq1b = (2.0f * invB) * (q1b - qt), dq2b = (2.0f * invB) * (q2b - qt);
-    s_row[S_DQ1][1] = dq1b;
-    s_row[S_DQ2][1] = dq2b;
-    a.sc.q_dq[0][r] = dq1b;
-    a.sc.q_dq[1][r] = dq2b;
-    const float logp = s_row[S_LOGP][0], act = s_row[S_A][0];
-    a.sc.p_pl[r] = alpha * logp - qmin + (a.hp.areg != 0.0f ? a.hp.areg * (act * act) : 0.0f);
-    a.sc.p_q1l[r] = (q1b - qt) * (q1b - qt);
-    a.sc.p_q2l[r] = (q2b - qt) * (q2b - qt);
-    a.sc.p_la[r] = -(log_alpha * (logp + a.hp.tent));
-    a.sc.p_ga[r] = -(logp + a.hp.tent);
-    float* st = a.stats + 8;
-    st[r] = q1b;
-    st[B + r] = q2b;
-    st[2 * B + r] = qt;
-    st[3 * B + r] = logp;
-    st[4 * B + r] = tanhf(s_row[S_MEAN][0]);
-    st[5 * B + r] = s_row[S_STD][0];
-  } else if (tid >= 64 && tid < 64 + kXLd) {
-    const int m = tid - 64;
-    const float x = m < O ? s_x[0][m] : (m == O ? s_act : 0.0f);
-    a.sc.q_x[0][(int64_t)r * kXLd + m] = x;
-    a.sc.q_x[1][(int64_t)r * kXLd + m] = x;
-    a.sc.a_x[(int64_t)r * kXLd + m] = m < O ? s_x[0][m] : 0.0f;
-  }
-  __syncthreads();
-  SAC_MARK(7);
-
-  // ---- critic backward: dg2 = dq·w3 ⊙ [g2 > 0] (groups 0, 1), then dg1 = (W2ᵀ dg2) ⊙ [g1 > 0] ----
-  if (col && kg < 2) {
-    const float* dq = s_row[kg == 0 ? S_DQ1 : S_DQ2];
-    const float w3 = C[L.c_w3 + j];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float g2 = s_g2[kg][i][j];
-      const float dg2 = g2 > 0.0f ? dq[i] * w3 : 0.0f;
-      if (i == 1) {
-        const int64_t o = (int64_t)r * H + j;
-        a.sc.q_g2[kg][o] = g2;
-        a.sc.q_dg2[kg][o] = dg2;
-      }
-      s_g2[kg][i][j] = dg2;
-    }
-  }
-  __syncthreads();
-  SAC_MARK(8);
-  {
-    // groups 0, 1 -> critic 0 (k halves), groups 2, 3 -> critic 1
-    const int k = kg >> 1, half = kg & 1;
-    const float* Ck = P + L.q_base[k];
-    float acc[2] = {0.0f, 0.0f};
-    if (col) mv_part<2, 2>(Ck + L.c_w2, H, &s_g2[k][0][0], SACF_MAX_HIDDEN, j, half, acc);
-    if (half) {
-      s_part[(k * 2 + 0) * kCols + j] = acc[0];
-      s_part[(k * 2 + 1) * kCols + j] = acc[1];
-    }
-    __syncthreads();
-    float v[2] = {0.0f, 0.0f};
-    if (!half && col) {
-      acc[0] += s_part[(k * 2 + 0) * kCols + j];
-      acc[1] += s_part[(k * 2 + 1) * kCols + j];
-      const float wa = Ck[L.c_w1 + (int64_t)j * (O + 1) + O];
-      const float g1a = s_g1[k][0][j], g1b = s_g1[k][1][j];
-      v[k] = wa * (g1a > 0.0f ? acc[0] : 0.0f);
-      const int64_t o = (int64_t)r * H + j;
-      a.sc.q_g1[k][o] = g1b;
-      a.sc.q_dg1[k][o] = g1b > 0.0f ? acc[1] : 0.0f;
-    }
-    block_sum_w<2, NW>(v, s_red, s_sum);
-  }
-
-  // ---- actor backward on the obs row ----
-  if (tid == 0) {
-    const float act = s_row[S_A][0], z = s_row[S_Z][0], mean = s_row[S_MEAN][0], std = s_row[S_STD][0];
-    const float ls_raw = s_row[S_LSRAW][0];
-    float dA = s_sum[0] + s_sum[1];
-    if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
-    const float ainv = alpha * invB;
-    const float d = z - mean, var = std * std;
-    const float sig = 1.0f / (1.0f + expf(2.0f * z));  // sigmoid(-2z)
-    const float gz = dA * (1.0f - act * act) + ainv * (-(d / var) + (2.0f - 4.0f * sig));
-    const float dmean = gz + ainv * (d / var);
-    const float dstd = gz * s_eps[0] + ainv * ((d * d) / (var * std) - 1.0f / std);
-    const float dls = (ls_raw >= -20.0f && ls_raw <= 2.0f) ? dstd * std : 0.0f;
-    s_row[S_DMEAN][0] = dmean;
-    s_row[S_DLS][0] = dls;
-    a.sc.a_dhead[(int64_t)r * 2] = dmean;
-    a.sc.a_dhead[(int64_t)r * 2 + 1] = dls;
-  }
-  __syncthreads();
-  SAC_MARK(9);
-  if (lead) {
-    const float wm = P[L.p_wm + j], ws = P[L.p_ws + j];
-    const float h2 = s_h2[0][j];
-    const float dh2 = h2 > 0.0f ? (wm * s_row[S_DMEAN][0] + ws * s_row[S_DLS][0]) : 0.0f;
-    const int64_t o = (int64_t)r * H + j;
-    a.sc.a_h2[o] = h2;
-    a.sc.a_dh2[o] = dh2;
-    s_h2[0][j] = dh2;
-  }
-  __syncthreads();
-  SAC_MARK(10);
-  {
-    float acc[1] = {0.0f};
-    if (col) mv_part<1, 4>(P + L.p_w2, H, &s_h2[0][0], SACF_MAX_HIDDEN, j, kg, acc);
-    kreduce<1, 4>(acc, s_part, j, kg);
-    if (lead) {
-      const float h1 = s_h1[0][j];
-      const int64_t o = (int64_t)r * H + j;
-      a.sc.a_h1[o] = h1;
-      a.sc.a_dh1[o] = h1 > 0.0f ? acc[0] : 0.0f;
-    }
-  }
-  SAC_MARK(11);
-}
-
-// ---------------------------------------------------------------------------------------------
-// weight gradients: out[j][k] = Σ_r dY[r·ldY + j] · X[r·ldX + k]  (X == nullptr: ones -> bias)
+// weight-gradient matrices: out[j][k] = Σ_r dY[r·ldY + j] · X[r·ldX + k]  (X == nullptr: ones -> bias)
 // ---------------------------------------------------------------------------------------------
 struct GMat {
   const float* dY;
@@ -871,23 +141,412 @@ struct GMat {
   int ldY, ldX, M, N;
   int64_t out_off;
 };
-struct GTask {
-  int mat, j0, k0;
-};
 constexpr int kMaxMats = 24;
-// Row split of the weight gradients: grid.y = kParts blocks per tile each reduce B / kParts rows
-// into partial gradient p (same layout as the flat gradient); sac_gsum_kernel adds the kParts
-// partials in a fixed order (deterministic) into the gradient.
-#ifndef SAC_KPARTS
-#define SAC_KPARTS 8
-#endif
-constexpr int kParts = SAC_KPARTS;
-struct WgradArgs {
+
+// ---------------------------------------------------------------------------------------------
+// MFMA path: the grad step as batched GEMMs on v_mfma_f32_32x32x2_f32 (exact fp32: an fmaf chain
+// in k order, MI355X_MICROARCH.md "Matrix cores"). Every GEMM runs in 32-row x 32-column output
+// tiles, one 256-thread block (4 waves) per tile, the K dimension split over the 4 waves and the 4
+// partial tiles summed in LDS in a fixed order. MFMA operand maps (cdna_hip_programming.md §3):
+// lane l holds A[l & 31][k] and B[k][l & 31] with k = kb + (l >> 5)·K/8 + i for MFMA i of the wave's
+// K/4-slice (a permuted k order: the sum is the same, the loads stay contiguous per lane / per half
+// wave); C/D: col = l & 31, row = (reg & 3) + 8·(reg >> 2) + 4·(l >> 5).
+//   sac_actor_fwd_kernel  : batch gather (replay sampling), h1 (VALU), h2 = relu(h1 W2ᵀ + b2) on 2B rows
+//   sac_critic_fwd_kernel : actor heads + TanhNormal sample per row, g1 (VALU), g2 = relu(g1 W2ᵀ + b2) for
+//                           Q1, Q2 on [(obs, ã); (obs, a)] and T1, T2 on (next_obs, ã')
+//   sac_critic_bwd_kernel : q heads, losses, dq, dg2 = dq·w3 ⊙ [g2 > 0], dg1 = (dg2 W2) ⊙ [g1 > 0]
+//   sac_actor_bwd_kernel  : dA, TanhNormal backward, dh2 = (wm dmean + ws dls) ⊙ [h2 > 0], dh1 = (dh2 W2) ⊙ [h1 > 0]
+//   sac_wgrad_mfma_kernel : dW = dYᵀ X for the H x H matrices (rows = K), the small ones on the VALU,
+//                           the loss scalars and d(log α)
+// ---------------------------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kTile2 = 32;  // output tile edge of the MFMA kernels
+constexpr int kMaxN2 = 32;  // MFMAs per wave per tile (K / 8 <= 32, i.e. K <= 256)
+
+struct MScratch {
+  float *x, *xn, *act, *rew, *term, *eps;  // gathered batch: obs / next_obs [B][kXLd], per row [B] (eps [2][B])
+  float *h2n;                              // actor h2 of the next_obs rows [B][H]
+  float *hd;                               // actor head of the obs rows [6][B]: mean, ls_raw, std, z, a, logp
+  float *hdn;                              // actor head of the next_obs rows [6][B]
+  float *g1pi[2], *g2pi[2];                // critics on (obs, ã) rows [B][H]
+  float *tg2[2];                           // target critics on (next_obs, ã') [B][H]
+  float *dg1pi[2];                         // critic input gradient on (obs, ã) rows [B][H]
+};
+enum { HD_MEAN, HD_LSRAW, HD_STD, HD_Z, HD_A, HD_LOGP };
+
+struct MArgs {
+  const float* params;
+  const float* targets;
+  const float* T;  // [actor W2ᵀ | q1 W2ᵀ | q2 W2ᵀ | t1 W2ᵀ | t2 W2ᵀ]
+  const float *obs, *act, *rew, *term, *nobs;
+  const int64_t* size_dev;
+  int64_t capacity;
+  uint64_t seed;
+  int sampled;
+  const float* eps;
+  const int64_t* step;
+  float* stats;
+  Scratch sc;
+  MScratch ms;
+  Layout L;
+  Hyper hp;
+};
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) z[g] = 0.0f;
+  return z;
+}
+
+// acc += Σ_i A_i ⊗ B_i over the wave's n2 MFMAs (a[i], b[i]: this lane's operands, see above)
+__device__ __forceinline__ void mfma_chain(f32x16& acc, const float (&a)[kMaxN2], const float (&b)[kMaxN2], int n2) {
+#pragma unroll
+  for (int i = 0; i < kMaxN2; ++i)
+    if (i < n2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[i], acc, 0, 0, 0);
+}
+
+// Sum of the 4 waves' partial tiles (wave 0 + 1 + 2 + 3, in that order), then epi(row, col, v) on the
+// 1024 outputs: wave w finishes accumulator registers 4w .. 4w + 3.
+template <class EPI>
+__device__ __forceinline__ void splitk_finish(const f32x16& acc, float* lds, EPI&& epi) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) lds[(w * 16 + g) * 64 + lane] = acc[g];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int g = 4 * w + q;
+    float v = lds[(0 * 16 + g) * 64 + lane];
+    v += lds[(1 * 16 + g) * 64 + lane];
+    v += lds[(2 * 16 + g) * 64 + lane];
+    v += lds[(3 * 16 + g) * 64 + lane];
+    epi((g & 3) + 8 * (g >> 2) + 4 * (lane >> 5), lane & 31, v);
+  }
+}
+
+// Σ_j x[j] w[j] over the row, split between the lane and its partner lane ^ 32 (halves of j);
+// both lanes return the same value (the two halves added in one order: lower half + upper half)
+__device__ __forceinline__ float row_dot(const float* __restrict__ x, const float* __restrict__ w, int H) {
+  const int h = (threadIdx.x >> 5) & 1, half = H / 2;
+  float s = 0.0f;
+  for (int j = h * half; j < (h + 1) * half; ++j) s = fmaf(x[j], w[j], s);  // w: flat params, not 16-B aligned
+  const float o = __shfl_xor(s, 32, 64);
+  return h ? o + s : s + o;
+}
+
+// one batch item (replay sample or given batch) and its two reparameterisation normals
+__device__ __forceinline__ int64_t batch_item(const MArgs& a, int r, float& e0, float& e1) {
+  int64_t idx = r;
+  uint32_t c[4] = {(uint32_t)r, (uint32_t)*a.step, (uint32_t)((uint64_t)*a.step >> 32), 0x5AC0u};
+  if (a.sampled || !a.eps) philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+  if (a.sampled) {
+    const int64_t size = *a.size_dev > 0 ? *a.size_dev : 1;
+    const double u = ((double)c[0] + 0.5) * (1.0 / 4294967296.0);
+    idx = (int64_t)(u * (double)size);
+    if (idx >= a.capacity) idx = a.capacity - 1;
+  }
+  if (a.eps) {
+    e0 = a.eps[r];
+    e1 = a.eps[a.L.B + r];
+  } else {
+    const float u1 = ((float)c[1] + 1.0f) * 2.3283064365386963e-10f;
+    const float u2 = (float)c[2] * 2.3283064365386963e-10f;
+    const float rad = sqrtf(-2.0f * logf(u1));
+    e0 = rad * cosf(6.283185307179586f * u2);
+    e1 = rad * sinf(6.283185307179586f * u2);
+  }
+  return idx;
+}
+
+// grid (2B / 32, H / 32): rows [0, B) are the obs rows, [B, 2B) the next_obs rows of the batch
+__global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
+  __shared__ float lds[4 * 16 * 64];
+  const Layout& L = a.L;
+  const int H = L.H, O = L.O, B = L.B;
+  const float* P = a.params;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
+  const int row = r0 + (lane & 31);
+  const bool nrow = row >= B;
+  const int item = nrow ? row - B : row;
+  float e0, e1;
+  const int64_t idx = batch_item(a, item, e0, e1);
+  const float* src = nrow ? a.nobs : a.obs;
+  float x[kXLd];
+#pragma unroll
+  for (int m = 0; m < kXLd; ++m) x[m] = m < O ? src[idx * O + m] : 0.0f;
+  if (blockIdx.y == 0 && w == 0 && h == 0) {  // the gathered batch for the later kernels
+    float* xd = (nrow ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
+    for (int m = 0; m < kXLd; ++m) xd[m] = x[m];
+    if (!nrow) {
+      a.ms.act[item] = a.act[idx];
+      a.ms.rew[item] = a.rew[idx];
+      a.ms.term[item] = a.term[idx];
+      a.ms.eps[item] = e0;
+      a.ms.eps[B + item] = e1;
+      for (int m = 0; m < kXLd; ++m) a.sc.a_x[(int64_t)item * kXLd + m] = m < O ? x[m] : 0.0f;
+    }
+  }
+  // h1 for this lane's k (fmaf chain from the bias, as fc0 computes it) and the W2ᵀ operand
+  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < kMaxN2; ++i) {
+    if (i >= n2) break;
+    const int k = kb + i;
+    float acc = P[L.p_b1 + k];
+    for (int m = 0; m < O; ++m) acc = fmaf(P[L.p_w1 + (int64_t)k * O + m], x[m], acc);
+    av[i] = relu(acc);
+    bv[i] = a.T[(int64_t)k * H + c0 + (lane & 31)];
+  }
+  if (blockIdx.y == 0 && !nrow)
+    for (int i = 0; i < n2; ++i) a.sc.a_h1[(int64_t)item * H + kb + i] = av[i];
+  f32x16 acc = zero16();
+  mfma_chain(acc, av, bv, n2);
+  splitk_finish(acc, lds, [&](int rr, int cc, float v) {
+    const int r = r0 + rr, col = c0 + cc;
+    const float y = relu(v + P[L.p_b2 + col]);
+    if (r < B) a.sc.a_h2[(int64_t)r * H + col] = y;
+    else a.ms.h2n[(int64_t)(r - B) * H + col] = y;
+  });
+}
+
+// TanhNormal.rsample_and_logprob (distributions.py:346-392) of one row's head
+__device__ __forceinline__ void tanh_normal(float mean, float ls_raw, float eps, float out[6]) {
+  const float log_std = fminf(fmaxf(ls_raw, -20.0f), 2.0f);
+  const float std = expf(log_std);
+  const float z = mean + std * eps;
+  const float act = tanhf(z);
+  const float var = std * std;
+  const float d = z - mean;
+  const float lp = -(d * d) / (2.0f * var) - logf(std) - kLogSqrt2Pi;
+  const float corr = -2.0f * (kLog2 - z - softplus(-2.0f * z));
+  out[HD_MEAN] = mean; out[HD_LSRAW] = ls_raw; out[HD_STD] = std; out[HD_Z] = z; out[HD_A] = act;
+  out[HD_LOGP] = lp + corr;
+}
+
+// grid (row tiles of [Q1: 2B | Q2: 2B | T1: B | T2: B], H / 32). Q rows [0, B): (obs, ã), [B, 2B): (obs, a)
+__global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
+  __shared__ float lds[4 * 16 * 64];
+  const Layout& L = a.L;
+  const int H = L.H, O = L.O, B = L.B;
+  const float* P = a.params;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  const int qt = 2 * B / kTile2, tt = B / kTile2;  // row tiles per critic / per target critic
+  int net, rt = blockIdx.x;
+  if (rt < 2 * qt) { net = rt / qt; rt %= qt; }
+  else { rt -= 2 * qt; net = 2 + rt / tt; rt %= tt; }
+  const bool is_t = net >= 2;
+  const float* C = is_t ? a.targets + (int64_t)(net - 2) * L.q_size : P + L.q_base[net];
+  const int r0 = rt * kTile2, c0 = blockIdx.y * kTile2;
+  const int row = r0 + (lane & 31);
+  const bool data = !is_t && row >= B;  // (obs, a) row
+  const int item = data ? row - B : row;
+  const bool store_rows = blockIdx.y == 0 && w == 0 && h == 0;
+  // input row: (obs, ã) / (obs, a) / (next_obs, ã')
+  const float* xr = (is_t ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
+  float act;
+  if (data) {
+    act = a.ms.act[item];
+  } else {  // actor head of the row and its sample
+    const float* h2 = (is_t ? a.ms.h2n : a.sc.a_h2) + (int64_t)item * H;
+    const float mean = row_dot(h2, P + L.p_wm, H) + P[L.p_bm];
+    const float ls = row_dot(h2, P + L.p_ws, H) + P[L.p_bs];
+    float hd[6];
+    tanh_normal(mean, ls, a.ms.eps[(is_t ? B : 0) + item], hd);
+    act = hd[HD_A];
+    if (store_rows && (net == 0 || net == 2))
+      for (int q = 0; q < 6; ++q) (is_t ? a.ms.hdn : a.ms.hd)[q * B + item] = hd[q];
+  }
+  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+  const float* WT = a.T + (int64_t)(1 + net) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
+#pragma unroll
+  for (int i = 0; i < kMaxN2; ++i) {
+    if (i >= n2) break;
+    const int k = kb + i;
+    float base = C[L.c_b1 + k];
+    for (int m = 0; m < O; ++m) base = fmaf(C[L.c_w1 + (int64_t)k * (O + 1) + m], xr[m], base);
+    av[i] = relu(fmaf(C[L.c_w1 + (int64_t)k * (O + 1) + O], act, base));
+    bv[i] = WT[(int64_t)k * H + c0 + (lane & 31)];
+  }
+  if (blockIdx.y == 0 && !is_t) {
+    float* g1 = (data ? a.sc.q_g1[net] : a.ms.g1pi[net]) + (int64_t)item * H;
+    for (int i = 0; i < n2; ++i) g1[kb + i] = av[i];
+    if (data && w == 0 && h == 0)
+      for (int m = 0; m < kXLd; ++m) a.sc.q_x[net][(int64_t)item * kXLd + m] = m < O ? xr[m] : (m == O ? act : 0.0f);
+  }
+  f32x16 acc = zero16();
+  mfma_chain(acc, av, bv, n2);
+  splitk_finish(acc, lds, [&](int rr, int cc, float v) {
+    const int r = r0 + rr, col = c0 + cc;
+    const float y = relu(v + C[L.c_b2 + col]);
+    if (is_t) a.ms.tg2[net - 2][(int64_t)r * H + col] = y;
+    else if (r >= B) a.sc.q_g2[net][(int64_t)(r - B) * H + col] = y;
+    else a.ms.g2pi[net][(int64_t)r * H + col] = y;
+  });
+}
+
+// grid (2 critics x 2B / 32 row tiles, H / 32): losses and dq (sac.py:170-247), dg2, dg1 = (dg2 W2) ⊙ [g1 > 0]
+__global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
+  __shared__ float lds[4 * 16 * 64];
+  const Layout& L = a.L;
+  const int H = L.H, B = L.B;
+  const float* P = a.params;
+  const float* TG = a.targets;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  const int qt = 2 * B / kTile2;
+  const int net = blockIdx.x / qt, rt = blockIdx.x % qt;
+  const float* C = P + L.q_base[net];
+  const int r0 = rt * kTile2, c0 = blockIdx.y * kTile2;
+  const int row = r0 + (lane & 31);
+  const bool data = row >= B;
+  const int item = data ? row - B : row;
+  const bool store_rows = net == 0 && blockIdx.y == 0 && w == 0 && h == 0;
+  const float log_alpha = P[0];
+  const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
+  const float invB = 1.0f / (float)B;
+  const float* g2row;
+  float dq;
+  if (data) {  // Q losses on (obs, a)
+    const float q1b = row_dot(a.sc.q_g2[0] + (int64_t)item * H, P + L.q_base[0] + L.c_w3, H) + P[L.q_base[0] + L.c_b3];
+    const float q2b = row_dot(a.sc.q_g2[1] + (int64_t)item * H, P + L.q_base[1] + L.c_w3, H) + P[L.q_base[1] + L.c_b3];
+    const float t1 = row_dot(a.ms.tg2[0] + (int64_t)item * H, TG + L.c_w3, H) + TG[L.c_b3];
+    const float t2 = row_dot(a.ms.tg2[1] + (int64_t)item * H, TG + L.q_size + L.c_w3, H) + TG[L.q_size + L.c_b3];
+    const float tq = fminf(t1, t2) - alpha * a.ms.hdn[HD_LOGP * B + item];
+    float qtv = a.hp.rscale * a.ms.rew[item] + ((1.0f - a.ms.term[item]) * a.hp.gamma) * tq;
+    qtv = fminf(fmaxf(qtv, -a.hp.clip), a.hp.clip);
+    const float dq1b = (2.0f * invB) * (q1b - qtv), dq2b = (2.0f * invB) * (q2b - qtv);
+    dq = net == 0 ? dq1b : dq2b;
+    g2row = a.sc.q_g2[net] + (int64_t)item * H;
+    if (store_rows) {
+      a.sc.q_dq[0][item] = dq1b;
+      a.sc.q_dq[1][item] = dq2b;
+      a.sc.p_q1l[item] = (q1b - qtv) * (q1b - qtv);
+      a.sc.p_q2l[item] = (q2b - qtv) * (q2b - qtv);
+      float* st = a.stats + 8;
+      st[item] = q1b;
+      st[B + item] = q2b;
+      st[2 * B + item] = qtv;
+    }
+  } else {  // policy loss through min(Q1, Q2)(obs, ã)
+    const float q1a = row_dot(a.ms.g2pi[0] + (int64_t)item * H, P + L.q_base[0] + L.c_w3, H) + P[L.q_base[0] + L.c_b3];
+    const float q2a = row_dot(a.ms.g2pi[1] + (int64_t)item * H, P + L.q_base[1] + L.c_w3, H) + P[L.q_base[1] + L.c_b3];
+    const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
+    dq = net == 0 ? -w1 * invB : -(1.0f - w1) * invB;
+    g2row = a.ms.g2pi[net] + (int64_t)item * H;
+    if (store_rows) {
+      const float logp = a.ms.hd[HD_LOGP * B + item], act = a.ms.hd[HD_A * B + item];
+      const float qmin = fminf(q1a, q2a);
+      a.sc.p_pl[item] = alpha * logp - qmin + (a.hp.areg != 0.0f ? a.hp.areg * (act * act) : 0.0f);
+      a.sc.p_la[item] = -(log_alpha * (logp + a.hp.tent));
+      a.sc.p_ga[item] = -(logp + a.hp.tent);
+      float* st = a.stats + 8;
+      st[3 * B + item] = logp;
+      st[4 * B + item] = tanhf(a.ms.hd[HD_MEAN * B + item]);
+      st[5 * B + item] = a.ms.hd[HD_STD * B + item];
+    }
+  }
+  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < kMaxN2; ++i) {
+    if (i >= n2) break;
+    const int j = kb + i;
+    const float g2 = g2row[j];
+    av[i] = g2 > 0.0f ? dq * C[L.c_w3 + j] : 0.0f;
+    bv[i] = C[L.c_w2 + (int64_t)j * H + c0 + (lane & 31)];
+  }
+  if (data && blockIdx.y == 0)
+    for (int i = 0; i < n2; ++i) a.sc.q_dg2[net][(int64_t)item * H + kb + i] = av[i];
+  f32x16 acc = zero16();
+  mfma_chain(acc, av, bv, n2);
+  splitk_finish(acc, lds, [&](int rr, int cc, float v) {
+    const int r = r0 + rr, col = c0 + cc;
+    if (r >= B) {
+      const int64_t o = (int64_t)(r - B) * H + col;
+      a.sc.q_dg1[net][o] = a.sc.q_g1[net][o] > 0.0f ? v : 0.0f;
+    } else {
+      const int64_t o = (int64_t)r * H + col;
+      a.ms.dg1pi[net][o] = a.ms.g1pi[net][o] > 0.0f ? v : 0.0f;
+    }
+  });
+}
+
+// grid (B / 32, H / 32): policy backward through the action (obs rows)
+__global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
+  __shared__ float lds[4 * 16 * 64];
+  const Layout& L = a.L;
+  const int H = L.H, O = L.O, B = L.B;
+  const float* P = a.params;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
+  const int item = r0 + (lane & 31);
+  const float log_alpha = P[0];
+  const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
+  const float invB = 1.0f / (float)B;
+  // dA = Σ_m wa1[m] dg1_Q1[m] + Σ_m wa2[m] dg1_Q2[m] (wa: the action column of each critic's fc0)
+  float dA;
+  {
+    const int half = H / 2;
+    float s[2] = {0.0f, 0.0f};
+    for (int k = 0; k < 2; ++k) {
+      const float* dg = a.ms.dg1pi[k] + (int64_t)item * H;
+      const float* C = P + L.q_base[k];
+      for (int m = h * half; m < (h + 1) * half; ++m) s[k] = fmaf(C[L.c_w1 + (int64_t)m * (O + 1) + O], dg[m], s[k]);
+      const float o = __shfl_xor(s[k], 32, 64);
+      s[k] = h ? o + s[k] : s[k] + o;
+    }
+    dA = s[0] + s[1];
+  }
+  const float act = a.ms.hd[HD_A * B + item], z = a.ms.hd[HD_Z * B + item], mean = a.ms.hd[HD_MEAN * B + item];
+  const float std = a.ms.hd[HD_STD * B + item], ls_raw = a.ms.hd[HD_LSRAW * B + item];
+  if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
+  const float ainv = alpha * invB;
+  const float d = z - mean, var = std * std;
+  const float sig = 1.0f / (1.0f + expf(2.0f * z));  // sigmoid(-2z)
+  const float gz = dA * (1.0f - act * act) + ainv * (-(d / var) + (2.0f - 4.0f * sig));
+  const float dmean = gz + ainv * (d / var);
+  const float dstd = gz * a.ms.eps[item] + ainv * ((d * d) / (var * std) - 1.0f / std);
+  const float dls = (ls_raw >= -20.0f && ls_raw <= 2.0f) ? dstd * std : 0.0f;
+  if (blockIdx.y == 0 && w == 0 && h == 0) {
+    a.sc.a_dhead[(int64_t)item * 2] = dmean;
+    a.sc.a_dhead[(int64_t)item * 2 + 1] = dls;
+  }
+  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < kMaxN2; ++i) {
+    if (i >= n2) break;
+    const int j = kb + i;
+    const float h2 = a.sc.a_h2[(int64_t)item * H + j];
+    av[i] = h2 > 0.0f ? (P[L.p_wm + j] * dmean + P[L.p_ws + j] * dls) : 0.0f;
+    bv[i] = P[L.p_w2 + (int64_t)j * H + c0 + (lane & 31)];
+  }
+  if (blockIdx.y == 0)
+    for (int i = 0; i < n2; ++i) a.sc.a_dh2[(int64_t)item * H + kb + i] = av[i];
+  f32x16 acc = zero16();
+  mfma_chain(acc, av, bv, n2);
+  splitk_finish(acc, lds, [&](int rr, int cc, float v) {
+    const int64_t o = (int64_t)(r0 + rr) * H + c0 + cc;
+    a.sc.a_dh1[o] = a.sc.a_h1[o] > 0.0f ? v : 0.0f;
+  });
+}
+
+// weight gradients into the flat gradient: out[j][k] = Σ_r dY[r][j] X[r][k] (X null: ones -> bias).
+// Blocks [0, n_mfma): 32 x 32 tiles of the H x H matrices on MFMA (rows split over the 4 waves);
+// then VALU blocks, one output element per thread (rows summed in order); the last block: the loss
+// scalars, d(log α), α, the Adam bias corrections of this step and step += 1.
+struct WgArgs {
   GMat mats[kMaxMats];
-  const GTask* tasks;
-  int n_tasks;
-  float* partials;          // [kParts][n_params]
-  int64_t n_params;
+  int n_mats;
+  int big[3];        // indices of the H x H matrices in mats
+  int n_mfma;        // MFMA tile blocks
+  int n_small;       // elements of the other matrices
+  int small_mat[kMaxMats];
+  int64_t small_start[kMaxMats + 1];  // prefix sums of M·N over the non-big matrices
+  int n_small_mats;
   float* grads;
   int B;
   Scratch sc;
@@ -897,10 +556,11 @@ struct WgradArgs {
   Hyper hp;
 };
 
-__global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
+__global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
+  __shared__ float lds[4 * 16 * 64];
   const int tid = threadIdx.x;
-  if ((int)blockIdx.x == a.n_tasks) {  // scalars: losses, α and d(log α); step += 1
-    if (blockIdx.y != 0) return;
+  const int n_small_blocks = (a.n_small + 255) / 256;
+  if ((int)blockIdx.x == a.n_mfma + n_small_blocks) {  // scalars
     float v[5] = {0, 0, 0, 0, 0};
     for (int r = tid; r < a.B; r += kThreads) {
       v[0] += a.sc.p_pl[r];
@@ -922,7 +582,6 @@ __global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
       a.grads[0] = a.hp.auto_ent ? sum[4] * invB : 0.0f;
       const int64_t step = *a.step + 1;
       *a.step = step;
-      // Adam bias corrections of this step for sac_apply_kernel (stats[5..7])
       const double t = (double)step;
       const double bc1 = 1.0 - pow((double)a.hp.beta1, t);
       const double bc2 = 1.0 - pow((double)a.hp.beta2, t);
@@ -932,64 +591,46 @@ __global__ __launch_bounds__(kThreads) void sac_wgrad_kernel(WgradArgs a) {
     }
     return;
   }
-  const GTask t = a.tasks[blockIdx.x];
-  const GMat m = a.mats[t.mat];
-  __shared__ float sY[32][64 + 1];
-  __shared__ float sX[32][64 + 1];
-  const int tj = tid >> 4, tk = tid & 15;
-  float acc[4][4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[p][q] = 0.0f;
-  const int part = blockIdx.y;
-  const int rows = (a.B + kParts - 1) / kParts;
-  const int r_lo = part * rows, r_hi = min(a.B, r_lo + rows);
-  for (int rb = r_lo; rb < r_hi; rb += 32) {
-    for (int e = tid; e < 32 * 64; e += kThreads) {
-      const int rr = e >> 6, cc = e & 63, r = rb + rr;
-      const int jj = t.j0 + cc, kk = t.k0 + cc;
-      sY[rr][cc] = (r < r_hi && jj < m.M) ? m.dY[(int64_t)r * m.ldY + jj] : 0.0f;
-      sX[rr][cc] = (r < r_hi && kk < m.N) ? (m.X ? m.X[(int64_t)r * m.ldX + kk] : 1.0f) : 0.0f;
+  if ((int)blockIdx.x >= a.n_mfma) {  // VALU elements
+    const int64_t e = (int64_t)(blockIdx.x - a.n_mfma) * 256 + tid;
+    if (e >= a.n_small) return;
+    int s = 0;
+    while (s + 1 < a.n_small_mats && e >= a.small_start[s + 1]) ++s;
+    const GMat m = a.mats[a.small_mat[s]];
+    const int64_t l = e - a.small_start[s];
+    const int j = (int)(l / m.N), k = (int)(l % m.N);
+    float acc = 0.0f;
+    for (int r = 0; r < a.B; ++r) {
+      const float x = m.X ? m.X[(int64_t)r * m.ldX + k] : 1.0f;
+      acc = fmaf(m.dY[(int64_t)r * m.ldY + j], x, acc);
     }
-    __syncthreads();
-#pragma unroll 4
-    for (int rr = 0; rr < 32; ++rr) {
-      float y[4], x[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) y[p] = sY[rr][tj * 4 + p];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[q] = sX[rr][tk * 4 + q];
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[p][q] = fmaf(y[p], x[q], acc[p][q]);
-    }
-    __syncthreads();
+    a.grads[m.out_off + l] = acc;
+    return;
   }
-  float* P = a.partials + (size_t)part * a.n_params;
+  // MFMA tile of an H x H matrix: A[j][r] = dY[r][j], B[r][k] = X[r][k]
+  const int H = a.mats[a.big[0]].M;
+  const int tiles = (H / kTile2) * (H / kTile2);
+  const GMat m = a.mats[a.big[blockIdx.x / tiles]];
+  const int t = blockIdx.x % tiles;
+  const int j0 = (t / (H / kTile2)) * kTile2, k0 = (t % (H / kTile2)) * kTile2;
+  const int w = tid >> 6, lane = tid & 63, h = lane >> 5;
+  const int rows_w = a.B / 4;  // this wave's rows, in chunks of up to 64 (32 MFMAs)
+  f32x16 acc = zero16();
+  for (int rc = 0; rc < rows_w; rc += 2 * kMaxN2) {
+    const int n2 = min(kMaxN2, (rows_w - rc) / 2), rb = w * rows_w + rc + h * n2;
+    float av[kMaxN2], bv[kMaxN2];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int jj = t.j0 + tj * 4 + p;
-    if (jj >= m.M) continue;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int kk = t.k0 + tk * 4 + q;
-      if (kk < m.N) P[m.out_off + (int64_t)jj * m.N + kk] = acc[p][q];
+    for (int i = 0; i < kMaxN2; ++i) {
+      if (i >= n2) break;
+      const int64_t r = rb + i;
+      av[i] = m.dY[r * m.ldY + j0 + (lane & 31)];
+      bv[i] = m.X[r * m.ldX + k0 + (lane & 31)];
     }
+    mfma_chain(acc, av, bv, n2);
   }
+  splitk_finish(acc, lds, [&](int rr, int cc, float v) { a.grads[m.out_off + (int64_t)(j0 + rr) * m.N + k0 + cc] = v; });
 }
 
-// gradient = Σ_p partial_p (p = 0..kParts-1 in order); element 0 (d log α) is the scalar block's
-__global__ __launch_bounds__(kThreads) void sac_gsum_kernel(const float* __restrict__ partials, float* grads,
-                                                            int64_t n_params) {
-  const int64_t e = 1 + (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (e >= n_params) return;
-  float g = partials[e];
-#pragma unroll
-  for (int p = 1; p < kParts; ++p) g += partials[(size_t)p * n_params + e];
-  grads[e] = g;
-}
 
 // ---------------------------------------------------------------------------------------------
 // Adam (torch.optim.Adam, amsgrad=False, no weight decay) + soft target update + transposes
@@ -998,7 +639,6 @@ struct ApplyArgs {
   float* params;
   float* targets;
   float* grads;
-  const float* partials;  // non-null: the gradient is Σ of the kParts partials (single process, no all-reduce)
   float* m;
   float* v;
   const int64_t* step;
@@ -1016,18 +656,10 @@ struct AdamStep {
   float step_pi, step_q, bc2_sqrt;
 };
 
-// one element: gradient (Σ partials or the all-reduced flat gradient), torch.optim.Adam, soft update
+// one element: gradient (the flat gradient, all-reduced when data parallel), torch.optim.Adam, soft update
 __device__ __forceinline__ float adam_elem(const ApplyArgs& a, const AdamStep& st, int64_t e, float* tp_out) {
   const Layout& L = a.L;
-  float g;
-  if (a.partials && e != 0) {
-    g = a.partials[e];
-#pragma unroll
-    for (int p = 1; p < kParts; ++p) g += a.partials[(size_t)p * L.n_params + e];
-    a.grads[e] = g;
-  } else {
-    g = a.grads[e];
-  }
+  float g = a.grads[e];
   g *= a.hp.inv_world;
   const bool is_q = e >= L.q_base[0];
   float m = a.m[e], v = a.v[e];
@@ -1123,11 +755,8 @@ struct sacf_handle {
   float* T;
   float* scratch;
   Scratch sc;
-  GTask* tasks;
-  int n_tasks;
-  float* partials;
-  GMat mats[kMaxMats];
-  int n_mats;
+  MScratch ms;
+  WgArgs wg;
   char err[512];
 };
 
@@ -1164,7 +793,8 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   *out = nullptr;
   if (!cfg || cfg->abi_version != SACF_ABI_VERSION) return SACF_EINVAL;
   const int O = cfg->obs_dim, H = cfg->hidden, B = cfg->batch;
-  if (O < 1 || O + 1 > kXLd || H < 32 || H > SACF_MAX_HIDDEN || H % 32 || B < R || B % R || cfg->world_size < 1)
+  if (O < 1 || O + 1 > kXLd || H < 32 || H > SACF_MAX_HIDDEN || H % 32 || B < kTile2 || B % kTile2 || B > 1024 ||
+      cfg->world_size < 1)
     return SACF_EINVAL;
   sacf_handle* h = new (std::nothrow) sacf_handle();
   if (!h) return SACF_EINVAL;
@@ -1212,9 +842,11 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   hp.inv_world = 1.0f / (float)cfg->world_size;
 
   SDev g(device);
-  // scratch: actor 4·B·H + B·16 + 2B; critics 2·(4·B·H + B·16 + B); partials 5B
+  // scratch: actor 4·B·H + B·16 + 2B; critics 2·(4·B·H + B·16 + B); per-row losses 5B;
+  // MFMA path: batch 2·B·16 + 5B, h2n B·H, heads 12B, (g1, g2, dg1) on (obs, ã) 6·B·H, targets 2·B·H
   const int64_t BH = (int64_t)B * H;
-  const int64_t n_scr = 4 * BH + B * kXLd + 2 * B + 2 * (4 * BH + B * kXLd + B) + 5 * B;
+  const int64_t n_scr = 4 * BH + B * kXLd + 2 * B + 2 * (4 * BH + B * kXLd + B) + 5 * B +
+                        2 * B * kXLd + 5 * B + BH + 12 * B + 6 * BH + 2 * BH;
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
     *out = h;
@@ -1241,15 +873,33 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   sc.p_q2l = s; s += B;
   sc.p_la = s; s += B;
   sc.p_ga = s; s += B;
+  MScratch& ms = h->ms;
+  ms.x = s; s += B * kXLd;
+  ms.xn = s; s += B * kXLd;
+  ms.act = s; s += B;
+  ms.rew = s; s += B;
+  ms.term = s; s += B;
+  ms.eps = s; s += 2 * B;
+  ms.h2n = s; s += BH;
+  ms.hd = s; s += 6 * B;
+  ms.hdn = s; s += 6 * B;
+  for (int k = 0; k < 2; ++k) {
+    ms.g1pi[k] = s; s += BH;
+    ms.g2pi[k] = s; s += BH;
+    ms.dg1pi[k] = s; s += BH;
+    ms.tg2[k] = s; s += BH;
+  }
   e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);
   if (e != hipSuccess) {
     *out = h;
     return sfail(h, SACF_EHIP, "hipMalloc(T): %s", hipGetErrorString(e));
   }
-  // weight-gradient matrices and their 64×64 tiles
+  // weight-gradient matrices: the three H x H ones on MFMA tiles, the rest one element per thread
+  WgArgs& wg = h->wg;
+  memset(&wg, 0, sizeof(wg));
   int nm = 0;
   auto add = [&](const float* dY, int ldY, const float* X, int ldX, int M, int N, int64_t off) {
-    h->mats[nm++] = GMat{dY, X, ldY, ldX, M, N, off};
+    wg.mats[nm++] = GMat{dY, X, ldY, ldX, M, N, off};
   };
   add(sc.a_dh1, H, sc.a_x, kXLd, H, O, L.p_w1);
   add(sc.a_dh1, H, nullptr, 0, H, 1, L.p_b1);
@@ -1268,29 +918,25 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     add(sc.q_dq[k], 1, sc.q_g2[k], H, 1, H, b + L.c_w3);
     add(sc.q_dq[k], 1, nullptr, 0, 1, 1, b + L.c_b3);
   }
-  h->n_mats = nm;
-  std::vector<GTask> tasks;
-  // the big H×H tiles first so they start early
-  for (int pass = 0; pass < 2; ++pass)
-    for (int mi = 0; mi < nm; ++mi) {
-      const GMat& m = h->mats[mi];
-      const bool big = m.M == H && m.N == H;
-      if ((pass == 0) != big) continue;
-      for (int j0 = 0; j0 < m.M; j0 += 64)
-        for (int k0 = 0; k0 < m.N; k0 += 64) tasks.push_back(GTask{mi, j0, k0});
+  wg.n_mats = nm;
+  int nb = 0;
+  wg.n_small_mats = 0;
+  wg.small_start[0] = 0;
+  for (int mi = 0; mi < nm; ++mi) {
+    const GMat& m = wg.mats[mi];
+    if (m.M == H && m.N == H && m.X) {
+      wg.big[nb++] = mi;
+    } else {
+      wg.small_mat[wg.n_small_mats] = mi;
+      wg.small_start[wg.n_small_mats + 1] = wg.small_start[wg.n_small_mats] + (int64_t)m.M * m.N;
+      wg.n_small_mats++;
     }
-  h->n_tasks = (int)tasks.size();
-  e = hipMalloc(&h->partials, sizeof(float) * kParts * L.n_params);
-  if (e != hipSuccess) {
-    *out = h;
-    return sfail(h, SACF_EHIP, "partials: %s", hipGetErrorString(e));
   }
-  e = hipMalloc(&h->tasks, sizeof(GTask) * tasks.size());
-  if (e == hipSuccess) e = hipMemcpy(h->tasks, tasks.data(), sizeof(GTask) * tasks.size(), hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    *out = h;
-    return sfail(h, SACF_EHIP, "tasks: %s", hipGetErrorString(e));
-  }
+  wg.n_small = (int)wg.small_start[wg.n_small_mats];
+  wg.n_mfma = nb * (H / kTile2) * (H / kTile2);
+  wg.B = B;
+  wg.sc = sc;
+  wg.hp = h->hp;
   *out = h;
   return SACF_OK;
 }
@@ -1300,8 +946,6 @@ int sacf_destroy(sacf_handle* h) {
   SDev g(h->device);
   if (h->scratch) (void)hipFree(h->scratch);
   if (h->T) (void)hipFree(h->T);
-  if (h->tasks) (void)hipFree(h->tasks);
-  if (h->partials) (void)hipFree(h->partials);
   delete h;
   return SACF_OK;
 }
@@ -1365,7 +1009,7 @@ int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const fl
 int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
                const float* next_obs, const float* eps) {
   if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_grads: buffers not bound");
-  RowsArgs a;
+  MArgs a;
   memset(&a, 0, sizeof(a));
   a.params = h->params;
   a.targets = h->targets;
@@ -1386,46 +1030,21 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   a.step = h->step;
   a.stats = h->stats;
   a.sc = h->sc;
+  a.ms = h->ms;
   a.L = h->L;
   a.hp = h->hp;
+  const int B = h->L.B, H = h->L.H, ct = H / kTile2;
   SDev g(h->device);
-  // rows-kernel shape: RR batch rows per block x KS k-groups (SACF_ROWS=RRxKS overrides, e.g. 4x1).
-  // Measured on MI355X, H = 256, B = 256 (grad steps/s): 4x1 5131, 2x2 7430, 2x4 8364, 1x4 9682.
-  int rr = 1, ks = 4;
-  if (const char* e = getenv("SACF_ROWS")) {
-    if (sscanf(e, "%dx%d", &rr, &ks) != 2) rr = 1, ks = 4;
-  }
-  if (h->L.H / ks < 8 || (h->L.H / ks) % 8) ks = 1;
-#define ROWS(RR_, KS_) \
-  hipLaunchKernelGGL((sac_rows_kernel<RR_, KS_>), dim3(h->L.B / RR_), dim3(kCols * KS_), 0, h->stream, a)
-  if (!getenv("SACF_ROWS") && h->L.H <= kCols) {  // default: the four-group one-row kernel
-    hipLaunchKernelGGL(sac_rows_g4_kernel, dim3(h->L.B), dim3(kCols * 4), 0, h->stream, a);
-  } else if (rr == 4 && ks == 1) ROWS(4, 1);
-  else if (rr == 4 && ks == 2) ROWS(4, 2);
-  else if (rr == 2 && ks == 2) ROWS(2, 2);
-  else if (rr == 1 && ks == 4) ROWS(1, 4);
-  else if (rr == 2 && ks == 4) ROWS(2, 4);
-  else if (ks == 1) ROWS(2, 1);
-  else ROWS(1, 4);
-#undef ROWS
-  WgradArgs w;
-  memset(&w, 0, sizeof(w));
-  for (int i = 0; i < h->n_mats; ++i) w.mats[i] = h->mats[i];
-  w.tasks = h->tasks;
-  w.n_tasks = h->n_tasks;
-  w.partials = h->partials;
-  w.n_params = h->L.n_params;
+  hipLaunchKernelGGL(sac_actor_fwd_kernel, dim3(2 * B / kTile2, ct), dim3(256), 0, h->stream, a);
+  hipLaunchKernelGGL(sac_critic_fwd_kernel, dim3(6 * B / kTile2, ct), dim3(256), 0, h->stream, a);
+  hipLaunchKernelGGL(sac_critic_bwd_kernel, dim3(4 * B / kTile2, ct), dim3(256), 0, h->stream, a);
+  hipLaunchKernelGGL(sac_actor_bwd_kernel, dim3(B / kTile2, ct), dim3(256), 0, h->stream, a);
+  WgArgs& w = h->wg;
   w.grads = h->grads;
-  w.B = h->L.B;
-  w.sc = h->sc;
   w.params = h->params;
   w.step = h->step;
   w.stats = h->stats;
-  w.hp = h->hp;
-  hipLaunchKernelGGL(sac_wgrad_kernel, dim3(h->n_tasks + 1, kParts), dim3(kThreads), 0, h->stream, w);
-  if (h->cfg.world_size > 1)  // the flat gradient is all-reduced before sacf_apply; single process: summed there
-    hipLaunchKernelGGL(sac_gsum_kernel, dim3((unsigned)((h->L.n_params - 1 + kThreads - 1) / kThreads)), dim3(kThreads),
-                       0, h->stream, h->partials, h->grads, h->L.n_params);
+  hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_mfma + (w.n_small + 255) / 256 + 1), dim3(256), 0, h->stream, w);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
 }
@@ -1442,7 +1061,6 @@ int sacf_apply(sacf_handle* h) {
   a.T = h->T;
   a.L = h->L;
   a.hp = h->hp;
-  a.partials = h->cfg.world_size > 1 ? nullptr : h->partials;
   a.stats = h->stats;
   const int64_t HH = (int64_t)h->L.H * h->L.H;
   a.n_tile_blocks = 3 * (h->L.H / kTile) * (h->L.H / kTile);

@@ -118,6 +118,21 @@ def cpu_baseline(cfg, seconds, n_threads, n_envs=4096):
                 c2_ship_ticks_per_s=c2, c2_sample=f"{n_envs} single ships x whole 10,000 s horizon (dt 30, dt 4)")
 
 
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense, = FP32 vector rate
+
+
+def sac_flops_per_step(B, H, O):
+    """Matrix flops (2 per multiply-add) of one SAC grad step with two hidden layers of width H, obs_dim O,
+    act_dim 1 (sac.py compute_loss :156-270): forward over 2B actor rows (obs, next_obs) and 6B critic rows
+    (Q1/Q2 at (obs, a) and (obs, ã), targets at (next_obs, ã')); backward through the critics at (obs, a)
+    for the Q losses and (obs, ã) for the policy loss (4B rows, down to dQ/dã), through the actor at obs
+    (B rows); weight gradients of policy (B rows) and both critics (B rows each)."""
+    mac_fwd = 2 * B * (H * O + H * H + 2 * H) + 6 * B * (H * (O + 1) + H * H + H)
+    mac_bwd = 4 * B * (H + H * H + H) + B * (2 * H + H * H)
+    mac_wg = B * (H * O + H * H + 2 * H) + 2 * B * (H * (O + 1) + H * H + H)
+    return 2 * (mac_fwd + mac_bwd + mac_wg)
+
+
 def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
     """SAC grad-steps/s (secondary metric): FusedSACTrainer HIP-graph step (runner networks: 2x256
     hidden, batch `batch` per GPU, on-device uniform sampling from a 300k-row DeviceReplayBuffer,
@@ -171,10 +186,20 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
         return timed(lambda k: tr.train_from_buffer(rb, k), steps)
 
     dt = fused("hip")
+    H, O = 256, 8
+    flops = sac_flops_per_step(batch, H, O)
     res = {"grad_steps_per_s": steps / dt, "ms_per_grad_step": dt / steps * 1e3, "batch_per_gpu": batch,
-           "global_batch": batch * world, "hidden": [256, 256], "dtype": "f32",
-           "impl": "FusedSACTrainer hip backend (csrc/sac_kernels.hip: rows + weight-grad + Adam kernels, "
-                   "HIP graph" + (", RCCL all-reduce between graph halves)" if world > 1 else ")")}
+           "global_batch": batch * world, "hidden": [H, H], "dtype": "f32",
+           "impl": "FusedSACTrainer hip backend (csrc/sac_kernels.hip: four MFMA f32 forward/backward GEMM "
+                   "kernels + MFMA weight-gradient kernel + Adam/soft-update kernel, HIP graph" +
+                   (", RCCL all-reduce between graph halves)" if world > 1 else ")"),
+           "roofline": {"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_F32_PEAK_TFLOPS,
+                        "flops_per_step": flops,
+                        "achieved": flops / (dt / steps) / 1e12,
+                        "frac": flops / (dt / steps) / 1e12 / MFMA_F32_PEAK_TFLOPS,
+                        "note": "algorithmic matrix flops of one grad step (2 per multiply-add: forward, "
+                                "backward and weight-gradient products of every layer, per rank) / whole-step "
+                                "wall time (all six launches); v_mfma_f32_32x32x2_f32 dense f32 peak"}}
     if world == 1:
         res["torch_ops_graph_grad_steps_per_s"] = steps / fused("torch")
     if world == 1 and eager_steps:

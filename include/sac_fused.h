@@ -45,7 +45,7 @@ typedef struct sacf_config {
   int32_t abi_version;   /* = SACF_ABI_VERSION */
   int32_t obs_dim;       /* <= SACF_MAX_OBS (8 for the AST env) */
   int32_t hidden;        /* H, multiple of 32, <= SACF_MAX_HIDDEN (runner: 256) */
-  int32_t batch;         /* B per call (per rank), multiple of 4 */
+  int32_t batch;         /* B per call (per rank), multiple of 32, <= 1024 */
   float discount;        /* sac.py:31  γ */
   float reward_scale;    /* sac.py:32 */
   float soft_target_tau; /* sac.py:37  τ */

@@ -165,7 +165,7 @@ def test_device_replay_buffer_ring_order():
 
 
 # ------------------------------------------------------------------------------------------------
-# HIP backend (csrc/sac_kernels.hip): fused rows / weight-gradient / Adam kernels
+# HIP backend (csrc/sac_kernels.hip): MFMA forward/backward GEMMs, weight-gradient and Adam kernels
 # ------------------------------------------------------------------------------------------------
 def _seeded_nets(H, device, seed=0):
     torch.manual_seed(seed)
@@ -202,7 +202,7 @@ def _assert_grads_close(g_hip, g_ref, tr, what):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,B", [(32, 64), (256, 256)])
+@pytest.mark.parametrize("H,B", [(32, 64), (64, 96), (256, 32), (256, 256), (256, 1024)])
 def test_hip_sac_gradients_match_torch_autograd(H, B):
     """One update's flat gradient (α | π | Q1 | Q2) from the fused kernels == torch autograd's."""
     batch, eps = _rand_batch(B, "cuda")
