@@ -5,9 +5,19 @@ Per epoch (rank-local counts; with R ranks the job does R× the decisions and ev
 averages R local batches of batch_size, i.e. a global batch of R·batch_size):
   epoch 0: collect ≥ min_num_steps_before_training exploration decisions into the buffer;
   every epoch: ≥ num_eval_steps_per_epoch decisions with the deterministic policy (eval env),
-  then per train loop ≥ num_expl_steps_per_train_loop exploration decisions + num_trains_per_train_loop
-  grad steps, each on a fresh on-device uniform batch.
+  then per train loop ≥ num_expl_steps_per_train_loop exploration decisions + grad steps, each on a
+  fresh on-device uniform batch.
+
+Update-to-data ratio. The reference collects exactly num_expl_steps_per_train_loop (256) decisions per
+loop and then runs num_trains_per_train_loop (240) grad steps of batch_size (256): 240/256 grad steps
+per collected decision. A sliced pass over thousands of envs overshoots 256 by a wide margin, so with
+match_update_ratio (default) the loop runs round(collected_on_all_ranks × 240/256) grad steps (the
+fraction carried to the next loop) — the reference's ratio of grad steps and of sampled rows (global
+batch = batch_size, split over the ranks by the runner) per environment decision. With
+match_update_ratio=False it runs num_trains_per_train_loop per loop, as written.
 """
+import torch
+
 from .batch_rl_algorithm import BaseRLAlgorithm
 
 
@@ -15,7 +25,8 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
     def __init__(self, trainer, exploration_env, evaluation_env, exploration_data_collector,
                  evaluation_data_collector, replay_buffer, batch_size, max_path_length, num_epochs,
                  num_eval_steps_per_epoch, num_expl_steps_per_train_loop, num_trains_per_train_loop,
-                 num_train_loops_per_epoch=1, min_num_steps_before_training=0, start_epoch=0):
+                 num_train_loops_per_epoch=1, min_num_steps_before_training=0, start_epoch=0,
+                 match_update_ratio=True):
         super().__init__(trainer, exploration_env, evaluation_env, exploration_data_collector,
                          evaluation_data_collector, replay_buffer)
         self.batch_size = batch_size
@@ -27,6 +38,25 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
         self.num_expl_steps_per_train_loop = num_expl_steps_per_train_loop
         self.min_num_steps_before_training = min_num_steps_before_training
         self._start_epoch = start_epoch
+        self.match_update_ratio = match_update_ratio
+        self._utd_carry = 0.0
+        self.num_train_steps_total = 0
+        self.num_loop_expl_steps_total = 0  # rank-local decisions collected inside train loops
+
+    def _n_grad_steps(self, collected):
+        """Grad steps for `collected` rank-local decisions (same count on every rank)."""
+        if not self.match_update_ratio:
+            return self.num_trains_per_train_loop
+        pg = getattr(self.trainer, "pg", None)
+        if pg is not None and torch.distributed.get_world_size(pg) > 1:
+            dev = "cuda" if torch.distributed.get_backend(pg) == "nccl" else "cpu"
+            t = torch.tensor([collected], dtype=torch.int64, device=dev)
+            torch.distributed.all_reduce(t, group=pg)
+            collected = int(t.item())
+        x = self._utd_carry + collected * self.num_trains_per_train_loop / self.num_expl_steps_per_train_loop
+        k = int(x)
+        self._utd_carry = x - k
+        return k
 
     def train(self):
         for self.epoch in range(self._start_epoch, self.num_epochs):
@@ -37,17 +67,21 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
     def _train(self):
         if self.epoch == 0 and self.min_num_steps_before_training > 0:
             self.expl_data_collector.collect(self.min_num_steps_before_training, self.replay_buffer)
-            self.expl_data_collector.end_epoch(-1)
-            self.timer.stamp("initial exploration")
+            self.expl_data_collector.end_epoch(-1)  # (unstamped, as in the reference: counts as evaluation sampling)
         if self.num_eval_steps_per_epoch > 0:
             self.eval_data_collector.collect(self.num_eval_steps_per_epoch, None, record_paths=True)
         self.timer.stamp("evaluation sampling")
         for _ in range(self.num_train_loops_per_epoch):
-            self.expl_data_collector.collect(self.num_expl_steps_per_train_loop, self.replay_buffer,
-                                             record_paths=True)
+            got = self.expl_data_collector.collect(self.num_expl_steps_per_train_loop, self.replay_buffer,
+                                                   record_paths=True)
             self.timer.stamp("exploration sampling")
+            self.timer.stamp("data storing")  # the collector already wrote the buffer on the device
             self.training_mode(True)
-            self.trainer.train_from_buffer(self.replay_buffer, self.num_trains_per_train_loop)
+            self.num_loop_expl_steps_total += got
+            k = self._n_grad_steps(got)
+            if k:
+                self.trainer.train_from_buffer(self.replay_buffer, k)
+            self.num_train_steps_total += k
             self.timer.stamp("training")
             self.training_mode(False)
 

@@ -7,13 +7,19 @@ env_info['terminal']) is recorded, and the episode ends on done or after max_pat
 decisions. Unlike the reference, thousands of envs advance together: one sliced
 `step_async(max_ticks)` call advances every env by ≤ max_ticks ticks, envs that complete a
 decision emit their transition straight into a DeviceReplayBuffer, and finished envs are reset
-in the same pass (masked reset). Nothing crosses to the host inside `collect`.
+in the same pass (masked reset). The policy runs only on the envs that wait for a decision (their
+count is known on the host from the previous pass, so the compaction needs no extra sync). Inside
+`collect` the only host traffic is the transition count per pass, plus, with record_paths, the
+rewards/actions of the episodes that ended in that pass: those become the epoch's paths
+(get_epoch_paths, as MdpPathCollector's, path_collector.py:77-78) from which the algorithm logs
+eval_util.get_generic_path_information (Rewards/Returns/Actions/Num Paths/Average Returns).
 """
 from collections import OrderedDict, deque
 
 import numpy as np
 import torch
 
+from .... import shipsim_abi as abi
 from ...core.eval_util import create_stats_ordered_dict
 
 
@@ -41,9 +47,14 @@ class BatchedPathCollector:
         self._steps_total = torch.zeros((), dtype=torch.int64, device=dev)
         self._paths_total = torch.zeros((), dtype=torch.int64, device=dev)
         self._ticks_total = torch.zeros((), dtype=torch.int64, device=dev)
-        self._epoch_returns = []
-        self._epoch_lens = []
         self._max_saved = max_num_epoch_paths_saved
+        self._epoch_paths = deque(maxlen=max_num_epoch_paths_saved)
+        self._n_awaiting = N                                      # host copy, None when unknown
+        T = self.max_path_length
+        self._path_rew = torch.zeros((N, T), dtype=torch.float64, device=dev)   # current episode, per decision
+        self._path_act = torch.zeros((N, T), dtype=torch.float32, device=dev)
+        self._path_ev = torch.zeros((N, T), dtype=torch.int32, device=dev)
+        self._rows = torch.arange(N, device=dev)
 
     @torch.no_grad()
     def _actions(self, obs):
@@ -55,8 +66,16 @@ class BatchedPathCollector:
     @torch.no_grad()
     def step(self, replay_buffer=None):
         """One sliced pass over all envs. Returns (ready mask, #transitions) as device tensors."""
-        new_a = self._actions(self._obs)
-        self._act = torch.where(self._awaiting.unsqueeze(1), new_a.to(torch.float32), self._act)
+        k = self._n_awaiting
+        if k is None:  # count unknown (step() called on its own): evaluate everywhere, keep the awaiting rows
+            new_a = self._actions(self._obs)
+            self._act = torch.where(self._awaiting.unsqueeze(1), new_a.to(torch.float32), self._act)
+        elif k == self.N:
+            self._act = self._actions(self._obs).to(torch.float32)
+        elif k > 0:
+            idx = torch.nonzero_static(self._awaiting, size=k).squeeze(1)
+            self._act.index_copy_(0, idx, self._actions(self._obs.index_select(0, idx)).to(torch.float32))
+        self._n_awaiting = None
         out = self._env.step_async(self._act, max_ticks=self.max_ticks, out=self._out)
         ready = out["ready"].bool()
         done = out["done"].bool()
@@ -65,6 +84,9 @@ class BatchedPathCollector:
         if replay_buffer is not None:
             replay_buffer.add_batch(self._obs, self._act, rew.to(torch.float32).unsqueeze(1), out["obs"],
                                     terminal.to(torch.float32).unsqueeze(1), mask=ready)
+        pos = self._path_len.clamp(max=self.max_path_length - 1).long()
+        for buf, v in ((self._path_rew, rew), (self._path_act, self._act[:, 0]), (self._path_ev, out["events"])):
+            buf[self._rows, pos] = torch.where(ready, v.to(buf.dtype), buf[self._rows, pos])
         self._path_len += ready.to(torch.int32)
         self._ret += torch.where(ready, rew, torch.zeros_like(rew))
         end = ready & (done | (self._path_len >= self.max_path_length))
@@ -75,7 +97,6 @@ class BatchedPathCollector:
         self._paths_total += end.sum()
         self._ticks_total += out["ticks"].sum()
         self._last_end = end
-        self._last_end_ret = torch.where(end, self._ret, torch.zeros_like(self._ret))
         self._last_end_len = torch.where(end, self._path_len, torch.zeros_like(self._path_len))
         # masked auto-reset of finished episodes
         self._env.reset(mask=end.to(torch.uint8), obs_out=self._obs_reset)
@@ -89,30 +110,45 @@ class BatchedPathCollector:
         got = 0
         while got < num_steps:
             _, n = self.step(replay_buffer)
-            got += int(n.item())
+            self._n_awaiting = int(n.item())
+            got += self._n_awaiting
             if record_paths:
-                e = self._last_end
-                self._epoch_returns.append(self._last_end_ret[e].cpu().numpy())
-                self._epoch_lens.append(self._last_end_len[e].cpu().numpy())
+                self._record_ended()
         return got
+
+    def _record_ended(self):
+        """The episodes that ended in the last pass -> reference path dicts (rollout_functions.py:161-181:
+        rewards and actions (T, 1), terminals, env_infos with the reference's keys)."""
+        e = self._last_end  # the per-episode buffers keep those rows until the next pass writes them
+        lens = self._last_end_len[e].cpu().numpy()
+        if lens.size == 0:
+            return
+        rews = self._path_rew[e].cpu().numpy()
+        acts = self._path_act[e].cpu().numpy()
+        evs = self._path_ev[e].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        for L, r, a, ev in zip(lens, rews, acts, evs):
+            L = int(L)
+            ev = ev[:L]
+            infos = [dict(terminal=bool(x & abi.EV_TERMINAL), test_ship_stop=bool(x & abi.EV_TEST_STOP),
+                          obs_ship_stop=bool(x & abi.EV_OBS_STOP)) for x in ev]
+            self._epoch_paths.append(dict(rewards=r[:L, None].copy(), actions=a[:L, None].copy(),
+                                          terminals=np.array([[i["terminal"]] for i in infos]),
+                                          env_infos=infos, agent_infos=[{} for _ in range(L)]))
 
     # reference collector surface -------------------------------------------------------------
     def get_epoch_paths(self):
-        return []
+        return self._epoch_paths
 
     def end_epoch(self, epoch):
-        self._epoch_returns, self._epoch_lens = [], []
+        self._epoch_paths = deque(maxlen=self._max_saved)
 
     def get_diagnostics(self):
+        """MdpPathCollector.get_diagnostics (path_collector.py:83-92) + the env-tick count."""
         st = OrderedDict([("num steps total", int(self._steps_total.item())),
                           ("num paths total", int(self._paths_total.item())),
                           ("num env ticks total", int(self._ticks_total.item()))])
-        if self._epoch_lens:
-            lens = np.concatenate(self._epoch_lens)
-            rets = np.concatenate(self._epoch_returns)
-            if lens.size:
-                st.update(create_stats_ordered_dict("path length", lens, always_show_all_stats=True))
-                st.update(create_stats_ordered_dict("Returns", rets, always_show_all_stats=True))
+        st.update(create_stats_ordered_dict("path length", [len(p["actions"]) for p in self._epoch_paths],
+                                            always_show_all_stats=True))
         return st
 
     def get_snapshot(self):

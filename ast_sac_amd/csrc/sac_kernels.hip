@@ -39,18 +39,33 @@ namespace {
 constexpr int kThreads = 256;
 
 #ifdef SACF_PHASE_TIMING
-// timing build only: shader-clock stamps of block 0 at the phase boundaries of sac_rows_g4_kernel
-__device__ unsigned long long g_sac_stamp[16];
-#define SAC_MARK(k)                                                              \
-  do {                                                                           \
-    if (blockIdx.x == 0 && threadIdx.x == 0) g_sac_stamp[k] = clock64();         \
+// timing build only (scripts/build_timing.sh): wall-clock stamps of block (0, 0) thread 0 at phase
+// boundaries, each after waiting for that wave's outstanding memory operations
+__device__ unsigned long long g_sac_stamp[64];
+#define SAC_TB(kern, k, cond)                                    \
+  do {                                                           \
+    if ((cond) && threadIdx.x == 0) {                            \
+      __builtin_amdgcn_s_waitcnt(0);                             \
+      g_sac_stamp[(kern) * 12 + (k)] = wall_clock64();           \
+    }                                                            \
   } while (0)
 #else
-#define SAC_MARK(k) \
-  do {              \
+#define SAC_TB(kern, k, cond) \
+  do {                        \
   } while (0)
 #endif
-constexpr int R = 4;           // batch granularity: B must be a multiple of R (rows-kernel tiles)
+#define SAC_T(kern, k) SAC_TB(kern, k, blockIdx.x == 0 && blockIdx.y == 0)
+#ifdef SACF_PHASE_TIMING
+// every block: earliest start (slot 9) and latest end (slot 10) of the kernel, via vector atomics
+#define SAC_SPAN_BEGIN(kern)                                                                  \
+  if (threadIdx.x == 0) atomicMin(&g_sac_stamp[(kern) * 12 + 9], (unsigned long long)wall_clock64())
+#define SAC_SPAN_END(kern)                                                                    \
+  if (threadIdx.x == 0) atomicMax(&g_sac_stamp[(kern) * 12 + 10], (unsigned long long)wall_clock64())
+#else
+#define SAC_SPAN_BEGIN(kern)
+#define SAC_SPAN_END(kern)
+#endif
+
 constexpr int kXLd = 16;       // leading dim of the per-row input scratch (obs | act)
 constexpr float kLog2 = 0.69314718055994530942f;
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
@@ -77,22 +92,17 @@ struct Hyper {
   float inv_world;
 };
 
-struct RowsArgs {
-  const float* params;
-  const float* targets;
-  const float* T;  // transposed copies: [actor W2ᵀ | q1 W2ᵀ | q2 W2ᵀ | t1 W2ᵀ | t2 W2ᵀ], each H×H
-  const float *obs, *act, *rew, *term, *nobs;
-  const int64_t* size_dev;
-  int64_t capacity;
-  uint64_t seed;
-  int sampled;
-  const float* eps;
-  const int64_t* step;
-  float* stats;
-  Scratch sc;
-  Layout L;
-  Hyper hp;
+// Adam bias corrections of step t (torch.optim.Adam: step_size = lr / (1 - beta1^t), denominator
+// sqrt(v) / sqrt(1 - beta2^t) + eps), in double as torch computes them on the host, then rounded once
+struct AdamStep {
+  float step_pi, step_q, bc2_sqrt;
 };
+__device__ __forceinline__ AdamStep adam_step(const Hyper& hp, int64_t step) {
+  const double t = (double)step;
+  const double bc1 = 1.0 - pow((double)hp.beta1, t);
+  const double bc2 = 1.0 - pow((double)hp.beta2, t);
+  return AdamStep{(float)(hp.lr_pi / bc1), (float)(hp.lr_q / bc1), (float)sqrt(bc2)};
+}
 
 // ---------------------------------------------------------------------------------------------
 // Philox4x32-10 (counter-based; one 4-word draw per batch row and step)
@@ -135,6 +145,11 @@ __device__ __forceinline__ float softplus(float x) { return x > 20.0f ? x : log1
 // ---------------------------------------------------------------------------------------------
 // weight-gradient matrices: out[j][k] = Σ_r dY[r·ldY + j] · X[r·ldX + k]  (X == nullptr: ones -> bias)
 // ---------------------------------------------------------------------------------------------
+// a pointer read from LDS has no address space for the compiler (flat loads, which also count on the
+// LDS counter and get conservative waits): these matrices are all device memory
+typedef const float __attribute__((address_space(1)))* gptr;
+__device__ __forceinline__ gptr as_global(const float* p) { return (gptr)p; }
+
 struct GMat {
   const float* dY;
   const float* X;
@@ -171,6 +186,11 @@ struct MScratch {
   float *g1pi[2], *g2pi[2];                // critics on (obs, ã) rows [B][H]
   float *tg2[2];                           // target critics on (next_obs, ã') [B][H]
   float *dg1pi[2];                         // critic input gradient on (obs, ã) rows [B][H]
+  // per-row dot products of a layer output with a head weight vector, one partial per 32-column
+  // block (the epilogue of the tile that produced those columns), summed in block order by the consumer
+  float *hpart;  // actor heads: [mean | log_std][H/32][2B] over the obs and next_obs rows
+  float *qpart;  // critic heads g2 · w3: [Q1 | Q2 | T1 | T2][H/32][2B] (targets: rows [0, B))
+  float *apart;  // dg1 · (fc0 action column) on the (obs, ã) rows: [Q1 | Q2][H/32][B]
 };
 enum { HD_MEAN, HD_LSRAW, HD_STD, HD_Z, HD_A, HD_LOGP };
 
@@ -209,7 +229,7 @@ __device__ __forceinline__ void mfma_chain(f32x16& acc, const float (&a)[kMaxN2]
 // Sum of the 4 waves' partial tiles (wave 0 + 1 + 2 + 3, in that order), then epi(row, col, v) on the
 // 1024 outputs: wave w finishes accumulator registers 4w .. 4w + 3.
 template <class EPI>
-__device__ __forceinline__ void splitk_finish(const f32x16& acc, float* lds, EPI&& epi) {
+__device__ __forceinline__ void splitk_finish_q(const f32x16& acc, float* lds, EPI&& epi) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int g = 0; g < 16; ++g) lds[(w * 16 + g) * 64 + lane] = acc[g];
@@ -221,18 +241,107 @@ __device__ __forceinline__ void splitk_finish(const f32x16& acc, float* lds, EPI
     v += lds[(1 * 16 + g) * 64 + lane];
     v += lds[(2 * 16 + g) * 64 + lane];
     v += lds[(3 * 16 + g) * 64 + lane];
-    epi((g & 3) + 8 * (g >> 2) + 4 * (lane >> 5), lane & 31, v);
+    epi(q, (g & 3) + 8 * (g >> 2) + 4 * (lane >> 5), lane & 31, v);
   }
 }
 
-// Σ_j x[j] w[j] over the row, split between the lane and its partner lane ^ 32 (halves of j);
-// both lanes return the same value (the two halves added in one order: lower half + upper half)
-__device__ __forceinline__ float row_dot(const float* __restrict__ x, const float* __restrict__ w, int H) {
-  const int h = (threadIdx.x >> 5) & 1, half = H / 2;
-  float s = 0.0f;
-  for (int j = h * half; j < (h + 1) * half; ++j) s = fmaf(x[j], w[j], s);  // w: flat params, not 16-B aligned
-  const float o = __shfl_xor(s, 32, 64);
-  return h ? o + s : s + o;
+template <class EPI>
+__device__ __forceinline__ void splitk_finish(const f32x16& acc, float* lds, EPI&& epi) {
+  splitk_finish_q(acc, lds, [&](int, int rr, int cc, float v) { epi(rr, cc, v); });
+}
+// the row of output register q (0..3) of this wave in splitk_finish's order
+__device__ __forceinline__ int finish_row(int q) {
+  const int g = 4 * (threadIdx.x >> 6) + q;
+  return (g & 3) + 8 * (g >> 2) + 4 * ((threadIdx.x & 63) >> 5);
+}
+
+// Σ of x over the 32 lanes of this half-wave (the 32 columns of one output row in the C/D layout),
+// butterfly order: every lane gets the same bits
+__device__ __forceinline__ float halfwave_sum(float x) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// Σ over the column blocks of one row's head partials (block order), from part[cb * stride + row]
+__device__ __forceinline__ float sum_parts(const float* part, int n_cb, int64_t stride, int64_t row) {
+  float s = part[row];
+  for (int cb = 1; cb < n_cb; ++cb) s += part[cb * stride + row];
+  return s;
+}
+
+// a contiguous run of n floats of the parameters into LDS (the block's first-layer weights)
+__device__ __forceinline__ void stage(float* dst, const float* src, int n) {
+  for (int e = threadIdx.x; e < n; e += kThreads) dst[e] = src[e];
+}
+
+// W1 [H][nin] (row-major in the parameters) into LDS as W1ᵀ [nin][H], and b1 [H] after it
+__device__ __forceinline__ void stage_w1t(float* dst, const float* w1, const float* b1, int H, int nin) {
+  for (int e = threadIdx.x; e < H * nin; e += kThreads) dst[(e % nin) * H + e / nin] = w1[e];
+  for (int e = threadIdx.x; e < H; e += kThreads) dst[nin * H + e] = b1[e];
+}
+
+// av[i] = relu(b1[k] + Σ_{m < nin} W1[k][m] · in[m]) for k = kb + i: an fmaf chain from the bias in
+// input order, as fc0 computes one output. W1ᵀ | b1 and the row's inputs come from LDS; the input loop
+// stays rolled (nin is a run-time size) around the unrolled k loop.
+template <int H>
+__device__ __forceinline__ void first_layer(const float* lw1t, const float* xin, int nin, int kb, float (&av)[kMaxN2]) {
+  constexpr int n2 = H / 8;
+#pragma unroll
+  for (int i = 0; i < n2; ++i) av[i] = lw1t[nin * H + kb + i];
+  for (int m = 0; m < nin; ++m) {
+    const float xm = xin[m];
+#pragma unroll
+    for (int i = 0; i < n2; ++i) av[i] = fmaf(lw1t[m * H + kb + i], xm, av[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < n2; ++i) av[i] = relu(av[i]);
+}
+
+// LDS of the forward/backward kernels. Region A: split-K partial tiles / a 32-row
+// tile of this lane-per-row operand layout. Region B: first-layer weights (W1ᵀ | b1) and the tile's
+// input rows (forward kernels), or a 32-row activation tile and head weights (backward kernels).
+constexpr int kLdsSplit = 4 * 16 * 64;
+constexpr int kTileLd = SACF_MAX_HIDDEN + 4;  // row pitch bound of a 32-row tile (H + 4 floats)
+constexpr int kLdsTile = 32 * kTileLd;
+constexpr int kLdsA = kLdsSplit > kLdsTile ? kLdsSplit : kLdsTile;
+constexpr int kLdsW1 = SACF_MAX_HIDDEN * kXLd + SACF_MAX_HIDDEN;
+constexpr int kLdsX = 32 * (kXLd + 1);
+constexpr int kLdsB = (kLdsW1 + kLdsX > kLdsTile + 2 * SACF_MAX_HIDDEN) ? kLdsW1 + kLdsX : kLdsTile + 2 * SACF_MAX_HIDDEN;
+constexpr int kLdsFloats = kLdsA + kLdsB;
+constexpr int kLdsW1Off = kLdsA;
+constexpr int kLdsXOff = kLdsA + kLdsW1;
+constexpr int kLdsTileOff = kLdsA;
+constexpr int kLdsHeadWOff = kLdsA + kLdsTile;
+
+// 32 consecutive rows of a row-major [*][H] activation matrix <-> an LDS tile of pitch H + 4, in
+// float4 pieces (coalesced: a wave moves whole 1 KiB rows). The MFMA A operand wants one row per lane
+// (lane & 31), which read straight from the matrix would touch 32 rows per instruction.
+template <int H>
+__device__ __forceinline__ void tile_load(float* t, const float* src) {
+  constexpr int C4 = H / 4;
+  for (int e = threadIdx.x; e < 32 * C4; e += kThreads) {
+    const int r = e / C4, c = e % C4;
+    *reinterpret_cast<float4*>(t + r * (H + 4) + 4 * c) = *reinterpret_cast<const float4*>(src + (int64_t)r * H + 4 * c);
+  }
+}
+template <int H>
+__device__ __forceinline__ void tile_store(float* dst, const float* t) {
+  constexpr int C4 = H / 4;
+  for (int e = threadIdx.x; e < 32 * C4; e += kThreads) {
+    const int r = e / C4, c = e % C4;
+    *reinterpret_cast<float4*>(dst + (int64_t)r * H + 4 * c) = *reinterpret_cast<const float4*>(t + r * (H + 4) + 4 * c);
+  }
+}
+// this lane's operands (row lane & 31, columns kb .. kb + H/8) into the tile, then the tile to memory
+template <int H>
+__device__ __forceinline__ void store_operands(float* dst, float* t, const float (&av)[kMaxN2], int kb) {
+  const int rr = threadIdx.x & 31;
+#pragma unroll
+  for (int i = 0; i < H / 8; ++i) t[rr * (H + 4) + kb + i] = av[i];
+  __syncthreads();
+  tile_store<H>(dst, t);
+  __syncthreads();
 }
 
 // one batch item (replay sample or given batch) and its two reparameterisation normals
@@ -260,13 +369,24 @@ __device__ __forceinline__ int64_t batch_item(const MArgs& a, int r, float& e0, 
 }
 
 // grid (2B / 32, H / 32): rows [0, B) are the obs rows, [B, 2B) the next_obs rows of the batch
+template <int H>
 __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
-  __shared__ float lds[4 * 16 * 64];
+  __shared__ float lds[kLdsFloats];
+  SAC_T(0, 0);
+  SAC_SPAN_BEGIN(0);
   const Layout& L = a.L;
-  const int H = L.H, O = L.O, B = L.B;
+  const int O = L.O, B = L.B;
   const float* P = a.params;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
+  constexpr int n2 = H / 8;
+  const int kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < n2; ++i) bv[i] = a.T[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // W2ᵀ operand, first
+  float* lw1 = lds + kLdsW1Off;  // W1ᵀ [O][H] | b1 [H]
+  float* lx = lds + kLdsXOff;    // the tile's input rows [32][kXLd + 1]
+  stage_w1t(lw1, P + L.p_w1, P + L.p_b1, H, O);
   const int row = r0 + (lane & 31);
   const bool nrow = row >= B;
   const int item = nrow ? row - B : row;
@@ -276,6 +396,8 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   float x[kXLd];
 #pragma unroll
   for (int m = 0; m < kXLd; ++m) x[m] = m < O ? src[idx * O + m] : 0.0f;
+  if (w == 0 && h == 0)
+    for (int m = 0; m < O; ++m) lx[(lane & 31) * (kXLd + 1) + m] = x[m];
   if (blockIdx.y == 0 && w == 0 && h == 0) {  // the gathered batch for the later kernels
     float* xd = (nrow ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
     for (int m = 0; m < kXLd; ++m) xd[m] = x[m];
@@ -288,28 +410,32 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
       for (int m = 0; m < kXLd; ++m) a.sc.a_x[(int64_t)item * kXLd + m] = m < O ? x[m] : 0.0f;
     }
   }
-  // h1 for this lane's k (fmaf chain from the bias, as fc0 computes it) and the W2ᵀ operand
-  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
-  float av[kMaxN2], bv[kMaxN2];
-#pragma unroll
-  for (int i = 0; i < kMaxN2; ++i) {
-    if (i >= n2) break;
-    const int k = kb + i;
-    float acc = P[L.p_b1 + k];
-    for (int m = 0; m < O; ++m) acc = fmaf(P[L.p_w1 + (int64_t)k * O + m], x[m], acc);
-    av[i] = relu(acc);
-    bv[i] = a.T[(int64_t)k * H + c0 + (lane & 31)];
-  }
-  if (blockIdx.y == 0 && !nrow)
-    for (int i = 0; i < n2; ++i) a.sc.a_h1[(int64_t)item * H + kb + i] = av[i];
+  SAC_T(0, 1);
+  __syncthreads();  // lw1 staged
+  SAC_T(0, 2);
+  // h1 for this lane's k (fmaf chain from the bias, as fc0 computes it)
+  first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O, kb, av);
+  if (blockIdx.y == 0 && r0 < B) store_operands<H>(a.sc.a_h1 + (int64_t)r0 * H, lds, av, kb);  // block-uniform
+  SAC_T(0, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
+  SAC_T(0, 4);
+  const float wm = P[L.p_wm + c0 + (lane & 31)], ws = P[L.p_ws + c0 + (lane & 31)];
+  constexpr int CB = H / kTile2;
   splitk_finish(acc, lds, [&](int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + P[L.p_b2 + col]);
     if (r < B) a.sc.a_h2[(int64_t)r * H + col] = y;
     else a.ms.h2n[(int64_t)(r - B) * H + col] = y;
+    // this column block's part of the mean / log_std heads of row r (rows [0, 2B))
+    const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
+    if (cc == 0) {
+      a.ms.hpart[(int64_t)blockIdx.y * 2 * B + r] = pm;
+      a.ms.hpart[(int64_t)(CB + blockIdx.y) * 2 * B + r] = ps;
+    }
   });
+  SAC_T(0, 5);
+  SAC_SPAN_END(0);
 }
 
 // TanhNormal.rsample_and_logprob (distributions.py:346-392) of one row's head
@@ -327,10 +453,13 @@ __device__ __forceinline__ void tanh_normal(float mean, float ls_raw, float eps,
 }
 
 // grid (row tiles of [Q1: 2B | Q2: 2B | T1: B | T2: B], H / 32). Q rows [0, B): (obs, ã), [B, 2B): (obs, a)
+template <int H>
 __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
-  __shared__ float lds[4 * 16 * 64];
+  __shared__ float lds[kLdsFloats];
+  SAC_T(1, 0);
+  SAC_SPAN_BEGIN(1);
   const Layout& L = a.L;
-  const int H = L.H, O = L.O, B = L.B;
+  const int O = L.O, B = L.B;
   const float* P = a.params;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int qt = 2 * B / kTile2, tt = B / kTile2;  // row tiles per critic / per target critic
@@ -340,6 +469,16 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   const bool is_t = net >= 2;
   const float* C = is_t ? a.targets + (int64_t)(net - 2) * L.q_size : P + L.q_base[net];
   const int r0 = rt * kTile2, c0 = blockIdx.y * kTile2;
+  constexpr int n2 = H / 8;
+  constexpr int CB = H / kTile2;
+  const int kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+  const float* WT = a.T + (int64_t)(1 + net) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
+#pragma unroll
+  for (int i = 0; i < n2; ++i) bv[i] = WT[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
+  float* lw1 = lds + kLdsW1Off;  // W1ᵀ [O + 1][H] | b1 [H]
+  float* lx = lds + kLdsXOff;    // the tile's input rows [32][kXLd + 1]: obs | action
+  stage_w1t(lw1, C + L.c_w1, C + L.c_b1, H, O + 1);
   const int row = r0 + (lane & 31);
   const bool data = !is_t && row >= B;  // (obs, a) row
   const int item = data ? row - B : row;
@@ -349,57 +488,80 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   float act;
   if (data) {
     act = a.ms.act[item];
-  } else {  // actor head of the row and its sample
-    const float* h2 = (is_t ? a.ms.h2n : a.sc.a_h2) + (int64_t)item * H;
-    const float mean = row_dot(h2, P + L.p_wm, H) + P[L.p_bm];
-    const float ls = row_dot(h2, P + L.p_ws, H) + P[L.p_bs];
+  } else {  // actor head of the row (the column-block parts of actor_fwd's epilogue) and its sample
+    const int64_t hr = (is_t ? B : 0) + item;
+    const float mean = sum_parts(a.ms.hpart, CB, 2 * B, hr) + P[L.p_bm];
+    const float ls = sum_parts(a.ms.hpart + (int64_t)CB * 2 * B, CB, 2 * B, hr) + P[L.p_bs];
     float hd[6];
     tanh_normal(mean, ls, a.ms.eps[(is_t ? B : 0) + item], hd);
     act = hd[HD_A];
     if (store_rows && (net == 0 || net == 2))
       for (int q = 0; q < 6; ++q) (is_t ? a.ms.hdn : a.ms.hd)[q * B + item] = hd[q];
   }
-  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
-  float av[kMaxN2], bv[kMaxN2];
-  const float* WT = a.T + (int64_t)(1 + net) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
-#pragma unroll
-  for (int i = 0; i < kMaxN2; ++i) {
-    if (i >= n2) break;
-    const int k = kb + i;
-    float base = C[L.c_b1 + k];
-    for (int m = 0; m < O; ++m) base = fmaf(C[L.c_w1 + (int64_t)k * (O + 1) + m], xr[m], base);
-    av[i] = relu(fmaf(C[L.c_w1 + (int64_t)k * (O + 1) + O], act, base));
-    bv[i] = WT[(int64_t)k * H + c0 + (lane & 31)];
+  SAC_T(1, 1);
+  __syncthreads();  // lw1 staged (also when the tile computed no heads)
+  SAC_T(1, 2);
+  if (w == 0 && h == 0) {
+    for (int m = 0; m < O; ++m) lx[(lane & 31) * (kXLd + 1) + m] = xr[m];
+    lx[(lane & 31) * (kXLd + 1) + O] = act;
   }
-  if (blockIdx.y == 0 && !is_t) {
-    float* g1 = (data ? a.sc.q_g1[net] : a.ms.g1pi[net]) + (int64_t)item * H;
-    for (int i = 0; i < n2; ++i) g1[kb + i] = av[i];
+  __syncthreads();
+  first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O + 1, kb, av);
+  if (blockIdx.y == 0 && !is_t) {  // block-uniform
     if (data && w == 0 && h == 0)
       for (int m = 0; m < kXLd; ++m) a.sc.q_x[net][(int64_t)item * kXLd + m] = m < O ? xr[m] : (m == O ? act : 0.0f);
+    store_operands<H>((data ? a.sc.q_g1[net] + (int64_t)(r0 - B) * H : a.ms.g1pi[net] + (int64_t)r0 * H), lds, av, kb);
   }
+  SAC_T(1, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
+  SAC_T(1, 4);
+  const float w3 = C[L.c_w3 + c0 + (lane & 31)];
   splitk_finish(acc, lds, [&](int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + C[L.c_b2 + col]);
     if (is_t) a.ms.tg2[net - 2][(int64_t)r * H + col] = y;
     else if (r >= B) a.sc.q_g2[net][(int64_t)(r - B) * H + col] = y;
     else a.ms.g2pi[net][(int64_t)r * H + col] = y;
+    const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
+    if (cc == 0) a.ms.qpart[((int64_t)net * CB + blockIdx.y) * 2 * B + r] = pq;
   });
+  SAC_T(1, 5);
+  SAC_SPAN_END(1);
 }
 
 // grid (2 critics x 2B / 32 row tiles, H / 32): losses and dq (sac.py:170-247), dg2, dg1 = (dg2 W2) ⊙ [g1 > 0]
+template <int H>
 __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
-  __shared__ float lds[4 * 16 * 64];
+  __shared__ float lds[kLdsFloats];
+  SAC_T(2, 0);
+  SAC_SPAN_BEGIN(2);
   const Layout& L = a.L;
-  const int H = L.H, B = L.B;
+  const int B = L.B;
   const float* P = a.params;
   const float* TG = a.targets;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int qt = 2 * B / kTile2;
+  if ((int)blockIdx.x >= 2 * qt) {  // extra blocks (8, keeping the row-tile -> XCD map of the other kernels):
+    if (blockIdx.x == 2 * qt && blockIdx.y == 0 && threadIdx.x == 0) {  // step t and Adam's bias corrections
+      const int64_t t = *a.step + 1;            // (only actor_fwd read the old value)
+      *const_cast<int64_t*>(a.step) = t;
+      const AdamStep st = adam_step(a.hp, t);
+      a.stats[5] = st.step_pi;
+      a.stats[6] = st.step_q;
+      a.stats[7] = st.bc2_sqrt;
+    }
+    return;
+  }
   const int net = blockIdx.x / qt, rt = blockIdx.x % qt;
   const float* C = P + L.q_base[net];
   const int r0 = rt * kTile2, c0 = blockIdx.y * kTile2;
+  constexpr int n2 = H / 8;
+  constexpr int CB = H / kTile2;
+  const int kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < n2; ++i) bv[i] = C[L.c_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
   const int row = r0 + (lane & 31);
   const bool data = row >= B;
   const int item = data ? row - B : row;
@@ -407,19 +569,24 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
   const float invB = 1.0f / (float)B;
-  const float* g2row;
   float dq;
+  const int ib = data ? r0 - B : r0;  // first batch item of the tile (tiles never straddle B)
+  float* tg = lds + kLdsTileOff;      // this critic's g2 rows of the tile
+  float* lw3 = lds + kLdsHeadWOff;    // this critic's w3
+  tile_load<H>(tg, (data ? a.sc.q_g2[net] : a.ms.g2pi[net]) + (int64_t)ib * H);
+  stage(lw3, C + L.c_w3, H);
+  const float* qp = a.ms.qpart;
+  const int64_t qs = (int64_t)CB * 2 * B;  // one net's parts
   if (data) {  // Q losses on (obs, a)
-    const float q1b = row_dot(a.sc.q_g2[0] + (int64_t)item * H, P + L.q_base[0] + L.c_w3, H) + P[L.q_base[0] + L.c_b3];
-    const float q2b = row_dot(a.sc.q_g2[1] + (int64_t)item * H, P + L.q_base[1] + L.c_w3, H) + P[L.q_base[1] + L.c_b3];
-    const float t1 = row_dot(a.ms.tg2[0] + (int64_t)item * H, TG + L.c_w3, H) + TG[L.c_b3];
-    const float t2 = row_dot(a.ms.tg2[1] + (int64_t)item * H, TG + L.q_size + L.c_w3, H) + TG[L.q_size + L.c_b3];
+    const float q1b = sum_parts(qp, CB, 2 * B, B + item) + P[L.q_base[0] + L.c_b3];
+    const float q2b = sum_parts(qp + qs, CB, 2 * B, B + item) + P[L.q_base[1] + L.c_b3];
+    const float t1 = sum_parts(qp + 2 * qs, CB, 2 * B, item) + TG[L.c_b3];
+    const float t2 = sum_parts(qp + 3 * qs, CB, 2 * B, item) + TG[L.q_size + L.c_b3];
     const float tq = fminf(t1, t2) - alpha * a.ms.hdn[HD_LOGP * B + item];
     float qtv = a.hp.rscale * a.ms.rew[item] + ((1.0f - a.ms.term[item]) * a.hp.gamma) * tq;
     qtv = fminf(fmaxf(qtv, -a.hp.clip), a.hp.clip);
     const float dq1b = (2.0f * invB) * (q1b - qtv), dq2b = (2.0f * invB) * (q2b - qtv);
     dq = net == 0 ? dq1b : dq2b;
-    g2row = a.sc.q_g2[net] + (int64_t)item * H;
     if (store_rows) {
       a.sc.q_dq[0][item] = dq1b;
       a.sc.q_dq[1][item] = dq2b;
@@ -431,11 +598,10 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
       st[2 * B + item] = qtv;
     }
   } else {  // policy loss through min(Q1, Q2)(obs, ã)
-    const float q1a = row_dot(a.ms.g2pi[0] + (int64_t)item * H, P + L.q_base[0] + L.c_w3, H) + P[L.q_base[0] + L.c_b3];
-    const float q2a = row_dot(a.ms.g2pi[1] + (int64_t)item * H, P + L.q_base[1] + L.c_w3, H) + P[L.q_base[1] + L.c_b3];
+    const float q1a = sum_parts(qp, CB, 2 * B, item) + P[L.q_base[0] + L.c_b3];
+    const float q2a = sum_parts(qp + qs, CB, 2 * B, item) + P[L.q_base[1] + L.c_b3];
     const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
     dq = net == 0 ? -w1 * invB : -(1.0f - w1) * invB;
-    g2row = a.ms.g2pi[net] + (int64_t)item * H;
     if (store_rows) {
       const float logp = a.ms.hd[HD_LOGP * B + item], act = a.ms.hd[HD_A * B + item];
       const float qmin = fminf(q1a, q2a);
@@ -448,58 +614,65 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
       st[5 * B + item] = a.ms.hd[HD_STD * B + item];
     }
   }
-  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
-  float av[kMaxN2], bv[kMaxN2];
+  SAC_T(2, 1);
+  __syncthreads();  // g2 tile and w3 staged
 #pragma unroll
-  for (int i = 0; i < kMaxN2; ++i) {
-    if (i >= n2) break;
+  for (int i = 0; i < n2; ++i) {
     const int j = kb + i;
-    const float g2 = g2row[j];
-    av[i] = g2 > 0.0f ? dq * C[L.c_w3 + j] : 0.0f;
-    bv[i] = C[L.c_w2 + (int64_t)j * H + c0 + (lane & 31)];
+    av[i] = tg[(lane & 31) * (H + 4) + j] > 0.0f ? dq * lw3[j] : 0.0f;
   }
-  if (data && blockIdx.y == 0)
-    for (int i = 0; i < n2; ++i) a.sc.q_dg2[net][(int64_t)item * H + kb + i] = av[i];
+  if (data && blockIdx.y == 0) store_operands<H>(a.sc.q_dg2[net] + (int64_t)ib * H, tg, av, kb);  // block-uniform
+  SAC_T(2, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
+  SAC_T(2, 4);
+  const float wa = C[L.c_w1 + (int64_t)(c0 + (lane & 31)) * (L.O + 1) + L.O];  // fc0's action column
   splitk_finish(acc, lds, [&](int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     if (r >= B) {
       const int64_t o = (int64_t)(r - B) * H + col;
       a.sc.q_dg1[net][o] = a.sc.q_g1[net][o] > 0.0f ? v : 0.0f;
-    } else {
+    } else {  // (tile-uniform branch: the half-wave sum below runs in every lane)
       const int64_t o = (int64_t)r * H + col;
-      a.ms.dg1pi[net][o] = a.ms.g1pi[net][o] > 0.0f ? v : 0.0f;
+      const float d = a.ms.g1pi[net][o] > 0.0f ? v : 0.0f;
+      a.ms.dg1pi[net][o] = d;
+      const float pa = halfwave_sum(d * wa);  // this column block's part of dQ/dã for row r
+      if (cc == 0) a.ms.apart[((int64_t)net * CB + blockIdx.y) * B + r] = pa;
     }
   });
+  SAC_T(2, 5);
+  SAC_SPAN_END(2);
 }
 
 // grid (B / 32, H / 32): policy backward through the action (obs rows)
+template <int H>
 __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
-  __shared__ float lds[4 * 16 * 64];
+  __shared__ float lds[kLdsFloats];
+  SAC_T(3, 0);
+  SAC_SPAN_BEGIN(3);
   const Layout& L = a.L;
-  const int H = L.H, O = L.O, B = L.B;
+  const int O = L.O, B = L.B;
   const float* P = a.params;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
+  constexpr int n2 = H / 8;
+  constexpr int CB = H / kTile2;
+  const int kb = w * (H / 4) + h * n2;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < n2; ++i) bv[i] = P[L.p_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
   const int item = r0 + (lane & 31);
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
   const float invB = 1.0f / (float)B;
+  float* th = lds + kLdsTileOff;     // actor h2 rows of the tile
+  float* lwh = lds + kLdsHeadWOff;   // wm | ws
+  tile_load<H>(th, a.sc.a_h2 + (int64_t)r0 * H);
+  stage(lwh, P + L.p_wm, H);
+  stage(lwh + H, P + L.p_ws, H);
   // dA = Σ_m wa1[m] dg1_Q1[m] + Σ_m wa2[m] dg1_Q2[m] (wa: the action column of each critic's fc0)
-  float dA;
-  {
-    const int half = H / 2;
-    float s[2] = {0.0f, 0.0f};
-    for (int k = 0; k < 2; ++k) {
-      const float* dg = a.ms.dg1pi[k] + (int64_t)item * H;
-      const float* C = P + L.q_base[k];
-      for (int m = h * half; m < (h + 1) * half; ++m) s[k] = fmaf(C[L.c_w1 + (int64_t)m * (O + 1) + O], dg[m], s[k]);
-      const float o = __shfl_xor(s[k], 32, 64);
-      s[k] = h ? o + s[k] : s[k] + o;
-    }
-    dA = s[0] + s[1];
-  }
+  float dA = sum_parts(a.ms.apart, CB, B, item) + sum_parts(a.ms.apart + (int64_t)CB * B, CB, B, item);
+  SAC_T(3, 1);
   const float act = a.ms.hd[HD_A * B + item], z = a.ms.hd[HD_Z * B + item], mean = a.ms.hd[HD_MEAN * B + item];
   const float std = a.ms.hd[HD_STD * B + item], ls_raw = a.ms.hd[HD_LSRAW * B + item];
   if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
@@ -514,123 +687,25 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
     a.sc.a_dhead[(int64_t)item * 2] = dmean;
     a.sc.a_dhead[(int64_t)item * 2 + 1] = dls;
   }
-  const int n2 = H / 8, kb = w * (H / 4) + h * n2;
-  float av[kMaxN2], bv[kMaxN2];
+  SAC_T(3, 2);
+  __syncthreads();  // h2 tile and head weights staged
 #pragma unroll
-  for (int i = 0; i < kMaxN2; ++i) {
-    if (i >= n2) break;
+  for (int i = 0; i < n2; ++i) {
     const int j = kb + i;
-    const float h2 = a.sc.a_h2[(int64_t)item * H + j];
-    av[i] = h2 > 0.0f ? (P[L.p_wm + j] * dmean + P[L.p_ws + j] * dls) : 0.0f;
-    bv[i] = P[L.p_w2 + (int64_t)j * H + c0 + (lane & 31)];
+    av[i] = th[(lane & 31) * (H + 4) + j] > 0.0f ? (lwh[j] * dmean + lwh[H + j] * dls) : 0.0f;
   }
-  if (blockIdx.y == 0)
-    for (int i = 0; i < n2; ++i) a.sc.a_dh2[(int64_t)item * H + kb + i] = av[i];
+  if (blockIdx.y == 0) store_operands<H>(a.sc.a_dh2 + (int64_t)r0 * H, th, av, kb);
+  SAC_T(3, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
+  SAC_T(3, 4);
   splitk_finish(acc, lds, [&](int rr, int cc, float v) {
     const int64_t o = (int64_t)(r0 + rr) * H + c0 + cc;
     a.sc.a_dh1[o] = a.sc.a_h1[o] > 0.0f ? v : 0.0f;
   });
+  SAC_T(3, 5);
+  SAC_SPAN_END(3);
 }
-
-// weight gradients into the flat gradient: out[j][k] = Σ_r dY[r][j] X[r][k] (X null: ones -> bias).
-// Blocks [0, n_mfma): 32 x 32 tiles of the H x H matrices on MFMA (rows split over the 4 waves);
-// then VALU blocks, one output element per thread (rows summed in order); the last block: the loss
-// scalars, d(log α), α, the Adam bias corrections of this step and step += 1.
-struct WgArgs {
-  GMat mats[kMaxMats];
-  int n_mats;
-  int big[3];        // indices of the H x H matrices in mats
-  int n_mfma;        // MFMA tile blocks
-  int n_small;       // elements of the other matrices
-  int small_mat[kMaxMats];
-  int64_t small_start[kMaxMats + 1];  // prefix sums of M·N over the non-big matrices
-  int n_small_mats;
-  float* grads;
-  int B;
-  Scratch sc;
-  const float* params;
-  int64_t* step;
-  float* stats;
-  Hyper hp;
-};
-
-__global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
-  __shared__ float lds[4 * 16 * 64];
-  const int tid = threadIdx.x;
-  const int n_small_blocks = (a.n_small + 255) / 256;
-  if ((int)blockIdx.x == a.n_mfma + n_small_blocks) {  // scalars
-    float v[5] = {0, 0, 0, 0, 0};
-    for (int r = tid; r < a.B; r += kThreads) {
-      v[0] += a.sc.p_pl[r];
-      v[1] += a.sc.p_q1l[r];
-      v[2] += a.sc.p_q2l[r];
-      v[3] += a.sc.p_la[r];
-      v[4] += a.sc.p_ga[r];
-    }
-    __shared__ float red[4][32];
-    __shared__ float sum[32];
-    block_sum<5>(v, red, sum);
-    if (tid == 0) {
-      const float invB = 1.0f / (float)a.B;
-      a.stats[0] = sum[0] * invB;
-      a.stats[1] = sum[1] * invB;
-      a.stats[2] = sum[2] * invB;
-      a.stats[3] = a.hp.auto_ent ? sum[3] * invB : 0.0f;
-      a.stats[4] = a.hp.auto_ent ? expf(a.params[0]) : 1.0f;
-      a.grads[0] = a.hp.auto_ent ? sum[4] * invB : 0.0f;
-      const int64_t step = *a.step + 1;
-      *a.step = step;
-      const double t = (double)step;
-      const double bc1 = 1.0 - pow((double)a.hp.beta1, t);
-      const double bc2 = 1.0 - pow((double)a.hp.beta2, t);
-      a.stats[5] = (float)(a.hp.lr_pi / bc1);
-      a.stats[6] = (float)(a.hp.lr_q / bc1);
-      a.stats[7] = (float)sqrt(bc2);
-    }
-    return;
-  }
-  if ((int)blockIdx.x >= a.n_mfma) {  // VALU elements
-    const int64_t e = (int64_t)(blockIdx.x - a.n_mfma) * 256 + tid;
-    if (e >= a.n_small) return;
-    int s = 0;
-    while (s + 1 < a.n_small_mats && e >= a.small_start[s + 1]) ++s;
-    const GMat m = a.mats[a.small_mat[s]];
-    const int64_t l = e - a.small_start[s];
-    const int j = (int)(l / m.N), k = (int)(l % m.N);
-    float acc = 0.0f;
-    for (int r = 0; r < a.B; ++r) {
-      const float x = m.X ? m.X[(int64_t)r * m.ldX + k] : 1.0f;
-      acc = fmaf(m.dY[(int64_t)r * m.ldY + j], x, acc);
-    }
-    a.grads[m.out_off + l] = acc;
-    return;
-  }
-  // MFMA tile of an H x H matrix: A[j][r] = dY[r][j], B[r][k] = X[r][k]
-  const int H = a.mats[a.big[0]].M;
-  const int tiles = (H / kTile2) * (H / kTile2);
-  const GMat m = a.mats[a.big[blockIdx.x / tiles]];
-  const int t = blockIdx.x % tiles;
-  const int j0 = (t / (H / kTile2)) * kTile2, k0 = (t % (H / kTile2)) * kTile2;
-  const int w = tid >> 6, lane = tid & 63, h = lane >> 5;
-  const int rows_w = a.B / 4;  // this wave's rows, in chunks of up to 64 (32 MFMAs)
-  f32x16 acc = zero16();
-  for (int rc = 0; rc < rows_w; rc += 2 * kMaxN2) {
-    const int n2 = min(kMaxN2, (rows_w - rc) / 2), rb = w * rows_w + rc + h * n2;
-    float av[kMaxN2], bv[kMaxN2];
-#pragma unroll
-    for (int i = 0; i < kMaxN2; ++i) {
-      if (i >= n2) break;
-      const int64_t r = rb + i;
-      av[i] = m.dY[r * m.ldY + j0 + (lane & 31)];
-      bv[i] = m.X[r * m.ldX + k0 + (lane & 31)];
-    }
-    mfma_chain(acc, av, bv, n2);
-  }
-  splitk_finish(acc, lds, [&](int rr, int cc, float v) { a.grads[m.out_off + (int64_t)(j0 + rr) * m.N + k0 + cc] = v; });
-}
-
 
 // ---------------------------------------------------------------------------------------------
 // Adam (torch.optim.Adam, amsgrad=False, no weight decay) + soft target update + transposes
@@ -651,33 +726,221 @@ struct ApplyArgs {
 
 constexpr int kTile = 32;
 
-// Adam bias corrections of this step, computed once by the weight-gradient kernel (stats[5..7])
-struct AdamStep {
-  float step_pi, step_q, bc2_sqrt;
+
+// one element: gradient (the flat gradient, all-reduced when data parallel), torch.optim.Adam, soft
+// update. Loads (ld) and update/stores (st) are split so a thread can put several elements' loads in
+// flight before the first update.
+struct AdamElem {
+  float g, m, v, p, t;
+  bool q;
 };
 
-// one element: gradient (the flat gradient, all-reduced when data parallel), torch.optim.Adam, soft update
-__device__ __forceinline__ float adam_elem(const ApplyArgs& a, const AdamStep& st, int64_t e, float* tp_out) {
+__device__ __forceinline__ AdamElem adam_ld(const ApplyArgs& a, int64_t e) {
   const Layout& L = a.L;
-  float g = a.grads[e];
-  g *= a.hp.inv_world;
-  const bool is_q = e >= L.q_base[0];
-  float m = a.m[e], v = a.v[e];
-  m = m + (1.0f - a.hp.beta1) * (g - m);             // exp_avg.lerp_(grad, 1 - beta1)
-  v = v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+  AdamElem x;
+  x.q = e >= L.q_base[0];
+  x.g = a.grads[e];
+  x.m = a.m[e];
+  x.v = a.v[e];
+  x.p = a.params[e];
+  x.t = x.q ? a.targets[e - L.q_base[0]] : 0.0f;
+  return x;
+}
+
+__device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, int64_t e, AdamElem& x) {
+  const float g = x.g * a.hp.inv_world;
+  const float m = x.m + (1.0f - a.hp.beta1) * (g - x.m);         // exp_avg.lerp_(grad, 1 - beta1)
+  const float v = x.v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
   const float denom = sqrtf(v) / st.bc2_sqrt + a.hp.eps;
-  const float p = a.params[e] + (-(is_q ? st.step_q : st.step_pi)) * (m / denom);
+  const float p = x.p + (-(x.q ? st.step_q : st.step_pi)) * (m / denom);
   a.m[e] = m;
   a.v[e] = v;
   a.params[e] = p;
-  if (is_q) {
-    const int64_t qe = e - L.q_base[0];
-    const float tp = a.targets[qe] * (1.0f - a.hp.tau) + p * a.hp.tau;
-    a.targets[qe] = tp;
-    *tp_out = tp;
+  x.p = p;
+  if (x.q) {
+    x.t = x.t * (1.0f - a.hp.tau) + p * a.hp.tau;
+    a.targets[e - a.L.q_base[0]] = x.t;
   }
-  return p;
 }
+
+// weight gradients into the flat gradient: out[j][k] = Σ_r dY[r][j] X[r][k] (X null: ones -> bias).
+// Blocks [0, n_mfma): 32 x 32 tiles of the H x H matrices on MFMA (rows split over the 4 waves);
+// then VALU blocks, one output element per thread (rows summed in order); the last block: the loss
+// scalars, d(log α), α, the Adam bias corrections of this step and step += 1.
+// the matrix table lives in device memory (a kernel-argument array indexed by a run-time value would
+// be copied to scratch in every thread)
+struct WgTable {
+  GMat mats[kMaxMats];
+  int n_mats;
+  int big[3];                         // indices of the H x H matrices in mats
+  int big_slot[3];                    // their W2ᵀ slot in T (0 actor, 1 / 2 Q1 / Q2; targets at + 2)
+  int has_scalar;                     // the last block reduces the losses and updates log α
+  int small_mat[kMaxMats];
+  int64_t small_start[kMaxMats + 1];  // prefix sums of M·N over the non-big matrices
+  int n_small_mats;
+};
+
+struct WgArgs {
+  const WgTable* tab;
+  int n_mfma;   // MFMA tile blocks
+  int n_small;  // elements of the other matrices
+  float* grads;
+  int B;
+  Scratch sc;
+  const float* params;
+  const int64_t* step;  // this step's number t (critic_fwd advanced it)
+  float* stats;
+  Hyper hp;
+  int n_blocks;  // grid
+  int fuse;      // single process: each block also applies Adam / soft update / W2ᵀ to the elements it finished
+  ApplyArgs ap;  // (fuse) parameters, optimizer state, targets, transposed copies
+};
+
+__global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
+  __shared__ float lds[4 * 16 * 64];
+  __shared__ WgTable tab;  // one coalesced copy instead of a chain of dependent global loads
+  __shared__ AdamStep sst;
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tab);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&tab);
+    for (int e = threadIdx.x; e < (int)(sizeof(WgTable) / 4); e += 256) dst[e] = src[e];
+    if (threadIdx.x == 0) sst = AdamStep{a.stats[5], a.stats[6], a.stats[7]};  // (critic_fwd)
+    __syncthreads();
+  }
+  const int tid = threadIdx.x;
+  SAC_T(4, 0);
+  SAC_SPAN_BEGIN(4);
+  SAC_TB(4, 6, (int)blockIdx.x == a.n_mfma);
+  const int n_small_blocks = (a.n_small + 63) / 64;
+  if (tab.has_scalar && (int)blockIdx.x == a.n_mfma + n_small_blocks) {  // scalars
+    float v[5] = {0, 0, 0, 0, 0};
+    for (int r = tid; r < a.B; r += kThreads) {
+      v[0] += a.sc.p_pl[r];
+      v[1] += a.sc.p_q1l[r];
+      v[2] += a.sc.p_q2l[r];
+      v[3] += a.sc.p_la[r];
+      v[4] += a.sc.p_ga[r];
+    }
+    __shared__ float red[4][32];
+    __shared__ float sum[32];
+    block_sum<5>(v, red, sum);
+    if (tid == 0) {
+      const float invB = 1.0f / (float)a.B;
+      a.stats[0] = sum[0] * invB;
+      a.stats[1] = sum[1] * invB;
+      a.stats[2] = sum[2] * invB;
+      a.stats[3] = a.hp.auto_ent ? sum[3] * invB : 0.0f;
+      a.stats[4] = a.hp.auto_ent ? expf(a.params[0]) : 1.0f;
+      const float g0 = a.hp.auto_ent ? sum[4] * invB : 0.0f;
+      a.grads[0] = g0;
+      if (a.fuse && a.hp.auto_ent) {  // log α
+        AdamElem x = adam_ld(a.ap, 0);
+        x.g = g0;
+        adam_st(a.ap, sst, 0, x);
+      }
+    }
+    SAC_SPAN_END(4);
+    return;
+  }
+  if ((int)blockIdx.x >= a.n_mfma) {  // VALU elements: 64 per block, wave w sums rows [wB/4, (w+1)B/4)
+    const int w = tid >> 6;
+    const int64_t e = (int64_t)(blockIdx.x - a.n_mfma) * 64 + (tid & 63);
+    float acc = 0.0f;
+    int s = 0;
+    int64_t l = 0;
+    const GMat* m = nullptr;
+    if (e < a.n_small) {
+      const WgTable& tb = tab;
+      while (s + 1 < tb.n_small_mats && e >= tb.small_start[s + 1]) ++s;
+      m = &tb.mats[tb.small_mat[s]];
+      l = e - tb.small_start[s];
+      const int j = (int)(l / m->N), k = (int)(l % m->N);
+      const int rq = a.B / 4, rb = w * rq;
+      const gptr dy = as_global(m->dY) + (int64_t)rb * m->ldY + j;
+      const gptr x = m->X ? as_global(m->X) + (int64_t)rb * m->ldX + k : nullptr;
+      for (int r0 = 0; r0 < rq; r0 += 32) {  // 32 rows' loads in flight, then the fmaf chain in row order
+        float yv[32], xv[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+          const bool ok = r0 + u < rq;
+          yv[u] = ok ? dy[(int64_t)(r0 + u) * m->ldY] : 0.0f;
+          xv[u] = ok ? (x ? x[(int64_t)(r0 + u) * m->ldX] : 1.0f) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 32; ++u) acc = fmaf(yv[u], xv[u], acc);
+      }
+    }
+    SAC_TB(4, 7, (int)blockIdx.x == a.n_mfma);
+    float* part = lds;  // [4][64]
+    part[w * 64 + (tid & 63)] = acc;
+    __syncthreads();
+    if (w == 0 && m) {
+      const int c = tid & 63;
+      const int64_t e = m->out_off + l;
+      AdamElem x;
+      if (a.fuse) x = adam_ld(a.ap, e);  // (in flight while the partials are added)
+      x.g = ((part[c] + part[64 + c]) + part[128 + c]) + part[192 + c];
+      a.grads[e] = x.g;
+      if (a.fuse) adam_st(a.ap, sst, e, x);
+    }
+    SAC_TB(4, 8, (int)blockIdx.x == a.n_mfma);
+    SAC_SPAN_END(4);
+    return;
+  }
+  // MFMA tile of an H x H matrix: A[j][r] = dY[r][j], B[r][k] = X[r][k]
+  const WgTable& tb = tab;
+  const int H = tb.mats[tb.big[0]].M;
+  const int tiles = (H / kTile2) * (H / kTile2);
+  const GMat m = tb.mats[tb.big[blockIdx.x / tiles]];
+  const int t = blockIdx.x % tiles;
+  const int j0 = (t / (H / kTile2)) * kTile2, k0 = (t % (H / kTile2)) * kTile2;
+  const int w = tid >> 6, lane = tid & 63, h = lane >> 5;
+  const int mat = tb.big_slot[blockIdx.x / tiles];  // 0: actor W2, 1 / 2: Q1 / Q2 W2
+  AdamElem x[4];
+  if (a.fuse)  // the optimizer state of the four outputs this lane finishes, in flight during the GEMM
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = adam_ld(a.ap, m.out_off + (int64_t)(j0 + finish_row(q)) * m.N + k0 + (lane & 31));
+  const int rows_w = a.B / 4;  // this wave's rows, in chunks of up to 64 (32 MFMAs)
+  f32x16 acc = zero16();
+  for (int rc = 0; rc < rows_w; rc += 2 * kMaxN2) {
+    const int n2 = min(kMaxN2, (rows_w - rc) / 2), rb = w * rows_w + rc + h * n2;
+    float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+    for (int i = 0; i < kMaxN2; ++i) {
+      if (i >= n2) continue;  // (continue, not break: the constant trip count keeps the loop unrolled)
+      const int64_t r = rb + i;
+      av[i] = as_global(m.dY)[r * m.ldY + j0 + (lane & 31)];
+      bv[i] = as_global(m.X)[r * m.ldX + k0 + (lane & 31)];
+    }
+    SAC_T(4, 1);
+    mfma_chain(acc, av, bv, n2);
+  }
+  SAC_T(4, 2);
+  __shared__ float tt[2][kTile][kTile + 1];  // (fuse) updated parameters / targets, transposed
+  splitk_finish_q(acc, lds, [&](int q, int rr, int cc, float v) {
+    const int64_t e = m.out_off + (int64_t)(j0 + rr) * m.N + k0 + cc;
+    a.grads[e] = v;
+    if (a.fuse) {
+      x[q].g = v;
+      adam_st(a.ap, sst, e, x[q]);
+      tt[0][cc][rr] = x[q].p;
+      tt[1][cc][rr] = x[q].t;
+    }
+  });
+  if (a.fuse) {  // W2ᵀ (and the target's) for the next step's forward passes: T[col][row]
+    __syncthreads();
+    const int64_t HH = (int64_t)H * H;
+    const int tc = tid % kTile, tr = tid / kTile;
+    for (int cc = tr; cc < kTile; cc += kThreads / kTile) {
+      const int64_t o = (int64_t)(k0 + cc) * H + j0 + tc;
+      a.ap.T[(size_t)mat * HH + o] = tt[0][cc][tc];
+      if (mat > 0) a.ap.T[(size_t)(2 + mat) * HH + o] = tt[1][cc][tc];
+    }
+  }
+  SAC_T(4, 3);
+  SAC_SPAN_END(4);
+}
+
 
 __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
   __shared__ float tile[2][kTile][kTile + 1];
@@ -688,16 +951,20 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
   const int64_t w2[3] = {L.p_w2, L.q_base[0] + L.c_w2, L.q_base[1] + L.c_w2};
   if ((int)blockIdx.x < a.n_tile_blocks) {
     // 32 x 32 tile of one W2: Adam on row-major elements, transposed copies written through LDS
+    constexpr int kPer = kTile / (kThreads / kTile);  // 4 rows per thread
     const int tpm = (H / kTile) * (H / kTile);
     const int mat = blockIdx.x / tpm, t = blockIdx.x % tpm;
     const int r0 = (t / (H / kTile)) * kTile, c0 = (t % (H / kTile)) * kTile;
     const int tc = threadIdx.x % kTile, tr = threadIdx.x / kTile;  // 8 rows per pass
-    for (int rr = tr; rr < kTile; rr += kThreads / kTile) {
-      float tp = 0.0f;
-      const int64_t l = (int64_t)(r0 + rr) * H + c0 + tc;
-      const float p = adam_elem(a, st, w2[mat] + l, &tp);
-      tile[0][tc][rr] = p;
-      tile[1][tc][rr] = tp;
+    AdamElem x[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) x[u] = adam_ld(a, w2[mat] + (int64_t)(r0 + tr + u * 8) * H + c0 + tc);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int rr = tr + u * 8;
+      adam_st(a, st, w2[mat] + (int64_t)(r0 + rr) * H + c0 + tc, x[u]);
+      tile[0][tc][rr] = x[u].p;
+      tile[1][tc][rr] = x[u].t;
     }
     __syncthreads();
     for (int cc = tr; cc < kTile; cc += kThreads / kTile) {
@@ -719,8 +986,8 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
     if (e >= w2[k]) e += HH;
   if (e >= L.n_params) return;
   if (e == 0 && !a.hp.auto_ent) return;
-  float tp;
-  adam_elem(a, st, e, &tp);
+  AdamElem x = adam_ld(a, e);
+  adam_st(a, st, e, x);
 }
 
 __global__ void sac_transpose_kernel(const float* params, const float* targets, float* T, Layout L) {
@@ -733,6 +1000,21 @@ __global__ void sac_transpose_kernel(const float* params, const float* targets, 
                      : which <= 2 ? params + L.q_base[which - 1] + L.c_w2
                                   : targets + (int64_t)(which - 3) * L.q_size + L.c_w2;
   T[which * HH + (l % L.H) * L.H + l / L.H] = src[l];
+}
+
+// the four forward/backward passes of one grad step for hidden width H (a compile-time tile count)
+template <int H>
+void launch_passes(const MArgs& a, hipStream_t st, int part) {
+  const int B = a.L.B, ct = H / kTile2;
+  if (part == 0) {
+    hipLaunchKernelGGL(sac_actor_fwd_kernel<H>, dim3(2 * B / kTile2, ct), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sac_critic_fwd_kernel<H>, dim3(6 * B / kTile2, ct), dim3(256), 0, st, a);
+    // (grid x a multiple of 8 everywhere: block i runs on XCD i % 8, so row tile r of every kernel
+    //  lands on XCD r % 8, the L2 that holds what the previous kernel wrote for those rows)
+    hipLaunchKernelGGL(sac_critic_bwd_kernel<H>, dim3(4 * B / kTile2 + 8, ct), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(sac_actor_bwd_kernel<H>, dim3(B / kTile2, ct), dim3(256), 0, st, a);
+  }
 }
 
 }  // namespace
@@ -756,7 +1038,8 @@ struct sacf_handle {
   float* scratch;
   Scratch sc;
   MScratch ms;
-  WgArgs wg;
+  WgArgs wg[1];       // weight gradients (+ losses, log α, and the update when world_size == 1)
+  WgTable* wtab[1];
   char err[512];
 };
 
@@ -845,8 +1128,10 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   // scratch: actor 4·B·H + B·16 + 2B; critics 2·(4·B·H + B·16 + B); per-row losses 5B;
   // MFMA path: batch 2·B·16 + 5B, h2n B·H, heads 12B, (g1, g2, dg1) on (obs, ã) 6·B·H, targets 2·B·H
   const int64_t BH = (int64_t)B * H;
+  const int64_t CB = H / kTile2;
   const int64_t n_scr = 4 * BH + B * kXLd + 2 * B + 2 * (4 * BH + B * kXLd + B) + 5 * B +
-                        2 * B * kXLd + 5 * B + BH + 12 * B + 6 * BH + 2 * BH;
+                        2 * B * kXLd + 5 * B + BH + 12 * B + 6 * BH + 2 * BH +
+                        2 * CB * 2 * B + 4 * CB * 2 * B + 2 * CB * B;
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
     *out = h;
@@ -889,54 +1174,69 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     ms.dg1pi[k] = s; s += BH;
     ms.tg2[k] = s; s += BH;
   }
+  ms.hpart = s; s += 2 * CB * 2 * B;
+  ms.qpart = s; s += 4 * CB * 2 * B;
+  ms.apart = s; s += 2 * CB * B;
   e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);
   if (e != hipSuccess) {
     *out = h;
     return sfail(h, SACF_EHIP, "hipMalloc(T): %s", hipGetErrorString(e));
   }
-  // weight-gradient matrices: the three H x H ones on MFMA tiles, the rest one element per thread
-  WgArgs& wg = h->wg;
-  memset(&wg, 0, sizeof(wg));
-  int nm = 0;
-  auto add = [&](const float* dY, int ldY, const float* X, int ldX, int M, int N, int64_t off) {
-    wg.mats[nm++] = GMat{dY, X, ldY, ldX, M, N, off};
-  };
-  add(sc.a_dh1, H, sc.a_x, kXLd, H, O, L.p_w1);
-  add(sc.a_dh1, H, nullptr, 0, H, 1, L.p_b1);
-  add(sc.a_dh2, H, sc.a_h1, H, H, H, L.p_w2);
-  add(sc.a_dh2, H, nullptr, 0, H, 1, L.p_b2);
-  add(sc.a_dhead, 2, sc.a_h2, H, 1, H, L.p_wm);
-  add(sc.a_dhead, 2, nullptr, 0, 1, 1, L.p_bm);
-  add(sc.a_dhead + 1, 2, sc.a_h2, H, 1, H, L.p_ws);
-  add(sc.a_dhead + 1, 2, nullptr, 0, 1, 1, L.p_bs);
-  for (int k = 0; k < 2; ++k) {
-    const int64_t b = L.q_base[k];
-    add(sc.q_dg1[k], H, sc.q_x[k], kXLd, H, O + 1, b + L.c_w1);
-    add(sc.q_dg1[k], H, nullptr, 0, H, 1, b + L.c_b1);
-    add(sc.q_dg2[k], H, sc.q_g1[k], H, H, H, b + L.c_w2);
-    add(sc.q_dg2[k], H, nullptr, 0, H, 1, b + L.c_b2);
-    add(sc.q_dq[k], 1, sc.q_g2[k], H, 1, H, b + L.c_w3);
-    add(sc.q_dq[k], 1, nullptr, 0, 1, 1, b + L.c_b3);
-  }
-  wg.n_mats = nm;
-  int nb = 0;
-  wg.n_small_mats = 0;
-  wg.small_start[0] = 0;
-  for (int mi = 0; mi < nm; ++mi) {
-    const GMat& m = wg.mats[mi];
-    if (m.M == H && m.N == H && m.X) {
-      wg.big[nb++] = mi;
-    } else {
-      wg.small_mat[wg.n_small_mats] = mi;
-      wg.small_start[wg.n_small_mats + 1] = wg.small_start[wg.n_small_mats] + (int64_t)m.M * m.N;
-      wg.n_small_mats++;
+  // weight-gradient matrices: the H x H ones on MFMA tiles, the rest one element per thread (one launch;
+  // a fork of the critics' part onto a second stream beside actor_bwd measured slower, and the critics'
+  // log α update would race with actor_bwd's read of α)
+  for (int part = 0; part < 1; ++part) {
+    WgArgs& wg = h->wg[part];
+    memset(&wg, 0, sizeof(wg));
+    WgTable tab;
+    memset(&tab, 0, sizeof(tab));
+    int nm = 0, nb = 0;
+    auto add = [&](const float* dY, int ldY, const float* X, int ldX, int M, int N, int64_t off, int slot) {
+      if (M == H && N == H && X) {
+        tab.big[nb] = nm;
+        tab.big_slot[nb++] = slot;
+      } else {
+        tab.small_mat[tab.n_small_mats] = nm;
+        tab.small_start[tab.n_small_mats + 1] = tab.small_start[tab.n_small_mats] + (int64_t)M * N;
+        tab.n_small_mats++;
+      }
+      tab.mats[nm++] = GMat{dY, X, ldY, ldX, M, N, off};
+    };
+    {
+      add(sc.a_dh1, H, sc.a_x, kXLd, H, O, L.p_w1, -1);
+      add(sc.a_dh1, H, nullptr, 0, H, 1, L.p_b1, -1);
+      add(sc.a_dh2, H, sc.a_h1, H, H, H, L.p_w2, 0);
+      add(sc.a_dh2, H, nullptr, 0, H, 1, L.p_b2, -1);
+      add(sc.a_dhead, 2, sc.a_h2, H, 1, H, L.p_wm, -1);
+      add(sc.a_dhead, 2, nullptr, 0, 1, 1, L.p_bm, -1);
+      add(sc.a_dhead + 1, 2, sc.a_h2, H, 1, H, L.p_ws, -1);
+      add(sc.a_dhead + 1, 2, nullptr, 0, 1, 1, L.p_bs, -1);
+      for (int k = 0; k < 2; ++k) {
+        const int64_t b = L.q_base[k];
+        add(sc.q_dg1[k], H, sc.q_x[k], kXLd, H, O + 1, b + L.c_w1, -1);
+        add(sc.q_dg1[k], H, nullptr, 0, H, 1, b + L.c_b1, -1);
+        add(sc.q_dg2[k], H, sc.q_g1[k], H, H, H, b + L.c_w2, 1 + k);
+        add(sc.q_dg2[k], H, nullptr, 0, H, 1, b + L.c_b2, -1);
+        add(sc.q_dq[k], 1, sc.q_g2[k], H, 1, H, b + L.c_w3, -1);
+        add(sc.q_dq[k], 1, nullptr, 0, 1, 1, b + L.c_b3, -1);
+      }
+      tab.has_scalar = 1;
     }
+    tab.n_mats = nm;
+    wg.n_small = (int)tab.small_start[tab.n_small_mats];
+    e = hipMalloc(&h->wtab[part], sizeof(WgTable));
+    if (e == hipSuccess) e = hipMemcpy(h->wtab[part], &tab, sizeof(WgTable), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      *out = h;
+      return sfail(h, SACF_EHIP, "wgrad table: %s", hipGetErrorString(e));
+    }
+    wg.tab = h->wtab[part];
+    wg.n_mfma = nb * (H / kTile2) * (H / kTile2);
+    wg.n_blocks = wg.n_mfma + (wg.n_small + 63) / 64 + tab.has_scalar;
+    wg.B = B;
+    wg.sc = sc;
+    wg.hp = h->hp;
   }
-  wg.n_small = (int)wg.small_start[wg.n_small_mats];
-  wg.n_mfma = nb * (H / kTile2) * (H / kTile2);
-  wg.B = B;
-  wg.sc = sc;
-  wg.hp = h->hp;
   *out = h;
   return SACF_OK;
 }
@@ -946,13 +1246,19 @@ int sacf_destroy(sacf_handle* h) {
   SDev g(h->device);
   if (h->scratch) (void)hipFree(h->scratch);
   if (h->T) (void)hipFree(h->T);
+  if (h->wtab[0]) (void)hipFree(h->wtab[0]);
   delete h;
   return SACF_OK;
 }
 
 #ifdef SACF_PHASE_TIMING
-int sacf_debug_stamps(unsigned long long* out16) {
-  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_sac_stamp), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -1;
+int sacf_debug_reset(void) {
+  unsigned long long init[64];
+  for (int i = 0; i < 64; ++i) init[i] = i % 12 == 9 ? ~0ull : 0ull;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sac_stamp), init, sizeof(init)) == hipSuccess ? 0 : -1;
+}
+int sacf_debug_stamps(unsigned long long* out64) {
+  return hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_sac_stamp), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -1006,6 +1312,38 @@ int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const fl
   return SACF_OK;
 }
 
+// the forward/backward passes for the handle's hidden width: part 0 = actor_fwd, critic_fwd, critic_bwd;
+// part 1 = actor_bwd
+static bool launch_hidden(int H, const MArgs& a, hipStream_t st, int part) {
+  switch (H) {
+    case 32: launch_passes<32>(a, st, part); return true;
+    case 64: launch_passes<64>(a, st, part); return true;
+    case 96: launch_passes<96>(a, st, part); return true;
+    case 128: launch_passes<128>(a, st, part); return true;
+    case 160: launch_passes<160>(a, st, part); return true;
+    case 192: launch_passes<192>(a, st, part); return true;
+    case 224: launch_passes<224>(a, st, part); return true;
+    case 256: launch_passes<256>(a, st, part); return true;
+    default: return false;
+  }
+}
+
+static ApplyArgs apply_args(const sacf_handle* h) {
+  ApplyArgs a;
+  a.params = h->params;
+  a.targets = h->targets;
+  a.grads = h->grads;
+  a.m = h->adam_m;
+  a.v = h->adam_v;
+  a.step = h->step;
+  a.T = h->T;
+  a.L = h->L;
+  a.hp = h->hp;
+  a.stats = h->stats;
+  a.n_tile_blocks = 3 * (h->L.H / kTile) * (h->L.H / kTile);
+  return a;
+}
+
 int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
                const float* next_obs, const float* eps) {
   if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_grads: buffers not bound");
@@ -1033,37 +1371,26 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   a.ms = h->ms;
   a.L = h->L;
   a.hp = h->hp;
-  const int B = h->L.B, H = h->L.H, ct = H / kTile2;
   SDev g(h->device);
-  hipLaunchKernelGGL(sac_actor_fwd_kernel, dim3(2 * B / kTile2, ct), dim3(256), 0, h->stream, a);
-  hipLaunchKernelGGL(sac_critic_fwd_kernel, dim3(6 * B / kTile2, ct), dim3(256), 0, h->stream, a);
-  hipLaunchKernelGGL(sac_critic_bwd_kernel, dim3(4 * B / kTile2, ct), dim3(256), 0, h->stream, a);
-  hipLaunchKernelGGL(sac_actor_bwd_kernel, dim3(B / kTile2, ct), dim3(256), 0, h->stream, a);
-  WgArgs& w = h->wg;
+  if (!launch_hidden(h->L.H, a, h->stream, 0)) return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);
+  launch_hidden(h->L.H, a, h->stream, 1);
+  WgArgs& w = h->wg[0];
   w.grads = h->grads;
   w.params = h->params;
   w.step = h->step;
   w.stats = h->stats;
-  hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_mfma + (w.n_small + 255) / 256 + 1), dim3(256), 0, h->stream, w);
+  w.fuse = h->cfg.world_size == 1;  // no all-reduce between gradient and update: apply in the same kernel
+  w.ap = apply_args(h);
+  hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_blocks), dim3(256), 0, h->stream, w);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
 }
 
 int sacf_apply(sacf_handle* h) {
   if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_apply: buffers not bound");
-  ApplyArgs a;
-  a.params = h->params;
-  a.targets = h->targets;
-  a.grads = h->grads;
-  a.m = h->adam_m;
-  a.v = h->adam_v;
-  a.step = h->step;
-  a.T = h->T;
-  a.L = h->L;
-  a.hp = h->hp;
-  a.stats = h->stats;
+  if (h->cfg.world_size == 1) return SACF_OK;  // sacf_grads already applied the update
+  ApplyArgs a = apply_args(h);
   const int64_t HH = (int64_t)h->L.H * h->L.H;
-  a.n_tile_blocks = 3 * (h->L.H / kTile) * (h->L.H / kTile);
   const int64_t rest = h->L.n_params - 3 * HH;
   SDev g(h->device);
   hipLaunchKernelGGL(sac_apply_kernel, dim3((unsigned)(a.n_tile_blocks + (rest + kThreads - 1) / kThreads)),

@@ -62,6 +62,9 @@ def build_parser():
     p.add_argument("--n_envs", type=int, default=4096, help="device envs per GPU (0 = reference single-env graph)")
     p.add_argument("--eval_envs", type=int, default=256)
     p.add_argument("--slice_ticks", type=int, default=64)
+    p.add_argument("--match_update_ratio", type=_bool, default=True,
+                   help="grad steps per train loop = collected decisions (all ranks) x num_trains / num_expl_steps "
+                        "(the reference's ratio); false: num_trains_per_train_loop per loop")
     p.add_argument("--machinery", type=str, default="detailed", choices=["detailed", "simplified"])
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--log_dir", type=str, default=None)
@@ -86,7 +89,8 @@ def make_variant(args):
                             qf_lr=args.qf_lr, reward_scale=args.reward_scale,
                             use_automatic_entropy_tuning=args.use_automatic_entropy_tuning,
                             action_reg_coeff=args.action_reg_coeff, clip_val=args.clip_val),
-        n_envs=args.n_envs, slice_ticks=args.slice_ticks, machinery=args.machinery)
+        n_envs=args.n_envs, slice_ticks=args.slice_ticks, machinery=args.machinery,
+        match_update_ratio=args.match_update_ratio)
 
 
 def _networks(obs_dim, act_dim, M, device):
@@ -162,7 +166,7 @@ def experiment_device(variant, args, device, process_group=None):
     trainer.broadcast_parameters(0)
     return DeviceBatchRLAlgorithm(trainer=trainer, exploration_env=expl_env, evaluation_env=eval_env,
                                   exploration_data_collector=expl_coll, evaluation_data_collector=eval_coll,
-                                  replay_buffer=rb, **ak)
+                                  replay_buffer=rb, match_update_ratio=variant.get("match_update_ratio", True), **ak)
 
 
 def main(argv=None):

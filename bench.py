@@ -133,7 +133,7 @@ def sac_flops_per_step(B, H, O):
     return 2 * (mac_fwd + mac_bwd + mac_wg)
 
 
-def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
+def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
     """SAC grad-steps/s (secondary metric): FusedSACTrainer HIP-graph step (runner networks: 2x256
     hidden, batch `batch` per GPU, on-device uniform sampling from a 300k-row DeviceReplayBuffer,
     RCCL gradient all-reduce when world > 1), beside the reference-order eager SACTrainer."""
@@ -180,7 +180,7 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
     def fused(backend):
         pol, q = nets()
         tr = FusedSACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3],
-                             batch_size=batch, process_group=pg, backend=backend, **hp)
+                             batch_size=batch, process_group=pg, backend=backend, use_graph=graph, **hp)
         tr.broadcast_parameters(0)
         tr.train_from_buffer(rb, 10)  # captures the graph
         return timed(lambda k: tr.train_from_buffer(rb, k), steps)
@@ -200,7 +200,7 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40):
                         "note": "algorithmic matrix flops of one grad step (2 per multiply-add: forward, "
                                 "backward and weight-gradient products of every layer, per rank) / whole-step "
                                 "wall time (all six launches); v_mfma_f32_32x32x2_f32 dense f32 peak"}}
-    if world == 1:
+    if world == 1 and eager_steps:
         res["torch_ops_graph_grad_steps_per_s"] = steps / fused("torch")
     if world == 1 and eager_steps:
         pol, q = nets()

@@ -6,13 +6,14 @@
  * torch.optim.Adam for log_alpha / policy / qf1 / qf2) for the runner's networks:
  *   policy  TanhGaussianPolicy(obs_dim -> H -> H -> (mean, log_std)), act_dim = 1
  *   qf1/qf2 ConcatMlp(obs_dim + 1 -> H -> H -> 1), targets likewise
- * with three launches per grad step:
- *   sacf_grads : rows kernel (batch gather/sampling, every forward, losses, per-row backward)
- *                + weight-gradient kernel (flat fp32 gradient of [log_alpha | policy | qf1 | qf2])
- *   sacf_apply : Adam (torch.optim.Adam semantics, betas/eps as configured) on every parameter,
- *                soft target update, refresh of the library's transposed weight copies.
- * Between the two a caller may all-reduce the flat gradient (data parallel); sacf_apply divides
- * it by world_size.
+ * as batched fp32 GEMMs on the matrix cores (v_mfma_f32_32x32x2_f32):
+ *   sacf_grads : four forward/backward kernels (batch gather/sampling, every layer, losses) and the
+ *                weight-gradient kernel (flat fp32 gradient of [log_alpha | policy | qf1 | qf2]);
+ *                with world_size == 1 that kernel also applies Adam (torch.optim.Adam semantics,
+ *                betas/eps as configured), the soft target update and the refresh of the library's
+ *                transposed weight copies to the elements it finishes: five launches per grad step.
+ *   sacf_apply : world_size > 1 only (a no-op otherwise): the same update as a sixth launch, after the
+ *                caller all-reduced the flat gradient; the gradient is divided by world_size.
  *
  * Memory: the caller owns the flat buffers (torch tensors) bound with sacf_bind; the library owns
  * its scratch (per-row activations, ≈12·B·H floats) and transposed copies of the H×H weights.
@@ -73,7 +74,8 @@ int sacf_set_stream(sacf_handle* h, void* stream);
 /* element counts of the flat params / targets buffers */
 int64_t sacf_param_count(const sacf_handle* h);
 int64_t sacf_target_count(const sacf_handle* h);
-/* stats buffer: [policy_loss, qf1_loss, qf2_loss, alpha_loss, alpha, 0, 0, 0] then per row
+/* stats buffer: [policy_loss, qf1_loss, qf2_loss, alpha_loss, alpha, Adam step sizes (pi, q) and
+ * sqrt(1 - beta2^t) of this step] then per row
  * q1_pred[B], q2_pred[B], q_target[B], log_pi[B], tanh(mean)[B], std[B] */
 int64_t sacf_stats_count(const sacf_handle* h);
 /* Bind caller-owned device buffers (params/targets/grads/adam_m/adam_v: param or target count
@@ -85,12 +87,13 @@ int sacf_sync_params(sacf_handle* h);
 /* Replay ring (DeviceReplayBuffer storage, float32 rows) sampled uniformly with replacement. */
 int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
                     const float* next_obs, const int64_t* size_dev, int64_t capacity, uint64_t seed);
-/* Gradient of one update into `grads` (and step += 1). With obs == NULL the batch is sampled from
+/* Gradient of one update into `grads` (and step += 1); with world_size == 1 also the update itself
+ * (grads keeps the gradient for inspection). With obs == NULL the batch is sampled from
  * the replay ring; with eps == NULL the 2·B reparameterisation normals come from the in-kernel
  * Philox stream, else eps = [B normals for obs rows | B normals for next_obs rows]. */
 int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
                const float* next_obs, const float* eps);
-/* Adam + soft target update from `grads` (divided by world_size). */
+/* Adam + soft target update from `grads` (divided by world_size); a no-op when world_size == 1. */
 int sacf_apply(sacf_handle* h);
 
 #ifdef __cplusplus

@@ -1,0 +1,222 @@
+"""BatchedPathCollector host logic on a scripted CPU env (no GPU): the policy runs only on the envs
+that wait for a decision, every decision's transition reaches the buffer with the action chosen at its
+start, and the episodes that end become reference-shaped epoch paths (MdpPathCollector.get_epoch_paths,
+path_collector.py:77-78) from which eval_util.get_generic_path_information builds the progress.csv
+columns (eval_util.py:10-60)."""
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from ast_sac_amd import shipsim_abi as abi
+from ast_sac_amd.ast_sac.core import eval_util
+from ast_sac_amd.ast_sac.samplers.data_collector.batched_collector import BatchedPathCollector
+
+
+class _ScriptedEnv:
+    """Env i takes 1 + i % 3 passes per decision and ends (done) after 2 + i % 4 decisions; reward of a
+    decision = 10·i + decision index; observation = (i, decision index, episode, 0...)."""
+
+    def __init__(self, n):
+        self.n_envs, self.device, self._reward_scale = n, torch.device("cpu"), 0.5
+        self.dur = 1 + torch.arange(n) % 3
+        self.eplen = 2 + torch.arange(n) % 4
+        self.left = self.dur.clone()
+        self.dec = torch.zeros(n, dtype=torch.int64)
+        self.ep = torch.zeros(n, dtype=torch.int64)
+        self.actions_seen = [[] for _ in range(n)]
+        self.ready_counts = []
+
+    def _obs(self):
+        o = torch.zeros((self.n_envs, 8))
+        o[:, 0] = torch.arange(self.n_envs)
+        o[:, 1] = self.dec.float()
+        o[:, 2] = self.ep.float()
+        return o
+
+    def reset(self, mask=None, obs_out=None):
+        m = torch.ones(self.n_envs, dtype=torch.bool) if mask is None else mask.bool()
+        self.dec[m] = 0
+        self.ep[m] += 0 if mask is None else 1
+        self.left[m] = self.dur[m]
+        o = self._obs()
+        if obs_out is not None:
+            obs_out.copy_(o)
+        return o
+
+    def step_async(self, act, max_ticks=64, out=None):
+        self.left -= 1
+        ready = self.left == 0
+        self.ready_counts.append(int(ready.sum()))
+        for i in torch.nonzero(ready).flatten().tolist():
+            self.actions_seen[i].append(float(act[i, 0]))
+        rew = (10 * torch.arange(self.n_envs) + self.dec).double()
+        self.dec += ready.long()
+        done = ready & (self.dec >= self.eplen)
+        self.left = torch.where(ready, self.dur, self.left)
+        ev = torch.where(done, torch.full_like(self.dec, abi.EV_TERMINAL | abi.EV_TEST_STOP), torch.zeros_like(self.dec))
+        out.update(obs=self._obs(), reward=rew, done=done.to(torch.uint8), events=ev.to(torch.int32),
+                   ticks=torch.full((self.n_envs,), 5, dtype=torch.int32), ready=ready.to(torch.uint8))
+        return out
+
+
+class _Dist:
+    def __init__(self, a):
+        self.a = a
+
+    def mle_estimate(self):
+        return self.a
+
+
+class _Policy:
+    def __init__(self):
+        self.batch_sizes = []
+
+    def __call__(self, obs):
+        self.batch_sizes.append(obs.shape[0])
+        return _Dist(torch.tanh(0.01 * obs[:, :1] + 0.1 * obs[:, 1:2] - 0.05 * obs[:, 2:3]))
+
+
+class _Buffer:
+    def __init__(self):
+        self.rows = []
+
+    def add_batch(self, obs, act, rew, nobs, term, mask):
+        for i in torch.nonzero(mask).flatten().tolist():
+            self.rows.append((obs[i].clone(), float(act[i, 0]), float(rew[i, 0]), float(term[i, 0])))
+
+
+def test_policy_only_on_awaiting_envs_and_paths():
+    N = 24
+    env, pol, rb = _ScriptedEnv(N), _Policy(), _Buffer()
+    coll = BatchedPathCollector(env, pol, max_path_length=9, deterministic=True)
+    got = coll.collect(200, rb, record_paths=True)
+    assert got >= 200 and got == len(rb.rows)
+    # first pass: all N wait; afterwards exactly the envs that completed a decision in the pass before
+    assert pol.batch_sizes[0] == N
+    assert pol.batch_sizes[1:] == env.ready_counts[:-1]
+    assert sum(pol.batch_sizes) < N * len(pol.batch_sizes) * 3 // 4
+    # every transition: the action is the policy's at the decision's observation
+    for obs, a, r, t in rb.rows:
+        i, d, ep = (int(x) for x in obs[:3])
+        assert abs(a - float(torch.tanh(torch.tensor(0.01 * i + 0.1 * d - 0.05 * ep)))) < 1e-6
+        assert r == 0.5 * (10 * i + d)
+        assert t == float(d + 1 == int(env.eplen[i]))
+    # executed actions == buffered actions, env by env
+    per_env = [[a for (o, a, _, _) in rb.rows if int(o[0]) == i] for i in range(N)]
+    assert per_env == env.actions_seen
+    paths = list(coll.get_epoch_paths())
+    assert paths and all(p["rewards"].shape == p["actions"].shape == (len(p["env_infos"]), 1) for p in paths)
+    for p in paths:
+        i = int(round((p["rewards"][0, 0] / 0.5) / 10))
+        L = int(env.eplen[i])
+        np.testing.assert_array_equal(p["rewards"][:, 0], 0.5 * (10 * i + np.arange(L)))
+        assert p["env_infos"][-1]["terminal"] and p["env_infos"][-1]["test_ship_stop"]
+        assert not any(x["terminal"] for x in p["env_infos"][:-1])
+    st = eval_util.get_generic_path_information(paths)
+    for k in ("Rewards Mean", "Returns Mean", "Actions Mean", "Num Paths", "Average Returns"):
+        assert k in st
+    assert st["Num Paths"] == len(paths)
+    d = coll.get_diagnostics()
+    assert isinstance(d, OrderedDict) and d["num steps total"] == got and "path length Mean" in d
+    coll.end_epoch(0)
+    assert len(coll.get_epoch_paths()) == 0
+
+
+def test_max_num_epoch_paths_saved():
+    env, pol = _ScriptedEnv(8), _Policy()
+    coll = BatchedPathCollector(env, pol, max_path_length=9, deterministic=True, max_num_epoch_paths_saved=3)
+    coll.collect(100, None, record_paths=True)
+    assert len(coll.get_epoch_paths()) == 3
+
+
+def test_path_cut_at_max_path_length():
+    env, pol = _ScriptedEnv(8), _Policy()
+    coll = BatchedPathCollector(env, pol, max_path_length=2, deterministic=True)
+    coll.collect(60, None, record_paths=True)
+    assert {len(p["actions"]) for p in coll.get_epoch_paths()} == {2}
+
+
+class _Trainer:
+    networks = []
+
+    def __init__(self):
+        self.n = 0
+
+    def train_from_buffer(self, rb, k):
+        self.n += k
+
+    def get_diagnostics(self):
+        return OrderedDict([("QF1 Loss", 1.0), ("num train calls", self.n)])
+
+    def end_epoch(self, epoch):
+        pass
+
+    def get_snapshot(self):
+        return {}
+
+
+class _RB(_Buffer):
+    def get_diagnostics(self):
+        return OrderedDict(size=len(self.rows))
+
+    def end_epoch(self, epoch):
+        pass
+
+    def get_snapshot(self):
+        return {}
+
+
+def test_device_algorithm_progress_columns(tmp_path):
+    """DeviceBatchRLAlgorithm's progress.csv carries the reference's columns: time/<stamp> (s) for every
+    gtimer stamp of batch_rl_algorithm.py / rl_algorithm.py (evaluation sampling, exploration sampling,
+    data storing, training, saving, logging, epoch, total) and the expl/ eval/ path statistics."""
+    import csv
+    from ast_sac_amd.ast_sac.core.device_rl_algorithm import DeviceBatchRLAlgorithm
+    from ast_sac_amd.ast_sac.core.logging import logger
+    env_x, env_e = _ScriptedEnv(16), _ScriptedEnv(8)
+    cx = BatchedPathCollector(env_x, _Policy(), max_path_length=9, deterministic=True)
+    ce = BatchedPathCollector(env_e, _Policy(), max_path_length=9, deterministic=True)
+    algo = DeviceBatchRLAlgorithm(_Trainer(), env_x, env_e, cx, ce, _RB(), batch_size=32, max_path_length=9,
+                                  num_epochs=2, num_eval_steps_per_epoch=20, num_expl_steps_per_train_loop=30,
+                                  num_trains_per_train_loop=5, min_num_steps_before_training=40)
+    f = str(tmp_path / "progress.csv")
+    logger.add_tabular_output(f)
+    try:
+        algo.train()
+    finally:
+        logger.remove_tabular_output(f)
+    rows = list(csv.DictReader(open(f)))
+    assert len(rows) == 2
+    cols = set(rows[0])
+    for k in ("evaluation sampling", "exploration sampling", "data storing", "training", "saving", "logging",
+              "epoch", "total"):
+        assert f"time/{k} (s)" in cols, k
+    assert not any(c.startswith("time/") and "initial" in c for c in cols)
+    for pre in ("expl/", "eval/"):
+        for k in ("num steps total", "num paths total", "path length Mean", "Rewards Mean", "Returns Mean",
+                  "Actions Mean", "Num Paths", "Average Returns"):
+            assert pre + k in cols, pre + k
+    assert "trainer/QF1 Loss" in cols and "Epoch" in cols and rows[1]["Epoch"] == "1"
+
+
+def test_update_ratio_follows_collected_decisions():
+    """match_update_ratio: grad steps = collected x num_trains / num_expl (fraction carried); off: as set."""
+    from ast_sac_amd.ast_sac.core.device_rl_algorithm import DeviceBatchRLAlgorithm
+    for match in (True, False):
+        env_x, env_e = _ScriptedEnv(40), _ScriptedEnv(8)
+        tr = _Trainer()
+        algo = DeviceBatchRLAlgorithm(tr, env_x, env_e, BatchedPathCollector(env_x, _Policy(), deterministic=True),
+                                      BatchedPathCollector(env_e, _Policy(), deterministic=True), _RB(),
+                                      batch_size=32, max_path_length=9, num_epochs=3, num_eval_steps_per_epoch=0,
+                                      num_expl_steps_per_train_loop=7, num_trains_per_train_loop=5,
+                                      num_train_loops_per_epoch=2, min_num_steps_before_training=0,
+                                      match_update_ratio=match)
+        algo.log_stats = False
+        algo.train()
+        n = algo.num_loop_expl_steps_total
+        assert n > 6 * 7  # the 40-env passes overshoot 7 decisions per loop
+        if match:
+            assert tr.n == algo.num_train_steps_total == int(n * 5 / 7 + 1e-9)
+        else:
+            assert tr.n == 6 * 5

@@ -108,6 +108,16 @@ def _collector_vs_single(BatchedMultiShipRLEnv, MultiShipRLEnv, default_args, No
         np.testing.assert_allclose(act[d], ref["actions"][d, 0], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(rew[d], ref["rewards"][d, 0], rtol=1e-5, atol=1e-6)
         np.testing.assert_array_equal(term[d], float(ref["terminals"][d, 0]))
+    # collect(record_paths): the ended episodes are the reference path, env by env
+    coll2 = BatchedPathCollector(BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(args, N), reward_scale=0.75), det,
+                                 max_path_length=9, max_ticks=48, deterministic=True)
+    coll2.collect(N * n_dec, None, record_paths=True)
+    paths = list(coll2.get_epoch_paths())
+    assert len(paths) == N
+    for p in paths:
+        np.testing.assert_allclose(p["rewards"], ref["rewards"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(p["actions"], ref["actions"], rtol=1e-5, atol=1e-6)
+        assert [i["terminal"] for i in p["env_infos"]] == [bool(i["terminal"]) for i in ref["env_infos"]]
 
 
 def test_device_training_loop_runs():
@@ -118,9 +128,12 @@ def test_device_training_loop_runs():
                            "--num_trains_per_train_loop", "120", "--num_eval_steps_per_epoch", "64",
                            "--collav_mode", "none", "--do_logging", "false"])
     algo = experiment_device(make_variant(args), args, torch.device("cuda", 0))
-    algo.log_stats = False
-    algo.train()
+    algo.train()  # logs to a throwaway dir (do_logging false): exercises _log_stats with epoch paths
     d = algo.trainer.get_diagnostics()
     assert np.isfinite(d["QF1 Loss"]) and np.isfinite(d["Policy Loss"])
     assert algo.replay_buffer.num_steps_can_sample() >= 1024 + 2 * 256
-    assert algo.trainer._n_train_steps_total == 240
+    # num_trains / num_expl grad steps per collected exploration decision (the reference's ratio)
+    n_expl = algo.num_loop_expl_steps_total
+    assert algo.num_train_steps_total == algo.trainer._n_train_steps_total
+    assert abs(algo.num_train_steps_total - n_expl * 120 / 256) < 1 + 1e-9  # --num_trains_per_train_loop 120
+    assert n_expl >= 2 * 256
