@@ -55,6 +55,40 @@ class BatchedPathCollector:
         self._path_act = torch.zeros((N, T), dtype=torch.float32, device=dev)
         self._path_ev = torch.zeros((N, T), dtype=torch.int32, device=dev)
         self._rows = torch.arange(N, device=dev)
+        self._trace_idx = None                                    # see trace()
+
+    def trace(self, env_indices):
+        """Record every decision of the given envs (test / audit hook: one small host copy per pass).
+        trace_log()[j] lists env_indices[j]'s decisions in order as dicts: episode, decision, action
+        (the policy's normalized action), obs (next observation), reward (the env's, unscaled),
+        done, events, ticks (the decision's ticks summed over the slices it took)."""
+        self._trace_idx = torch.as_tensor(env_indices, dtype=torch.long, device=self.device)
+        self._trace_log = [[] for _ in range(len(env_indices))]
+        self._trace_ticks = np.zeros(len(env_indices), dtype=np.int64)
+        self._trace_ep = np.zeros(len(env_indices), dtype=np.int64)
+        self._trace_dec = np.zeros(len(env_indices), dtype=np.int64)
+
+    def trace_log(self):
+        return self._trace_log
+
+    def _trace_pass(self, out, end):
+        i = self._trace_idx
+        rows = torch.stack([out["ready"][i].double(), self._act[i, 0].double(), out["reward"][i].double(),
+                            out["done"][i].double(), out["events"][i].double(), out["ticks"][i].double(),
+                            end[i].double()], 1).cpu().numpy()
+        obs = out["obs"][i].cpu().numpy()
+        for j, (ready, a, r, d, ev, tk, e) in enumerate(rows):
+            self._trace_ticks[j] += int(tk)
+            if not ready:
+                continue
+            self._trace_log[j].append(dict(episode=int(self._trace_ep[j]), decision=int(self._trace_dec[j]),
+                                           action=np.float32(a), obs=obs[j].copy(), reward=float(r), done=bool(d),
+                                           events=int(ev) & 0xFFFFFFFF, ticks=int(self._trace_ticks[j])))
+            self._trace_ticks[j] = 0
+            self._trace_dec[j] += 1
+            if e:
+                self._trace_ep[j] += 1
+                self._trace_dec[j] = 0
 
     @torch.no_grad()
     def _actions(self, obs):
@@ -98,6 +132,8 @@ class BatchedPathCollector:
         self._ticks_total += out["ticks"].sum()
         self._last_end = end
         self._last_end_len = torch.where(end, self._path_len, torch.zeros_like(self._path_len))
+        if self._trace_idx is not None:
+            self._trace_pass(out, end)
         # masked auto-reset of finished episodes
         self._env.reset(mask=end.to(torch.uint8), obs_out=self._obs_reset)
         self._obs = torch.where(end.unsqueeze(1), self._obs_reset, self._obs)

@@ -220,3 +220,22 @@ def test_update_ratio_follows_collected_decisions():
             assert tr.n == algo.num_train_steps_total == int(n * 5 / 7 + 1e-9)
         else:
             assert tr.n == 6 * 5
+
+
+def test_trace_records_each_decision():
+    """trace(): every decision of the traced envs in order, ticks summed over the slices it took,
+    episode / decision counters following the collector's episode ends."""
+    env, pol = _ScriptedEnv(12), _Policy()
+    coll = BatchedPathCollector(env, pol, max_path_length=9, deterministic=True)
+    idx = [0, 5, 7, 11]
+    coll.trace(idx)
+    coll.collect(150, None)
+    for j, i in enumerate(idx):
+        log = coll.trace_log()[j]
+        assert [d["action"] for d in log] == [np.float32(a) for a in env.actions_seen[i]]
+        assert all(d["ticks"] == 5 * int(env.dur[i]) for d in log)  # 5 ticks per pass, dur passes
+        L = int(env.eplen[i])
+        for k, d in enumerate(log):
+            assert (d["episode"], d["decision"]) == (k // L, k % L)
+            assert d["done"] == (k % L == L - 1) and d["reward"] == 10 * i + k % L
+            assert bool(d["events"] & abi.EV_TERMINAL) == d["done"]
