@@ -869,8 +869,58 @@ def gen_sac():
     print("sac: losses", out["step0/losses"], out[f"step{n_steps - 1}/losses"])
 
 
+def gen_replay():
+    """EnvReplayBuffer / SimpleReplayBuffer (data_management/env_replay_buffer.py:8-50,
+    simple_replay_buffer.py:44-103, replay_buffer.py:34-77): three paths shaped like ast_sac_rollout's
+    (rollout_functions.py:161-181) added to a 7-row ring (it wraps), without and with env_info
+    sizes, then random_batch(5) under np.random.seed(123). Inputs and the buffers' arrays are saved."""
+    from ast_sac.data_management.env_replay_buffer import EnvReplayBuffer
+    from gymnasium.spaces import Box
+    rng = np.random.default_rng(5)
+    out = {}
+    paths = []
+    for k, T in enumerate((4, 5, 3)):
+        obs = rng.normal(size=(T, 8)).astype(np.float32) * 100
+        nobs = rng.normal(size=(T, 8)).astype(np.float32) * 100
+        act = rng.uniform(-1, 1, size=(T, 1)).astype(np.float32)
+        rew = rng.normal(size=(T, 1))
+        term = np.zeros((T, 1), dtype=bool)
+        term[-1, 0] = k != 1  # path 1 ends by max_path_length, not terminal
+        info = rng.normal(size=(T, 2))
+        env_infos = [dict(x=info[t], terminal=bool(term[t, 0]), events="") for t in range(T)]
+        paths.append(dict(observations=obs, actions=act, rewards=rew, next_observations=nobs, terminals=term,
+                          agent_infos=[{} for _ in range(T)], env_infos=env_infos))
+        for key, v in (("obs", obs), ("nobs", nobs), ("act", act), ("rew", rew), ("term", term), ("info", info)):
+            out[f"path{k}/{key}"] = v
+
+    class _Env:
+        observation_space = Box(-np.inf, np.inf, shape=(8,))
+        action_space = Box(-1.0, 1.0, shape=(1,))
+
+    class _EnvInfo(_Env):
+        info_sizes = {"x": 2}
+
+    for tag, env in (("plain", _Env()), ("info", _EnvInfo())):
+        rb = EnvReplayBuffer(7, env)
+        rb.add_paths(paths)
+        np.random.seed(123)
+        b = rb.random_batch(5)
+        for key in ("_observations", "_actions", "_rewards", "_terminals", "_next_obs"):
+            out[f"{tag}/{key}"] = getattr(rb, key)
+        out[f"{tag}/top_size"] = np.array([rb._top, rb._size])
+        for key, v in b.items():
+            out[f"{tag}/batch/{key}"] = v
+        if tag == "info":
+            out["info/env_info_x"] = rb._env_infos["x"]
+    np.savez_compressed(os.path.join(OUT, "replay_buffer.npz"), **out)
+    print("replay: top/size", out["plain/top_size"])
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["c2", "c1", "ast", "rl", "sbmpc", "sac"]
+    if "replay" in what:
+        os.chdir(REF)
+        gen_replay()
     os.chdir(REF)
     if "c2" in what:
         gen_c2()
