@@ -43,6 +43,12 @@ FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector spec (the resource the env k
 ALGO_BYTES_PER_ENV_TICK = 616  # C3/C5 detailed dynamics, one obstacle ship
 
 
+def algo_bytes_per_env_tick(n_obs_ships=1):
+    """SURVEY.md §8(d)'s 616 B = 2·(2·112 + 84) (ship state 112 B per ship, env state 84 B, read and
+    written once per tick), for 1 + K ships."""
+    return 2 * ((1 + n_obs_ships) * 112 + 84)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -57,6 +63,8 @@ def parse():
                    help="table: shipsim_run_table, decisions chained and episodes reset inside the kernel (the "
                         "C3 open-loop decision stream); step: shipsim_step slices + host-side table lookup and "
                         "masked shipsim_reset between calls (the RL collector's call pattern)")
+    p.add_argument("--obs-ships", type=int, default=1,
+                   help="obstacle ships per env (C5 multi-obstacle generalisation; 1 = the reference env)")
     p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library choice from envs per GPU)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -191,15 +199,16 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
     res = {"grad_steps_per_s": steps / dt, "ms_per_grad_step": dt / steps * 1e3, "batch_per_gpu": batch,
            "global_batch": batch * world, "hidden": [H, H], "dtype": "f32",
            "impl": "FusedSACTrainer hip backend (csrc/sac_kernels.hip: four MFMA f32 forward/backward GEMM "
-                   "kernels + MFMA weight-gradient kernel + Adam/soft-update kernel, HIP graph" +
-                   (", RCCL all-reduce between graph halves)" if world > 1 else ")"),
+                   "kernels + the MFMA weight-gradient kernel" +
+                   (", RCCL all-reduce, Adam/soft-update kernel; HIP graph halves)" if world > 1 else
+                    " with Adam, soft target update and W2T refresh fused in: five launches, HIP graph)"),
            "roofline": {"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_F32_PEAK_TFLOPS,
                         "flops_per_step": flops,
                         "achieved": flops / (dt / steps) / 1e12,
                         "frac": flops / (dt / steps) / 1e12 / MFMA_F32_PEAK_TFLOPS,
                         "note": "algorithmic matrix flops of one grad step (2 per multiply-add: forward, "
                                 "backward and weight-gradient products of every layer, per rank) / whole-step "
-                                "wall time (all six launches); v_mfma_f32_32x32x2_f32 dense f32 peak"}}
+                                "wall time (every launch of the step); v_mfma_f32_32x32x2_f32 dense f32 peak"}}
     if world == 1 and eager_steps:
         res["torch_ops_graph_grad_steps_per_s"] = steps / fused("torch")
     if world == 1 and eager_steps:
@@ -312,10 +321,11 @@ def main():
         dist.all_reduce(used, op=dist.ReduceOp.MAX)
     n_devices = int(used.sum().item())
     mach = abi.MACH_DETAILED if args.machinery == "detailed" else abi.MACH_SIMPLIFIED
-    cfg = abi.ast_config(args.collav, machinery=mach)
+    cfg = abi.ast_config(args.collav, machinery=mach, n_obs_ships=args.obs_ships)
     cfg.lanes_per_env = args.lpe
     N = args.envs_per_gpu
-    sim = ShipSim(cfg, N, device=dev)
+    sim = ShipSim(cfg, N, device=dev, n_obs_ships=args.obs_ships)
+    bytes_per_tick = algo_bytes_per_env_tick(args.obs_ships)
 
     # device-resident synthetic decision table: 9 decisions per episode, new table row per episode
     n_dec = cfg.max_sampling_frequency
@@ -418,7 +428,7 @@ def main():
     if rank == 0:
         value = all_ticks / elapsed
         ticks_per_launch = local_ticks / args.steps
-        achieved = ALGO_BYTES_PER_ENV_TICK * ticks_per_launch / (kmean * 1e-3) / 1e9
+        achieved = bytes_per_tick * ticks_per_launch / (kmean * 1e-3) / 1e9
         def pmc_record(path):
             # a separate rocprofv3 --pmc pass of this same bench command (profiles/), used only when it was
             # taken on this workload
@@ -427,7 +437,8 @@ def main():
                     rec = json.load(f)
             except (OSError, ValueError):
                 return None
-            same = rec.get("collav") == args.collav and rec.get("envs") == N and rec.get("slice") == args.slice
+            same = (rec.get("collav") == args.collav and rec.get("envs") == N and rec.get("slice") == args.slice
+                    and rec.get("obs_ships", 1) == args.obs_ships and rec.get("machinery", "detailed") == args.machinery)
             return rec if same else None
         pmc = pmc_record(args.pmc_json)
         traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -472,8 +483,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded PCG64 scoping-angle table, reference scenario of record)",
-            "config": {"workload": "C3: two-ship AST envs (ShipModelAST PTI machinery, sampled-route LOS, "
-                                   "reward_designs), dt 4 s",
+            "config": {"workload": ("C3: two-ship AST envs (ShipModelAST PTI machinery, sampled-route LOS, "
+                                    "reward_designs), dt 4 s") if args.obs_ships == 1 else
+                                   (f"C5 multi-obstacle: test ship + {args.obs_ships} obstacle ships per env "
+                                    "(parity unpinned beyond 1), otherwise C3"),
+                       "obs_ships": args.obs_ships,
                        "envs_per_gpu": N, "global_envs": N * world, "collav": args.collav,
                        "machinery": args.machinery, "slice_ticks": args.slice, "lanes_per_env": sim.lanes_per_env,
                        "mode": args.mode,
@@ -485,7 +499,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"ast_step_kernel (avg {kmean:.3f} ms/launch, "
-                                   f"{ticks_per_launch:.0f} env-ticks x {ALGO_BYTES_PER_ENV_TICK} B)",
+                                   f"{ticks_per_launch:.0f} env-ticks x {bytes_per_tick} B)",
                          "kernel_ms_timed": kmean, "kernel_ms_all_launches": float(all_ms.mean()),
                          "launches": int(len(all_ms)), "fp64_valu": fp64_valu},
             "cpu_baseline": cpu,
