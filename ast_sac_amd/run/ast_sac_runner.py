@@ -61,7 +61,7 @@ def build_parser():
     # MI355X execution shape
     p.add_argument("--n_envs", type=int, default=4096, help="device envs per GPU (0 = reference single-env graph)")
     p.add_argument("--eval_envs", type=int, default=256)
-    p.add_argument("--slice_ticks", type=int, default=64)
+    p.add_argument("--slice_ticks", type=int, default=128)  # collector slice: best of 64/128/256/512
     p.add_argument("--match_update_ratio", type=_bool, default=True,
                    help="grad steps per train loop = collected decisions (all ranks) x num_trains / num_expl_steps "
                         "(the reference's ratio); false: num_trains_per_train_loop per loop")

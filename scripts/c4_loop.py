@@ -54,6 +54,14 @@ def main():
     s1, k1 = counters()
     res["collect"] = dict(decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
                           env_ticks_per_s=(k1 - k0) / t)
+    for sl in (64, 128, 256, 512):  # longer slices: fewer passes (policy + host sync) per decision
+        coll.max_ticks = sl
+        s0, k0 = counters()
+        _, t = timed(lambda: coll.collect(32 * n_envs, rb))
+        s1, k1 = counters()
+        res[f"collect_slice{sl}"] = dict(decisions=s1 - s0, env_ticks=k1 - k0, seconds=t,
+                                         decisions_per_s=(s1 - s0) / t, env_ticks_per_s=(k1 - k0) / t)
+    coll.max_ticks = args.slice_ticks
     # SAC alone
     n_sac = 2400
     _, t = timed(lambda: tr.train_from_buffer(rb, n_sac))
