@@ -383,6 +383,31 @@ __device__ __forceinline__ double p_ca_of(int jp) {
   return jp == 0 ? 0.4 : (jp == 1 ? 0.6 : (jp == 2 ? 0.8 : 1.0));
 }
 
+// the scenario's own terms of the cost (sbmpc.py:200-214: P_ca, Chi_ca and their changes); the whole
+// cost when no obstacle sample comes within max_d_safe
+__device__ __forceinline__ double sbmpc_h2(const SbIn& in, int ichi, int jp) {
+  const double P_ca = p_ca_of(jp);
+  const double Chi_ca = (-30.0 + 10.0 * ichi) * (kPi / 180.0);
+  const double dChi0 = Chi_ca - in.chi_last;
+  return 25 * (1 - P_ca) + 30 * (Chi_ca * Chi_ca) + 20 * fabs(in.p_last - P_ca) +
+         ((dChi0 > 0) ? 20 * dChi0 * dChi0 : (dChi0 < 0 ? 30 * dChi0 * dChi0 : 0));
+}
+
+// No scenario can bring this obstacle within max_d_safe over the horizon: the distance now minus the
+// most either ship can travel (own ship: sample 0 at its current sway, then straight at <= u_d; the
+// obstacle: straight at its speed) stays beyond max_d_safe with a 1 m margin (the incremental
+// predictions round at ~1e-12 relative). Then every scenario's cost for it is exactly sbmpc_h2.
+__device__ __forceinline__ bool sbmpc_far(const SbIn& in, int n_samp, double DT) {
+  const double os_l = 25.0, d_safe = 1000.0;
+  const double max_d_safe = py_max(py_max(d_safe + in.obs_l / 2, 0.5 * d_safe + in.obs_l / 2),
+                                   py_max(d_safe + in.obs_w / 2, d_safe + os_l / 2 + in.obs_l / 2));
+  const double ex = in.ob_x - in.os_x, ey = in.ob_y - in.os_y;
+  const double own = DT * sqrt(in.u_d * in.u_d + in.os_v * in.os_v) + (n_samp - 2 > 0 ? n_samp - 2 : 0) * DT * in.u_d;
+  const double obs = (n_samp - 1) * DT * sqrt(in.ob_u * in.ob_u + in.ob_v * in.ob_v);
+  const double lim = max_d_safe + 1.0 + own + obs;
+  return ex * ex + ey * ey > lim * lim;
+}
+
 __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
 #ifdef SHIPSIM_PHASE_TIMING
   SbTimer sb_timer;
@@ -412,9 +437,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   double sp0 = sp, cp0 = cp;
   const double psi_w = wrap_pmpi(psi_d);
   if (psi_w != psi_d) sincos(psi_w, &sp0, &cp0);
-  double dChi0 = Chi_ca - in.chi_last;
-  const double H2 = 25 * (1 - P_ca) + 30 * (Chi_ca * Chi_ca) + 20 * fabs(in.p_last - P_ca) +
-                    ((dChi0 > 0) ? 20 * dChi0 * dChi0 : (dChi0 < 0 ? 30 * dChi0 * dChi0 : 0));
+  const double H2 = sbmpc_h2(in, ichi, jp);
   // Exact skip of the horizon loop: H0 can only be non-zero at samples with dist < max_d_safe.
   // After sample 0 both predictions are straight lines (the own ship's sway is zeroed after the
   // first step), so the relative position is P1 + k·W, k = 0..n_samp-2; if its continuous minimum
@@ -574,7 +597,7 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
 // per scenario the worst obstacle's cost (cost_i = -1, then every strictly larger cost_k), the scenario
 // with the least worst cost wins (lowest index on ties). Same wave-cooperative layout as
 // sbmpc_cooperative; slots of an env that duplicate its last ship repeat an obstacle, which changes
-// neither the max nor the D_INIT test.
+// neither the max nor the D_INIT test, and are not evaluated.
 template <int NOB>
 struct SbMulti {
   double u_d, chi_d, os_x, os_y, os_v, p_last, chi_last;
@@ -582,8 +605,8 @@ struct SbMulti {
 };
 
 template <int NOB>
-__device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n_samp, double DT, double& p_best,
-                                        double& chi_best) {
+__device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n_obs, int n_samp, double DT,
+                                        double& p_best, double& chi_best) {
   const int lane = threadIdx.x & 63;
   const int half = lane >> 5;
   const int scen = lane & 31;
@@ -605,17 +628,27 @@ __device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n
     double cost = INFINITY;
     int idx = 64;
     double worst = -1.0;
+    bool any_far = false;
+    const bool act = src >= 0 && scen < 28;
 #pragma unroll
     for (int k = 0; k < NOB; ++k) {
+      if (k >= n_obs) break;  // (wave-uniform) slots past the env's K obstacles duplicate the last one
       g.ob_x = shfl_d(in.ob_x[k], srcc); g.ob_y = shfl_d(in.ob_y[k], srcc); g.ob_psi = shfl_d(in.ob_psi[k], srcc);
       g.ob_u = shfl_d(in.ob_u[k], srcc); g.ob_v = shfl_d(in.ob_v[k], srcc);
       g.obs_l = shfl_d(in.obs_l[k], srcc); g.obs_w = shfl_d(in.obs_w[k], srcc);
-      if (src >= 0 && scen < 28) {
+      // an obstacle out of reach costs exactly sbmpc_h2 in every scenario (added once below)
+      const bool far = act && sbmpc_far(g, n_samp, DT);
+      any_far = any_far || far;
+      if (act && !far) {
         const double ck = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3);
         if (ck > worst) worst = ck;
       }
     }
-    if (src >= 0 && scen < 28) {
+    if (act) {
+      if (any_far) {
+        const double h2 = sbmpc_h2(g, scen >> 2, scen & 3);
+        if (h2 > worst) worst = h2;
+      }
       cost = worst;
       idx = scen;
     }
@@ -1163,7 +1196,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         in.p_last = p_last; in.chi_last = chi_last;
       }
       double pb = 1.0, cb = 0.0;
-      sbmpc_cooperative_multi<NOB>(need && sub == 0, in, n_samp, P.sbmpc_dt, pb, cb);
+      sbmpc_cooperative_multi<NOB>(need && sub == 0, in, nsh - 1, n_samp, P.sbmpc_dt, pb, cb);
       pb = env_lane_d<LPE, 0>(pb, env_lane0);
       cb = env_lane_d<LPE, 0>(cb, env_lane0);
       const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
