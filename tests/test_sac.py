@@ -202,7 +202,7 @@ def _assert_grads_close(g_hip, g_ref, tr, what):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,B", [(32, 64), (64, 96), (256, 32), (256, 256), (256, 1024)])
+@pytest.mark.parametrize("H,B", [(32, 64), (64, 96), (96, 64), (160, 128), (224, 32), (256, 32), (256, 256), (256, 1024)])
 def test_hip_sac_gradients_match_torch_autograd(H, B):
     """One update's flat gradient (α | π | Q1 | Q2) from the fused kernels == torch autograd's."""
     batch, eps = _rand_batch(B, "cuda")
