@@ -60,7 +60,11 @@ __device__ unsigned long long g_sac_stamp[64];
 #define SAC_SPAN_BEGIN(kern)                                                                  \
   if (threadIdx.x == 0) atomicMin(&g_sac_stamp[(kern) * 12 + 9], (unsigned long long)wall_clock64())
 #define SAC_SPAN_END(kern)                                                                    \
-  if (threadIdx.x == 0) atomicMax(&g_sac_stamp[(kern) * 12 + 10], (unsigned long long)wall_clock64())
+  if (threadIdx.x == 0) {                                                                     \
+    const unsigned long long t_ = (unsigned long long)wall_clock64();                        \
+    atomicMax(&g_sac_stamp[(kern) * 12 + 10], t_);                                            \
+    atomicMax(&g_sac_stamp[(kern) * 12 + 11], (t_ << 12) | (blockIdx.x & 4095));             \
+  }
 #else
 #define SAC_SPAN_BEGIN(kern)
 #define SAC_SPAN_END(kern)
@@ -263,10 +267,16 @@ __device__ __forceinline__ float halfwave_sum(float x) {
   return x;
 }
 
-// Σ over the column blocks of one row's head partials (block order), from part[cb * stride + row]
-__device__ __forceinline__ float sum_parts(const float* part, int n_cb, int64_t stride, int64_t row) {
-  float s = part[row];
-  for (int cb = 1; cb < n_cb; ++cb) s += part[cb * stride + row];
+// Σ over the CB column blocks of one row's head partials (block order), from part[cb * stride + row]
+// (unrolled: the CB loads are in flight together)
+template <int CB>
+__device__ __forceinline__ float sum_parts(const float* part, int64_t stride, int64_t row) {
+  float v[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) v[cb] = part[cb * stride + row];
+  float s = v[0];
+#pragma unroll
+  for (int cb = 1; cb < CB; ++cb) s += v[cb];
   return s;
 }
 
@@ -275,10 +285,30 @@ __device__ __forceinline__ void stage(float* dst, const float* src, int n) {
   for (int e = threadIdx.x; e < n; e += kThreads) dst[e] = src[e];
 }
 
-// W1 [H][nin] (row-major in the parameters) into LDS as W1ᵀ [nin][H], and b1 [H] after it
-__device__ __forceinline__ void stage_w1t(float* dst, const float* w1, const float* b1, int H, int nin) {
-  for (int e = threadIdx.x; e < H * nin; e += kThreads) dst[(e % nin) * H + e / nin] = w1[e];
-  for (int e = threadIdx.x; e < H; e += kThreads) dst[nin * H + e] = b1[e];
+// W1 [H][nin] (row-major in the parameters) into LDS as W1ᵀ [nin][H], and b1 [H] after it. Every
+// thread issues all its loads before its first LDS store (a load-store loop would wait on each load
+// in turn); element e = tid + 256 i sits at row e / nin, column e % nin, kept incrementally.
+template <int H>
+__device__ __forceinline__ void stage_w1t(float* dst, const float* w1, const float* b1, int nin) {
+  constexpr int kIt = (H * kXLd + kThreads - 1) / kThreads;
+  const int n = H * nin, tid = threadIdx.x;
+  float v[kIt];
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) v[i] = tid + i * kThreads < n ? w1[tid + i * kThreads] : 0.0f;
+  const float bb = tid < H ? b1[tid] : 0.0f;
+  int q = tid / nin, r = tid - q * nin;
+  const int dq = kThreads / nin, dr = kThreads - dq * nin;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    if (tid + i * kThreads < n) dst[r * H + q] = v[i];
+    q += dq;
+    r += dr;
+    if (r >= nin) {
+      r -= nin;
+      ++q;
+    }
+  }
+  if (tid < H) dst[nin * H + tid] = bb;
 }
 
 // av[i] = relu(b1[k] + Σ_{m < nin} W1[k][m] · in[m]) for k = kb + i: an fmaf chain from the bias in
@@ -319,18 +349,30 @@ constexpr int kLdsHeadWOff = kLdsA + kLdsTile;
 // (lane & 31), which read straight from the matrix would touch 32 rows per instruction.
 template <int H>
 __device__ __forceinline__ void tile_load(float* t, const float* src) {
-  constexpr int C4 = H / 4;
-  for (int e = threadIdx.x; e < 32 * C4; e += kThreads) {
-    const int r = e / C4, c = e % C4;
-    *reinterpret_cast<float4*>(t + r * (H + 4) + 4 * c) = *reinterpret_cast<const float4*>(src + (int64_t)r * H + 4 * c);
+  constexpr int C4 = H / 4, kIt = (32 * C4 + kThreads - 1) / kThreads;
+  constexpr bool kFull = (32 * C4) % kThreads == 0;
+  float vx[kIt], vy[kIt], vz[kIt], vw[kIt];  // every load in flight before the first LDS store
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int e = threadIdx.x + i * kThreads, r = e / C4, c = e % C4;
+    float4 x = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (kFull || e < 32 * C4) x = *reinterpret_cast<const float4*>(src + (int64_t)r * H + 4 * c);
+    vx[i] = x.x; vy[i] = x.y; vz[i] = x.z; vw[i] = x.w;
+  }
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int e = threadIdx.x + i * kThreads, r = e / C4, c = e % C4;
+    if (kFull || e < 32 * C4) *reinterpret_cast<float4*>(t + r * (H + 4) + 4 * c) = make_float4(vx[i], vy[i], vz[i], vw[i]);
   }
 }
 template <int H>
 __device__ __forceinline__ void tile_store(float* dst, const float* t) {
-  constexpr int C4 = H / 4;
-  for (int e = threadIdx.x; e < 32 * C4; e += kThreads) {
-    const int r = e / C4, c = e % C4;
-    *reinterpret_cast<float4*>(dst + (int64_t)r * H + 4 * c) = *reinterpret_cast<const float4*>(t + r * (H + 4) + 4 * c);
+  constexpr int C4 = H / 4, kIt = (32 * C4 + kThreads - 1) / kThreads;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int e = threadIdx.x + i * kThreads, r = e / C4, c = e % C4;
+    if (e < 32 * C4)
+      *reinterpret_cast<float4*>(dst + (int64_t)r * H + 4 * c) = *reinterpret_cast<const float4*>(t + r * (H + 4) + 4 * c);
   }
 }
 // this lane's operands (row lane & 31, columns kb .. kb + H/8) into the tile, then the tile to memory
@@ -384,9 +426,12 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   float av[kMaxN2], bv[kMaxN2];
 #pragma unroll
   for (int i = 0; i < n2; ++i) bv[i] = a.T[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // W2ᵀ operand, first
+  // the epilogue's per-column operands, in flight with the rest (one column per lane)
+  const float b2c = P[L.p_b2 + c0 + (lane & 31)];
+  const float wm = P[L.p_wm + c0 + (lane & 31)], ws = P[L.p_ws + c0 + (lane & 31)];
   float* lw1 = lds + kLdsW1Off;  // W1ᵀ [O][H] | b1 [H]
   float* lx = lds + kLdsXOff;    // the tile's input rows [32][kXLd + 1]
-  stage_w1t(lw1, P + L.p_w1, P + L.p_b1, H, O);
+  stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
   const int row = r0 + (lane & 31);
   const bool nrow = row >= B;
   const int item = nrow ? row - B : row;
@@ -420,11 +465,10 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
   SAC_T(0, 4);
-  const float wm = P[L.p_wm + c0 + (lane & 31)], ws = P[L.p_ws + c0 + (lane & 31)];
   constexpr int CB = H / kTile2;
   splitk_finish(acc, lds, [&](int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
-    const float y = relu(v + P[L.p_b2 + col]);
+    const float y = relu(v + b2c);
     if (r < B) a.sc.a_h2[(int64_t)r * H + col] = y;
     else a.ms.h2n[(int64_t)(r - B) * H + col] = y;
     // this column block's part of the mean / log_std heads of row r (rows [0, 2B))
@@ -476,23 +520,31 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   const float* WT = a.T + (int64_t)(1 + net) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
 #pragma unroll
   for (int i = 0; i < n2; ++i) bv[i] = WT[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
+  const float b2c = C[L.c_b2 + c0 + (lane & 31)], w3 = C[L.c_w3 + c0 + (lane & 31)];  // epilogue operands
+  SAC_T(1, 6);
   float* lw1 = lds + kLdsW1Off;  // W1ᵀ [O + 1][H] | b1 [H]
   float* lx = lds + kLdsXOff;    // the tile's input rows [32][kXLd + 1]: obs | action
-  stage_w1t(lw1, C + L.c_w1, C + L.c_b1, H, O + 1);
+  stage_w1t<H>(lw1, C + L.c_w1, C + L.c_b1, O + 1);
+  SAC_T(1, 7);
   const int row = r0 + (lane & 31);
   const bool data = !is_t && row >= B;  // (obs, a) row
   const int item = data ? row - B : row;
   const bool store_rows = blockIdx.y == 0 && w == 0 && h == 0;
   // input row: (obs, ã) / (obs, a) / (next_obs, ã')
   const float* xr = (is_t ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
+  float xin[kXLd];  // the row's observation, loaded now (it does not wait for the actor head)
+#pragma unroll
+  for (int m = 0; m < kXLd; ++m) xin[m] = xr[m];
   float act;
   if (data) {
     act = a.ms.act[item];
   } else {  // actor head of the row (the column-block parts of actor_fwd's epilogue) and its sample
     const int64_t hr = (is_t ? B : 0) + item;
-    const float mean = sum_parts(a.ms.hpart, CB, 2 * B, hr) + P[L.p_bm];
-    const float ls = sum_parts(a.ms.hpart + (int64_t)CB * 2 * B, CB, 2 * B, hr) + P[L.p_bs];
+
+    const float mean = sum_parts<CB>(a.ms.hpart, 2 * B, hr) + P[L.p_bm];
+    const float ls = sum_parts<CB>(a.ms.hpart + (int64_t)CB * 2 * B, 2 * B, hr) + P[L.p_bs];
     float hd[6];
+    SAC_T(1, 8);
     tanh_normal(mean, ls, a.ms.eps[(is_t ? B : 0) + item], hd);
     act = hd[HD_A];
     if (store_rows && (net == 0 || net == 2))
@@ -502,24 +554,26 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   __syncthreads();  // lw1 staged (also when the tile computed no heads)
   SAC_T(1, 2);
   if (w == 0 && h == 0) {
-    for (int m = 0; m < O; ++m) lx[(lane & 31) * (kXLd + 1) + m] = xr[m];
+#pragma unroll
+    for (int m = 0; m < kXLd; ++m)
+      if (m < O) lx[(lane & 31) * (kXLd + 1) + m] = xin[m];
     lx[(lane & 31) * (kXLd + 1) + O] = act;
   }
   __syncthreads();
   first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O + 1, kb, av);
   if (blockIdx.y == 0 && !is_t) {  // block-uniform
     if (data && w == 0 && h == 0)
-      for (int m = 0; m < kXLd; ++m) a.sc.q_x[net][(int64_t)item * kXLd + m] = m < O ? xr[m] : (m == O ? act : 0.0f);
+#pragma unroll
+      for (int m = 0; m < kXLd; ++m) a.sc.q_x[net][(int64_t)item * kXLd + m] = m < O ? xin[m] : (m == O ? act : 0.0f);
     store_operands<H>((data ? a.sc.q_g1[net] + (int64_t)(r0 - B) * H : a.ms.g1pi[net] + (int64_t)r0 * H), lds, av, kb);
   }
   SAC_T(1, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
   SAC_T(1, 4);
-  const float w3 = C[L.c_w3 + c0 + (lane & 31)];
   splitk_finish(acc, lds, [&](int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
-    const float y = relu(v + C[L.c_b2 + col]);
+    const float y = relu(v + b2c);
     if (is_t) a.ms.tg2[net - 2][(int64_t)r * H + col] = y;
     else if (r >= B) a.sc.q_g2[net][(int64_t)(r - B) * H + col] = y;
     else a.ms.g2pi[net][(int64_t)r * H + col] = y;
@@ -564,6 +618,15 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   for (int i = 0; i < n2; ++i) bv[i] = C[L.c_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
   const int row = r0 + (lane & 31);
   const bool data = row >= B;
+  // the epilogue's operands: fc0's action column at this lane's column, and the g1 > 0 masks of the
+  // four outputs this lane finishes
+  const float wa = C[L.c_w1 + (int64_t)(c0 + (lane & 31)) * (L.O + 1) + L.O];
+  float g1m[4];
+  {
+    const float* g1 = data ? a.sc.q_g1[net] + (int64_t)(r0 - B) * H : a.ms.g1pi[net] + (int64_t)r0 * H;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g1m[q] = g1[(int64_t)finish_row(q) * H + c0 + (lane & 31)];
+  }
   const int item = data ? row - B : row;
   const bool store_rows = net == 0 && blockIdx.y == 0 && w == 0 && h == 0;
   const float log_alpha = P[0];
@@ -578,10 +641,10 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   const float* qp = a.ms.qpart;
   const int64_t qs = (int64_t)CB * 2 * B;  // one net's parts
   if (data) {  // Q losses on (obs, a)
-    const float q1b = sum_parts(qp, CB, 2 * B, B + item) + P[L.q_base[0] + L.c_b3];
-    const float q2b = sum_parts(qp + qs, CB, 2 * B, B + item) + P[L.q_base[1] + L.c_b3];
-    const float t1 = sum_parts(qp + 2 * qs, CB, 2 * B, item) + TG[L.c_b3];
-    const float t2 = sum_parts(qp + 3 * qs, CB, 2 * B, item) + TG[L.q_size + L.c_b3];
+    const float q1b = sum_parts<CB>(qp, 2 * B, B + item) + P[L.q_base[0] + L.c_b3];
+    const float q2b = sum_parts<CB>(qp + qs, 2 * B, B + item) + P[L.q_base[1] + L.c_b3];
+    const float t1 = sum_parts<CB>(qp + 2 * qs, 2 * B, item) + TG[L.c_b3];
+    const float t2 = sum_parts<CB>(qp + 3 * qs, 2 * B, item) + TG[L.q_size + L.c_b3];
     const float tq = fminf(t1, t2) - alpha * a.ms.hdn[HD_LOGP * B + item];
     float qtv = a.hp.rscale * a.ms.rew[item] + ((1.0f - a.ms.term[item]) * a.hp.gamma) * tq;
     qtv = fminf(fmaxf(qtv, -a.hp.clip), a.hp.clip);
@@ -598,8 +661,8 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
       st[2 * B + item] = qtv;
     }
   } else {  // policy loss through min(Q1, Q2)(obs, ã)
-    const float q1a = sum_parts(qp, CB, 2 * B, item) + P[L.q_base[0] + L.c_b3];
-    const float q2a = sum_parts(qp + qs, CB, 2 * B, item) + P[L.q_base[1] + L.c_b3];
+    const float q1a = sum_parts<CB>(qp, 2 * B, item) + P[L.q_base[0] + L.c_b3];
+    const float q2a = sum_parts<CB>(qp + qs, 2 * B, item) + P[L.q_base[1] + L.c_b3];
     const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
     dq = net == 0 ? -w1 * invB : -(1.0f - w1) * invB;
     if (store_rows) {
@@ -626,15 +689,14 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
   SAC_T(2, 4);
-  const float wa = C[L.c_w1 + (int64_t)(c0 + (lane & 31)) * (L.O + 1) + L.O];  // fc0's action column
-  splitk_finish(acc, lds, [&](int rr, int cc, float v) {
+  splitk_finish_q(acc, lds, [&](int q, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     if (r >= B) {
       const int64_t o = (int64_t)(r - B) * H + col;
-      a.sc.q_dg1[net][o] = a.sc.q_g1[net][o] > 0.0f ? v : 0.0f;
+      a.sc.q_dg1[net][o] = g1m[q] > 0.0f ? v : 0.0f;
     } else {  // (tile-uniform branch: the half-wave sum below runs in every lane)
       const int64_t o = (int64_t)r * H + col;
-      const float d = a.ms.g1pi[net][o] > 0.0f ? v : 0.0f;
+      const float d = g1m[q] > 0.0f ? v : 0.0f;
       a.ms.dg1pi[net][o] = d;
       const float pa = halfwave_sum(d * wa);  // this column block's part of dQ/dã for row r
       if (cc == 0) a.ms.apart[((int64_t)net * CB + blockIdx.y) * B + r] = pa;
@@ -661,6 +723,9 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   float av[kMaxN2], bv[kMaxN2];
 #pragma unroll
   for (int i = 0; i < n2; ++i) bv[i] = P[L.p_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
+  float h1m[4];  // the h1 > 0 masks of the four outputs this lane finishes
+#pragma unroll
+  for (int q = 0; q < 4; ++q) h1m[q] = a.sc.a_h1[(int64_t)(r0 + finish_row(q)) * H + c0 + (lane & 31)];
   const int item = r0 + (lane & 31);
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
@@ -671,7 +736,7 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   stage(lwh, P + L.p_wm, H);
   stage(lwh + H, P + L.p_ws, H);
   // dA = Σ_m wa1[m] dg1_Q1[m] + Σ_m wa2[m] dg1_Q2[m] (wa: the action column of each critic's fc0)
-  float dA = sum_parts(a.ms.apart, CB, B, item) + sum_parts(a.ms.apart + (int64_t)CB * B, CB, B, item);
+  float dA = sum_parts<CB>(a.ms.apart, B, item) + sum_parts<CB>(a.ms.apart + (int64_t)CB * B, B, item);
   SAC_T(3, 1);
   const float act = a.ms.hd[HD_A * B + item], z = a.ms.hd[HD_Z * B + item], mean = a.ms.hd[HD_MEAN * B + item];
   const float std = a.ms.hd[HD_STD * B + item], ls_raw = a.ms.hd[HD_LSRAW * B + item];
@@ -699,9 +764,9 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
   SAC_T(3, 4);
-  splitk_finish(acc, lds, [&](int rr, int cc, float v) {
+  splitk_finish_q(acc, lds, [&](int q, int rr, int cc, float v) {
     const int64_t o = (int64_t)(r0 + rr) * H + c0 + cc;
-    a.sc.a_dh1[o] = a.sc.a_h1[o] > 0.0f ? v : 0.0f;
+    a.sc.a_dh1[o] = h1m[q] > 0.0f ? v : 0.0f;
   });
   SAC_T(3, 5);
   SAC_SPAN_END(3);
@@ -803,7 +868,13 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tab);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&tab);
-    for (int e = threadIdx.x; e < (int)(sizeof(WgTable) / 4); e += 256) dst[e] = src[e];
+    constexpr int kW = (int)(sizeof(WgTable) / 4), kIt = (kW + 255) / 256;
+    uint32_t v[kIt];
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) v[i] = threadIdx.x + i * 256 < kW ? src[threadIdx.x + i * 256] : 0u;
+#pragma unroll
+    for (int i = 0; i < kIt; ++i)
+      if (threadIdx.x + i * 256 < kW) dst[threadIdx.x + i * 256] = v[i];
     if (threadIdx.x == 0) sst = AdamStep{a.stats[5], a.stats[6], a.stats[7]};  // (critic_fwd)
     __syncthreads();
   }

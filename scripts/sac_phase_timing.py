@@ -58,15 +58,19 @@ def main():
         idx = [i for i in range(12) if (s[:, i] != 0).all()]
         if name == "wgrad":
             groups = [[0, 1, 2, 3], [6, 7, 8]]
+        elif name == "critic_fwd":
+            groups = [[0, 6, 7, 8, 1, 2, 3, 4, 5]]
         else:
-            groups = [idx]
+            groups = [[i for i in idx if i < 9]]
         for g in groups:
             g = [i for i in g if i in idx]
             d = [float(np.median(s[:, g[j + 1]] - s[:, g[j]])) / MHZ for j in range(len(g) - 1)]
             tot = float(np.median(s[:, g[-1]] - s[:, g[0]])) / MHZ
             print(f"  {name:10s} stamps {g}: " + " ".join(f"{x:6.2f}" for x in d) + f"  | total {tot:6.2f}")
         span = float(np.median(s[:, 10] - s[:, 9])) / MHZ
-        print(f"  {name:10s} all blocks: first start -> last end {span:6.2f}")
+        last = np.bincount((s[:, 11] & 4095).astype(np.int64)).argmax() if name == "wgrad" else -1
+        print(f"  {name:10s} all blocks: first start -> last end {span:6.2f}" +
+              (f" (most often last: block {last})" if last >= 0 else ""))
     t0 = st[:, 9]
     print("  kernel starts relative to actor_fwd, us: " + " ".join(
         f"{NAMES[k]} {float(np.median(st[:, k * 12 + 9] - t0)) / MHZ:6.2f}" for k in range(5)))
