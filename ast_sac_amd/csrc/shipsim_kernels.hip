@@ -438,6 +438,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   const double psi_w = wrap_pmpi(psi_d);
   if (psi_w != psi_d) sincos(psi_w, &sp0, &cp0);
   const double H2 = sbmpc_h2(in, ichi, jp);
+  int i_last = n_samp - 1;  // (set by the skip test below)
   // Exact skip of the horizon loop: H0 can only be non-zero at samples with dist < max_d_safe.
   // After sample 0 both predictions are straight lines (the own ship's sway is zeroed after the
   // first step), so the relative position is P1 + k·W, k = 0..n_samp-2; if its continuous minimum
@@ -456,6 +457,13 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     const double lim = max_d_safe + 1e-3;
     SB_MARK(0);
     if (e0x * e0x + e0y * e0y > lim * lim && mx * mx + my * my > lim * lim) return 0.0 + H2;
+    // Last sample that can still be within max_d_safe: |P1 + j·W| is convex in j, so past the larger
+    // root j2 of |P1 + j·W| = lim every later sample stays out of range (the incremental positions
+    // below differ from this closed form by ~1e-10 m, far inside the 1e-3 m of lim). Sample i = j + 1.
+    const double b = p1x * wx + p1y * wy, cq = p1x * p1x + p1y * p1y - lim * lim;
+    const double disc = b * b - ww * cq;
+    const double j2 = (ww > 0 && disc >= 0) ? (-b + sqrt(disc)) / ww : (double)n_samp;
+    i_last = (j2 < (double)(n_samp - 2)) ? (int)floor(j2) + 2 : n_samp - 1;
   }
   const double lim2 = (max_d_safe * (1.0 + 1e-9)) * (max_d_safe * (1.0 + 1e-9));
   // Sample 0 (own ship at wrap(psi_d) with its current sway) exactly as the reference.
@@ -496,6 +504,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   n_samp = 1;  // ablation build only: no horizon samples after sample 0
 #endif
   for (int i = 1; i < n_samp; ++i) {
+    if (!__any(i <= i_last)) break;  // every lane of the wave is past its last reachable sample
     ox = ox + dox;
     oy = oy + doy;
     if (i > 1) {
