@@ -457,6 +457,52 @@ __host__ __device__ __forceinline__ bool poly_contains(const Edge* __restrict__ 
   return !boundary && (crossings & 1);
 }
 
+// poly_contains over every other edge of the ring (edges half, half + 2, ...): the parity of this
+// half's crossings and whether this half saw the point on the boundary. Two halves combine exactly:
+// crossings parity = XOR of the halves' parities, boundary = OR (shapely/GEOS rule as poly_contains).
+__device__ __forceinline__ void poly_contains_half(const Edge* __restrict__ edges, int first, int count, double px,
+                                                   double py, int half, int& parity, bool& boundary) {
+  int crossings = 0;
+  boundary = false;
+  for (int i = half; i < count; i += 2) {
+    const Edge ed = edges[first + i];
+    double x1 = ed.ax, y1 = ed.ay, x2 = ed.bx, y2 = ed.by;
+    if (x1 < px && x2 < px) continue;
+    if (px == x2 && py == y2) boundary = true;
+    if (y1 == py && y2 == py) {
+      double mn = py_min(x1, x2), mx = py_max(x1, x2);
+      if (mn <= px && px <= mx) boundary = true;
+      continue;
+    }
+    if ((y1 > py && y2 <= py) || (y2 > py && y1 <= py)) {
+      double det = (x2 - x1) * (py - y1) - (y2 - y1) * (px - x1);
+      int sign = (det > 0) - (det < 0);
+      if (sign == 0) boundary = true;
+      if (y2 < y1) sign = -sign;
+      if (sign > 0) crossings++;
+    }
+  }
+  parity = crossings & 1;
+}
+
+// map_inside's per-polygon halves as bit masks (bit p: polygon p): par = this half's crossing parity,
+// bnd = this half saw the boundary; inside = ((par_a ^ par_b) & ~(bnd_a | bnd_b)) != 0
+__device__ __forceinline__ void map_inside_half(const Edge* __restrict__ edges, const PolyBox* __restrict__ boxes,
+                                                int n_polys, double n, double e, int half, uint32_t& par,
+                                                uint32_t& bnd) {
+  par = 0;
+  bnd = 0;
+  for (int p = 0; p < n_polys; ++p) {
+    const PolyBox b = boxes[p];
+    if (e < b.minx || e > b.maxx || n < b.miny || n > b.maxy) continue;
+    int pa;
+    bool bo;
+    poly_contains_half(edges, b.first, b.count, e, n, half, pa, bo);
+    par |= (uint32_t)pa << p;
+    bnd |= (uint32_t)bo << p;
+  }
+}
+
 // if_pos_inside_obstacles :126-129 (bbox rejection is exact for the crossing rule)
 __host__ __device__ __forceinline__ bool map_inside(const Edge* __restrict__ edges, const PolyBox* __restrict__ boxes,
                                            int n_polys, double n, double e) {

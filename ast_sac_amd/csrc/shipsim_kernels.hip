@@ -1282,10 +1282,26 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 #endif
       const double margin = c.l_ship / 2;  // check_condition.py:50-78 hull hard points
 #ifndef SHIPSIM_ABL_NO_GROUND
-      for (int k = sub; k < 4; k += NSUB) {
+      if constexpr (NSUB == 8) {
+        // 8 sub-lanes for 4 corners: sub-lanes k and k + 4 split corner k's ring edges (every other
+        // edge) and combine the crossing parity (XOR) and the boundary flag (OR) per polygon — the
+        // same boolean as corner_inside (the partner lane is 4·SLOTS lanes away, same env and ship)
+        const int k = sub & 3, half = sub >> 2;
         const double cn = (k < 2) ? s.n - margin : s.n + margin;
         const double ce = (k & 1) ? s.e + margin : s.e - margin;
-        if (corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) gr = true;
+        const int c = K.cell(cn, ce);
+        const int f = c >= 0 ? (int)K.grid_flag[c] : GRID_MIXED;
+        uint32_t par = 0, bnd = 0;
+        if (f == GRID_MIXED) map_inside_half(lds_edges_raw, lds_boxes, P.n_polys, cn, ce, half, par, bnd);
+        const uint32_t par_o = (uint32_t)__shfl_xor((int)par, 4 * SLOTS, 64);
+        const uint32_t bnd_o = (uint32_t)__shfl_xor((int)bnd, 4 * SLOTS, 64);
+        if (f == GRID_MIXED ? (((par ^ par_o) & ~(bnd | bnd_o)) != 0) : (f == GRID_IN)) gr = true;
+      } else {
+        for (int k = sub; k < 4; k += NSUB) {
+          const double cn = (k < 2) ? s.n - margin : s.n + margin;
+          const double ce = (k & 1) ? s.e + margin : s.e - margin;
+          if (corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) gr = true;
+        }
       }
 #endif
     }
