@@ -19,8 +19,18 @@ rewrites of the same math:
   single RCCL all-reduce between two graph halves (one ≈550 KB bucket, xGMI
   latency-bound; α + π and Q1 + Q2 in one bucket because each optimizer reads only its own).
 
+Two backends run this restructured step. backend="hip" (the default on a GPU; the runner's) calls
+libsacfused (include/sac_fused.h, csrc/sac_kernels.hip): the forward / backward passes and the
+H x H weight gradients as batched fp32 GEMMs on the matrix cores (v_mfma_f32_32x32x2_f32), with
+Adam, the soft target update and the transposed-weight refresh fused into the weight-gradient
+kernel when there is no all-reduce — five launches per step inside the HIP graph. It raises
+ValueError for networks it does not cover (two equal hidden layers <= 256 and a multiple of 32,
+act_dim 1, obs_dim <= 15, per-rank batch a multiple of 32 up to 1024). backend="torch" runs the same
+step with PyTorch ops (any shape).
+
 Numerics: fp32 like the reference; results equal SACTrainer's up to GEMM accumulation order
-(tests/test_sac.py checks both against the captured reference step, tests/golden/sac_step.npz).
+(tests/test_sac.py checks both against the captured reference step, tests/golden/sac_step.npz,
+and the hip gradients against torch autograd).
 """
 from collections import OrderedDict
 
