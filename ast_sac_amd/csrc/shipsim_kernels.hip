@@ -87,12 +87,14 @@ enum { SF_N = 0, SF_E, SF_YAW, SF_U, SF_V, SF_R, SF_OMEGA, SF_TIME, SF_ECT, SF_E
 struct ConstBuf {
   // edges [SHIPSIM_MAX_VERTS] | boxes [SHIPSIM_MAX_POLYS] | config routes n/e [MAX_SHIPS][kMaxRoute] each
   // | ShipConst [MAX_SHIPS] | map grid: cell edge masks [gny][gnx] uint64 | cell containment flags [gny][gnx] uint8
+  // | (8-B aligned) cell edge masks split by bit rank mod 8 [gny][gnx][8] uint64
   const char* base;
   int32_t n_edges;
   int32_t gnx, gny;            // grid cells (0 = no grid: every query runs over the full map)
   double gx0, gy0, ginv;       // grid origin (east, north) and 1 / cell size
   const uint64_t* grid_mask;   // edges whose distance to the (slightly enlarged) cell is <= kGroundReach
   const uint8_t* grid_flag;    // GRID_OUT: cell entirely outside every polygon, GRID_IN: inside one, GRID_MIXED
+  const uint64_t* grid_part;   // [cell][8]: the cell's mask split by bit rank mod 8 (sub-lane shares, no bit skipping)
   __host__ __device__ const Edge* edges() const { return (const Edge*)base; }
   __host__ __device__ const PolyBox* boxes() const { return (const PolyBox*)(base + sizeof(Edge) * SHIPSIM_MAX_VERTS); }
   __host__ __device__ const double* cfg_route_n() const {
@@ -803,14 +805,15 @@ __device__ __forceinline__ double map_dist2_grid(const ConstBuf& K, const EdgeX*
                                                  int sub, int nsub) {
   const int c = K.cell(n, e);
   if (c < 0) return map_dist2_part(E, K.n_edges, n, e, sub, nsub);
-  uint64_t m = K.grid_mask[c];
-  // this sub-lane takes every nsub-th set bit, starting at the sub-th
-  for (int k = 0; k < sub && m; ++k) m &= m - 1;
+  // this sub-lane's share of the cell's candidate edges: the set bits of rank = sub (mod nsub), read
+  // from the host-split masks (rank mod 8; nsub divides 8) — the min is over the same edges either way
+  uint64_t m = 0;
+  for (int q = sub; q < 8; q += nsub) m |= K.grid_part[(size_t)c * 8 + q];
   const double px = e, py = n;
   double best = INFINITY;
   while (m) {
     const int i = __builtin_ctzll(m);
-    for (int k = 0; k < nsub && m; ++k) m &= m - 1;
+    m &= m - 1;
     const EdgeX ed = E[i];
     const double qx = px - ed.ax, qy = py - ed.ay;
     const double t = qx * ed.dx + qy * ed.dy;
@@ -946,6 +949,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   static_assert(!(REC && CHAIN), "trajectory recording runs the per-decision step only");
   static_assert(SLOTS == 2 || (LPE == 16 && !REC && COLLAV != SHIPSIM_COLLAV_SIMPLE), "multi-obstacle layout");
   constexpr int NSUB = LPE / SLOTS;
+  static_assert(NSUB >= 1 && 8 % NSUB == 0, "sub-lanes per ship must divide 8 (grid_part shares)");
   static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 16, "LPE must be a power of two in [2, 16]");
   constexpr bool SIMPLE = COLLAV == SHIPSIM_COLLAV_SIMPLE;
   __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
@@ -2292,7 +2296,8 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
   const int gny = use_grid ? (int)ceil((mx_n - mn_n + 2 * kGridPad) / kGridCell) : 0;
   const size_t gcells = (size_t)gnx * gny;
   const size_t grid_off = (ConstBuf::kBytes + 255) & ~(size_t)255;
-  size_t cbytes = grid_off + gcells * (sizeof(uint64_t) + 1);
+  const size_t part_off = (grid_off + gcells * (sizeof(uint64_t) + 1) + 7) & ~(size_t)7;
+  size_t cbytes = part_off + gcells * 8 * sizeof(uint64_t);
   char* hostc = (char*)calloc(1, cbytes);
   Edge* E = (Edge*)hostc;
   PolyBox* B = (PolyBox*)(hostc + sizeof(Edge) * SHIPSIM_MAX_VERTS);
@@ -2321,9 +2326,17 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
       R[SHIPSIM_MAX_SHIPS * kMaxRoute + s * kMaxRoute + i] = cfg->ship[s].route_east[i];
     }
   memcpy(hostc + ConstBuf::kShipsOff, sc, sizeof(ShipConst) * SHIPSIM_MAX_SHIPS);
-  if (use_grid)
+  if (use_grid) {
     build_grid(E, nv, B, cfg->n_polys, mn_e - kGridPad, mn_n - kGridPad, gnx, gny, (uint64_t*)(hostc + grid_off),
                (uint8_t*)(hostc + grid_off + gcells * sizeof(uint64_t)));
+    const uint64_t* gm = (const uint64_t*)(hostc + grid_off);
+    uint64_t* gp = (uint64_t*)(hostc + part_off);
+    for (size_t c = 0; c < gcells; ++c) {
+      int rank = 0;
+      for (int k = 0; k < 64; ++k)
+        if (gm[c] >> k & 1) gp[c * 8 + (rank++ & 7)] |= (uint64_t)1 << k;
+    }
+  }
   hipError_t e = hipMalloc(&h->const_block, cbytes);
   if (e != hipSuccess) {
     free(hostc);
@@ -2347,6 +2360,7 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
   h->K.grid_mask = use_grid ? (const uint64_t*)((const char*)h->const_block + grid_off) : nullptr;
   h->K.grid_flag = use_grid ? (const uint8_t*)((const char*)h->const_block + grid_off + gcells * sizeof(uint64_t))
                             : nullptr;
+  h->K.grid_part = use_grid ? (const uint64_t*)((const char*)h->const_block + part_off) : nullptr;
 
   // state block (DevState layout: ship arrays | routes | env arrays)
   const size_t S = (size_t)n_envs * ns, N = (size_t)n_envs;
