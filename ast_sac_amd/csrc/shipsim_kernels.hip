@@ -1285,8 +1285,21 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
       d2 = map_dist2_grid(K, lds_edges, s.n, s.e, sub, NSUB);
 #endif
       const double margin = c.l_ship / 2;  // check_condition.py:50-78 hull hard points
+      // Every hull corner is within margin·√2 of the centre. With no coastline edge that close (the
+      // ship's min over its cell's candidate edges, which hold every edge within kGroundReach) and the
+      // centre's cell entirely outside / inside the land, the segment centre → corner crosses no edge:
+      // each corner has the centre cell's status, exactly what the four point-in-polygon tests return.
+      double d2s = d2;
+      int dummy = 0;
+      ship_reduce<LPE, SLOTS>(d2s, dummy);
+      const double lim = margin * 1.4142135623730951 + 1e-3;
+      const int cc = K.cell(s.n, s.e);
+      const int fcen = cc >= 0 ? (int)K.grid_flag[cc] : GRID_MIXED;
+      const bool far_shore = d2s > lim * lim && fcen != GRID_MIXED && lim < kGroundReach;
 #ifndef SHIPSIM_ABL_NO_GROUND
-      if constexpr (NSUB == 8) {
+      if (far_shore) {
+        gr = fcen == GRID_IN;
+      } else if constexpr (NSUB == 8) {
         // 8 sub-lanes for 4 corners: sub-lanes k and k + 4 split corner k's ring edges (every other
         // edge) and combine the crossing parity (XOR) and the boundary flag (OR) per polygon — the
         // same boolean as corner_inside (the partner lane is 4·SLOTS lanes away, same env and ship)
