@@ -916,6 +916,47 @@ def gen_replay():
     print("replay: top/size", out["plain/top_size"])
 
 
+def gen_policy():
+    """f3: run/ast-sac_run_trained_policy.py:50-66 — a deterministic TanhGaussianPolicy (as the runner
+    snapshots it, 'evaluation/policy' = MakeDeterministic) rolled out with ast_sac_rollout on the
+    NormalizedBoxEnv-wrapped env (no max_path_length, as the script), then the test/obs ships'
+    simulation_results and the env's waypoint_sampling_times. The policy is a seeded random init with
+    its first layer scaled down (raw observations are O(1e4): unscaled, every action saturates at +-1),
+    and its parameters are saved (no pickled snapshot is read or written here)."""
+    import torch
+    import ast_sac.torch.utils.pytorch_util as ptu
+    ptu.set_gpu_mode(False)
+    from ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac.torch.sac.policies.base import MakeDeterministic
+    from ast_sac.env_wrapper.normalized_box_env import NormalizedBoxEnv
+    from ast_sac.samplers.data_collector.rollout_functions import ast_sac_rollout
+    from run.env_setup import prepare_multiship_rl_env
+    out = {}
+    cases = [("none_a", "none", 4, 1e-4), ("sbmpc_a", "sbmpc", 5, 1e-3), ("sbmpc_b", "sbmpc", 2, 1e-4)]
+    for tag, collav, seed, scale in cases:
+        torch.manual_seed(seed)
+        pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[64, 64], init_w=0.5)
+        with torch.no_grad():
+            pol.fcs[0].weight.mul_(scale)
+        for pn, prm in pol.named_parameters():
+            out[f"{tag}/param/{pn}"] = prm.detach().numpy().copy()
+        out[f"{tag}/collav"] = np.array(collav)
+        env, _ = prepare_multiship_rl_env(rl_args(collav))
+        path = ast_sac_rollout(NormalizedBoxEnv(env), MakeDeterministic(pol))
+        for k in ("observations", "actions", "rewards", "next_observations", "terminals", "dones"):
+            out[f"{tag}/path/{k}"] = np.asarray(path[k])
+        out[f"{tag}/events"] = np.array([i["events"] for i in path["env_infos"]])
+        for name, ship in (("test", env.test), ("obs", env.obs)):
+            sr = ship.ship_model.simulation_results
+            keys = list(sr.keys())
+            out[f"{tag}/{name}_keys"] = np.array(keys)
+            out[f"{tag}/{name}_sr"] = np.array([sr[key] for key in keys], np.float64).T
+        out[f"{tag}/wst"] = np.array(env.waypoint_sampling_times, np.float64)
+        print("policy", tag, "decisions", len(path["actions"]), "rows", out[f"{tag}/test_sr"].shape,
+              "return", float(np.sum(path["rewards"])), out[f"{tag}/events"][-1])
+    np.savez_compressed(os.path.join(OUT, "trained_policy.npz"), **out)
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["c2", "c1", "ast", "rl", "sbmpc", "sac"]
     if "replay" in what:
@@ -942,3 +983,5 @@ if __name__ == "__main__":
         gen_draw()
     if "legacy" in what:
         gen_legacy()
+    if "policy" in what:
+        gen_policy()

@@ -242,6 +242,58 @@ def test_trained_policy_replay_from_snapshot(torch_cuda, tmp_path):
         logger.set_snapshot_dir(None)
 
 
+@pytest.mark.parametrize("tag", ["none_a", "sbmpc_a", "sbmpc_b"])
+def test_trained_policy_replay_matches_reference(golden, torch_cuda, tag, tmp_path):
+    """f3 against the reference: the policy the reference's trained-policy script replayed
+    (run/ast-sac_run_trained_policy.py:50-66, golden `trained_policy.npz`, parameters saved there) is
+    snapshotted by this package's logger and replayed through SimulatePolicyEnvSetup (policy on the
+    CPU, as the fixture was made): path, events, both ships' simulation_results and
+    waypoint_sampling_times equal the reference's."""
+    from ast_sac_amd.ast_sac.core.logging import logger
+    from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac_amd.ast_sac.torch.sac.policies.base import MakeDeterministic
+    from ast_sac_amd.rl_env.ship_in_transit.env import default_args
+    from ast_sac_amd.ast_sac.torch.utils import pytorch_util as ptu
+    from ast_sac_amd.run.ast_sac_run_trained_policy import SimulatePolicyEnvSetup
+    torch = torch_cuda
+    g = golden("trained_policy")
+    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[64, 64], init_w=0.5)
+    params = {k[len(tag) + 7:]: torch.from_numpy(g[k]) for k in g.files if k.startswith(tag + "/param/")}
+    pol.load_state_dict(params)
+    ptu.set_gpu_mode(False)  # the policy runs on the CPU, as in the fixture
+    logger.set_snapshot_dir(str(tmp_path))
+    logger.set_snapshot_mode("last")
+    logger.save_itr_params(0, {"evaluation/policy": MakeDeterministic(pol)})
+    try:
+        setup = SimulatePolicyEnvSetup(str(tmp_path / "params.pkl"), np.inf, False,
+                                       default_args(collav_mode=str(g[tag + "/collav"])))
+        path = setup.simulate_policy()
+    finally:
+        logger.set_snapshot_dir(None)
+    ref = {k: g[f"{tag}/path/{k}"] for k in ("observations", "actions", "rewards", "next_observations",
+                                              "terminals", "dones")}
+    assert len(path["actions"]) == len(ref["actions"]), tag
+    np.testing.assert_array_equal(path["observations"][0], ref["observations"][0])
+    # closed loop: the policy sees float32 observations within 1e-5 of the reference's
+    assert float(rel_err(path["next_observations"], ref["next_observations"]).max()) <= 1e-5, tag
+    np.testing.assert_allclose(path["actions"], ref["actions"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(path["rewards"], ref["rewards"], rtol=1e-5, atol=1e-8)
+    np.testing.assert_array_equal(path["terminals"], ref["terminals"])
+    np.testing.assert_array_equal(path["dones"], ref["dones"])
+    assert [i["events"] for i in path["env_infos"]] == [str(e) for e in g[tag + "/events"]]
+    for df, name in ((setup.ts_results_df, "test"), (setup.os_results_df, "obs")):
+        keys = [str(k) for k in g[f"{tag}/{name}_keys"]]
+        assert list(df.columns) == keys
+        got = df.to_numpy(np.float64)
+        want = g[f"{tag}/{name}_sr"]
+        assert got.shape == want.shape, (tag, name, got.shape, want.shape)
+        cmd = [i for i, k in enumerate(keys) if k in CMD_KEYS]
+        rest = [i for i in range(len(keys)) if i not in cmd]
+        assert_close(got[:, rest], want[:, rest], what=f"{tag} {name} simulation_results")
+        assert_close(got[:, cmd], want[:, cmd], rtol=1e-4, what=f"{tag} {name} load-derived columns")
+    np.testing.assert_allclose(setup.waypoint_sampling_times, g[tag + "/wst"], rtol=0, atol=1e-9)
+
+
 @pytest.mark.parametrize("collav,n_eps", [("none", 3), ("sbmpc", 2)])
 def test_ship_drawings_match_reference(golden, torch_cuda, collav, n_eps):
     """f4: MultiShipRLEnv(ship_draw=True, record_trajectory=True): test/obs ship_model.ship_drawings

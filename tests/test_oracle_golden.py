@@ -255,3 +255,41 @@ def test_legacy_multiship_env(golden, collav):
         np.testing.assert_array_equal(np.array(got_c, np.int8), ref_c, err_msg=p + " termination flags")
         np.testing.assert_array_equal(np.array(got_d, np.int8), ref_d, err_msg=p + " done")
         assert int(env.ship_state(1)[18]) == int(g[p + "_obs_stop"])
+
+
+@pytest.mark.parametrize("tag", ["none_a", "sbmpc_a", "sbmpc_b"])
+def test_trained_policy_closed_loop(golden, tag):
+    """f3 on the oracle: the reference's trained-policy replay (golden `trained_policy.npz`) closes the
+    loop through this package's deterministic TanhGaussianPolicy (CPU) and the oracle env, with
+    NormalizedBoxEnv's float32 action mapping (normalized_box_env.py:48-51)."""
+    import torch
+    from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac_amd.ast_sac.torch.sac.policies.base import MakeDeterministic
+    from ast_sac_amd.ast_sac.torch.utils import pytorch_util as ptu
+    g = golden("trained_policy")
+    ptu.set_gpu_mode(False)
+    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[64, 64], init_w=0.5)
+    pol.load_state_dict({k[len(tag) + 7:]: torch.from_numpy(g[k]) for k in g.files if k.startswith(tag + "/param/")})
+    agent = MakeDeterministic(pol)
+    env = O.OracleEnv(abi.ast_config(str(g[tag + "/collav"])))
+    lb, ub = np.float32(-np.deg2rad(30)), np.float32(np.deg2rad(30))
+    o = env.reset()
+    np.testing.assert_array_equal(o, g[tag + "/path/observations"][0])
+    acts, rews, obs, dones = [], [], [], []
+    while True:
+        a, _ = agent.get_action(o)
+        a = np.asarray(a, np.float32).reshape(1)
+        acts.append(a)
+        scaled = np.clip(lb + (a + np.float32(1.)) * np.float32(0.5) * (ub - lb), lb, ub)
+        o, r, d, bits, _ = env.step(scaled[0])
+        rews.append(r)
+        obs.append(o)
+        dones.append(d)
+        if d:
+            break
+    n = len(g[tag + "/path/actions"])
+    assert len(acts) == n, tag
+    np.testing.assert_allclose(np.array(acts), g[tag + "/path/actions"], rtol=1e-5, atol=1e-7)
+    assert_close(np.array(obs), g[tag + "/path/next_observations"], what=tag + " obs")
+    assert_close(np.array(rews), g[tag + "/path/rewards"][:, 0], what=tag + " rewards")
+    np.testing.assert_array_equal(dones, g[tag + "/path/dones"][:, 0])
