@@ -16,6 +16,9 @@ SOURCES = {
 # code-generation flags of both libraries (include paths are added by the build and not hashed, so the
 # hash is the same in every checkout of the same sources)
 HIPFLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shared", "-std=c++17"]
+# per-library additions (none at present; DESIGN.md §7a: an ILP-first machine scheduler build of the
+# env kernels faulted in the chained kernel and is not used)
+LIB_FLAGS = {"shipsim": [], "sacfused": []}
 
 
 def source_hash(lib):
@@ -23,7 +26,7 @@ def source_hash(lib):
     for rel in SOURCES[lib]:
         with open(os.path.join(_ROOT, rel), "rb") as f:
             h.update(rel.encode() + b"\0" + f.read() + b"\0")
-    h.update(" ".join(HIPFLAGS).encode())
+    h.update(" ".join(HIPFLAGS + LIB_FLAGS[lib]).encode())
     return h.hexdigest()[:16]
 
 
