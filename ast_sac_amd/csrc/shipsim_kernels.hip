@@ -956,6 +956,18 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
+#ifdef SHIPSIM_POISON_LDS
+  // diagnostics build (scripts, not the product): every LDS word gets a pattern before staging, so a
+  // read of LDS the kernel did not write sees the pattern instead of another kernel's leftovers
+  {
+    auto fill = [](void* p, size_t bytes) {
+      for (size_t i = threadIdx.x; i < bytes / 4; i += blockDim.x) ((uint32_t*)p)[i] = SHIPSIM_POISON_LDS;
+    };
+    fill(lds_sc, sizeof(lds_sc)); fill(lds_edges, sizeof(lds_edges));
+    fill(lds_edges_raw, sizeof(lds_edges_raw)); fill(lds_boxes, sizeof(lds_boxes));
+    __syncthreads();
+  }
+#endif
   const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
   for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) {
     const Edge ed = K.edges()[i];
