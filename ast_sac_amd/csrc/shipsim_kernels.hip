@@ -1240,6 +1240,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         const double los_arg = los_update(c, s, s.n, s.e);
         double d0 = pe - s.e, d1 = pn - s.n;
         need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
+#if defined(SHIPSIM_ABL_SB_NEVER)  // timing diagnostics: SBMPC code kept, never requested (run-time false)
+        need = need && P.max_sampling < 0;
+#elif defined(SHIPSIM_ABL_SB_NONE)  // timing diagnostics: SBMPC compiled out of the tick loop
+        need = false;
+#endif
         if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
         in.u_d = c.desired_speed;
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
@@ -1656,6 +1661,11 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevStat
         const double los_arg = los_update(c, s, s.n, s.e);
         const double d0 = pe - s.e, d1 = pn - s.n;
         need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
+#if defined(SHIPSIM_ABL_SB_NEVER)  // timing diagnostics: SBMPC code kept, never requested (run-time false)
+        need = need && P.max_sampling < 0;
+#elif defined(SHIPSIM_ABL_SB_NONE)  // timing diagnostics: SBMPC compiled out of the tick loop
+        need = false;
+#endif
         if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
         in.u_d = c.desired_speed;
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
