@@ -286,6 +286,28 @@ __device__ __forceinline__ double shfl_d(double x, int src) {
 constexpr double kCosPhiAh = 0.36650122672429719;  // cos(68.5°) (only used against a 1e-9 band)
 constexpr double kSinPhiAh = 0.93041756798202460;  // sin(68.5°)
 
+// sqrt(a) < c and sqrt(a) <= c (c > 0) decided on a against c², except within a relative 1e-12 of
+// it where the correctly rounded square root itself decides: the reference's boolean, without the
+// ~20-instruction f64 sqrt on every tick (NaN compares false either way)
+__device__ __forceinline__ bool sqrt_lt(double a, double c) {
+#ifdef SHIPSIM_PLAIN_SQRT  // diagnostics build: the square root on every call
+  return sqrt(a) < c;
+#endif
+  const double c2 = c * c;
+  if (a < c2 * (1.0 - 1e-12)) return true;
+  if (!(a <= c2 * (1.0 + 1e-12))) return false;
+  return sqrt(a) < c;
+}
+__device__ __forceinline__ bool sqrt_le(double a, double c) {
+#ifdef SHIPSIM_PLAIN_SQRT  // diagnostics build: the square root on every call
+  return sqrt(a) <= c;
+#endif
+  const double c2 = c * c;
+  if (a < c2 * (1.0 - 1e-12)) return true;
+  if (!(a <= c2 * (1.0 + 1e-12))) return false;
+  return sqrt(a) <= c;
+}
+
 // (d_safe / dist) ** Q_ with Q_ = 4 (sbmpc.py:262): x² = h + l and h² = h2 + e exactly (fma), so
 // h2 + (e + (2hl + l²)) carries ~100 bits into its one final rounding — the correctly rounded x⁴, which
 // is glibc's pow(x, 4.0) except where that pow's last 0.02 ulp decides (85 per 10⁵ random d_safe / dist
@@ -1230,7 +1252,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 #pragma unroll
         for (int k = 0; k < NOB; ++k) {  // sbmpc.py:150-156: active when any obstacle is within D_INIT
           const double d0 = obe[k] - s.e, d1 = obn[k] - s.n;
-          need = need || sqrt(d0 * d0 + d1 * d1) < 2000.0;
+          need = need || sqrt_lt(d0 * d0 + d1 * d1, 2000.0);
         }
         if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
         in.u_d = c.desired_speed;
@@ -1256,7 +1278,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         // course (atan) only feeds the optimisation, so it is evaluated for requesting envs only.
         const double los_arg = los_update(c, s, s.n, s.e);
         double d0 = pe - s.e, d1 = pn - s.n;
-        need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
+        need = sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_
 #if defined(SHIPSIM_ABL_SB_NEVER)  // timing diagnostics: SBMPC code kept, never requested (run-time false)
         need = need && P.max_sampling < 0;
 #elif defined(SHIPSIM_ABL_SB_NONE)  // timing diagnostics: SBMPC compiled out of the tick loop
@@ -1362,7 +1384,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     PT_MARK(2);
     bool my_end = false, my_outside = false, my_roa = false, my_nf = false;
     if (going) {
-      my_end = sqrt((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e)) <= 200;
+      my_end = sqrt_le((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e), 200.0);
       double margin = c.l_ship / 2;
       my_outside = (s.n < P.min_north + margin || s.n > P.max_north - margin) ||
                    (s.e < P.min_east + margin || s.e > P.max_east - margin);
@@ -1677,7 +1699,7 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevStat
       if (going && is_test) {
         const double los_arg = los_update(c, s, s.n, s.e);
         const double d0 = pe - s.e, d1 = pn - s.n;
-        need = sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_
+        need = sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_
 #if defined(SHIPSIM_ABL_SB_NEVER)  // timing diagnostics: SBMPC code kept, never requested (run-time false)
         need = need && P.max_sampling < 0;
 #elif defined(SHIPSIM_ABL_SB_NONE)  // timing diagnostics: SBMPC compiled out of the tick loop
@@ -1721,7 +1743,7 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevStat
     bool my_end = false, my_out = false, my_gr = false;
     if (going) {
       const double margin = c.l_ship / 2;
-      my_end = sqrt((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e)) <= 200;
+      my_end = sqrt_le((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e), 200.0);
       my_out = (s.n < P.min_north + margin || s.n > P.max_north - margin) ||
                (s.e < P.min_east + margin || s.e > P.max_east - margin);
       for (int q = 0; q < 4; ++q) {
@@ -1784,7 +1806,7 @@ __global__ __launch_bounds__(64) void sbmpc_eval_kernel(int n, double tf, double
   q.ob_x = r[10]; q.ob_y = r[11]; q.ob_psi = r[12]; q.ob_u = r[13]; q.ob_v = r[14];
   q.obs_l = r[15]; q.obs_w = r[16];
   const double d0 = q.ob_x - q.os_x, d1 = q.ob_y - q.os_y;
-  const bool active = valid && sqrt(d0 * d0 + d1 * d1) < 2000.0;  // D_INIT_ (sbmpc.py:154-159)
+  const bool active = valid && sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_ (sbmpc.py:154-159)
   double pb = 1.0, cb = 0.0;
   sbmpc_cooperative(active, q, (int)(tf / dt), dt, pb, cb);
   if (valid) {
