@@ -274,7 +274,10 @@ __device__ __forceinline__ void record_last(const Traj& T, int q, int t, double 
 // ---------------------------------------------------------------------------------------------
 struct SbIn {
   double u_d, chi_d, os_x, os_y, os_v, ob_x, ob_y, ob_psi, ob_u, ob_v, obs_l, obs_w, p_last, chi_last;
+  double ob_so, ob_co;  // sin / cos(ob_psi): the AST kernels pass the obstacle ship's carried sin/cos(yaw)
 };
+// sin/cos(ob_psi) of a request built from its heading alone
+__device__ __forceinline__ void sb_set_heading_trig(SbIn& q) { sincos(q.ob_psi, &q.ob_so, &q.ob_co); }
 
 __device__ __forceinline__ double shfl_d(double x, int src) {
   int lo = __double2loint(x), hi = __double2hiint(x);
@@ -466,8 +469,16 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   const double ud = in.u_d * P_ca;
   const double psi_d = in.chi_d + Chi_ca;
   // Obstacle trajectory (sbmpc_misc.py:65-83) and linear_pred (:103-123), advanced incrementally
+  // the obstacle heading's sin/cos come with the request (ob_so, ob_co): the same values as
+  // sincos(in.ob_psi) — in the AST kernels they are the obstacle ship's own carried sin/cos(yaw) with
+  // ob_psi = -yaw, and the device sin is odd and cos even (both reduce |x|), so nothing is recomputed
+  // per scenario
+#ifdef SHIPSIM_OB_SINCOS_CALL  // diagnostics build: the per-scenario call
   double so, co;
   sincos(in.ob_psi, &so, &co);
+#else
+  const double so = in.ob_so, co = in.ob_co;
+#endif
   const double r11 = -so, r12 = co, r21 = co, r22 = so;
   const double vo0 = -so * in.ob_u + co * in.ob_v;  // rot2d(obstacle.psi_, [u, v])
   const double vo1 = co * in.ob_u + so * in.ob_v;
@@ -617,6 +628,7 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
     g.ob_u = shfl_d(in.ob_u, srcc); g.ob_v = shfl_d(in.ob_v, srcc);
     g.obs_l = shfl_d(in.obs_l, srcc); g.obs_w = shfl_d(in.obs_w, srcc);
     g.p_last = shfl_d(in.p_last, srcc); g.chi_last = shfl_d(in.chi_last, srcc);
+    g.ob_so = shfl_d(in.ob_so, srcc); g.ob_co = shfl_d(in.ob_co, srcc);
     double cost = INFINITY;
     int idx = 64;
     if (src >= 0 && scen < 28) {
@@ -690,6 +702,7 @@ __device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n
       const bool far = act && sbmpc_far(g, n_samp, DT);
       any_far = any_far || far;
       if (act && !far) {
+        sb_set_heading_trig(g);
         const double ck = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3);
         if (ck > worst) worst = ck;
       }
@@ -1216,6 +1229,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
+    const double psy = pair_swap(sy), pcy = pair_swap(cy);  // sin/cos(pyaw), carried by the partner
     double sf = 1.0, off = 0.0;
     bool sb_active = false;
     if (COLLAV == SHIPSIM_COLLAV_SBMPC && SLOTS > 2) {  // do_list of every obstacle ship (env.py:366-370)
@@ -1288,6 +1302,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         in.u_d = c.desired_speed;
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
         in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
+        in.ob_so = -psy; in.ob_co = pcy;  // sin(-yaw) = -sin(yaw), cos(-yaw) = cos(yaw)
         in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
         in.p_last = p_last; in.chi_last = chi_last;
       }
@@ -1709,6 +1724,7 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevStat
         in.u_d = c.desired_speed;
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
         in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
+        sb_set_heading_trig(in);
         in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
         in.p_last = p_last; in.chi_last = chi_last;
       }
@@ -1804,6 +1820,7 @@ __global__ __launch_bounds__(64) void sbmpc_eval_kernel(int n, double tf, double
   q.p_last = r[0]; q.chi_last = r[1]; q.u_d = r[2]; q.chi_d = r[3];
   q.os_x = r[4]; q.os_y = r[5]; q.os_v = r[8];  // os_state (x, y, psi, u, v, r): linear_pred uses x, y, v
   q.ob_x = r[10]; q.ob_y = r[11]; q.ob_psi = r[12]; q.ob_u = r[13]; q.ob_v = r[14];
+  sb_set_heading_trig(q);
   q.obs_l = r[15]; q.obs_w = r[16];
   const double d0 = q.ob_x - q.os_x, d1 = q.ob_y - q.os_y;
   const bool active = valid && sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_ (sbmpc.py:154-159)
