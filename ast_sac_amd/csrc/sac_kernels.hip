@@ -423,15 +423,8 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
   constexpr int n2 = H / 8;
   const int kb = w * (H / 4) + h * n2;
-  float av[kMaxN2], bv[kMaxN2];
-#pragma unroll
-  for (int i = 0; i < n2; ++i) bv[i] = a.T[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // W2ᵀ operand, first
-  // the epilogue's per-column operands, in flight with the rest (one column per lane)
-  const float b2c = P[L.p_b2 + c0 + (lane & 31)];
-  const float wm = P[L.p_wm + c0 + (lane & 31)], ws = P[L.p_ws + c0 + (lane & 31)];
-  float* lw1 = lds + kLdsW1Off;  // W1ᵀ [O][H] | b1 [H]
-  float* lx = lds + kLdsXOff;    // the tile's input rows [32][kXLd + 1]
-  stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
+  // the batch gather first: its chain (step / size -> Philox -> replay row) is the longest of the
+  // prologue, and vector loads complete in issue order, so the staging loads queue behind it
   const int row = r0 + (lane & 31);
   const bool nrow = row >= B;
   const int item = nrow ? row - B : row;
@@ -441,6 +434,15 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   float x[kXLd];
 #pragma unroll
   for (int m = 0; m < kXLd; ++m) x[m] = m < O ? src[idx * O + m] : 0.0f;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < n2; ++i) bv[i] = a.T[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // W2ᵀ operand
+  // the epilogue's per-column operands, in flight with the rest (one column per lane)
+  const float b2c = P[L.p_b2 + c0 + (lane & 31)];
+  const float wm = P[L.p_wm + c0 + (lane & 31)], ws = P[L.p_ws + c0 + (lane & 31)];
+  float* lw1 = lds + kLdsW1Off;  // W1ᵀ [O][H] | b1 [H]
+  float* lx = lds + kLdsXOff;    // the tile's input rows [32][kXLd + 1]
+  stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
   if (w == 0 && h == 0)
     for (int m = 0; m < O; ++m) lx[(lane & 31) * (kXLd + 1) + m] = x[m];
   if (blockIdx.y == 0 && w == 0 && h == 0) {  // the gathered batch for the later kernels
@@ -516,36 +518,54 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   constexpr int n2 = H / 8;
   constexpr int CB = H / kTile2;
   const int kb = w * (H / 4) + h * n2;
+  const int row = r0 + (lane & 31);
+  const bool data = !is_t && row >= B;  // (obs, a) row (block-uniform: B is a multiple of 32)
+  const int item = data ? row - B : row;
+  const bool store_rows = blockIdx.y == 0 && w == 0 && h == 0;
+  // the row's inputs first — observation, actor-head partials (or the replayed action), noise — as
+  // they end the prologue's longest chain; vector loads complete in issue order, so the staging loads
+  // below queue behind them instead of delaying them. Every load is issued unconditionally (the
+  // addresses are valid for either row kind) so no branch splits the batch of loads.
+  const float* xr = (is_t ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
+  float xin[kXLd];
+#pragma unroll
+  for (int m = 0; m < kXLd; ++m) xin[m] = xr[m];
+  const int64_t hr = (is_t ? B : 0) + item;
+  float pm[CB], pls[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    pm[cb] = a.ms.hpart[cb * (int64_t)(2 * B) + hr];
+    pls[cb] = a.ms.hpart[(CB + cb) * (int64_t)(2 * B) + hr];
+  }
+  const float bm = P[L.p_bm], bs = P[L.p_bs];
+  const float ev = a.ms.eps[(is_t ? B : 0) + item];
+  const float act_data = a.ms.act[item];
   float av[kMaxN2], bv[kMaxN2];
   const float* WT = a.T + (int64_t)(1 + net) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
 #pragma unroll
-  for (int i = 0; i < n2; ++i) bv[i] = WT[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
+  for (int i = 0; i < n2; ++i) bv[i] = WT[(int64_t)(kb + i) * H + c0 + (lane & 31)];
   const float b2c = C[L.c_b2 + c0 + (lane & 31)], w3 = C[L.c_w3 + c0 + (lane & 31)];  // epilogue operands
   SAC_T(1, 6);
   float* lw1 = lds + kLdsW1Off;  // W1ᵀ [O + 1][H] | b1 [H]
   float* lx = lds + kLdsXOff;    // the tile's input rows [32][kXLd + 1]: obs | action
   stage_w1t<H>(lw1, C + L.c_w1, C + L.c_b1, O + 1);
   SAC_T(1, 7);
-  const int row = r0 + (lane & 31);
-  const bool data = !is_t && row >= B;  // (obs, a) row
-  const int item = data ? row - B : row;
-  const bool store_rows = blockIdx.y == 0 && w == 0 && h == 0;
-  // input row: (obs, ã) / (obs, a) / (next_obs, ã')
-  const float* xr = (is_t ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
-  float xin[kXLd];  // the row's observation, loaded now (it does not wait for the actor head)
-#pragma unroll
-  for (int m = 0; m < kXLd; ++m) xin[m] = xr[m];
   float act;
   if (data) {
-    act = a.ms.act[item];
-  } else {  // actor head of the row (the column-block parts of actor_fwd's epilogue) and its sample
-    const int64_t hr = (is_t ? B : 0) + item;
-
-    const float mean = sum_parts<CB>(a.ms.hpart, 2 * B, hr) + P[L.p_bm];
-    const float ls = sum_parts<CB>(a.ms.hpart + (int64_t)CB * 2 * B, 2 * B, hr) + P[L.p_bs];
+    act = act_data;
+  } else {  // actor head of the row (the column-block parts of actor_fwd's epilogue, summed in block
+            // order as sum_parts does) and its sample
+    float sm = pm[0], sl = pls[0];
+#pragma unroll
+    for (int cb = 1; cb < CB; ++cb) {
+      sm += pm[cb];
+      sl += pls[cb];
+    }
+    const float mean = sm + bm;
+    const float ls = sl + bs;
     float hd[6];
     SAC_T(1, 8);
-    tanh_normal(mean, ls, a.ms.eps[(is_t ? B : 0) + item], hd);
+    tanh_normal(mean, ls, ev, hd);
     act = hd[HD_A];
     if (store_rows && (net == 0 || net == 2))
       for (int q = 0; q < 6; ++q) (is_t ? a.ms.hdn : a.ms.hd)[q * B + item] = hd[q];
@@ -613,11 +633,29 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   constexpr int n2 = H / 8;
   constexpr int CB = H / kTile2;
   const int kb = w * (H / 4) + h * n2;
+  const int row = r0 + (lane & 31);
+  const bool data = row >= B;  // (block-uniform: B is a multiple of 32)
+  const int item = data ? row - B : row;
+  // the row's Q / target-Q head partials and batch terms first: they end the prologue's longest chain
+  // and vector loads complete in issue order, so the staging loads below queue behind them. All are
+  // issued for both row kinds (valid addresses either way), keeping the batch of loads in one block.
+  const float* qp = a.ms.qpart;
+  const int64_t qs = (int64_t)CB * 2 * B;  // one net's parts
+  const int64_t qrow = data ? B + item : item;
+  float q1p[CB], q2p[CB], t1p[CB], t2p[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    q1p[cb] = qp[cb * (int64_t)(2 * B) + qrow];
+    q2p[cb] = qp[qs + cb * (int64_t)(2 * B) + qrow];
+    t1p[cb] = qp[2 * qs + cb * (int64_t)(2 * B) + item];
+    t2p[cb] = qp[3 * qs + cb * (int64_t)(2 * B) + item];
+  }
+  const float bq1 = P[L.q_base[0] + L.c_b3], bq2 = P[L.q_base[1] + L.c_b3];
+  const float bt1 = TG[L.c_b3], bt2 = TG[L.q_size + L.c_b3];
+  const float logp_n = a.ms.hdn[HD_LOGP * B + item], rew_i = a.ms.rew[item], term_i = a.ms.term[item];
   float av[kMaxN2], bv[kMaxN2];
 #pragma unroll
-  for (int i = 0; i < n2; ++i) bv[i] = C[L.c_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
-  const int row = r0 + (lane & 31);
-  const bool data = row >= B;
+  for (int i = 0; i < n2; ++i) bv[i] = C[L.c_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];
   // the epilogue's operands: fc0's action column at this lane's column, and the g1 > 0 masks of the
   // four outputs this lane finishes
   const float wa = C[L.c_w1 + (int64_t)(c0 + (lane & 31)) * (L.O + 1) + L.O];
@@ -627,7 +665,6 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) g1m[q] = g1[(int64_t)finish_row(q) * H + c0 + (lane & 31)];
   }
-  const int item = data ? row - B : row;
   const bool store_rows = net == 0 && blockIdx.y == 0 && w == 0 && h == 0;
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
@@ -638,15 +675,22 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   float* lw3 = lds + kLdsHeadWOff;    // this critic's w3
   tile_load<H>(tg, (data ? a.sc.q_g2[net] : a.ms.g2pi[net]) + (int64_t)ib * H);
   stage(lw3, C + L.c_w3, H);
-  const float* qp = a.ms.qpart;
-  const int64_t qs = (int64_t)CB * 2 * B;  // one net's parts
+  // Σ of the column-block parts in block order (sum_parts), then the head bias
+  float s_q1 = q1p[0], s_q2 = q2p[0], s_t1 = t1p[0], s_t2 = t2p[0];
+#pragma unroll
+  for (int cb = 1; cb < CB; ++cb) {
+    s_q1 += q1p[cb];
+    s_q2 += q2p[cb];
+    s_t1 += t1p[cb];
+    s_t2 += t2p[cb];
+  }
   if (data) {  // Q losses on (obs, a)
-    const float q1b = sum_parts<CB>(qp, 2 * B, B + item) + P[L.q_base[0] + L.c_b3];
-    const float q2b = sum_parts<CB>(qp + qs, 2 * B, B + item) + P[L.q_base[1] + L.c_b3];
-    const float t1 = sum_parts<CB>(qp + 2 * qs, 2 * B, item) + TG[L.c_b3];
-    const float t2 = sum_parts<CB>(qp + 3 * qs, 2 * B, item) + TG[L.q_size + L.c_b3];
-    const float tq = fminf(t1, t2) - alpha * a.ms.hdn[HD_LOGP * B + item];
-    float qtv = a.hp.rscale * a.ms.rew[item] + ((1.0f - a.ms.term[item]) * a.hp.gamma) * tq;
+    const float q1b = s_q1 + bq1;
+    const float q2b = s_q2 + bq2;
+    const float t1 = s_t1 + bt1;
+    const float t2 = s_t2 + bt2;
+    const float tq = fminf(t1, t2) - alpha * logp_n;
+    float qtv = a.hp.rscale * rew_i + ((1.0f - term_i) * a.hp.gamma) * tq;
     qtv = fminf(fmaxf(qtv, -a.hp.clip), a.hp.clip);
     const float dq1b = (2.0f * invB) * (q1b - qtv), dq2b = (2.0f * invB) * (q2b - qtv);
     dq = net == 0 ? dq1b : dq2b;
@@ -661,8 +705,8 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
       st[2 * B + item] = qtv;
     }
   } else {  // policy loss through min(Q1, Q2)(obs, ã)
-    const float q1a = sum_parts<CB>(qp, 2 * B, item) + P[L.q_base[0] + L.c_b3];
-    const float q2a = sum_parts<CB>(qp + qs, 2 * B, item) + P[L.q_base[1] + L.c_b3];
+    const float q1a = s_q1 + bq1;
+    const float q2a = s_q2 + bq2;
     const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
     dq = net == 0 ? -w1 * invB : -(1.0f - w1) * invB;
     if (store_rows) {
@@ -720,13 +764,24 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   constexpr int n2 = H / 8;
   constexpr int CB = H / kTile2;
   const int kb = w * (H / 4) + h * n2;
+  const int item = r0 + (lane & 31);
+  // the row's dQ/dã partials, head and noise first (the prologue's longest chain; vector loads complete
+  // in issue order, so the staging loads below queue behind them)
+  float ap1[CB], ap2[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    ap1[cb] = a.ms.apart[cb * (int64_t)B + item];
+    ap2[cb] = a.ms.apart[(int64_t)CB * B + cb * (int64_t)B + item];
+  }
+  const float act = a.ms.hd[HD_A * B + item], z = a.ms.hd[HD_Z * B + item], mean = a.ms.hd[HD_MEAN * B + item];
+  const float std = a.ms.hd[HD_STD * B + item], ls_raw = a.ms.hd[HD_LSRAW * B + item];
+  const float eps_i = a.ms.eps[item];
   float av[kMaxN2], bv[kMaxN2];
 #pragma unroll
-  for (int i = 0; i < n2; ++i) bv[i] = P[L.p_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];  // first
+  for (int i = 0; i < n2; ++i) bv[i] = P[L.p_w2 + (int64_t)(kb + i) * H + c0 + (lane & 31)];
   float h1m[4];  // the h1 > 0 masks of the four outputs this lane finishes
 #pragma unroll
   for (int q = 0; q < 4; ++q) h1m[q] = a.sc.a_h1[(int64_t)(r0 + finish_row(q)) * H + c0 + (lane & 31)];
-  const int item = r0 + (lane & 31);
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
   const float invB = 1.0f / (float)B;
@@ -735,18 +790,23 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   tile_load<H>(th, a.sc.a_h2 + (int64_t)r0 * H);
   stage(lwh, P + L.p_wm, H);
   stage(lwh + H, P + L.p_ws, H);
-  // dA = Σ_m wa1[m] dg1_Q1[m] + Σ_m wa2[m] dg1_Q2[m] (wa: the action column of each critic's fc0)
-  float dA = sum_parts<CB>(a.ms.apart, B, item) + sum_parts<CB>(a.ms.apart + (int64_t)CB * B, B, item);
+  // dA = Σ_m wa1[m] dg1_Q1[m] + Σ_m wa2[m] dg1_Q2[m] (wa: the action column of each critic's fc0), each
+  // sum over the column-block parts in block order (sum_parts)
+  float s1 = ap1[0], s2 = ap2[0];
+#pragma unroll
+  for (int cb = 1; cb < CB; ++cb) {
+    s1 += ap1[cb];
+    s2 += ap2[cb];
+  }
+  float dA = s1 + s2;
   SAC_T(3, 1);
-  const float act = a.ms.hd[HD_A * B + item], z = a.ms.hd[HD_Z * B + item], mean = a.ms.hd[HD_MEAN * B + item];
-  const float std = a.ms.hd[HD_STD * B + item], ls_raw = a.ms.hd[HD_LSRAW * B + item];
   if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
   const float ainv = alpha * invB;
   const float d = z - mean, var = std * std;
   const float sig = 1.0f / (1.0f + expf(2.0f * z));  // sigmoid(-2z)
   const float gz = dA * (1.0f - act * act) + ainv * (-(d / var) + (2.0f - 4.0f * sig));
   const float dmean = gz + ainv * (d / var);
-  const float dstd = gz * a.ms.eps[item] + ainv * ((d * d) / (var * std) - 1.0f / std);
+  const float dstd = gz * eps_i + ainv * ((d * d) / (var * std) - 1.0f / std);
   const float dls = (ls_raw >= -20.0f && ls_raw <= 2.0f) ? dstd * std : 0.0f;
   if (blockIdx.y == 0 && w == 0 && h == 0) {
     a.sc.a_dhead[(int64_t)item * 2] = dmean;
