@@ -64,6 +64,10 @@ class BaseRLAlgorithm(metaclass=abc.ABCMeta):
         logger.record_dict(self.timer.epoch_timings())
         logger.record_tabular("Epoch", epoch)
         logger.dump_tabular(with_prefix=False, with_timestamp=False)
+        for coll, pre in ((self.expl_data_collector, "expl/"), (self.eval_data_collector, "eval/")):
+            dev = getattr(coll, "device_diagnostics", None)  # build-only counters: text log, not progress.csv
+            if dev is not None:
+                logger.log(" ".join(f"{pre}{k}={v}" for k, v in dev().items()))
 
     @abc.abstractmethod
     def training_mode(self, mode):
@@ -114,5 +118,6 @@ class BatchRLAlgorithm(BaseRLAlgorithm, metaclass=abc.ABCMeta):
             self.training_mode(True)
             for _ in range(self.num_trains_per_train_loop):
                 self.trainer.train(self.replay_buffer.random_batch(self.batch_size))
+                self.timer.stamp("sac training")  # SACTrainer.train_from_torch's own stamp (sac.py:142)
             self.timer.stamp("training")
             self.training_mode(False)

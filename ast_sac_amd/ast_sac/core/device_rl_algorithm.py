@@ -82,6 +82,7 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
             if k:
                 self.trainer.train_from_buffer(self.replay_buffer, k)
             self.num_train_steps_total += k
+            self.timer.stamp("sac training")  # the reference stamps it in SACTrainer.train_from_torch (sac.py:142)
             self.timer.stamp("training")
             self.training_mode(False)
 

@@ -13,7 +13,16 @@ count is known on the host from the previous pass, so the compaction needs no ex
 rewards/actions of the episodes that ended in that pass: those become the epoch's paths
 (get_epoch_paths, as MdpPathCollector's, path_collector.py:77-78) from which the algorithm logs
 eval_util.get_generic_path_information (Rewards/Returns/Actions/Num Paths/Average Returns).
+
+Shared envs (quirk Q10, run/ast-sac_runner.py:113-114): the reference's exploration and evaluation
+wrappers share ONE env object, so evaluation episodes reset and advance the same env, and what reset()
+leaves alone (the SBMPC memory P_ca_last / Chi_ca_last, quirk Q7) carries from evaluation episodes into
+exploration ones. Two collectors over the same batched env reproduce that: a collector that finds the env
+last driven by the other one resets every env first (the reference starts every path with env.reset(),
+rollout_functions.py:100-106) and starts all its episodes afresh; the library's reset keeps the SBMPC
+memory, as the reference's does.
 """
+import warnings
 from collections import OrderedDict, deque
 
 import numpy as np
@@ -35,6 +44,7 @@ class BatchedPathCollector:
         dev = env.device
         self.N, self.device = N, dev
         self._obs = env.reset().clone()                           # (N, 8) obs at the pending decision
+        self._base_env().__dict__["_batched_collector_owner"] = id(self)
         self._act = torch.zeros((N, 1), dtype=torch.float32, device=dev)
         self._awaiting = torch.ones(N, dtype=torch.bool, device=dev)
         self._path_len = torch.zeros(N, dtype=torch.int32, device=dev)
@@ -47,6 +57,7 @@ class BatchedPathCollector:
         self._steps_total = torch.zeros((), dtype=torch.int64, device=dev)
         self._paths_total = torch.zeros((), dtype=torch.int64, device=dev)
         self._ticks_total = torch.zeros((), dtype=torch.int64, device=dev)
+        self._nonfinite_total = torch.zeros((), dtype=torch.int64, device=dev)
         self._max_saved = max_num_epoch_paths_saved
         self._epoch_paths = deque(maxlen=max_num_epoch_paths_saved)
         self._n_awaiting = N                                      # host copy, None when unknown
@@ -56,6 +67,25 @@ class BatchedPathCollector:
         self._path_ev = torch.zeros((N, T), dtype=torch.int32, device=dev)
         self._rows = torch.arange(N, device=dev)
         self._trace_idx = None                                    # see trace()
+
+    def _base_env(self):
+        e = self._env
+        while hasattr(type(e), "wrapped_env") or "_wrapped_env" in getattr(e, "__dict__", {}):
+            e = e.wrapped_env
+        return e
+
+    def _take_over(self):
+        """The env was last driven by another collector over the same env (Q10): its in-flight episodes
+        are not ours. Reset every env and start all episodes afresh (SBMPC memory is not reset, Q7)."""
+        base = self._base_env()
+        if base.__dict__.get("_batched_collector_owner") == id(self):
+            return
+        base.__dict__["_batched_collector_owner"] = id(self)
+        self._obs = self._env.reset().clone()
+        self._awaiting.fill_(True)
+        self._path_len.zero_()
+        self._ret.zero_()
+        self._n_awaiting = self.N
 
     def trace(self, env_indices):
         """Record every decision of the given envs (test / audit hook: one small host copy per pass).
@@ -114,19 +144,24 @@ class BatchedPathCollector:
         ready = out["ready"].bool()
         done = out["done"].bool()
         rew = out["reward"] * self._env._reward_scale
-        terminal = (out["events"] & (1 << 16)) != 0
+        terminal = (out["events"] & abi.EV_TERMINAL) != 0
+        # a decision that ended on a NaN/Inf ship state (EV_NONFINITE; the env reports it done) is not a
+        # transition: it never reaches the replay buffer or the epoch paths, the episode just ends
+        nonfinite = (out["events"] & abi.EV_NONFINITE) != 0
+        good = ready & ~nonfinite
         if replay_buffer is not None:
             replay_buffer.add_batch(self._obs, self._act, rew.to(torch.float32).unsqueeze(1), out["obs"],
-                                    terminal.to(torch.float32).unsqueeze(1), mask=ready)
+                                    terminal.to(torch.float32).unsqueeze(1), mask=good)
         pos = self._path_len.clamp(max=self.max_path_length - 1).long()
         for buf, v in ((self._path_rew, rew), (self._path_act, self._act[:, 0]), (self._path_ev, out["events"])):
-            buf[self._rows, pos] = torch.where(ready, v.to(buf.dtype), buf[self._rows, pos])
-        self._path_len += ready.to(torch.int32)
-        self._ret += torch.where(ready, rew, torch.zeros_like(rew))
-        end = ready & (done | (self._path_len >= self.max_path_length))
+            buf[self._rows, pos] = torch.where(good, v.to(buf.dtype), buf[self._rows, pos])
+        self._path_len += good.to(torch.int32)
+        self._ret += torch.where(good, rew, torch.zeros_like(rew))
+        self._nonfinite_total += (ready & nonfinite).sum()
+        end = ready & (done | nonfinite | (self._path_len >= self.max_path_length))
         self._obs = torch.where(ready.unsqueeze(1), out["obs"], self._obs)
         self._awaiting = ready.clone()
-        n_ready = ready.sum()
+        n_ready = good.sum()
         self._steps_total += n_ready
         self._paths_total += end.sum()
         self._ticks_total += out["ticks"].sum()
@@ -143,6 +178,7 @@ class BatchedPathCollector:
 
     def collect(self, num_steps, replay_buffer=None, record_paths=False):
         """Advance until ≥ num_steps transitions were produced (host sync once per pass)."""
+        self._take_over()
         got = 0
         while got < num_steps:
             _, n = self.step(replay_buffer)
@@ -150,7 +186,21 @@ class BatchedPathCollector:
             got += self._n_awaiting
             if record_paths:
                 self._record_ended()
+        self.check_nonfinite()
         return got
+
+    def check_nonfinite(self):
+        """Warn (once per occurrence) when env decisions ended on a non-finite ship state since the last
+        check: the env library's status (shipsim_synchronize), those rows were kept out of the buffer."""
+        sim = getattr(self._env, "sim", None)
+        if sim is None:
+            return
+        from ....shipsim import ShipSimNonFiniteError
+        try:
+            sim.synchronize()
+        except ShipSimNonFiniteError as e:
+            warnings.warn(f"BatchedPathCollector: {e} (transitions dropped from the replay buffer and paths)",
+                          RuntimeWarning, stacklevel=2)
 
     def _record_ended(self):
         """The episodes that ended in the last pass -> reference path dicts (rollout_functions.py:161-181:
@@ -179,13 +229,19 @@ class BatchedPathCollector:
         self._epoch_paths = deque(maxlen=self._max_saved)
 
     def get_diagnostics(self):
-        """MdpPathCollector.get_diagnostics (path_collector.py:83-92) + the env-tick count."""
+        """MdpPathCollector.get_diagnostics (path_collector.py:83-92): the same keys, so progress.csv has
+        the reference's columns (tests/golden/progress_header.json)."""
         st = OrderedDict([("num steps total", int(self._steps_total.item())),
-                          ("num paths total", int(self._paths_total.item())),
-                          ("num env ticks total", int(self._ticks_total.item()))])
+                          ("num paths total", int(self._paths_total.item()))])
         st.update(create_stats_ordered_dict("path length", [len(p["actions"]) for p in self._epoch_paths],
                                             always_show_all_stats=True))
         return st
+
+    def device_diagnostics(self):
+        """What the batched collector counts beyond the reference's columns (logged as text, not to
+        progress.csv): env ticks advanced and decisions dropped for a non-finite ship state."""
+        return OrderedDict([("num env ticks total", int(self._ticks_total.item())),
+                            ("num nonfinite decisions dropped", int(self._nonfinite_total.item()))])
 
     def get_snapshot(self):
         return dict(policy=self._policy)

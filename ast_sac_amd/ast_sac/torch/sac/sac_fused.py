@@ -58,7 +58,7 @@ class FusedSACTrainer(TorchTrainer):
                  policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None, soft_target_tau=1e-2, target_update_period=1,
                  plotter=None, render_eval_paths=False, use_automatic_entropy_tuning=True, target_entropy=None,
                  action_reg_coeff=None, clip_val=np.inf, batch_size=256, use_graph=None, process_group=None,
-                 backend=None):
+                 backend=None, split_update=None):
         super().__init__()
         if target_update_period != 1:
             raise NotImplementedError("FusedSACTrainer soft-updates every step (runner: target_update_period=1)")
@@ -83,6 +83,10 @@ class FusedSACTrainer(TorchTrainer):
         self.log_alpha = torch.zeros(1, requires_grad=use_automatic_entropy_tuning, device=dev)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        # the data-parallel step shape: grads | all-reduce over process_group | update (two graph halves).
+        # Default: whenever world > 1; split_update=True forces it on one rank too (the all-reduce then runs
+        # over a world-size-1 group: the same code path as N ranks, an identity on the values)
+        self.split = (self.world > 1) if split_update is None else bool(split_update)
 
         self.pi_params = ([self.log_alpha] if use_automatic_entropy_tuning else []) + list(policy.parameters())
         self.q_params = list(qf1.parameters()) + list(qf2.parameters())
@@ -172,7 +176,8 @@ class FusedSACTrainer(TorchTrainer):
         self.optimizer = None
         self._sf = SacFused(obs_dim, H, self.batch_size, dev, self.discount, self.reward_scale, self.soft_target_tau,
                             self.action_reg_coeff, self.clip_val, float(self.target_entropy), policy_lr, qf_lr,
-                            auto_entropy=self.use_automatic_entropy_tuning, world_size=self.world)
+                            auto_entropy=self.use_automatic_entropy_tuning, world_size=self.world,
+                            split_update=self.split)
         if self._sf.n_params != flat.numel() or self._sf.n_targets != tflat.numel():
             raise RuntimeError("hip backend: flat layout mismatch")
         self._stats_t = torch.zeros(self._sf.n_stats, device=dev)
@@ -214,7 +219,7 @@ class FusedSACTrainer(TorchTrainer):
             return
         if self._graphs is None or self._graphs[0] != key:
             torch.cuda.synchronize(self.device)
-            parts = ("ab",) if self.world == 1 else ("a", "b")
+            parts = ("a", "b") if self.split else ("ab",)
             graphs = []
             for part in parts:
                 g = torch.cuda.CUDAGraph()
@@ -300,7 +305,7 @@ class FusedSACTrainer(TorchTrainer):
                     pi_mean=torch.tanh(mean[:B]).detach(), pi_std=std[:B].detach())
 
     def _apply(self):
-        if self.world > 1:
+        if self.split:
             self.flat_grad.mul_(1.0 / self.world)
         self.optimizer.step()
         with torch.no_grad():
@@ -309,7 +314,7 @@ class FusedSACTrainer(TorchTrainer):
             torch._foreach_add_(self.t_params, self.q_params, alpha=tau)
 
     def _allreduce(self):
-        if self.world > 1:
+        if self.split and self.pg is not None:
             torch.distributed.all_reduce(self.flat_grad, group=self.pg)
 
     # ---------------------------------------------------------------- graph
@@ -355,7 +360,7 @@ class FusedSACTrainer(TorchTrainer):
         self._restore_state(snap)
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         pool = torch.cuda.graph_pool_handle()
-        if self.world > 1:
+        if self.split:
             with torch.cuda.graph(ga, pool=pool):
                 self._body_a(replay_buffer)
             with torch.cuda.graph(gb, pool=pool):

@@ -1510,7 +1510,7 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   w.params = h->params;
   w.step = h->step;
   w.stats = h->stats;
-  w.fuse = h->cfg.world_size == 1;  // no all-reduce between gradient and update: apply in the same kernel
+  w.fuse = h->cfg.world_size == 1 && !h->cfg.split_update;  // no all-reduce in between: apply in the same kernel
   w.ap = apply_args(h);
   hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_blocks), dim3(256), 0, h->stream, w);
   hipError_t e = hipGetLastError();
@@ -1519,7 +1519,7 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
 
 int sacf_apply(sacf_handle* h) {
   if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_apply: buffers not bound");
-  if (h->cfg.world_size == 1) return SACF_OK;  // sacf_grads already applied the update
+  if (h->cfg.world_size == 1 && !h->cfg.split_update) return SACF_OK;  // sacf_grads already applied the update
   ApplyArgs a = apply_args(h);
   const int64_t HH = (int64_t)h->L.H * h->L.H;
   const int64_t rest = h->L.n_params - 3 * HH;

@@ -66,7 +66,7 @@ struct Params {
   double AB_seg, AB_seg_n, AB_seg_e, omega_iw, n_base0, e_base0;
   double min_north, max_north, min_east, max_east;
   float action_low, action_high;
-  int32_t normalize_action, pad2_;
+  int32_t normalize_action, sbmpc_nsamp;  // sbmpc_nsamp = int(sbmpc_tf / sbmpc_dt) (sbmpc.py:121), host-evaluated
   float initial_states[8];           // env.py:107-109
   // host-evaluated sin/cos of uniform angles: wind_direction (algebraic wind force of the AST
   // kernels) and the IW sampler's omega (env.py:151-161)

@@ -116,6 +116,7 @@ struct ConstBuf {
 #define GRID_OUT 0
 #define GRID_IN 1
 #define GRID_MIXED 2
+
 // The ground-distance reward terms only use the coastline distance when it is <= 1000 m
 // (reward_function.py:109-117: test_ship_grounding_reward / obs_ship_grounding_reward clip at 1 km),
 // so a cell only needs the edges that can come within 1000 m of it: the min over that subset equals
@@ -278,6 +279,12 @@ struct SbIn {
 };
 // sin/cos(ob_psi) of a request built from its heading alone
 __device__ __forceinline__ void sb_set_heading_trig(SbIn& q) { sincos(q.ob_psi, &q.ob_so, &q.ob_co); }
+
+// a lane value the compiler must re-derive after this point (loads indexed by it cannot be hoisted)
+__device__ __forceinline__ int opaque_v(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 
 __device__ __forceinline__ double shfl_d(double x, int src) {
   int lo = __double2loint(x), hi = __double2hiint(x);
@@ -607,7 +614,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
 // request an optimisation with inputs `in`; they receive (P_best, Chi_best).
 __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double DT, double& p_best,
                                   double& chi_best) {
-  const int lane = threadIdx.x & 63;
+  const int lane = opaque_v(threadIdx.x) & 63;  // (opaque: no lane masks held across the caller's loop)
   const int half = lane >> 5;
   const int scen = lane & 31;
   uint64_t req = __ballot(need);
@@ -669,7 +676,7 @@ struct SbMulti {
 template <int NOB>
 __device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n_obs, int n_samp, double DT,
                                         double& p_best, double& chi_best) {
-  const int lane = threadIdx.x & 63;
+  const int lane = opaque_v(threadIdx.x) & 63;
   const int half = lane >> 5;
   const int scen = lane & 31;
   uint64_t req = __ballot(need);
@@ -972,6 +979,34 @@ __device__ __forceinline__ bool overtaking_sector(double dx, double dy, double d
   return fabs(beta) > 165.0 * (kPi / 180.0);
 }
 
+// Everything ast_step_kernel is launched with, as its one by-value kernel argument. The kernel reads
+// it through step_args(): the kernarg segment pointer laundered through an empty asm, so every read is
+// a scalar load (constant cache) issued where the value is used. Read as ordinary kernel parameters
+// these ~120 loop-invariant dwords were loaded at the entry and held in SGPRs for the whole launch,
+// which put the kernel past the SGPR limit and spilled them to VGPR lanes.
+struct StepArgs {
+  Params P;
+  DevState S;
+  ConstBuf K;
+  Traj T;
+  const float* action;
+  const uint8_t* active_mask;
+  float* obs_out;
+  double* reward_out;
+  uint8_t* done_out;
+  uint32_t* events_out;
+  int32_t* ticks_out;
+  uint8_t* ready_out;
+  ChainArgs CH;
+  int32_t max_ticks;
+};
+typedef const __attribute__((address_space(4))) StepArgs* StepArgsPtr;
+__device__ __forceinline__ const StepArgs& step_args() {
+  StepArgsPtr q = (StepArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();  // the kernel's first argument
+  asm volatile("" : "+s"(q));
+  return *(const StepArgs*)q;
+}
+
 // env flag bits exchanged between the two ships of an env every tick
 #define XF_GROUND 1
 #define XF_END 2
@@ -992,12 +1027,14 @@ __device__ __forceinline__ bool overtaking_sector(double dx, double dy, double d
 // K > 1 obstacle ships (shipsim_create) ship k sits on the lanes of index k mod SLOTS, and slots past
 // the env's last ship repeat that ship (ghost lanes: same state and arithmetic, never stored).
 template <bool DETAILED, int COLLAV, int LPE, bool REC, bool CHAIN = false, int SLOTS = 2>
-__global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S, ConstBuf K, Traj T,
-                                                      const float* __restrict__ action,
-                                                      const uint8_t* __restrict__ active_mask, int max_ticks,
-                                                      float* obs_out, double* reward_out, uint8_t* done_out,
-                                                      uint32_t* events_out, int32_t* ticks_out, uint8_t* ready_out,
-                                                      const ChainArgs CH) {
+__global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
+  (void)A_arg;  // read through step_args() only (see StepArgs)
+  const StepArgs& A0 = step_args();
+  const Params& P = A0.P;
+  const DevState& S = A0.S;
+  const ConstBuf& K = A0.K;
+  const Traj& T = A0.T;
+  const int max_ticks = A0.max_ticks;
   static_assert(!(REC && CHAIN), "trajectory recording runs the per-decision step only");
   static_assert(SLOTS == 2 || (LPE == 16 && !REC && COLLAV != SHIPSIM_COLLAV_SIMPLE), "multi-obstacle layout");
   constexpr int NSUB = LPE / SLOTS;
@@ -1053,7 +1090,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   double* rn = S.route_n() + (size_t)qc * kMaxRoute;
   double* re = S.route_e() + (size_t)qc * kMaxRoute;
 
-  bool running = valid && (active_mask == nullptr || active_mask[envc]) && S.was_reset()[envc];
+  bool running = valid && (A0.active_mask == nullptr || A0.active_mask[envc]) && S.was_reset()[envc];
   const bool touched = running;
 
   Ship s;
@@ -1096,6 +1133,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 #endif
   // ---- intermediate waypoint sampling (env.py:659-696) for an env that waits for a decision ----
   auto decision_prologue = [&](float sa) __attribute__((always_inline)) {
+    const StepArgs& A = step_args();
+    const Params& P = A.P;
+    const ConstBuf& K = A.K;
     if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
     phase = 0;
     have_iw = false;
@@ -1144,14 +1184,22 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   // ---- CHAIN: in-place reset (env.py:238-342, as reset_kernel) and the next decision ----
   int ep_i = 0, dec_i = 0, n_decided = 0, log_n = 0;
   if (CHAIN) {
+    const ChainArgs& CH = A0.CH;
     ep_i = CH.ep_idx[envc];
     dec_i = CH.dec_idx[envc];
     log_n = CH.log_len ? CH.log_len[envc] : 0;
   }
   auto table_action = [&]() __attribute__((always_inline)) -> float {
+    const StepArgs& A = step_args();
+    const Params& P = A.P;
+    const ChainArgs& CH = A.CH;
     return CH.table[((size_t)(ep_i % CH.n_eps) * CH.n_dec + dec_i) * P.n_envs + envc];
   };
   auto reset_env = [&]() __attribute__((always_inline)) {
+    const StepArgs& A = step_args();
+    const Params& P = A.P;
+    const ConstBuf& K = A.K;
+    const ShipConst& c = lds_sc[opaque_v(shipc)];
     s.n = c.init_n; s.e = c.init_e; s.yaw = c.init_yaw; s.u = c.init_u; s.v = c.init_v; s.r = c.init_r;
     s.omega = c.init_omega; s.time = 0.0;
     s.e_ct = 0; s.e_ct_int = 0; s.hdg_ei = 0; s.hdg_prev = 0;
@@ -1183,6 +1231,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   constexpr int kChainBurst = 8;
   auto chain_next = [&]() __attribute__((always_inline)) {
     for (int burst = 0; ready; ++burst) {
+      const ChainArgs& CH = step_args().CH;
       if (CH.log && lie == 0 && log_n < CH.log_cap) {
         double* rec = CH.log + ((size_t)env * CH.log_cap + log_n) * SHIPSIM_DECLOG_COLS;
         rec[SHIPSIM_DL_REWARD] = out_r; rec[SHIPSIM_DL_EVENTS] = (double)out_bits;
@@ -1200,7 +1249,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         dec_i += 1;
       }
       if (lie == 0) {
-        const DevState So = opaque(S);
+        const DevState So = opaque(step_args().S);
         for (int i = 0; i < 8; ++i) So.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
       }
       ready = false;
@@ -1214,9 +1263,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     }
   };
 
-  if (running && (dflags & DF_AWAITING)) decision_prologue(CHAIN ? table_action() : action[envc]);
+  if (running && (dflags & DF_AWAITING)) decision_prologue(CHAIN ? table_action() : A0.action[envc]);
 
-  const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
   bool going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
 #ifdef SHIPSIM_PHASE_TIMING
   unsigned long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1226,6 +1274,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
   // wave completes, so the loop body itself is the per-decision kernel's.
   for (;;) {
   while (__any(going) && !(CHAIN && __any(ready && running))) {
+    // this tick's constants: re-read (scalar loads, LDS) rather than kept in registers across ticks
+    const StepArgs& A = step_args();
+    const Params& P = A.P;
+    const ConstBuf& K = A.K;
+    const Traj& T = A.T;
     // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
@@ -1274,7 +1327,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         in.p_last = p_last; in.chi_last = chi_last;
       }
       double pb = 1.0, cb = 0.0;
-      sbmpc_cooperative_multi<NOB>(need && sub == 0, in, nsh - 1, n_samp, P.sbmpc_dt, pb, cb);
+      sbmpc_cooperative_multi<NOB>(need && sub == 0, in, nsh - 1, P.sbmpc_nsamp, P.sbmpc_dt, pb, cb);
       pb = env_lane_d<LPE, 0>(pb, env_lane0);
       cb = env_lane_d<LPE, 0>(cb, env_lane0);
       const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
@@ -1307,7 +1360,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
         in.p_last = p_last; in.chi_last = chi_last;
       }
       double pb = 1.0, cb = 0.0;
-      sbmpc_cooperative(need && sub == 0, in, n_samp, P.sbmpc_dt, pb, cb);
+      sbmpc_cooperative(need && sub == 0, in, P.sbmpc_nsamp, P.sbmpc_dt, pb, cb);
       pb = env_lane_d<LPE, 0>(pb, env_lane0);
       cb = env_lane_d<LPE, 0>(cb, env_lane0);
       const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
@@ -1597,17 +1650,20 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
 #endif
 
   if (!valid || !touched) return;
+  const StepArgs& AE = step_args();  // not the values loaded before the loop (no live range across it)
+  const ChainArgs& CH = AE.CH;
+  const Traj& TE = AE.T;
 #ifdef SHIPSIM_DEBUG_ENV
   if (env == SHIPSIM_DEBUG_ENV)
     printf("[dbg] env %d lie %d end: ready %d ticks %d sc %d n_base %f phase %d have_iw %d\n", env, lie, (int)ready,
            ticks, sampling_count, n_base, phase, (int)have_iw);
 #endif
-  const DevState So = opaque(S);  // addresses recomputed here, not carried through the loop
+  const DevState So = opaque(AE.S);  // addresses recomputed here, not carried through the loop
   if (sub == 0 && !ghost) store_ship(So, qc, s);
   if (REC) {
     if (sub == 0)
-      for (int k = 0; k < 3; ++k) T.fuel[(size_t)qc * 3 + k] = fuel[k];
-    if (lie == 0) T.len[env] = rec_t;
+      for (int k = 0; k < 3; ++k) TE.fuel[(size_t)qc * 3 + k] = fuel[k];
+    if (lie == 0) TE.len[env] = rec_t;
   }
   if (CHAIN && lie == 0) {
     CH.ep_idx[env] = ep_i;
@@ -1631,15 +1687,15 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const Params P, DevState S
     So.dec_ticks()[env] = dec_ticks;
     if (n_nonfinite) atomicAdd(So.nonfinite, n_nonfinite);
     if (ready) {
-      if (reward_out) reward_out[env] = out_r;
-      if (done_out) done_out[env] = out_done ? 1 : 0;
-      if (events_out) events_out[env] = out_bits;
+      if (AE.reward_out) AE.reward_out[env] = out_r;
+      if (AE.done_out) AE.done_out[env] = out_done ? 1 : 0;
+      if (AE.events_out) AE.events_out[env] = out_bits;
     }
-    if (ticks_out) ticks_out[env] = ticks;
-    if (ready_out) ready_out[env] = ready ? 1 : 0;
+    if (AE.ticks_out) AE.ticks_out[env] = ticks;
+    if (AE.ready_out) AE.ready_out[env] = ready ? 1 : 0;
   }
-  if (ready && obs_out && sub == 0 && ship < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
-    for (int i = 0; i < 4; ++i) obs_out[env * 8 + ship * 4 + i] = ns[ship * 4 + i];
+  if (ready && AE.obs_out && sub == 0 && ship < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
+    for (int i = 0; i < 4; ++i) AE.obs_out[env * 8 + ship * 4 + i] = ns[ship * 4 + i];
   }
 }
 
@@ -1972,6 +2028,18 @@ static int lanes_per_env(const shipsim_config* cfg, int n_envs, int device) {
   return lpe;
 }
 
+static StepArgs step_args_of(const shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks,
+                            float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
+                            int32_t* ticks_out, uint8_t* ready_out, const ChainArgs& ch) {
+  StepArgs a;
+  memset(&a, 0, sizeof(a));
+  a.P = h->P; a.S = h->S; a.K = h->K; a.T = h->T;
+  a.action = action; a.active_mask = active; a.max_ticks = max_ticks;
+  a.obs_out = obs_out; a.reward_out = reward_out; a.done_out = done_out; a.events_out = events_out;
+  a.ticks_out = ticks_out; a.ready_out = ready_out; a.CH = ch;
+  return a;
+}
+
 template <bool D, int CA>
 static void launch_step(shipsim_handle* h, int lpe, const float* action, const uint8_t* active, int32_t max_ticks,
                         float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
@@ -1980,9 +2048,9 @@ static void launch_step(shipsim_handle* h, int lpe, const float* action, const u
   if (h->T.ship) lpe = 16;  // recording kernels are built for the default layout only
   const int lanes = h->P.n_envs * lpe, blocks = (lanes + threads - 1) / threads;
 #define L(LPE, REC)                                                                                              \
-  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, REC>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S,  \
-                     h->K, h->T, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, \
-                     ready_out, ChainArgs{})
+  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, REC>), dim3(blocks), dim3(threads), 0, h->stream,            \
+                     step_args_of(h, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, \
+                                  ready_out, ChainArgs{}))
   if (h->T.ship) {
     L(16, true);
     return;
@@ -2006,8 +2074,8 @@ static void launch_multi(shipsim_handle* h, const float* action, const uint8_t* 
   const int threads = 64, blocks = (h->P.n_envs * 16 + threads - 1) / threads;
 #define LM(SL)                                                                                                         \
   hipLaunchKernelGGL((ast_step_kernel<true, CA, 16, false, CHAIN, SL>), dim3(blocks), dim3(threads), 0, h->stream,  \
-                     h->P, h->S, h->K, h->T, action, active, max_ticks, obs_out, reward_out, done_out, events_out,    \
-                     ticks_out, ready_out, ch)
+                     step_args_of(h, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, \
+                                  ready_out, ch))
   if (ship_slots(h) == 4) LM(4);
   else LM(8);
 #undef LM
@@ -2294,14 +2362,23 @@ static int validate(const shipsim_config* cfg, char* err, size_t n) {
   return 0;
 }
 
-static char g_create_err[512];  // message of the last failed shipsim_create (shipsim_last_error(NULL))
+// message of this thread's last failed shipsim_create (shipsim_last_error(NULL)); set on every failing path
+static thread_local char g_create_err[512];
 
 int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_ships, int32_t device, void* stream,
                    shipsim_handle** out) {
-  if (!cfg_in || !out || n_envs <= 0) return SHIPSIM_EINVAL;
+  g_create_err[0] = 0;
+  if (!cfg_in || !out || n_envs <= 0) {
+    snprintf(g_create_err, sizeof(g_create_err), "shipsim_create: %s", !cfg_in ? "config is NULL" : !out ? "out is NULL"
+             : "n_envs must be > 0");
+    return SHIPSIM_EINVAL;
+  }
   *out = nullptr;
   shipsim_handle* h = new (std::nothrow) shipsim_handle();
-  if (!h) return SHIPSIM_ENOMEM;
+  if (!h) {
+    snprintf(g_create_err, sizeof(g_create_err), "shipsim_create: out of host memory");
+    return SHIPSIM_ENOMEM;
+  }
   memset(h, 0, sizeof(*h));
   h->cfg = *cfg_in;
   if (n_obs_ships > 0 && h->cfg.kind == SHIPSIM_KIND_AST) h->cfg.n_ships = 1 + n_obs_ships;
@@ -2338,6 +2415,7 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
   P.wind_speed = cfg->wind_speed;
   P.roa2 = cfg->env_radius_of_acceptance * cfg->env_radius_of_acceptance;
   P.sbmpc_tf = cfg->sbmpc_tf;
+  P.sbmpc_nsamp = (int32_t)(cfg->sbmpc_tf / cfg->sbmpc_dt);
   P.sbmpc_dt = cfg->sbmpc_dt;
   P.wind_sin = sin(cfg->wind_direction);
   P.wind_cos = cos(cfg->wind_direction);
@@ -2538,6 +2616,10 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
   const int lpe = h->lpe;
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
 #define LAUNCH(D, CA) launch_step<D, CA>(h, lpe, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, ready_out)
+#ifdef SHIPSIM_REGCHECK  // register-usage inspection builds (scripts/regcheck.sh): headline kernels only
+  (void)lpe; (void)det;
+  return fail(h, SHIPSIM_EINVAL, "REGCHECK build");
+#else
   if (ship_slots(h) > 2) {
     if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
       launch_multi<SHIPSIM_COLLAV_SBMPC, false>(h, action, active, max_ticks, obs_out, reward_out, done_out,
@@ -2553,6 +2635,7 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
     case SHIPSIM_COLLAV_SIMPLE: if (det) LAUNCH(true, 1); else LAUNCH(false, 1); break;
     default: if (det) LAUNCH(true, 2); else LAUNCH(false, 2); break;
   }
+#endif
 #undef LAUNCH
   HIPCHK(h, hipGetLastError());
   return SHIPSIM_OK;
@@ -2591,9 +2674,9 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
   const int lpe = (h->lpe == 8 || h->lpe == 4) ? h->lpe : (h->lpe == 2 ? 4 : 16);
   const int threads = 64, blocks = (h->P.n_envs * lpe + threads - 1) / threads;
 #define CHAINED_L(D, CA, LPE)                                                                                          \
-  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, true>), dim3(blocks), dim3(threads), 0, h->stream, h->P,      \
-                     h->S, h->K, h->T, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out,    \
-                     nullptr, ch)
+  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, true>), dim3(blocks), dim3(threads), 0, h->stream,        \
+                     step_args_of(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out,     \
+                                  nullptr, ch))
 #define CHAINED(D, CA)                              \
   do {                                              \
     if (lpe == 8) CHAINED_L(D, CA, 8);              \
@@ -2601,6 +2684,11 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
     else CHAINED_L(D, CA, 16);                      \
   } while (0)
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
+#ifdef SHIPSIM_REGCHECK
+  if (h->P.collav == SHIPSIM_COLLAV_SBMPC) CHAINED_L(true, SHIPSIM_COLLAV_SBMPC, 16);
+  else CHAINED_L(true, SHIPSIM_COLLAV_NONE, 16);
+  (void)det;
+#else
   if (ship_slots(h) > 2) {
     if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
       launch_multi<SHIPSIM_COLLAV_SBMPC, true>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr,
@@ -2616,6 +2704,7 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
     case SHIPSIM_COLLAV_SIMPLE: if (det) CHAINED(true, SHIPSIM_COLLAV_SIMPLE); else CHAINED(false, SHIPSIM_COLLAV_SIMPLE); break;
     default: if (det) CHAINED(true, SHIPSIM_COLLAV_NONE); else CHAINED(false, SHIPSIM_COLLAV_NONE); break;
   }
+#endif
 #undef CHAINED
 #undef CHAINED_L
   HIPCHK(h, hipGetLastError());
@@ -2633,11 +2722,16 @@ int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_
   hipLaunchKernelGGL((legacy_step_kernel<D, CA>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k, \
                      states_out, done_out, status_out)
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
+#ifdef SHIPSIM_REGCHECK
+  (void)det;
+  return fail(h, SHIPSIM_EINVAL, "REGCHECK build");
+#else
   switch (h->P.collav) {
     case SHIPSIM_COLLAV_SBMPC: if (det) LEGACY(true, SHIPSIM_COLLAV_SBMPC); else LEGACY(false, SHIPSIM_COLLAV_SBMPC); break;
     case SHIPSIM_COLLAV_SIMPLE: if (det) LEGACY(true, SHIPSIM_COLLAV_SIMPLE); else LEGACY(false, SHIPSIM_COLLAV_SIMPLE); break;
     default: if (det) LEGACY(true, SHIPSIM_COLLAV_NONE); else LEGACY(false, SHIPSIM_COLLAV_NONE); break;
   }
+#endif
 #undef LEGACY
   HIPCHK(h, hipGetLastError());
   return SHIPSIM_OK;

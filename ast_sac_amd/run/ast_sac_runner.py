@@ -60,7 +60,9 @@ def build_parser():
     p.add_argument("--clip_val", type=float, default=100)
     # MI355X execution shape
     p.add_argument("--n_envs", type=int, default=4096, help="device envs per GPU (0 = reference single-env graph)")
-    p.add_argument("--eval_envs", type=int, default=256)
+    p.add_argument("--eval_envs", type=int, default=0,
+                   help="0 (default): evaluation on the exploration envs, one env object as the reference (Q10); "
+                        "N > 0: a separate evaluation shard of N envs")
     p.add_argument("--slice_ticks", type=int, default=128)  # collector slice: best of 64/128/256/512
     p.add_argument("--match_update_ratio", type=_bool, default=True,
                    help="grad steps per train loop = collected decisions (all ranks) x num_trains / num_expl_steps "
@@ -140,11 +142,15 @@ def experiment_device(variant, args, device, process_group=None):
     from ..ast_sac.core.device_rl_algorithm import DeviceBatchRLAlgorithm
 
     cfg = config_from_args(args, args.machinery)
-    expl_env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(args, args.n_envs, device=device, cfg=cfg),
-                                       reward_scale=args.reward_scale)
-    eval_env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(args, max(1, args.eval_envs), device=device,
-                                                             cfg=config_from_args(args, args.machinery)),
-                                       reward_scale=args.reward_scale)
+    env = BatchedMultiShipRLEnv(args, args.n_envs, device=device, cfg=cfg)
+    expl_env = BatchedNormalizedBoxEnv(env, reward_scale=args.reward_scale)
+    if args.eval_envs > 0:  # a separate evaluation env shard (not the reference's shape, see below)
+        eval_env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(args, args.eval_envs, device=device,
+                                                                 cfg=config_from_args(args, args.machinery)),
+                                           reward_scale=args.reward_scale)
+    else:  # default: one env object under both wrappers, as run/ast-sac_runner.py:113-114 (quirk Q10): the
+        # evaluation episodes reset and advance the exploration envs, whose SBMPC memory carries over (Q7)
+        eval_env = BatchedNormalizedBoxEnv(env, reward_scale=args.reward_scale)
     obs_dim = expl_env.observation_space.low.size
     act_dim = expl_env.action_space.low.size
     policy, (qf1, qf2, tq1, tq2) = _networks(obs_dim, act_dim, variant["layer_size"], device)

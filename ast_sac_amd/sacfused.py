@@ -26,7 +26,7 @@ class Config(C.Structure):
                 ("action_reg_coeff", C.c_float), ("clip_val", C.c_float), ("target_entropy", C.c_float),
                 ("policy_lr", C.c_float), ("qf_lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
                 ("adam_eps", C.c_float), ("auto_entropy", C.c_int32), ("world_size", C.c_int32),
-                ("reserved", C.c_int32 * 6)]
+                ("split_update", C.c_int32), ("reserved", C.c_int32 * 5)]
 
 
 def load_library(path=LIB_PATH):
@@ -71,13 +71,14 @@ class SacFused:
     """One handle = one device + the caller's flat fp32 buffers (see sac_fused.h)."""
 
     def __init__(self, obs_dim, hidden, batch, device, discount, reward_scale, tau, action_reg, clip_val,
-                 target_entropy, policy_lr, qf_lr, auto_entropy=True, world_size=1, betas=(0.9, 0.999), eps=1e-8):
+                 target_entropy, policy_lr, qf_lr, auto_entropy=True, world_size=1, betas=(0.9, 0.999), eps=1e-8,
+                 split_update=False):
         self.L = load_library()
         cfg = Config(abi_version=ABI_VERSION, obs_dim=obs_dim, hidden=hidden, batch=batch, discount=discount,
                      reward_scale=reward_scale, soft_target_tau=tau, action_reg_coeff=action_reg or 0.0,
                      clip_val=clip_val, target_entropy=target_entropy, policy_lr=policy_lr, qf_lr=qf_lr,
                      beta1=betas[0], beta2=betas[1], adam_eps=eps, auto_entropy=int(bool(auto_entropy)),
-                     world_size=world_size)
+                     world_size=world_size, split_update=int(bool(split_update)))
         self.device = torch.device(device)
         h = C.c_void_p()
         with torch.cuda.device(self.device):

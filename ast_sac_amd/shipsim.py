@@ -95,10 +95,12 @@ class ShipSim:
         if not torch.cuda.is_available():
             raise ShipSimError("ShipSim needs a HIP device (torch.cuda.is_available() is False)")
         self.L = load_library()
-        self.cfg = cfg
+        # a private copy: the caller's config is left as it was (n_obs_ships only applies to this handle)
+        cfg = abi.Config.from_buffer_copy(cfg)
         self.n_envs = int(n_envs)
         if n_obs_ships > 0 and cfg.kind == abi.KIND_AST:
             cfg.n_ships = 1 + int(n_obs_ships)
+        self.cfg = cfg
         self.n_ships = int(cfg.n_ships)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
         with torch.cuda.device(self.device):

@@ -195,12 +195,14 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
 
     dt = fused("hip")
     H, O = 256, 8
+    backend = dist.get_backend(pg) if world > 1 else None
+    ar = {"nccl": "RCCL all-reduce", "gloo": "gloo all-reduce (rehearsal, not RCCL)"}.get(backend, f"{backend} all-reduce")
     flops = sac_flops_per_step(batch, H, O)
     res = {"grad_steps_per_s": steps / dt, "ms_per_grad_step": dt / steps * 1e3, "batch_per_gpu": batch,
-           "global_batch": batch * world, "hidden": [H, H], "dtype": "f32",
+           "global_batch": batch * world, "hidden": [H, H], "dtype": "f32", "dist_backend": backend,
            "impl": "FusedSACTrainer hip backend (csrc/sac_kernels.hip: four MFMA f32 forward/backward GEMM "
                    "kernels + the MFMA weight-gradient kernel" +
-                   (", RCCL all-reduce, Adam/soft-update kernel; HIP graph halves)" if world > 1 else
+                   (f", {ar}, Adam/soft-update kernel; HIP graph halves)" if world > 1 else
                     " with Adam, soft target update and W2T refresh fused in: five launches, HIP graph)"),
            "roofline": {"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_F32_PEAK_TFLOPS,
                         "flops_per_step": flops,
@@ -277,6 +279,18 @@ def spawn_ranks(n):
     return subprocess.call(cmd)
 
 
+def device_identity(torch, dev):
+    """A string naming the physical GPU behind `dev`: its UUID, else its PCI domain:bus:device."""
+    p = torch.cuda.get_device_properties(dev)
+    uuid = str(getattr(p, "uuid", "") or "")
+    if uuid and uuid.strip("0-"):
+        return "uuid:" + uuid
+    pci = tuple(getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if any(v is not None for v in pci):
+        return "pci:%s" % (pci,)
+    return "host:%s/ordinal:%d" % (os.uname().nodename, dev.index)
+
+
 def rank_layout(args, torch):
     """(world, rank, local device index) of this process, checked against --gpus."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -314,12 +328,14 @@ def main():
             dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    # distinct physical devices behind the ranks (= world over RCCL; fewer under a gloo rehearsal)
-    used = torch.zeros(64, dtype=torch.float64, device=dev)
-    used[local] = 1.0
+    # distinct physical devices behind the ranks (= world over RCCL; fewer under a gloo rehearsal), by
+    # device identity (UUID / PCI location), not by local ordinal (a launcher may give each rank
+    # HIP_VISIBLE_DEVICES=<one GPU>, where every rank sees its GPU as device 0)
+    ids = [device_identity(torch, dev)]
     if world > 1:
-        dist.all_reduce(used, op=dist.ReduceOp.MAX)
-    n_devices = int(used.sum().item())
+        ids = [None] * world
+        dist.all_gather_object(ids, device_identity(torch, dev))
+    n_devices = len(set(ids))
     mach = abi.MACH_DETAILED if args.machinery == "detailed" else abi.MACH_SIMPLIFIED
     cfg = abi.ast_config(args.collav, machinery=mach, n_obs_ships=args.obs_ships)
     cfg.lanes_per_env = args.lpe

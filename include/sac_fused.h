@@ -12,8 +12,9 @@
  *                with world_size == 1 that kernel also applies Adam (torch.optim.Adam semantics,
  *                betas/eps as configured), the soft target update and the refresh of the library's
  *                transposed weight copies to the elements it finishes: five launches per grad step.
- *   sacf_apply : world_size > 1 only (a no-op otherwise): the same update as a sixth launch, after the
- *                caller all-reduced the flat gradient; the gradient is divided by world_size.
+ *   sacf_apply : world_size > 1 or split_update only (a no-op otherwise): the same update as a sixth
+ *                launch, after the caller all-reduced the flat gradient; the gradient is divided by
+ *                world_size.
  *
  * Memory: the caller owns the flat buffers (torch tensors) bound with sacf_bind; the library owns
  * its scratch (per-row activations, ≈12·B·H floats) and transposed copies of the H×H weights.
@@ -58,7 +59,9 @@ typedef struct sacf_config {
   float beta1, beta2, adam_eps; /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
   int32_t auto_entropy;  /* use_automatic_entropy_tuning */
   int32_t world_size;    /* gradient is divided by this in sacf_apply */
-  int32_t reserved[6];
+  int32_t split_update;  /* 1: keep the update out of sacf_grads even with world_size 1 (the data-parallel
+                            call pattern grads | all-reduce | apply on one rank); 0: fused when world_size 1 */
+  int32_t reserved[5];
 } sacf_config;
 
 typedef struct sacf_handle sacf_handle;
@@ -87,13 +90,14 @@ int sacf_sync_params(sacf_handle* h);
 /* Replay ring (DeviceReplayBuffer storage, float32 rows) sampled uniformly with replacement. */
 int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
                     const float* next_obs, const int64_t* size_dev, int64_t capacity, uint64_t seed);
-/* Gradient of one update into `grads` (and step += 1); with world_size == 1 also the update itself
+/* Gradient of one update into `grads` (and step += 1); with world_size == 1 and no split_update also the
+ * update itself
  * (grads keeps the gradient for inspection). With obs == NULL the batch is sampled from
  * the replay ring; with eps == NULL the 2·B reparameterisation normals come from the in-kernel
  * Philox stream, else eps = [B normals for obs rows | B normals for next_obs rows]. */
 int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
                const float* next_obs, const float* eps);
-/* Adam + soft target update from `grads` (divided by world_size); a no-op when world_size == 1. */
+/* Adam + soft target update from `grads` (divided by world_size); a no-op when sacf_grads applied it. */
 int sacf_apply(sacf_handle* h);
 
 #ifdef __cplusplus

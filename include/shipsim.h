@@ -257,7 +257,8 @@ int shipsim_default_config(int32_t kind, int32_t machinery, int32_t collav, doub
 int shipsim_create(const shipsim_config* cfg, int32_t n_envs, int32_t n_obs_ships, int32_t device, void* stream,
                    shipsim_handle** out);
 int shipsim_destroy(shipsim_handle* h);
-/* Message of the last failed call on h; with h == NULL, of the last failed shipsim_create. */
+/* Message of the last failed call on h; with h == NULL, of the calling thread's last shipsim_create that
+ * failed before it could hand out a handle (every such path sets it; it is per thread). */
 const char* shipsim_last_error(const shipsim_handle* h);
 int32_t shipsim_num_envs(const shipsim_handle* h);
 /* Lanes per AST env the step / stream kernels run at (config lanes_per_env, or chosen at create from

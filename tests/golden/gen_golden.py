@@ -957,6 +957,101 @@ def gen_policy():
     np.savez_compressed(os.path.join(OUT, "trained_policy.npz"), **out)
 
 
+def gen_progress():
+    """f2: the progress.csv the reference's own training loop writes — TorchBatchRLAlgorithm
+    (core/batch_rl_algorithm.py:58-106, rl_algorithm.py:57-150) with SACTrainer, MdpPathCollector,
+    EnvReplayBuffer and the runner's NormalizedBoxEnv-wrapped MultiShipRLEnv (run/ast-sac_runner.py:110-205;
+    expl and eval envs share one env object, as there), for two epochs of a few decisions, on the CPU.
+    gtimer (1.0.0b5) is absent, so its published behaviour for these calls is restated: inside
+    `timed_for(..., save_itrs=True)` every `stamp(name)` appends the time since the previous stamp (or
+    the loop start) to `get_times().stamps.itrs[name]`, and `get_times().total` is the elapsed time.
+    Only the header (its column names; the logger writes them sorted, logging.py:285-305) and the
+    row count are kept: the values are timings and a random init's losses."""
+    import csv
+    import json
+    import tempfile
+    import time
+    import torch
+    import ast_sac.torch.utils.pytorch_util as ptu
+    ptu.set_gpu_mode(False)
+
+    class _Itrs(dict):
+        pass
+
+    class _Times:
+        def __init__(self):
+            self.stamps = types.SimpleNamespace(itrs=_Itrs())
+            self.total = 0.0
+
+    state = dict(t0=time.perf_counter(), last=time.perf_counter(), times=_Times())
+
+    def stamp(name, unique=True, **k):
+        now = time.perf_counter()
+        state["times"].stamps.itrs.setdefault(name, []).append(now - state["last"])
+        state["last"] = now
+
+    def timed_for(it, save_itrs=True, **k):
+        for x in it:
+            state["last"] = time.perf_counter()
+            yield x
+
+    def get_times():
+        state["times"].total = time.perf_counter() - state["t0"]
+        return state["times"]
+
+    gt = sys.modules["gtimer"]
+    saved = (gt.stamp, gt.timed_for, gt.get_times)
+    gt.stamp, gt.timed_for, gt.get_times = stamp, timed_for, get_times
+    try:
+        for m in [m for m in sys.modules if m.startswith("ast_sac.core") or m.startswith("ast_sac.torch.core")]:
+            del sys.modules[m]  # re-import the algorithm modules against the recording stand-in
+        from ast_sac.core.logging import logger
+        from ast_sac.data_management.env_replay_buffer import EnvReplayBuffer
+        from ast_sac.samplers.data_collector.path_collector import MdpPathCollector
+        from ast_sac.samplers.data_collector.rollout_functions import ast_sac_rollout
+        from ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy, MakeDeterministic
+        from ast_sac.torch.sac.sac import SACTrainer
+        from ast_sac.torch.networks.mlp import ConcatMlp
+        from ast_sac.torch.core.torch_rl_algorithm import TorchBatchRLAlgorithm
+        from ast_sac.env_wrapper.normalized_box_env import NormalizedBoxEnv
+        from run.env_setup import prepare_multiship_rl_env
+        torch.manual_seed(0)
+        np.random.seed(0)
+        env, _ = prepare_multiship_rl_env(rl_args("none"))
+        expl_env, eval_env = NormalizedBoxEnv(env, reward_scale=0.75), NormalizedBoxEnv(env, reward_scale=0.75)
+        M = 16
+        qf = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[M, M]) for _ in range(4)]
+        policy = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[M, M])
+        eval_col = MdpPathCollector(eval_env, MakeDeterministic(policy), rollout_fn=ast_sac_rollout)
+        expl_col = MdpPathCollector(expl_env, policy, rollout_fn=ast_sac_rollout)
+        rb = EnvReplayBuffer(1000, expl_env)
+        tr = SACTrainer(env=eval_env, policy=policy, qf1=qf[0], qf2=qf[1], target_qf1=qf[2], target_qf2=qf[3],
+                        discount=0.965, soft_target_tau=1e-3, target_update_period=1, policy_lr=8e-5, qf_lr=8e-5,
+                        reward_scale=0.75, use_automatic_entropy_tuning=True, action_reg_coeff=0.01, clip_val=100)
+        algo = TorchBatchRLAlgorithm(trainer=tr, exploration_env=expl_env, evaluation_env=eval_env,
+                                     exploration_data_collector=expl_col, evaluation_data_collector=eval_col,
+                                     replay_buffer=rb, batch_size=8, max_path_length=2, num_epochs=2,
+                                     num_eval_steps_per_epoch=3, num_expl_steps_per_train_loop=3,
+                                     num_trains_per_train_loop=2, min_num_steps_before_training=4)
+        d = tempfile.mkdtemp()
+        f = os.path.join(d, "progress.csv")
+        logger.add_tabular_output(f)
+        try:
+            algo.train()
+        finally:
+            logger.remove_tabular_output(f)
+        with open(f) as fh:
+            rows = list(csv.reader(fh))
+    finally:
+        gt.stamp, gt.timed_for, gt.get_times = saved
+    res = dict(columns=rows[0], n_rows=len(rows) - 1,
+               generator="tests/golden/gen_golden.py progress: reference TorchBatchRLAlgorithm, 2 epochs, "
+                         "MultiShipRLEnv (collav none), SACTrainer 2x16, gtimer restated (see gen_progress)")
+    with open(os.path.join(OUT, "progress_header.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+    print("progress:", len(rows[0]), "columns,", len(rows) - 1, "rows")
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["c2", "c1", "ast", "rl", "sbmpc", "sac"]
     if "replay" in what:
@@ -985,3 +1080,5 @@ if __name__ == "__main__":
         gen_legacy()
     if "policy" in what:
         gen_policy()
+    if "progress" in what:
+        gen_progress()

@@ -167,37 +167,55 @@ class _RB(_Buffer):
         return {}
 
 
-def test_device_algorithm_progress_columns(tmp_path):
-    """DeviceBatchRLAlgorithm's progress.csv carries the reference's columns: time/<stamp> (s) for every
-    gtimer stamp of batch_rl_algorithm.py / rl_algorithm.py (evaluation sampling, exploration sampling,
-    data storing, training, saving, logging, epoch, total) and the expl/ eval/ path statistics."""
+def test_device_algorithm_progress_header_equals_reference(tmp_path):
+    """f2: the progress.csv DeviceBatchRLAlgorithm writes has exactly the header the reference's own
+    TorchBatchRLAlgorithm writes (tests/golden/progress_header.json, generated by running it:
+    gen_golden.py progress): the same column names in the same (sorted, logging.py:285-305) order,
+    including the time/<stamp> (s) columns of every gtimer stamp (sac training included), the
+    replay-buffer / trainer / expl / eval statistics and no build-only columns. Here with the real
+    trainer (FusedSACTrainer, torch backend) and DeviceReplayBuffer on the CPU, scripted envs."""
     import csv
+    import json
+    import os
     from ast_sac_amd.ast_sac.core.device_rl_algorithm import DeviceBatchRLAlgorithm
     from ast_sac_amd.ast_sac.core.logging import logger
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    from ast_sac_amd.ast_sac.torch.networks.mlp import ConcatMlp
+    from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac_amd.ast_sac.torch.sac.sac_fused import FusedSACTrainer
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "progress_header.json")))
+
+    class _E:
+        class action_space:
+            shape = (1,)
+
+    torch.manual_seed(0)
+    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[16, 16])
+    qs = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[16, 16]) for _ in range(4)]
+    tr = FusedSACTrainer(env=_E, policy=pol, qf1=qs[0], qf2=qs[1], target_qf1=qs[2], target_qf2=qs[3],
+                         discount=0.965, reward_scale=0.75, policy_lr=8e-5, qf_lr=8e-5, soft_target_tau=1e-3,
+                         action_reg_coeff=0.01, clip_val=100.0, batch_size=8, use_graph=False, backend="torch")
     env_x, env_e = _ScriptedEnv(16), _ScriptedEnv(8)
     cx = BatchedPathCollector(env_x, _Policy(), max_path_length=9, deterministic=True)
     ce = BatchedPathCollector(env_e, _Policy(), max_path_length=9, deterministic=True)
-    algo = DeviceBatchRLAlgorithm(_Trainer(), env_x, env_e, cx, ce, _RB(), batch_size=32, max_path_length=9,
-                                  num_epochs=2, num_eval_steps_per_epoch=20, num_expl_steps_per_train_loop=30,
-                                  num_trains_per_train_loop=5, min_num_steps_before_training=40)
+    algo = DeviceBatchRLAlgorithm(tr, env_x, env_e, cx, ce, DeviceReplayBuffer(1000, 8, 1, "cpu"), batch_size=8,
+                                  max_path_length=9, num_epochs=2, num_eval_steps_per_epoch=20,
+                                  num_expl_steps_per_train_loop=30, num_trains_per_train_loop=5,
+                                  min_num_steps_before_training=40)
     f = str(tmp_path / "progress.csv")
     logger.add_tabular_output(f)
     try:
         algo.train()
     finally:
         logger.remove_tabular_output(f)
-    rows = list(csv.DictReader(open(f)))
-    assert len(rows) == 2
-    cols = set(rows[0])
-    for k in ("evaluation sampling", "exploration sampling", "data storing", "training", "saving", "logging",
-              "epoch", "total"):
-        assert f"time/{k} (s)" in cols, k
-    assert not any(c.startswith("time/") and "initial" in c for c in cols)
-    for pre in ("expl/", "eval/"):
-        for k in ("num steps total", "num paths total", "path length Mean", "Rewards Mean", "Returns Mean",
-                  "Actions Mean", "Num Paths", "Average Returns"):
-            assert pre + k in cols, pre + k
-    assert "trainer/QF1 Loss" in cols and "Epoch" in cols and rows[1]["Epoch"] == "1"
+    with open(f) as fh:
+        rows = list(csv.reader(fh))
+    assert len(rows) - 1 == ref["n_rows"] == 2
+    header = rows[0]
+    missing, extra = sorted(set(ref["columns"]) - set(header)), sorted(set(header) - set(ref["columns"]))
+    assert not missing and not extra, (missing, extra)
+    assert header == ref["columns"]
+    assert rows[2][header.index("Epoch")] == "1"
 
 
 def test_update_ratio_follows_collected_decisions():
@@ -239,3 +257,35 @@ def test_trace_records_each_decision():
             assert (d["episode"], d["decision"]) == (k // L, k % L)
             assert d["done"] == (k % L == L - 1) and d["reward"] == 10 * i + k % L
             assert bool(d["events"] & abi.EV_TERMINAL) == d["done"]
+
+
+def test_shared_env_eval_then_expl_resets_and_restarts_episodes():
+    """Q10 (run/ast-sac_runner.py:113-114): an evaluation collector over the exploration collector's env
+    takes it over — every env is reset and every episode starts afresh (the reference begins each path
+    with env.reset()) — and the exploration collector takes it back the same way; a collector that
+    already drives the env does not reset it again."""
+    env = _ScriptedEnv(12)
+    calls = []
+    real_reset = env.reset
+
+    def reset(mask=None, obs_out=None):
+        calls.append(None if mask is None else int(mask.sum()))
+        return real_reset(mask, obs_out)
+
+    env.reset = reset
+    expl = BatchedPathCollector(env, _Policy(), max_path_length=9, deterministic=True)
+    ev = BatchedPathCollector(env, _Policy(), max_path_length=9, deterministic=True)
+    calls.clear()
+    ev.collect(10, None, record_paths=True)        # the env was last set up by ev's constructor: no takeover
+    assert None not in calls
+    expl.collect(10, _Buffer())                     # takes over: one full reset, then only masked resets
+    assert calls.count(None) == 1
+    n_full = calls.count(None)
+    assert int(expl._path_len.max()) <= 9
+    expl.collect(10, _Buffer())                     # still the owner: no full reset
+    assert calls.count(None) == n_full
+    ev.collect(10, None, record_paths=True)
+    assert calls.count(None) == n_full + 1
+    # after the takeover the eval collector's episodes all restarted at decision 0
+    paths = ev.get_epoch_paths()
+    assert all(len(p["actions"]) >= 1 for p in paths)

@@ -137,3 +137,38 @@ def test_device_training_loop_runs():
     assert algo.num_train_steps_total == algo.trainer._n_train_steps_total
     assert abs(algo.num_train_steps_total - n_expl * 120 / 256) < 1 + 1e-9  # --num_trains_per_train_loop 120
     assert n_expl >= 2 * 256
+
+
+def test_shared_eval_env_carries_sbmpc_memory():
+    """Q10 + Q7 on the device runner's default shape: evaluation and exploration wrap ONE batched env
+    (run/ast-sac_runner.py:113-114). The evaluation collector's episodes advance those envs; when the
+    exploration collector takes them back it resets every env (each reference path starts with reset())
+    and the reset leaves the SBMPC memory P_ca_last / Chi_ca_last as the evaluation episodes left it
+    (sbmpc.py:143-145 is never reset, env.py:238-295): the same envs, the same carried state."""
+    from ast_sac_amd.rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, default_args
+    from ast_sac_amd.ast_sac.env_wrapper.normalized_box_env import BatchedNormalizedBoxEnv
+    from ast_sac_amd.ast_sac.samplers.data_collector.batched_collector import BatchedPathCollector
+    from ast_sac_amd.ast_sac.torch.sac.policies.base import MakeDeterministic
+    from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    N = 64
+    env = BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), N)
+    expl_env, eval_env = BatchedNormalizedBoxEnv(env, 0.75), BatchedNormalizedBoxEnv(env, 0.75)
+    torch.manual_seed(0)
+    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[32, 32]).cuda()
+    expl = BatchedPathCollector(expl_env, pol, max_path_length=9, max_ticks=128)
+    ev = BatchedPathCollector(eval_env, MakeDeterministic(pol), max_path_length=9, max_ticks=128, deterministic=True)
+    expl.collect(32, None)
+    ev.collect(64, None, record_paths=True)
+    assert len(ev.get_epoch_paths()) > 0
+    # distinctive SBMPC memory in the shared envs, as an evaluation episode in an encounter leaves it
+    p = torch.linspace(0.4, 1.0, N, dtype=torch.float64, device="cuda")
+    c = torch.linspace(-0.5, 0.5, N, dtype=torch.float64, device="cuda")
+    env.sim.set(abi.E_SBMPC_P_LAST, p)
+    env.sim.set(abi.E_SBMPC_CHI_LAST, c)
+    expl._take_over()  # what expl.collect does first: reset every env, restart every episode
+    torch.cuda.synchronize()
+    assert int(expl._path_len.max()) == 0 and bool(expl._awaiting.all())
+    assert torch.equal(env.sim.get(abi.E_SBMPC_P_LAST), p) and torch.equal(env.sim.get(abi.E_SBMPC_CHI_LAST), c)
+    assert int(env.sim.get(abi.E_SAMPLING_COUNT).max()) == 0  # everything else restarted
+    got = expl.collect(32, None)
+    assert got >= 32
