@@ -93,9 +93,10 @@ class NormalizedBoxEnv(ProxyEnv):
 
 
 def denormalize_action(a, low, high):
-    """float32 lb + (a + 1)·0.5·(ub − lb), clipped — normalized_box_env.py:48-51 on tensors."""
-    lb = torch.as_tensor(np.float32(low), dtype=torch.float32, device=a.device)
-    ub = torch.as_tensor(np.float32(high), dtype=torch.float32, device=a.device)
+    """float32 lb + (a + 1)·0.5·(ub − lb), clipped — normalized_box_env.py:48-51 on tensors. low / high:
+    numbers, or float32 tensors already on a's device (no host copy: graph-capturable)."""
+    lb = low if torch.is_tensor(low) else torch.as_tensor(np.float32(low), dtype=torch.float32, device=a.device)
+    ub = high if torch.is_tensor(high) else torch.as_tensor(np.float32(high), dtype=torch.float32, device=a.device)
     a = a.to(torch.float32)
     return torch.minimum(torch.maximum(lb + (a + 1.0) * 0.5 * (ub - lb), lb), ub)
 
@@ -121,7 +122,11 @@ class BatchedNormalizedBoxEnv:
         return self._wrapped_env.n_envs
 
     def scale_action(self, a):
-        return denormalize_action(a, self._lb, self._ub)
+        key = a.device
+        if getattr(self, "_bounds_dev", None) != key:  # the bounds as device scalars, made once per device
+            self._bounds = (torch.tensor(np.float32(self._lb), device=key), torch.tensor(np.float32(self._ub), device=key))
+            self._bounds_dev = key
+        return denormalize_action(a, *self._bounds)
 
     def reset(self, mask=None, obs_out=None):
         return self._wrapped_env.reset(mask, obs_out=obs_out)

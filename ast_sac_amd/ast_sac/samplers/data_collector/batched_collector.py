@@ -7,11 +7,18 @@ env_info['terminal']) is recorded, and the episode ends on done or after max_pat
 decisions. Unlike the reference, thousands of envs advance together: one sliced
 `step_async(max_ticks)` call advances every env by ≤ max_ticks ticks, envs that complete a
 decision emit their transition straight into a DeviceReplayBuffer, and finished envs are reset
-in the same pass (masked reset). The policy runs only on the envs that wait for a decision (their
-count is known on the host from the previous pass, so the compaction needs no extra sync). Inside
-`collect` the only host traffic is the transition count per pass, plus, with record_paths, the
-rewards/actions of the episodes that ended in that pass: those become the epoch's paths
-(get_epoch_paths, as MdpPathCollector's, path_collector.py:77-78) from which the algorithm logs
+in the same pass (masked reset).
+
+Two ways to pick the actions:
+* device_policy (the runner's, a FusedSACTrainer.device_policy): the trainer's current policy on the
+  matrix cores (libsacfused sacf_policy_act) for every env, the result kept only where an env waits for
+  a decision. A pass is then device work only — policy, env slice, replay append, path bookkeeping,
+  masked reset — and is captured once in a HIP graph and replayed. `collect` checks the transition count
+  on the host only every few passes (it plans the passes from the count per pass), and the episodes that
+  ended go to a device ring that is copied to the host once per collect (record_paths).
+* a torch policy module (any policy; the CPU tests): evaluated only on the envs that wait (their count is
+  known on the host from the previous pass), one host sync per pass.
+The epoch's paths (get_epoch_paths, as MdpPathCollector's, path_collector.py:77-78) feed
 eval_util.get_generic_path_information (Rewards/Returns/Actions/Num Paths/Average Returns).
 
 Shared envs (quirk Q10, run/ast-sac_runner.py:113-114): the reference's exploration and evaluation
@@ -22,6 +29,7 @@ last driven by the other one resets every env first (the reference starts every 
 rollout_functions.py:100-106) and starts all its episodes afresh; the library's reset keeps the SBMPC
 memory, as the reference's does.
 """
+import math
 import warnings
 from collections import OrderedDict, deque
 
@@ -34,7 +42,7 @@ from ...core.eval_util import create_stats_ordered_dict
 
 class BatchedPathCollector:
     def __init__(self, env, policy, max_path_length=9, max_ticks=64, deterministic=False,
-                 max_num_epoch_paths_saved=None):
+                 max_num_epoch_paths_saved=None, device_policy=None, use_graph=None, path_ring=None):
         self._env = env                       # BatchedNormalizedBoxEnv
         self._policy = policy
         self.max_path_length = int(max_path_length)
@@ -43,6 +51,12 @@ class BatchedPathCollector:
         N = env.n_envs
         dev = env.device
         self.N, self.device = N, dev
+        self._device_policy = device_policy
+        if device_policy is not None:
+            device_policy.reserve(N)
+        self.use_graph = (device_policy is not None and dev.type == "cuda") if use_graph is None else bool(use_graph)
+        if self.use_graph and device_policy is None:
+            raise ValueError("graph-captured passes need a device_policy (the torch-policy path syncs per pass)")
         self._obs = env.reset().clone()                           # (N, 8) obs at the pending decision
         self._base_env().__dict__["_batched_collector_owner"] = id(self)
         self._act = torch.zeros((N, 1), dtype=torch.float32, device=dev)
@@ -53,7 +67,7 @@ class BatchedPathCollector:
         self._out = dict(obs=torch.empty((N, 8), dtype=torch.float32, device=dev), reward=f(torch.float64),
                          done=f(torch.uint8), events=f(torch.int32), ticks=f(torch.int32), ready=f(torch.uint8))
         self._obs_reset = torch.empty((N, 8), dtype=torch.float32, device=dev)
-        # device-side counters (read by get_diagnostics only)
+        # device-side counters (read by get_diagnostics / collect's occasional checks)
         self._steps_total = torch.zeros((), dtype=torch.int64, device=dev)
         self._paths_total = torch.zeros((), dtype=torch.int64, device=dev)
         self._ticks_total = torch.zeros((), dtype=torch.int64, device=dev)
@@ -67,6 +81,14 @@ class BatchedPathCollector:
         self._path_ev = torch.zeros((N, T), dtype=torch.int32, device=dev)
         self._rows = torch.arange(N, device=dev)
         self._trace_idx = None                                    # see trace()
+        # ended episodes of the current collect (record_paths): a device ring, copied out once per collect
+        self._ring_cap = int(path_ring) if path_ring else max(4096, 4 * N)
+        self._ring_len = torch.zeros(self._ring_cap + 1, dtype=torch.int32, device=dev)   # + one spare row
+        self._ring_rew = torch.zeros((self._ring_cap + 1, T), dtype=torch.float64, device=dev)
+        self._ring_act = torch.zeros((self._ring_cap + 1, T), dtype=torch.float32, device=dev)
+        self._ring_ev = torch.zeros((self._ring_cap + 1, T), dtype=torch.int32, device=dev)
+        self._ring_top = torch.zeros((), dtype=torch.int64, device=dev)   # episodes written since the collect began
+        self._graphs = {}
 
     def _base_env(self):
         e = self._env
@@ -81,17 +103,18 @@ class BatchedPathCollector:
         if base.__dict__.get("_batched_collector_owner") == id(self):
             return
         base.__dict__["_batched_collector_owner"] = id(self)
-        self._obs = self._env.reset().clone()
+        self._obs.copy_(self._env.reset())
         self._awaiting.fill_(True)
         self._path_len.zero_()
         self._ret.zero_()
         self._n_awaiting = self.N
 
     def trace(self, env_indices):
-        """Record every decision of the given envs (test / audit hook: one small host copy per pass).
-        trace_log()[j] lists env_indices[j]'s decisions in order as dicts: episode, decision, action
-        (the policy's normalized action), obs (next observation), reward (the env's, unscaled),
-        done, events, ticks (the decision's ticks summed over the slices it took)."""
+        """Record every decision of the given envs (test / audit hook: one small host copy per pass, so
+        passes are not graph-captured while tracing). trace_log()[j] lists env_indices[j]'s decisions in
+        order as dicts: episode, decision, action (the policy's normalized action), obs (next observation),
+        reward (the env's, unscaled), done, events, ticks (the decision's ticks summed over the slices it
+        took)."""
         self._trace_idx = torch.as_tensor(env_indices, dtype=torch.long, device=self.device)
         self._trace_log = [[] for _ in range(len(env_indices))]
         self._trace_ticks = np.zeros(len(env_indices), dtype=np.int64)
@@ -127,19 +150,25 @@ class BatchedPathCollector:
             return dist.mle_estimate() if hasattr(dist, "mle_estimate") else dist.sample()
         return dist.sample()
 
-    @torch.no_grad()
-    def step(self, replay_buffer=None):
-        """One sliced pass over all envs. Returns (ready mask, #transitions) as device tensors."""
+    def _choose_actions(self):
+        if self._device_policy is not None:  # every row evaluated, kept where the env waits (in-kernel mask)
+            self._device_policy.act(self._obs, self._awaiting, self._act)
+            return
         k = self._n_awaiting
         if k is None:  # count unknown (step() called on its own): evaluate everywhere, keep the awaiting rows
             new_a = self._actions(self._obs)
             self._act = torch.where(self._awaiting.unsqueeze(1), new_a.to(torch.float32), self._act)
         elif k == self.N:
-            self._act = self._actions(self._obs).to(torch.float32)
+            self._act.copy_(self._actions(self._obs).to(torch.float32))
         elif k > 0:
             idx = torch.nonzero_static(self._awaiting, size=k).squeeze(1)
             self._act.index_copy_(0, idx, self._actions(self._obs.index_select(0, idx)).to(torch.float32))
-        self._n_awaiting = None
+
+    @torch.no_grad()
+    def _pass(self, replay_buffer, record):
+        """One sliced pass over all envs, device work only (graph-capturable with a device policy).
+        Returns the transitions of this pass as a device scalar."""
+        self._choose_actions()
         out = self._env.step_async(self._act, max_ticks=self.max_ticks, out=self._out)
         ready = out["ready"].bool()
         done = out["done"].bool()
@@ -159,8 +188,18 @@ class BatchedPathCollector:
         self._ret += torch.where(good, rew, torch.zeros_like(rew))
         self._nonfinite_total += (ready & nonfinite).sum()
         end = ready & (done | nonfinite | (self._path_len >= self.max_path_length))
-        self._obs = torch.where(ready.unsqueeze(1), out["obs"], self._obs)
-        self._awaiting = ready.clone()
+        if record:  # ended episodes with at least one transition -> the ring (prefix-sum scatter, as add_batch)
+            keep = end & (self._path_len > 0)
+            k64 = keep.to(torch.int64)
+            slot = (torch.cumsum(k64, 0) - k64 + self._ring_top) % self._ring_cap
+            idx = torch.where(keep, slot, torch.full_like(slot, self._ring_cap))
+            self._ring_len.index_copy_(0, idx, self._path_len)
+            self._ring_rew.index_copy_(0, idx, self._path_rew)
+            self._ring_act.index_copy_(0, idx, self._path_act)
+            self._ring_ev.index_copy_(0, idx, self._path_ev)
+            self._ring_top += k64.sum()
+        self._obs.copy_(torch.where(ready.unsqueeze(1), out["obs"], self._obs))
+        self._awaiting.copy_(ready)
         n_ready = good.sum()
         self._steps_total += n_ready
         self._paths_total += end.sum()
@@ -171,23 +210,88 @@ class BatchedPathCollector:
             self._trace_pass(out, end)
         # masked auto-reset of finished episodes
         self._env.reset(mask=end.to(torch.uint8), obs_out=self._obs_reset)
-        self._obs = torch.where(end.unsqueeze(1), self._obs_reset, self._obs)
+        self._obs.copy_(torch.where(end.unsqueeze(1), self._obs_reset, self._obs))
         self._path_len.masked_fill_(end, 0)
         self._ret.masked_fill_(end, 0.0)
-        return ready, n_ready
+        return n_ready
+
+    def step(self, replay_buffer=None):
+        """One sliced pass over all envs (eager). Returns (ready mask, #transitions) as device tensors."""
+        n = self._pass(replay_buffer, False)
+        self._n_awaiting = None
+        return self._awaiting, n
+
+    def _graph_pass(self, replay_buffer, record):
+        key = (id(replay_buffer) if replay_buffer is not None else None, bool(record), self.max_ticks)
+        g = self._graphs.get(key)
+        if g is None:
+            # one eager pass on a side stream (allocations, library scratch), then the capture
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._pass(replay_buffer, record)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._pass(replay_buffer, record)
+            self._graphs[key] = g
+            return  # the capture did not run the pass; the eager one did
+        g.replay()
 
     def collect(self, num_steps, replay_buffer=None, record_paths=False):
-        """Advance until ≥ num_steps transitions were produced (host sync once per pass)."""
+        """Advance until ≥ num_steps transitions were produced. Device-policy collectors replay the
+        graph-captured pass and read the transition count on the host only between batches of passes
+        (planned from the count per pass so far); torch-policy collectors sync once per pass."""
         self._take_over()
-        got = 0
-        while got < num_steps:
-            _, n = self.step(replay_buffer)
-            self._n_awaiting = int(n.item())
-            got += self._n_awaiting
-            if record_paths:
-                self._record_ended()
+        record = bool(record_paths)
+        if record:
+            self._ring_top.zero_()
+        if self._device_policy is None or self._trace_idx is not None:
+            got = 0
+            while got < num_steps:
+                n = self._pass(replay_buffer, record)
+                self._n_awaiting = int(n.item())
+                got += self._n_awaiting
+        else:
+            start = int(self._steps_total.item())
+            got, passes, batch = 0, 0, 1
+            while got < num_steps:
+                for _ in range(batch):
+                    if self.use_graph:
+                        self._graph_pass(replay_buffer, record)
+                    else:
+                        self._pass(replay_buffer, record)
+                passes += batch
+                got = int(self._steps_total.item()) - start
+                per = max(got / passes, 1.0)
+                batch = max(1, math.ceil((num_steps - got) / per))
+            self._n_awaiting = None
+        if record:
+            self._drain_ring()
         self.check_nonfinite()
         return got
+
+    def _drain_ring(self):
+        """The episodes that ended during this collect -> reference path dicts (rollout_functions.py:161-181:
+        rewards and actions (T, 1), terminals, env_infos with the reference's keys), one host copy."""
+        top = int(self._ring_top.item())
+        n = min(top, self._ring_cap)
+        if n == 0:
+            return
+        order = [(top - n + j) % self._ring_cap for j in range(n)]  # oldest first
+        sel = torch.as_tensor(order, dtype=torch.long, device=self.device)
+        lens = self._ring_len[sel].cpu().numpy()
+        rews = self._ring_rew[sel].cpu().numpy()
+        acts = self._ring_act[sel].cpu().numpy()
+        evs = self._ring_ev[sel].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        for L, r, a, ev in zip(lens, rews, acts, evs):
+            L = int(L)
+            ev = ev[:L]
+            infos = [dict(terminal=bool(x & abi.EV_TERMINAL), test_ship_stop=bool(x & abi.EV_TEST_STOP),
+                          obs_ship_stop=bool(x & abi.EV_OBS_STOP)) for x in ev]
+            self._epoch_paths.append(dict(rewards=r[:L, None].copy(), actions=a[:L, None].copy(),
+                                          terminals=np.array([[i["terminal"]] for i in infos]),
+                                          env_infos=infos, agent_infos=[{} for _ in range(L)]))
 
     def check_nonfinite(self):
         """Warn (once per occurrence) when env decisions ended on a non-finite ship state since the last
@@ -201,25 +305,6 @@ class BatchedPathCollector:
         except ShipSimNonFiniteError as e:
             warnings.warn(f"BatchedPathCollector: {e} (transitions dropped from the replay buffer and paths)",
                           RuntimeWarning, stacklevel=2)
-
-    def _record_ended(self):
-        """The episodes that ended in the last pass -> reference path dicts (rollout_functions.py:161-181:
-        rewards and actions (T, 1), terminals, env_infos with the reference's keys)."""
-        e = self._last_end  # the per-episode buffers keep those rows until the next pass writes them
-        lens = self._last_end_len[e].cpu().numpy()
-        if lens.size == 0:
-            return
-        rews = self._path_rew[e].cpu().numpy()
-        acts = self._path_act[e].cpu().numpy()
-        evs = self._path_ev[e].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
-        for L, r, a, ev in zip(lens, rews, acts, evs):
-            L = int(L)
-            ev = ev[:L]
-            infos = [dict(terminal=bool(x & abi.EV_TERMINAL), test_ship_stop=bool(x & abi.EV_TEST_STOP),
-                          obs_ship_stop=bool(x & abi.EV_OBS_STOP)) for x in ev]
-            self._epoch_paths.append(dict(rewards=r[:L, None].copy(), actions=a[:L, None].copy(),
-                                          terminals=np.array([[i["terminal"]] for i in infos]),
-                                          env_infos=infos, agent_infos=[{} for _ in range(L)]))
 
     # reference collector surface -------------------------------------------------------------
     def get_epoch_paths(self):

@@ -58,7 +58,7 @@ class FusedSACTrainer(TorchTrainer):
                  policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None, soft_target_tau=1e-2, target_update_period=1,
                  plotter=None, render_eval_paths=False, use_automatic_entropy_tuning=True, target_entropy=None,
                  action_reg_coeff=None, clip_val=np.inf, batch_size=256, use_graph=None, process_group=None,
-                 backend=None, split_update=None):
+                 backend=None, split_update=None, persistent_kernel=None):
         super().__init__()
         if target_update_period != 1:
             raise NotImplementedError("FusedSACTrainer soft-updates every step (runner: target_update_period=1)")
@@ -87,6 +87,8 @@ class FusedSACTrainer(TorchTrainer):
         # Default: whenever world > 1; split_update=True forces it on one rank too (the all-reduce then runs
         # over a world-size-1 group: the same code path as N ranks, an identity on the values)
         self.split = (self.world > 1) if split_update is None else bool(split_update)
+        # hip backend: the grad step as one persistent launch (libsacfused step_kernel 1) or five launches
+        self.persistent_kernel = True if persistent_kernel is None else bool(persistent_kernel)
 
         self.pi_params = ([self.log_alpha] if use_automatic_entropy_tuning else []) + list(policy.parameters())
         self.q_params = list(qf1.parameters()) + list(qf2.parameters())
@@ -177,7 +179,7 @@ class FusedSACTrainer(TorchTrainer):
         self._sf = SacFused(obs_dim, H, self.batch_size, dev, self.discount, self.reward_scale, self.soft_target_tau,
                             self.action_reg_coeff, self.clip_val, float(self.target_entropy), policy_lr, qf_lr,
                             auto_entropy=self.use_automatic_entropy_tuning, world_size=self.world,
-                            split_update=self.split)
+                            split_update=self.split, persistent=self.persistent_kernel)
         if self._sf.n_params != flat.numel() or self._sf.n_targets != tflat.numel():
             raise RuntimeError("hip backend: flat layout mismatch")
         self._stats_t = torch.zeros(self._sf.n_stats, device=dev)
@@ -467,6 +469,16 @@ class FusedSACTrainer(TorchTrainer):
                 for p in self.pi_params + self.q_params + self.t_params:
                     torch.distributed.broadcast(p.data, src, group=self.pg)
 
+    def device_policy(self, deterministic=False, seed=None):
+        """The collector's policy on the matrix cores (hip backend): DevicePolicy.act(obs, mask, out) writes
+        TanhGaussianPolicy samples (or MakeDeterministic's tanh(mean)) of the trainer's CURRENT parameters
+        for every row whose mask is set, with no host sync (graph-capturable). Same math as
+        `policy(obs)` + sample(), fp32 with the kernels' accumulation order."""
+        if self.backend != "hip":
+            raise ValueError("device_policy needs the hip backend")
+        s = int(torch.randint(0, 2 ** 62, (1,)).item()) if seed is None else int(seed)
+        return DevicePolicy(self._sf, deterministic, s, self.device)
+
     def get_diagnostics(self):
         stats = super().get_diagnostics()
         stats.update(self.eval_statistics)
@@ -486,3 +498,28 @@ class FusedSACTrainer(TorchTrainer):
     def get_snapshot(self):
         return dict(policy=self.policy, qf1=self.qf1, qf2=self.qf2, target_qf1=self.target_qf1,
                     target_qf2=self.target_qf2)
+
+
+class DevicePolicy:
+    """Policy actions through libsacfused's sacf_policy_act (see FusedSACTrainer.device_policy)."""
+
+    def __init__(self, sf, deterministic, seed, device):
+        self._sf, self.deterministic, self.seed = sf, bool(deterministic), seed
+        self.counter = torch.zeros(1, dtype=torch.int64, device=device)  # Philox counter, advanced per call
+        self._n = 0
+
+    def reserve(self, n):
+        if n > self._n:
+            self._sf.policy_reserve(n)
+            self._n = n
+
+    def act(self, obs, mask, out, eps_out=None):
+        """out[i] = action of obs[i] where mask[i] (uint8 / bool tensor or None), on the current stream."""
+        if obs.shape[0] > self._n:
+            raise RuntimeError("DevicePolicy.reserve(n) first (outside any graph capture)")
+        m = None if mask is None else (mask if mask.dtype == torch.uint8 else mask.view(torch.uint8))
+        self._sf.set_stream()
+        self._sf.policy_act(obs, out, mask=m, deterministic=self.deterministic, seed=self.seed,
+                            counter=self.counter, eps_out=eps_out)
+        if not self.deterministic:
+            self.counter.add_(1)

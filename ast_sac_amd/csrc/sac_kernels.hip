@@ -412,15 +412,14 @@ __device__ __forceinline__ int64_t batch_item(const MArgs& a, int r, float& e0, 
 
 // grid (2B / 32, H / 32): rows [0, B) are the obs rows, [B, 2B) the next_obs rows of the batch
 template <int H>
-__global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
-  __shared__ float lds[kLdsFloats];
+__device__ __forceinline__ void actor_fwd_tile(const MArgs& a, int bx, int by, float* lds) {
   SAC_T(0, 0);
   SAC_SPAN_BEGIN(0);
   const Layout& L = a.L;
   const int O = L.O, B = L.B;
   const float* P = a.params;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
-  const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
+  const int r0 = bx * kTile2, c0 = by * kTile2;
   constexpr int n2 = H / 8;
   const int kb = w * (H / 4) + h * n2;
   // the batch gather first: its chain (step / size -> Philox -> replay row) is the longest of the
@@ -445,7 +444,7 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
   if (w == 0 && h == 0)
     for (int m = 0; m < O; ++m) lx[(lane & 31) * (kXLd + 1) + m] = x[m];
-  if (blockIdx.y == 0 && w == 0 && h == 0) {  // the gathered batch for the later kernels
+  if (by == 0 && w == 0 && h == 0) {  // the gathered batch for the later kernels
     float* xd = (nrow ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
     for (int m = 0; m < kXLd; ++m) xd[m] = x[m];
     if (!nrow) {
@@ -462,7 +461,7 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   SAC_T(0, 2);
   // h1 for this lane's k (fmaf chain from the bias, as fc0 computes it)
   first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O, kb, av);
-  if (blockIdx.y == 0 && r0 < B) store_operands<H>(a.sc.a_h1 + (int64_t)r0 * H, lds, av, kb);  // block-uniform
+  if (by == 0 && r0 < B) store_operands<H>(a.sc.a_h1 + (int64_t)r0 * H, lds, av, kb);  // block-uniform
   SAC_T(0, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
@@ -476,12 +475,19 @@ __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
     // this column block's part of the mean / log_std heads of row r (rows [0, 2B))
     const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
     if (cc == 0) {
-      a.ms.hpart[(int64_t)blockIdx.y * 2 * B + r] = pm;
-      a.ms.hpart[(int64_t)(CB + blockIdx.y) * 2 * B + r] = ps;
+      a.ms.hpart[(int64_t)by * 2 * B + r] = pm;
+      a.ms.hpart[(int64_t)(CB + by) * 2 * B + r] = ps;
     }
   });
   SAC_T(0, 5);
   SAC_SPAN_END(0);
+}
+
+
+template <int H>
+__global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
+  __shared__ float lds[kLdsFloats];
+  actor_fwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
 }
 
 // TanhNormal.rsample_and_logprob (distributions.py:346-392) of one row's head
@@ -500,8 +506,7 @@ __device__ __forceinline__ void tanh_normal(float mean, float ls_raw, float eps,
 
 // grid (row tiles of [Q1: 2B | Q2: 2B | T1: B | T2: B], H / 32). Q rows [0, B): (obs, ã), [B, 2B): (obs, a)
 template <int H>
-__global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
-  __shared__ float lds[kLdsFloats];
+__device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, float* lds) {
   SAC_T(1, 0);
   SAC_SPAN_BEGIN(1);
   const Layout& L = a.L;
@@ -509,19 +514,19 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   const float* P = a.params;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int qt = 2 * B / kTile2, tt = B / kTile2;  // row tiles per critic / per target critic
-  int net, rt = blockIdx.x;
+  int net, rt = bx;
   if (rt < 2 * qt) { net = rt / qt; rt %= qt; }
   else { rt -= 2 * qt; net = 2 + rt / tt; rt %= tt; }
   const bool is_t = net >= 2;
   const float* C = is_t ? a.targets + (int64_t)(net - 2) * L.q_size : P + L.q_base[net];
-  const int r0 = rt * kTile2, c0 = blockIdx.y * kTile2;
+  const int r0 = rt * kTile2, c0 = by * kTile2;
   constexpr int n2 = H / 8;
   constexpr int CB = H / kTile2;
   const int kb = w * (H / 4) + h * n2;
   const int row = r0 + (lane & 31);
   const bool data = !is_t && row >= B;  // (obs, a) row (block-uniform: B is a multiple of 32)
   const int item = data ? row - B : row;
-  const bool store_rows = blockIdx.y == 0 && w == 0 && h == 0;
+  const bool store_rows = by == 0 && w == 0 && h == 0;
   // the row's inputs first — observation, actor-head partials (or the replayed action), noise — as
   // they end the prologue's longest chain; vector loads complete in issue order, so the staging loads
   // below queue behind them instead of delaying them. Every load is issued unconditionally (the
@@ -581,7 +586,7 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   }
   __syncthreads();
   first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O + 1, kb, av);
-  if (blockIdx.y == 0 && !is_t) {  // block-uniform
+  if (by == 0 && !is_t) {  // block-uniform
     if (data && w == 0 && h == 0)
 #pragma unroll
       for (int m = 0; m < kXLd; ++m) a.sc.q_x[net][(int64_t)item * kXLd + m] = m < O ? xin[m] : (m == O ? act : 0.0f);
@@ -598,16 +603,22 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
     else if (r >= B) a.sc.q_g2[net][(int64_t)(r - B) * H + col] = y;
     else a.ms.g2pi[net][(int64_t)r * H + col] = y;
     const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
-    if (cc == 0) a.ms.qpart[((int64_t)net * CB + blockIdx.y) * 2 * B + r] = pq;
+    if (cc == 0) a.ms.qpart[((int64_t)net * CB + by) * 2 * B + r] = pq;
   });
   SAC_T(1, 5);
   SAC_SPAN_END(1);
 }
 
+
+template <int H>
+__global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
+  __shared__ float lds[kLdsFloats];
+  critic_fwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
+}
+
 // grid (2 critics x 2B / 32 row tiles, H / 32): losses and dq (sac.py:170-247), dg2, dg1 = (dg2 W2) ⊙ [g1 > 0]
 template <int H>
-__global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
-  __shared__ float lds[kLdsFloats];
+__device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, float* lds) {
   SAC_T(2, 0);
   SAC_SPAN_BEGIN(2);
   const Layout& L = a.L;
@@ -616,8 +627,8 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   const float* TG = a.targets;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int qt = 2 * B / kTile2;
-  if ((int)blockIdx.x >= 2 * qt) {  // extra blocks (8, keeping the row-tile -> XCD map of the other kernels):
-    if (blockIdx.x == 2 * qt && blockIdx.y == 0 && threadIdx.x == 0) {  // step t and Adam's bias corrections
+  if ((int)bx >= 2 * qt) {  // extra blocks (8, keeping the row-tile -> XCD map of the other kernels):
+    if (bx == 2 * qt && by == 0 && threadIdx.x == 0) {  // step t and Adam's bias corrections
       const int64_t t = *a.step + 1;            // (only actor_fwd read the old value)
       *const_cast<int64_t*>(a.step) = t;
       const AdamStep st = adam_step(a.hp, t);
@@ -627,9 +638,9 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
     }
     return;
   }
-  const int net = blockIdx.x / qt, rt = blockIdx.x % qt;
+  const int net = bx / qt, rt = bx % qt;
   const float* C = P + L.q_base[net];
-  const int r0 = rt * kTile2, c0 = blockIdx.y * kTile2;
+  const int r0 = rt * kTile2, c0 = by * kTile2;
   constexpr int n2 = H / 8;
   constexpr int CB = H / kTile2;
   const int kb = w * (H / 4) + h * n2;
@@ -665,7 +676,7 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) g1m[q] = g1[(int64_t)finish_row(q) * H + c0 + (lane & 31)];
   }
-  const bool store_rows = net == 0 && blockIdx.y == 0 && w == 0 && h == 0;
+  const bool store_rows = net == 0 && by == 0 && w == 0 && h == 0;
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
   const float invB = 1.0f / (float)B;
@@ -728,7 +739,7 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
     const int j = kb + i;
     av[i] = tg[(lane & 31) * (H + 4) + j] > 0.0f ? dq * lw3[j] : 0.0f;
   }
-  if (data && blockIdx.y == 0) store_operands<H>(a.sc.q_dg2[net] + (int64_t)ib * H, tg, av, kb);  // block-uniform
+  if (data && by == 0) store_operands<H>(a.sc.q_dg2[net] + (int64_t)ib * H, tg, av, kb);  // block-uniform
   SAC_T(2, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
@@ -743,24 +754,30 @@ __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
       const float d = g1m[q] > 0.0f ? v : 0.0f;
       a.ms.dg1pi[net][o] = d;
       const float pa = halfwave_sum(d * wa);  // this column block's part of dQ/dã for row r
-      if (cc == 0) a.ms.apart[((int64_t)net * CB + blockIdx.y) * B + r] = pa;
+      if (cc == 0) a.ms.apart[((int64_t)net * CB + by) * B + r] = pa;
     }
   });
   SAC_T(2, 5);
   SAC_SPAN_END(2);
 }
 
+
+template <int H>
+__global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
+  __shared__ float lds[kLdsFloats];
+  critic_bwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
+}
+
 // grid (B / 32, H / 32): policy backward through the action (obs rows)
 template <int H>
-__global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
-  __shared__ float lds[kLdsFloats];
+__device__ __forceinline__ void actor_bwd_tile(const MArgs& a, int bx, int by, float* lds) {
   SAC_T(3, 0);
   SAC_SPAN_BEGIN(3);
   const Layout& L = a.L;
   const int O = L.O, B = L.B;
   const float* P = a.params;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
-  const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
+  const int r0 = bx * kTile2, c0 = by * kTile2;
   constexpr int n2 = H / 8;
   constexpr int CB = H / kTile2;
   const int kb = w * (H / 4) + h * n2;
@@ -808,7 +825,7 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   const float dmean = gz + ainv * (d / var);
   const float dstd = gz * eps_i + ainv * ((d * d) / (var * std) - 1.0f / std);
   const float dls = (ls_raw >= -20.0f && ls_raw <= 2.0f) ? dstd * std : 0.0f;
-  if (blockIdx.y == 0 && w == 0 && h == 0) {
+  if (by == 0 && w == 0 && h == 0) {
     a.sc.a_dhead[(int64_t)item * 2] = dmean;
     a.sc.a_dhead[(int64_t)item * 2 + 1] = dls;
   }
@@ -819,7 +836,7 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
     const int j = kb + i;
     av[i] = th[(lane & 31) * (H + 4) + j] > 0.0f ? (lwh[j] * dmean + lwh[H + j] * dls) : 0.0f;
   }
-  if (blockIdx.y == 0) store_operands<H>(a.sc.a_dh2 + (int64_t)r0 * H, th, av, kb);
+  if (by == 0) store_operands<H>(a.sc.a_dh2 + (int64_t)r0 * H, th, av, kb);
   SAC_T(3, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
@@ -830,6 +847,13 @@ __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   });
   SAC_T(3, 5);
   SAC_SPAN_END(3);
+}
+
+
+template <int H>
+__global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
+  __shared__ float lds[kLdsFloats];
+  actor_bwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -921,29 +945,42 @@ struct WgArgs {
   ApplyArgs ap;  // (fuse) parameters, optimizer state, targets, transposed copies
 };
 
-__global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
-  __shared__ float lds[4 * 16 * 64];
-  __shared__ WgTable tab;  // one coalesced copy instead of a chain of dependent global loads
-  __shared__ AdamStep sst;
-  {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tab);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&tab);
-    constexpr int kW = (int)(sizeof(WgTable) / 4), kIt = (kW + 255) / 256;
-    uint32_t v[kIt];
+// the weight-gradient kernel's LDS (also one region of the persistent step kernel's)
+struct WgLds {
+  float lds[4 * 16 * 64];
+  WgTable tab;   // one coalesced copy instead of a chain of dependent global loads
+  AdamStep sst;  // this step's Adam bias corrections (critic_bwd wrote them)
+  float red[4][32];
+  float sum[32];
+  float tt[2][kTile][kTile + 1];
+};
+
+// the matrix table and this step's Adam bias corrections into LDS (every thread of the block)
+__device__ __forceinline__ void wgrad_stage(const WgArgs& a, WgLds& S) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tab);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&S.tab);
+  constexpr int kW = (int)(sizeof(WgTable) / 4), kIt = (kW + 255) / 256;
+  uint32_t v[kIt];
 #pragma unroll
-    for (int i = 0; i < kIt; ++i) v[i] = threadIdx.x + i * 256 < kW ? src[threadIdx.x + i * 256] : 0u;
+  for (int i = 0; i < kIt; ++i) v[i] = threadIdx.x + i * 256 < kW ? src[threadIdx.x + i * 256] : 0u;
 #pragma unroll
-    for (int i = 0; i < kIt; ++i)
-      if (threadIdx.x + i * 256 < kW) dst[threadIdx.x + i * 256] = v[i];
-    if (threadIdx.x == 0) sst = AdamStep{a.stats[5], a.stats[6], a.stats[7]};  // (critic_fwd)
-    __syncthreads();
-  }
+  for (int i = 0; i < kIt; ++i)
+    if (threadIdx.x + i * 256 < kW) dst[threadIdx.x + i * 256] = v[i];
+  if (threadIdx.x == 0) S.sst = AdamStep{a.stats[5], a.stats[6], a.stats[7]};
+  __syncthreads();
+}
+
+// block bx of the weight-gradient pass (see above); S staged by wgrad_stage
+__device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
+  float* lds = S.lds;
+  const WgTable& tab = S.tab;
+  const AdamStep& sst = S.sst;
   const int tid = threadIdx.x;
   SAC_T(4, 0);
   SAC_SPAN_BEGIN(4);
-  SAC_TB(4, 6, (int)blockIdx.x == a.n_mfma);
+  SAC_TB(4, 6, (int)bx == a.n_mfma);
   const int n_small_blocks = (a.n_small + 63) / 64;
-  if (tab.has_scalar && (int)blockIdx.x == a.n_mfma + n_small_blocks) {  // scalars
+  if (tab.has_scalar && (int)bx == a.n_mfma + n_small_blocks) {  // scalars
     float v[5] = {0, 0, 0, 0, 0};
     for (int r = tid; r < a.B; r += kThreads) {
       v[0] += a.sc.p_pl[r];
@@ -952,8 +989,8 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
       v[3] += a.sc.p_la[r];
       v[4] += a.sc.p_ga[r];
     }
-    __shared__ float red[4][32];
-    __shared__ float sum[32];
+    float (*red)[32] = S.red;
+    float* sum = S.sum;
     block_sum<5>(v, red, sum);
     if (tid == 0) {
       const float invB = 1.0f / (float)a.B;
@@ -973,9 +1010,9 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
     SAC_SPAN_END(4);
     return;
   }
-  if ((int)blockIdx.x >= a.n_mfma) {  // VALU elements: 64 per block, wave w sums rows [wB/4, (w+1)B/4)
+  if ((int)bx >= a.n_mfma) {  // VALU elements: 64 per block, wave w sums rows [wB/4, (w+1)B/4)
     const int w = tid >> 6;
-    const int64_t e = (int64_t)(blockIdx.x - a.n_mfma) * 64 + (tid & 63);
+    const int64_t e = (int64_t)(bx - a.n_mfma) * 64 + (tid & 63);
     float acc = 0.0f;
     int s = 0;
     int64_t l = 0;
@@ -1001,7 +1038,7 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
         for (int u = 0; u < 32; ++u) acc = fmaf(yv[u], xv[u], acc);
       }
     }
-    SAC_TB(4, 7, (int)blockIdx.x == a.n_mfma);
+    SAC_TB(4, 7, (int)bx == a.n_mfma);
     float* part = lds;  // [4][64]
     part[w * 64 + (tid & 63)] = acc;
     __syncthreads();
@@ -1014,7 +1051,7 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
       a.grads[e] = x.g;
       if (a.fuse) adam_st(a.ap, sst, e, x);
     }
-    SAC_TB(4, 8, (int)blockIdx.x == a.n_mfma);
+    SAC_TB(4, 8, (int)bx == a.n_mfma);
     SAC_SPAN_END(4);
     return;
   }
@@ -1022,11 +1059,11 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
   const WgTable& tb = tab;
   const int H = tb.mats[tb.big[0]].M;
   const int tiles = (H / kTile2) * (H / kTile2);
-  const GMat m = tb.mats[tb.big[blockIdx.x / tiles]];
-  const int t = blockIdx.x % tiles;
+  const GMat m = tb.mats[tb.big[bx / tiles]];
+  const int t = bx % tiles;
   const int j0 = (t / (H / kTile2)) * kTile2, k0 = (t % (H / kTile2)) * kTile2;
   const int w = tid >> 6, lane = tid & 63, h = lane >> 5;
-  const int mat = tb.big_slot[blockIdx.x / tiles];  // 0: actor W2, 1 / 2: Q1 / Q2 W2
+  const int mat = tb.big_slot[bx / tiles];  // 0: actor W2, 1 / 2: Q1 / Q2 W2
   AdamElem x[4];
   if (a.fuse)  // the optimizer state of the four outputs this lane finishes, in flight during the GEMM
 #pragma unroll
@@ -1047,7 +1084,7 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
     mfma_chain(acc, av, bv, n2);
   }
   SAC_T(4, 2);
-  __shared__ float tt[2][kTile][kTile + 1];  // (fuse) updated parameters / targets, transposed
+  auto& tt = S.tt;  // (fuse) updated parameters / targets, transposed
   splitk_finish_q(acc, lds, [&](int q, int rr, int cc, float v) {
     const int64_t e = m.out_off + (int64_t)(j0 + rr) * m.N + k0 + cc;
     a.grads[e] = v;
@@ -1072,6 +1109,115 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
   SAC_SPAN_END(4);
 }
 
+
+__global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
+  __shared__ WgLds S;
+  wgrad_stage(a, S);
+  wgrad_tile(a, blockIdx.x, S);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// One grad step in ONE launch (sacf_config.step_kernel = 1): the five passes above as phases of a
+// persistent kernel, G co-resident blocks (2 per CU) looping over each phase's tiles and meeting at a
+// grid barrier between phases. The tile code, tile order and arithmetic are the five-launch kernels'
+// own (tile t of a phase = (t mod gx, t / gx), the same work), so the results are bit-identical; what
+// goes is four kernel boundaries and their cold prologues (instruction fetch, kernel arguments).
+// ---------------------------------------------------------------------------------------------
+struct PArgs {
+  MArgs m;
+  WgArgs w;
+  unsigned* bar;  // [arrive, generation]: a sense-reversing grid barrier, both back at rest after a launch
+  int* err;       // set when a barrier wait exceeds its bound (blocks not co-resident): results invalid
+};
+
+// Every block arrives once per barrier; the last one to arrive resets the count and advances the
+// generation the others wait on. Writes before the barrier are released device-wide (the L2 of every
+// XCD) and acquired after it. The wait is bounded: a launch whose blocks are not all resident (which
+// the host sizing rules out) ends with *err set instead of hanging the device.
+__device__ __forceinline__ void grid_barrier(unsigned* bar, int* err, unsigned nblocks) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    const unsigned prev = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == nblocks - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned spins = 0;
+      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {
+          atomicOr(err, 1);
+          break;
+        }
+      }
+    }
+    __threadfence();
+  }
+  __syncthreads();
+}
+
+// the kernel's PArgs read through the kernarg segment pointer, laundered: every field is re-read (scalar
+// loads) where a tile uses it instead of ~200 argument dwords held in SGPRs across all five phases
+typedef const __attribute__((address_space(4))) PArgs* PArgsPtr;
+__device__ __forceinline__ const PArgs& persist_args() {
+  PArgsPtr q = (PArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return *(const PArgs*)q;
+}
+
+template <int H>
+__global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg) {
+  (void)p_arg;  // read through persist_args()
+  constexpr int kRaw = (kLdsFloats * 4 > (int)sizeof(WgLds) ? kLdsFloats * 4 : (int)sizeof(WgLds)) / 16;
+  __shared__ float4 raw[kRaw];  // the passes' LDS, then (last phase) the weight-gradient pass's WgLds
+  float* lds = reinterpret_cast<float*>(raw);
+  const int G = gridDim.x, ct = H / kTile2;
+  const int B = persist_args().m.L.B;
+  {  // actor_fwd
+    const int gx = 2 * B / kTile2, nt = gx * ct;
+    for (int t = blockIdx.x; t < nt; t += G) {
+      actor_fwd_tile<H>(persist_args().m, t % gx, t / gx, lds);
+      __syncthreads();
+    }
+  }
+  grid_barrier(persist_args().bar, persist_args().err, G);
+  {  // critic_fwd
+    const int gx = 6 * B / kTile2, nt = gx * ct;
+    for (int t = blockIdx.x; t < nt; t += G) {
+      critic_fwd_tile<H>(persist_args().m, t % gx, t / gx, lds);
+      __syncthreads();
+    }
+  }
+  grid_barrier(persist_args().bar, persist_args().err, G);
+  {  // critic_bwd
+    const int gx = 4 * B / kTile2 + 8, nt = gx * ct;
+    for (int t = blockIdx.x; t < nt; t += G) {
+      critic_bwd_tile<H>(persist_args().m, t % gx, t / gx, lds);
+      __syncthreads();
+    }
+  }
+  grid_barrier(persist_args().bar, persist_args().err, G);
+  {  // actor_bwd
+    const int gx = B / kTile2, nt = gx * ct;
+    for (int t = blockIdx.x; t < nt; t += G) {
+      actor_bwd_tile<H>(persist_args().m, t % gx, t / gx, lds);
+      __syncthreads();
+    }
+  }
+  grid_barrier(persist_args().bar, persist_args().err, G);
+  {  // weight gradients (+ Adam / soft update / W2T when fused)
+    WgLds& S = *reinterpret_cast<WgLds*>(raw);
+    const int nb = persist_args().w.n_blocks;
+    if ((int)blockIdx.x < nb) wgrad_stage(persist_args().w, S);
+    for (int t = blockIdx.x; t < nb; t += G) {
+      wgrad_tile(persist_args().w, t, S);
+      __syncthreads();
+    }
+  }
+}
 
 __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
   __shared__ float tile[2][kTile][kTile + 1];
@@ -1133,6 +1279,104 @@ __global__ void sac_transpose_kernel(const float* params, const float* targets, 
   T[which * HH + (l % L.H) * L.H + l / L.H] = src[l];
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Policy actions for the collector (sacf_policy_act): TanhGaussianPolicy.forward + TanhNormal.sample
+// (gaussian_policy.py:105-118, distributions.py:394-425; MakeDeterministic: tanh(mean), policies/base.py:
+// 54-64) for n observation rows, from the trainer's own parameters and transposed W2 copy.
+//   sac_act_fwd_kernel  : grid (n / 32, H / 32): h1 (VALU), h2 = relu(h1 W2ᵀ + b2) on MFMA, and this column
+//                         block's part of the mean / log_std heads of each row (as actor_fwd's epilogue)
+//   sac_act_head_kernel : per row: the parts summed in block order + biases, log_std clamped, std = exp,
+//                         a = tanh(mean + std·ε) (ε from Philox(seed, counter, row)) or tanh(mean); rows
+//                         whose mask byte is 0 keep their previous action
+// ---------------------------------------------------------------------------------------------
+struct ActArgs {
+  const float* params;
+  const float* T;
+  const float* obs;    // [n][obs_stride]
+  int64_t n;
+  int obs_stride;
+  Layout L;
+  float* hpart;        // [2][H/32][n_pad]
+  int64_t n_pad;
+  const uint8_t* mask;
+  int deterministic;
+  uint64_t seed;
+  const int64_t* counter;
+  float* act;          // [n]
+  float* eps_out;      // [n] or null
+};
+
+template <int H>
+__global__ __launch_bounds__(256) void sac_act_fwd_kernel(ActArgs a) {
+  __shared__ float lds[kLdsFloats];
+  const Layout& L = a.L;
+  const int O = L.O;
+  const float* P = a.params;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  const int r0 = blockIdx.x * kTile2, c0 = blockIdx.y * kTile2;
+  constexpr int n2 = H / 8;
+  const int kb = w * (H / 4) + h * n2;
+  const int64_t row = r0 + (lane & 31);
+  const int64_t rowc = row < a.n ? row : a.n - 1;  // rows past n (last tile) repeat the last row
+  float x[kXLd];
+#pragma unroll
+  for (int m = 0; m < kXLd; ++m) x[m] = m < O ? a.obs[rowc * a.obs_stride + m] : 0.0f;
+  float av[kMaxN2], bv[kMaxN2];
+#pragma unroll
+  for (int i = 0; i < n2; ++i) bv[i] = a.T[(int64_t)(kb + i) * H + c0 + (lane & 31)];  // policy W2ᵀ
+  const float b2c = P[L.p_b2 + c0 + (lane & 31)];
+  const float wm = P[L.p_wm + c0 + (lane & 31)], ws = P[L.p_ws + c0 + (lane & 31)];
+  float* lw1 = lds + kLdsW1Off;
+  float* lx = lds + kLdsXOff;
+  stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
+  if (w == 0 && h == 0)
+    for (int m = 0; m < O; ++m) lx[(lane & 31) * (kXLd + 1) + m] = x[m];
+  __syncthreads();
+  first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O, kb, av);
+  f32x16 acc = zero16();
+  mfma_chain(acc, av, bv, n2);
+  constexpr int CB = H / kTile2;
+  splitk_finish(acc, lds, [&](int rr, int cc, float v) {
+    const float y = relu(v + b2c);
+    const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
+    if (cc == 0) {
+      a.hpart[(int64_t)blockIdx.y * a.n_pad + r0 + rr] = pm;
+      a.hpart[(int64_t)(CB + blockIdx.y) * a.n_pad + r0 + rr] = ps;
+    }
+  });
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void sac_act_head_kernel(ActArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.n) return;
+  constexpr int CB = H / kTile2;
+  const float* P = a.params;
+  const float mean = sum_parts<CB>(a.hpart, a.n_pad, r) + P[a.L.p_bm];
+  const float ls = sum_parts<CB>(a.hpart + CB * a.n_pad, a.n_pad, r) + P[a.L.p_bs];
+  float eps = 0.0f;
+  if (!a.deterministic) {
+    const uint64_t ctr = a.counter ? (uint64_t)*a.counter : 0;
+    uint32_t c[4] = {(uint32_t)r, (uint32_t)ctr, (uint32_t)(ctr >> 32), 0xAC70u};
+    philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+    const float u1 = ((float)c[0] + 1.0f) * 2.3283064365386963e-10f;
+    const float u2 = (float)c[1] * 2.3283064365386963e-10f;
+    eps = sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+  }
+  const float log_std = fminf(fmaxf(ls, -20.0f), 2.0f);
+  const float z = a.deterministic ? mean : mean + expf(log_std) * eps;
+  if (a.eps_out) a.eps_out[r] = eps;
+  if (a.mask && !a.mask[r]) return;
+  a.act[r] = tanhf(z);
+}
+
+template <int H>
+void launch_act(const ActArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(sac_act_fwd_kernel<H>, dim3((unsigned)(a.n_pad / kTile2), H / kTile2), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(sac_act_head_kernel<H>, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
+}
+
 // the four forward/backward passes of one grad step for hidden width H (a compile-time tile count)
 template <int H>
 void launch_passes(const MArgs& a, hipStream_t st, int part) {
@@ -1146,6 +1390,29 @@ void launch_passes(const MArgs& a, hipStream_t st, int part) {
   } else {
     hipLaunchKernelGGL(sac_actor_bwd_kernel<H>, dim3(B / kTile2, ct), dim3(256), 0, st, a);
   }
+}
+
+template <int H>
+hipError_t occupancy_of(int* per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, sac_step_persistent_kernel<H>, 256, 0);
+}
+hipError_t persistent_occupancy(int H, int* per_cu) {
+  switch (H) {
+    case 32: return occupancy_of<32>(per_cu);
+    case 64: return occupancy_of<64>(per_cu);
+    case 96: return occupancy_of<96>(per_cu);
+    case 128: return occupancy_of<128>(per_cu);
+    case 160: return occupancy_of<160>(per_cu);
+    case 192: return occupancy_of<192>(per_cu);
+    case 224: return occupancy_of<224>(per_cu);
+    case 256: return occupancy_of<256>(per_cu);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int H>
+void launch_persistent(const PArgs& p, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(sac_step_persistent_kernel<H>, dim3(grid), dim3(256), 0, st, p);
 }
 
 }  // namespace
@@ -1171,6 +1438,10 @@ struct sacf_handle {
   MScratch ms;
   WgArgs wg[1];       // weight gradients (+ losses, log α, and the update when world_size == 1)
   WgTable* wtab[1];
+  float* act_part;      // sacf_policy_act head partials [2][H/32][act_cap]
+  int64_t act_cap;
+  unsigned* bar;        // step_kernel 1: grid barrier [arrive, generation] + error flag (int) after them
+  int grid;             // step_kernel 1: co-resident blocks of the persistent kernel
   char err[512];
 };
 
@@ -1368,6 +1639,22 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     wg.sc = sc;
     wg.hp = h->hp;
   }
+  if (cfg->step_kernel == 1) {  // persistent single-launch step: barrier state and a co-resident grid
+    e = hipMalloc(&h->bar, 4 * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(h->bar, 0, 4 * sizeof(unsigned));
+    int per_cu = 0, cus = 0;
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e == hipSuccess) e = persistent_occupancy(H, &per_cu);
+    if (e != hipSuccess) {
+      *out = h;
+      return sfail(h, SACF_EHIP, "persistent step kernel: %s", hipGetErrorString(e));
+    }
+    h->grid = (per_cu >= 2 ? 2 : per_cu) * cus / 8 * 8;  // a multiple of 8: tile t stays on XCD t % 8
+    if (h->grid < 8) {
+      *out = h;
+      return sfail(h, SACF_EINVAL, "persistent step kernel: %d blocks per CU", per_cu);
+    }
+  }
   *out = h;
   return SACF_OK;
 }
@@ -1378,6 +1665,8 @@ int sacf_destroy(sacf_handle* h) {
   if (h->scratch) (void)hipFree(h->scratch);
   if (h->T) (void)hipFree(h->T);
   if (h->wtab[0]) (void)hipFree(h->wtab[0]);
+  if (h->act_part) (void)hipFree(h->act_part);
+  if (h->bar) (void)hipFree(h->bar);
   delete h;
   return SACF_OK;
 }
@@ -1394,6 +1683,17 @@ int sacf_debug_stamps(unsigned long long* out64) {
 #endif
 
 const char* sacf_last_error(const sacf_handle* h) { return h ? h->err : "null handle"; }
+
+int sacf_step_kernel_status(sacf_handle* h) {
+  if (!h) return SACF_EINVAL;
+  if (!h->bar) return SACF_OK;
+  SDev g(h->device);
+  int flag = 0;
+  hipError_t e = hipMemcpy(&flag, h->bar + 2, sizeof(int), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return sfail(h, SACF_EHIP, "sacf_step_kernel_status: %s", hipGetErrorString(e));
+  return flag ? sfail(h, SACF_ESTATE, "persistent step kernel: a grid barrier wait timed out (results invalid)")
+              : SACF_OK;
+}
 int64_t sacf_param_count(const sacf_handle* h) { return h ? h->L.n_params : -1; }
 int64_t sacf_target_count(const sacf_handle* h) { return h ? h->L.n_targets : -1; }
 int64_t sacf_stats_count(const sacf_handle* h) { return h ? 8 + 6 * (int64_t)h->L.B : -1; }
@@ -1503,8 +1803,6 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   a.L = h->L;
   a.hp = h->hp;
   SDev g(h->device);
-  if (!launch_hidden(h->L.H, a, h->stream, 0)) return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);
-  launch_hidden(h->L.H, a, h->stream, 1);
   WgArgs& w = h->wg[0];
   w.grads = h->grads;
   w.params = h->params;
@@ -1512,6 +1810,28 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   w.stats = h->stats;
   w.fuse = h->cfg.world_size == 1 && !h->cfg.split_update;  // no all-reduce in between: apply in the same kernel
   w.ap = apply_args(h);
+  if (h->cfg.step_kernel == 1) {  // the whole step in one launch
+    PArgs p;
+    p.m = a;
+    p.w = w;
+    p.bar = h->bar;
+    p.err = reinterpret_cast<int*>(h->bar + 2);
+    switch (h->L.H) {
+      case 32: launch_persistent<32>(p, h->grid, h->stream); break;
+      case 64: launch_persistent<64>(p, h->grid, h->stream); break;
+      case 96: launch_persistent<96>(p, h->grid, h->stream); break;
+      case 128: launch_persistent<128>(p, h->grid, h->stream); break;
+      case 160: launch_persistent<160>(p, h->grid, h->stream); break;
+      case 192: launch_persistent<192>(p, h->grid, h->stream); break;
+      case 224: launch_persistent<224>(p, h->grid, h->stream); break;
+      case 256: launch_persistent<256>(p, h->grid, h->stream); break;
+      default: return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
+  }
+  if (!launch_hidden(h->L.H, a, h->stream, 0)) return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);
+  launch_hidden(h->L.H, a, h->stream, 1);
   hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_blocks), dim3(256), 0, h->stream, w);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
@@ -1528,6 +1848,48 @@ int sacf_apply(sacf_handle* h) {
                      dim3(kThreads), 0, h->stream, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_apply: %s", hipGetErrorString(e));
+}
+
+int sacf_policy_reserve(sacf_handle* h, int64_t n) {
+  if (!h || n < 1) return sfail(h, SACF_EINVAL, "sacf_policy_reserve: bad argument");
+  const int64_t n_pad = (n + kTile2 - 1) / kTile2 * kTile2;
+  if (n_pad <= h->act_cap) return SACF_OK;
+  SDev g(h->device);
+  if (h->act_part) (void)hipFree(h->act_part);
+  h->act_part = nullptr;
+  h->act_cap = 0;
+  hipError_t e = hipMalloc(&h->act_part, sizeof(float) * 2 * (size_t)(h->L.H / kTile2) * n_pad);
+  if (e != hipSuccess) return sfail(h, SACF_EHIP, "sacf_policy_reserve: %s", hipGetErrorString(e));
+  h->act_cap = n_pad;
+  return SACF_OK;
+}
+
+int sacf_policy_act(sacf_handle* h, const float* obs, int64_t n, int32_t obs_stride, const uint8_t* mask,
+                    int32_t deterministic, uint64_t seed, const int64_t* counter, float* act, float* eps_out) {
+  if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_policy_act: buffers not bound");
+  if (!obs || !act || n < 1 || obs_stride < h->L.O) return sfail(h, SACF_EINVAL, "sacf_policy_act: bad argument");
+  const int64_t n_pad = (n + kTile2 - 1) / kTile2 * kTile2;
+  if (n_pad > h->act_cap)
+    return sfail(h, SACF_ESTATE, "sacf_policy_act: %lld rows need sacf_policy_reserve first", (long long)n);
+  ActArgs a;
+  memset(&a, 0, sizeof(a));
+  a.params = h->params; a.T = h->T; a.obs = obs; a.n = n; a.obs_stride = obs_stride; a.L = h->L;
+  a.hpart = h->act_part; a.n_pad = n_pad; a.mask = mask; a.deterministic = deterministic;
+  a.seed = seed; a.counter = counter; a.act = act; a.eps_out = eps_out;
+  SDev g(h->device);
+  switch (h->L.H) {
+    case 32: launch_act<32>(a, h->stream); break;
+    case 64: launch_act<64>(a, h->stream); break;
+    case 96: launch_act<96>(a, h->stream); break;
+    case 128: launch_act<128>(a, h->stream); break;
+    case 160: launch_act<160>(a, h->stream); break;
+    case 192: launch_act<192>(a, h->stream); break;
+    case 224: launch_act<224>(a, h->stream); break;
+    case 256: launch_act<256>(a, h->stream); break;
+    default: return sfail(h, SACF_EINVAL, "sacf_policy_act: hidden %d", h->L.H);
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_policy_act: %s", hipGetErrorString(e));
 }
 
 }  // extern "C"

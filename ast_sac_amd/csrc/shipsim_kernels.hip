@@ -2582,6 +2582,12 @@ int shipsim_destroy(shipsim_handle* h) {
 }
 
 const char* shipsim_last_error(const shipsim_handle* h) { return h ? h->err : g_create_err; }
+
+int shipsim_set_stream(shipsim_handle* h, void* stream) {
+  if (!h) return SHIPSIM_EINVAL;
+  h->stream = (hipStream_t)stream;
+  return SHIPSIM_OK;
+}
 int32_t shipsim_num_envs(const shipsim_handle* h) { return h ? h->P.n_envs : -1; }
 int32_t shipsim_lanes_per_env(const shipsim_handle* h) { return h ? h->lpe : -1; }
 

@@ -155,10 +155,6 @@ def experiment_device(variant, args, device, process_group=None):
     act_dim = expl_env.action_space.low.size
     policy, (qf1, qf2, tq1, tq2) = _networks(obs_dim, act_dim, variant["layer_size"], device)
     ak = variant["algorithm_kwargs"]
-    expl_coll = BatchedPathCollector(expl_env, policy, max_path_length=ak["max_path_length"],
-                                     max_ticks=args.slice_ticks)
-    eval_coll = BatchedPathCollector(eval_env, MakeDeterministic(policy), max_path_length=ak["max_path_length"],
-                                     max_ticks=args.slice_ticks, deterministic=True)
     rb = DeviceReplayBuffer(variant["replay_buffer_size"], obs_dim, act_dim, device)
     # --batch_size is the GLOBAL batch (the reference's 256, run/ast-sac_runner.py:55): each of the
     # `world` ranks samples batch_size / world rows from its own buffer shard and the averaged
@@ -170,6 +166,13 @@ def experiment_device(variant, args, device, process_group=None):
                               batch_size=ak["batch_size"] // world, process_group=process_group,
                               backend="hip", **variant["trainer_kwargs"])
     trainer.broadcast_parameters(0)
+    # the collectors sample the trainer's current policy on the matrix cores (sacf_policy_act) and replay
+    # each slice pass as a HIP graph (batched_collector.py); the torch modules stay their snapshot surface
+    expl_coll = BatchedPathCollector(expl_env, policy, max_path_length=ak["max_path_length"],
+                                     max_ticks=args.slice_ticks, device_policy=trainer.device_policy(False))
+    eval_coll = BatchedPathCollector(eval_env, MakeDeterministic(policy), max_path_length=ak["max_path_length"],
+                                     max_ticks=args.slice_ticks, deterministic=True,
+                                     device_policy=trainer.device_policy(True))
     return DeviceBatchRLAlgorithm(trainer=trainer, exploration_env=expl_env, evaluation_env=eval_env,
                                   exploration_data_collector=expl_coll, evaluation_data_collector=eval_coll,
                                   replay_buffer=rb, match_update_ratio=variant.get("match_update_ratio", True), **ak)

@@ -41,6 +41,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_destroy.argtypes = [P]
     L.shipsim_last_error.argtypes = [P]
     L.shipsim_last_error.restype = C.c_char_p
+    L.shipsim_set_stream.argtypes = [P, P]
     L.shipsim_num_envs.argtypes = [P]
     L.shipsim_num_envs.restype = C.c_int32
     L.shipsim_lanes_per_env.argtypes = [P]
@@ -72,7 +73,7 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
                     "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
                     "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
-                    "shipsim_nonfinite_count", "shipsim_lanes_per_env")
+                    "shipsim_nonfinite_count", "shipsim_lanes_per_env", "shipsim_set_stream")
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
@@ -114,7 +115,16 @@ class ShipSim:
                     self.L.shipsim_destroy(h)
                 raise ShipSimError(f"shipsim_create failed ({rc}): {msg}")
         self.h = h
+        self._stream_ptr = self.stream.cuda_stream
         self.lanes_per_env = int(self.L.shipsim_lanes_per_env(h))
+
+    def _follow_stream(self):
+        """Launch on torch's current stream of the device (e.g. a graph-capturing one): shipsim_set_stream
+        when it changed since the last call."""
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != self._stream_ptr:
+            self._check(self.L.shipsim_set_stream(self.h, C.c_void_p(s)), "shipsim_set_stream")
+            self._stream_ptr = s
 
     def _check(self, rc, what):
         if rc:
@@ -140,6 +150,7 @@ class ShipSim:
     def reset(self, mask=None, obs_out=None):
         m = self._dev(mask, torch.uint8) if mask is not None else None
         obs = obs_out if obs_out is not None else torch.empty((self.n_envs, 8), dtype=torch.float32, device=self.device)
+        self._follow_stream()
         self._check(self.L.shipsim_reset(self.h, _ptr(m), _ptr(obs)), "shipsim_reset")
         return obs
 
@@ -158,6 +169,7 @@ class ShipSim:
                        events=torch.empty(self.n_envs, dtype=torch.int32, device=self.device),
                        ticks=torch.empty(self.n_envs, dtype=torch.int32, device=self.device),
                        ready=torch.empty(self.n_envs, dtype=torch.uint8, device=self.device))
+        self._follow_stream()
         self._check(self.L.shipsim_step(self.h, _ptr(a), _ptr(act), int(max_ticks), _ptr(out["obs"]), _ptr(out["reward"]),
                                         _ptr(out["done"]), _ptr(out["events"]), _ptr(out["ticks"]),
                                         _ptr(out.get("ready"))), "shipsim_step")
@@ -165,6 +177,7 @@ class ShipSim:
         return out
 
     def tick(self, k=1):
+        self._follow_stream()
         self._check(self.L.shipsim_tick(self.h, int(k), None), "shipsim_tick")
 
     def run_table(self, table, max_ticks, ep_idx, dec_idx, out=None, log=None, log_len=None):
@@ -182,6 +195,7 @@ class ShipSim:
             out = dict(ticks=torch.zeros(self.n_envs, dtype=torch.int32, device=self.device),
                        decisions=torch.zeros(self.n_envs, dtype=torch.int32, device=self.device))
         cap = int(log.shape[1]) if log is not None else 0
+        self._follow_stream()
         self._check(self.L.shipsim_run_table(self.h, _ptr(t), int(t.shape[0]), int(t.shape[1]), int(max_ticks),
                                              _ptr(ep_idx), _ptr(dec_idx), _ptr(out["ticks"]), _ptr(out["decisions"]),
                                              _ptr(log), cap, _ptr(log_len)), "shipsim_run_table")
@@ -196,6 +210,7 @@ class ShipSim:
             out = dict(states=torch.zeros((N, 8), dtype=torch.float64, device=self.device),
                        done=torch.zeros(N, dtype=torch.uint8, device=self.device),
                        status=torch.zeros(N, dtype=torch.int32, device=self.device))
+        self._follow_stream()
         self._check(self.L.shipsim_legacy_step(self.h, int(k), _ptr(out["states"]), _ptr(out["done"]),
                                                _ptr(out["status"])), "shipsim_legacy_step")
         return out
@@ -213,12 +228,14 @@ class ShipSim:
     def get(self, field):
         shape, dt = self._field_shape(field)
         t = torch.empty(shape, dtype=dt, device=self.device)
+        self._follow_stream()
         self._check(self.L.shipsim_get_state(self.h, int(field), _ptr(t)), "shipsim_get_state")
         return t
 
     def set(self, field, value):
         shape, dt = self._field_shape(field)
         t = self._dev(value, dt).reshape(shape)
+        self._follow_stream()
         self._check(self.L.shipsim_set_state(self.h, int(field), _ptr(t)), "shipsim_set_state")
         self._keep_set = t
 

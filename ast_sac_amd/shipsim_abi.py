@@ -13,7 +13,7 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 ENONFINITE = -5  # shipsim_synchronize status (include/shipsim.h)
 MAX_ROUTE = 16
 MAX_POLYS = 16

@@ -61,7 +61,9 @@ typedef struct sacf_config {
   int32_t world_size;    /* gradient is divided by this in sacf_apply */
   int32_t split_update;  /* 1: keep the update out of sacf_grads even with world_size 1 (the data-parallel
                             call pattern grads | all-reduce | apply on one rank); 0: fused when world_size 1 */
-  int32_t reserved[5];
+  int32_t step_kernel;   /* 0: sacf_grads = five launches; 1: one persistent launch (the same tiles as phases
+                            between grid barriers, bit-identical results; see sacf_step_kernel_status) */
+  int32_t reserved[4];
 } sacf_config;
 
 typedef struct sacf_handle sacf_handle;
@@ -99,6 +101,19 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
                const float* next_obs, const float* eps);
 /* Adam + soft target update from `grads` (divided by world_size); a no-op when sacf_grads applied it. */
 int sacf_apply(sacf_handle* h);
+/* step_kernel 1: SACF_ESTATE when a launch's grid barrier ever timed out (its results are invalid); syncs. */
+int sacf_step_kernel_status(sacf_handle* h);
+
+/* Collector actions from the CURRENT policy parameters (the bound params and the library's W2ᵀ copy):
+ * TanhGaussianPolicy.forward + TanhNormal.sample (gaussian_policy.py:105-118, distributions.py:394-425)
+ * for n rows obs[i * obs_stride + 0..obs_dim), act[i] = tanh(mean + std·ε) with ε ~ N(0, 1) from
+ * Philox(seed, *counter, i) (the caller advances *counter between calls), or tanh(mean) with
+ * deterministic != 0 (MakeDeterministic). Rows with mask[i] == 0 keep act[i] (mask may be NULL).
+ * eps_out (NULL or n floats) receives ε. Two launches on the handle's stream; graph-capturable once
+ * sacf_policy_reserve(h, >= n) has sized the scratch (outside the capture). */
+int sacf_policy_reserve(sacf_handle* h, int64_t n);
+int sacf_policy_act(sacf_handle* h, const float* obs, int64_t n, int32_t obs_stride, const uint8_t* mask,
+                    int32_t deterministic, uint64_t seed, const int64_t* counter, float* act, float* eps_out);
 
 #ifdef __cplusplus
 }

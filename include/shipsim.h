@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 5
+#define SHIPSIM_ABI_VERSION 6
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -260,6 +260,8 @@ int shipsim_destroy(shipsim_handle* h);
 /* Message of the last failed call on h; with h == NULL, of the calling thread's last shipsim_create that
  * failed before it could hand out a handle (every such path sets it; it is per thread). */
 const char* shipsim_last_error(const shipsim_handle* h);
+/* Launches of this handle go to `stream` from now on (e.g. a graph-capturing stream; ABI 6). */
+int shipsim_set_stream(shipsim_handle* h, void* stream);
 int32_t shipsim_num_envs(const shipsim_handle* h);
 /* Lanes per AST env the step / stream kernels run at (config lanes_per_env, or chosen at create from
  * n_envs and the device's SIMD count; a performance knob only, results are identical). */

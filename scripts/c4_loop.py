@@ -34,7 +34,7 @@ def main():
 
     def counters():
         d = coll.get_diagnostics()
-        return d["num steps total"], d["num env ticks total"]
+        return d["num steps total"], coll.device_diagnostics()["num env ticks total"]
 
     def timed(fn):
         torch.cuda.synchronize()
@@ -54,7 +54,7 @@ def main():
     s1, k1 = counters()
     res["collect"] = dict(decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
                           env_ticks_per_s=(k1 - k0) / t)
-    for sl in (64, 128, 256, 512):  # longer slices: fewer passes (policy + host sync) per decision
+    for sl in (32, 64, 128, 256, 512):  # slice length: envs idle after their decision until the pass ends
         coll.max_ticks = sl
         s0, k0 = counters()
         _, t = timed(lambda: coll.collect(32 * n_envs, rb))

@@ -158,7 +158,7 @@ def test_shared_eval_env_carries_sbmpc_memory():
     expl = BatchedPathCollector(expl_env, pol, max_path_length=9, max_ticks=128)
     ev = BatchedPathCollector(eval_env, MakeDeterministic(pol), max_path_length=9, max_ticks=128, deterministic=True)
     expl.collect(32, None)
-    ev.collect(64, None, record_paths=True)
+    ev.collect(1000, None, record_paths=True)  # > 12 passes of 128 ticks: episodes (~1,400 ticks) end
     assert len(ev.get_epoch_paths()) > 0
     # distinctive SBMPC memory in the shared envs, as an evaluation episode in an encounter leaves it
     p = torch.linspace(0.4, 1.0, N, dtype=torch.float64, device="cuda")

@@ -269,3 +269,28 @@ def test_hip_sac_graph_replay_equals_eager_launches():
         assert int(tr._step_t.item()) == 20
         assert np.isfinite(float(tr.last_losses().qf1_loss))
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,B,split", [(256, 256, False), (256, 256, True), (64, 96, False), (256, 1024, False)])
+def test_hip_sac_persistent_step_equals_five_launches(H, B, split):
+    """libsacfused step_kernel 1 (the whole grad step in one persistent launch, grid barriers between the
+    passes) runs the five-launch kernels' own tiles in the same order: 20 graph-replayed steps from the
+    replay ring give bitwise the same parameters, targets and Adam state, fused or split (grads | apply)."""
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    rb = DeviceReplayBuffer(5000, 8, 1, "cuda")
+    b, _ = _rand_batch(3000, "cuda", seed=4)
+    rb.add_batch(b["observations"], b["actions"], b["rewards"], b["next_observations"], b["terminals"])
+    res = []
+    for persistent in (False, True):
+        pol, qs = _seeded_nets(H, "cuda", 7)
+        tr = FusedSACTrainer(env=_Env, policy=pol, qf1=qs[0], qf2=qs[1], target_qf1=qs[2], target_qf2=qs[3],
+                             discount=0.965, reward_scale=0.75, policy_lr=8e-5, qf_lr=8e-5, soft_target_tau=1e-3,
+                             action_reg_coeff=0.01, clip_val=100.0, batch_size=B, use_graph=True, backend="hip",
+                             split_update=split, persistent_kernel=persistent)
+        tr._seed = 1234
+        tr.train_from_buffer(rb, 20)
+        torch.cuda.synchronize()
+        tr._sf.step_kernel_status()
+        res.append(torch.cat([tr.flat_param, tr.flat_target, tr._adam_m, tr._adam_v, tr._stats_t]).cpu())
+    assert torch.equal(res[0], res[1])
