@@ -16,6 +16,13 @@ Two ways to pick the actions:
   masked reset — and is captured once in a HIP graph and replayed. `collect` checks the transition count
   on the host only every few passes (it plans the passes from the count per pass), and the episodes that
   ended go to a device ring that is copied to the host once per collect (record_paths).
+  With `fused` (the default when the env library can run this policy itself: one obstacle ship, the
+  TanhGaussianPolicy's obs dim 8 and hidden 64/128/192/256), the policy is evaluated INSIDE the env launch
+  (shipsim_run_policy): an env that completes a decision gets its next action at once and keeps ticking,
+  an ended episode is reset in place, so no env idles until the pass ends. The launch logs every decision
+  (observation, action, reward, next observation, events); the pass turns the log into replay rows and
+  path records. Same transitions as the sliced pass (test_gpu_run_policy.py pins the env side bitwise);
+  only the noise stream differs.
 * a torch policy module (any policy; the CPU tests): evaluated only on the envs that wait (their count is
   known on the host from the previous pass), one host sync per pass.
 The epoch's paths (get_epoch_paths, as MdpPathCollector's, path_collector.py:77-78) feed
@@ -42,7 +49,7 @@ from ...core.eval_util import create_stats_ordered_dict
 
 class BatchedPathCollector:
     def __init__(self, env, policy, max_path_length=9, max_ticks=64, deterministic=False,
-                 max_num_epoch_paths_saved=None, device_policy=None, use_graph=None, path_ring=None):
+                 max_num_epoch_paths_saved=None, device_policy=None, use_graph=None, path_ring=None, fused=None):
         self._env = env                       # BatchedNormalizedBoxEnv
         self._policy = policy
         self.max_path_length = int(max_path_length)
@@ -76,9 +83,10 @@ class BatchedPathCollector:
         self._epoch_paths = deque(maxlen=max_num_epoch_paths_saved)
         self._n_awaiting = N                                      # host copy, None when unknown
         T = self.max_path_length
-        self._path_rew = torch.zeros((N, T), dtype=torch.float64, device=dev)   # current episode, per decision
-        self._path_act = torch.zeros((N, T), dtype=torch.float32, device=dev)
-        self._path_ev = torch.zeros((N, T), dtype=torch.int32, device=dev)
+        # current episode, per decision: (N, T) views of flat buffers with one spare element (masked scatters)
+        self._path_flat = [torch.zeros(N * T + 1, dtype=dt, device=dev) for dt in (torch.float64, torch.float32,
+                                                                                  torch.int32)]
+        self._path_rew, self._path_act, self._path_ev = [b[:N * T].view(N, T) for b in self._path_flat]
         self._rows = torch.arange(N, device=dev)
         self._trace_idx = None                                    # see trace()
         # ended episodes of the current collect (record_paths): a device ring, copied out once per collect
@@ -89,6 +97,36 @@ class BatchedPathCollector:
         self._ring_ev = torch.zeros((self._ring_cap + 1, T), dtype=torch.int32, device=dev)
         self._ring_top = torch.zeros((), dtype=torch.int64, device=dev)   # episodes written since the collect began
         self._graphs = {}
+        self.fused = self._fused_supported() if fused is None else bool(fused)
+        if self.fused and not self._fused_supported():
+            raise ValueError("fused collection needs a device policy the env library can run (see _fused_supported)")
+        self._mode = None                                         # "fused" / "sliced": the last pass's kind
+        self._ep_idx = torch.zeros(N, dtype=torch.int32, device=dev)   # fused: episodes started per env
+        self._dec_idx = torch.zeros(N, dtype=torch.int32, device=dev)  # fused: decisions of the current episode
+        self._logs = {}                                           # fused: decision log per log capacity
+        self._fused_out = dict(ticks=torch.zeros(N, dtype=torch.int32, device=dev),
+                               decisions=torch.zeros(N, dtype=torch.int32, device=dev))
+
+    def _fused_supported(self):
+        """The env library can run this collector's policy inside the env launch (shipsim_run_policy): a
+        device policy exposing its weights, one obstacle ship, obs dim 8, hidden 64/128/192/256, and the
+        wrapper's action bounds equal to the env's (so the in-kernel NormalizedBoxEnv mapping is the
+        wrapper's)."""
+        dp = self._device_policy
+        if dp is None or not hasattr(dp, "weights") or self.device.type != "cuda":
+            return False
+        base = self._base_env()
+        sim = getattr(base, "sim", None)
+        if sim is None or sim.n_ships != 2 or not hasattr(sim, "run_policy"):
+            return False
+        _, _, o, h = dp.weights()
+        if o != 8 or h % 64 or not 64 <= h <= 256:
+            return False
+        cfg = sim.cfg
+        lb, ub = (-1.0, 1.0) if cfg.normalize_action else (cfg.action_low, cfg.action_high)
+        w = self._env
+        return (np.float32(getattr(w, "_lb", np.nan)) == np.float32(lb) and
+                np.float32(getattr(w, "_ub", np.nan)) == np.float32(ub))
 
     def _base_env(self):
         e = self._env
@@ -108,6 +146,21 @@ class BatchedPathCollector:
         self._path_len.zero_()
         self._ret.zero_()
         self._n_awaiting = self.N
+        self._mode = None
+
+    def _enter(self, mode):
+        """Switching from fused to sliced passes: the sliced pass keeps the pending observations and the
+        awaiting flags on the host side, which fused passes do not maintain — start every episode afresh
+        (as _take_over). Sliced -> fused continues the episodes (the env holds everything it needs)."""
+        if self._mode == "fused" and mode == "sliced":
+            self._obs.copy_(self._env.reset())
+            self._awaiting.fill_(True)
+            self._path_len.zero_()
+            self._ret.zero_()
+            self._n_awaiting = self.N
+        elif mode == "fused" and self._mode != "fused":
+            self._dec_idx.copy_(self._path_len)
+        self._mode = mode
 
     def trace(self, env_indices):
         """Record every decision of the given envs (test / audit hook: one small host copy per pass, so
@@ -164,6 +217,74 @@ class BatchedPathCollector:
             idx = torch.nonzero_static(self._awaiting, size=k).squeeze(1)
             self._act.index_copy_(0, idx, self._actions(self._obs.index_select(0, idx)).to(torch.float32))
 
+    def _log_cap(self):
+        return max(4, self.max_ticks // 16)
+
+    @torch.no_grad()
+    def _fused_pass(self, replay_buffer, record):
+        """One pass with the policy inside the env launch: every env runs max_ticks ticks (less if its
+        log fills), chaining decisions and resetting ended episodes in place; then the decision log ->
+        replay rows (all at once) and, with record, the path buffers / ring (record by record). Device
+        work only (graph-capturable). Returns the transitions of this pass as a device scalar."""
+        N, T, cap = self.N, self.max_path_length, self._log_cap()
+        lg = self._logs.get(cap)
+        if lg is None:
+            lg = self._logs[cap] = (torch.zeros((N, cap, abi.DECLOG_COLS), dtype=torch.float64, device=self.device),
+                                    torch.zeros(N, dtype=torch.int32, device=self.device))
+        log, log_len = lg
+        dp = self._device_policy
+        log_len.zero_()
+        sim = self._base_env().sim
+        sim.run_policy(dp.weights(), self.max_ticks, T, self._ep_idx, self._dec_idx, deterministic=dp.deterministic,
+                       seed=dp.seed, counter=None if dp.deterministic else dp.counter, out=self._fused_out,
+                       log=log, log_len=log_len)
+        if not dp.deterministic:
+            dp.counter.add_(1)
+        valid = torch.arange(cap, device=self.device).unsqueeze(0) < log_len.unsqueeze(1)        # (N, cap)
+        ev = log[:, :, abi.DL_EVENTS].to(torch.int64)
+        rew = log[:, :, abi.DL_REWARD] * self._env._reward_scale
+        nonfinite = (ev & abi.EV_NONFINITE) != 0
+        good = valid & ~nonfinite
+        dec = log[:, :, abi.DL_DECISION].to(torch.int64)
+        end = valid & ((log[:, :, abi.DL_DONE] != 0) | nonfinite | (dec + 1 >= T))
+        act = log[:, :, abi.DL_ACTION].to(torch.float32)
+        if replay_buffer is not None:
+            replay_buffer.add_batch(log[:, :, abi.DL_OBS0:abi.DL_OBS0 + 8].reshape(N * cap, 8).to(torch.float32),
+                                    act.reshape(N * cap, 1), rew.reshape(N * cap, 1).to(torch.float32),
+                                    log[:, :, abi.DL_OBS:abi.DL_OBS + 8].reshape(N * cap, 8).to(torch.float32),
+                                    ((ev & abi.EV_TERMINAL) != 0).reshape(N * cap, 1).to(torch.float32),
+                                    mask=good.reshape(-1))
+        if record:  # record by record, in each env's order: the episode buffers, ended episodes -> the ring
+            evi = ev.to(torch.int32)
+            for j in range(cap):
+                g, e = good[:, j], end[:, j]
+                pos = dec[:, j].clamp(0, T - 1)
+                for buf, v in ((self._path_rew, rew[:, j]), (self._path_act, act[:, j]), (self._path_ev, evi[:, j])):
+                    buf[self._rows, pos] = torch.where(g, v.to(buf.dtype), buf[self._rows, pos])
+                length = torch.where(e, dec[:, j] + g.to(torch.int64), torch.zeros_like(dec[:, j])).to(torch.int32)
+                keep = e & (length > 0)
+                k64 = keep.to(torch.int64)
+                slot = (torch.cumsum(k64, 0) - k64 + self._ring_top) % self._ring_cap
+                idx = torch.where(keep, slot, torch.full_like(slot, self._ring_cap))
+                self._ring_len.index_copy_(0, idx, length)
+                self._ring_rew.index_copy_(0, idx, self._path_rew)
+                self._ring_act.index_copy_(0, idx, self._path_act)
+                self._ring_ev.index_copy_(0, idx, self._path_ev)
+                self._ring_top += k64.sum()
+        else:  # the unfinished episode's decisions only (one write per element: graph-capturable scatter)
+            cur = good & (log[:, :, abi.DL_EPISODE].to(torch.int32) == self._ep_idx.unsqueeze(1))
+            flat = self._rows.unsqueeze(1) * T + dec.clamp(0, T - 1)
+            idx = torch.where(cur, flat, torch.full_like(flat, N * T)).reshape(-1)
+            for b, v in zip(self._path_flat, (rew, act, ev.to(torch.int32))):
+                b.index_copy_(0, idx, v.reshape(-1).to(b.dtype))
+        n_good = good.sum()
+        self._steps_total += n_good
+        self._paths_total += end.sum()
+        self._ticks_total += self._fused_out["ticks"].sum()
+        self._nonfinite_total += (valid & nonfinite).sum()
+        self._path_len.copy_(self._dec_idx)  # the sliced pass's episode length, for a switch back (_enter)
+        return n_good
+
     @torch.no_grad()
     def _pass(self, replay_buffer, record):
         """One sliced pass over all envs, device work only (graph-capturable with a device policy).
@@ -217,23 +338,25 @@ class BatchedPathCollector:
 
     def step(self, replay_buffer=None):
         """One sliced pass over all envs (eager). Returns (ready mask, #transitions) as device tensors."""
+        self._enter("sliced")
         n = self._pass(replay_buffer, False)
         self._n_awaiting = None
         return self._awaiting, n
 
-    def _graph_pass(self, replay_buffer, record):
-        key = (id(replay_buffer) if replay_buffer is not None else None, bool(record), self.max_ticks)
+    def _graph_pass(self, replay_buffer, record, fused=False):
+        key = (id(replay_buffer) if replay_buffer is not None else None, bool(record), self.max_ticks, fused)
         g = self._graphs.get(key)
+        pass_fn = self._fused_pass if fused else self._pass
         if g is None:
             # one eager pass on a side stream (allocations, library scratch), then the capture
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
-                self._pass(replay_buffer, record)
+                pass_fn(replay_buffer, record)
             torch.cuda.current_stream(self.device).wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._pass(replay_buffer, record)
+                pass_fn(replay_buffer, record)
             self._graphs[key] = g
             return  # the capture did not run the pass; the eager one did
         g.replay()
@@ -246,6 +369,8 @@ class BatchedPathCollector:
         record = bool(record_paths)
         if record:
             self._ring_top.zero_()
+        fused = self.fused and self._trace_idx is None
+        self._enter("fused" if fused else "sliced")
         if self._device_policy is None or self._trace_idx is not None:
             got = 0
             while got < num_steps:
@@ -258,7 +383,9 @@ class BatchedPathCollector:
             while got < num_steps:
                 for _ in range(batch):
                     if self.use_graph:
-                        self._graph_pass(replay_buffer, record)
+                        self._graph_pass(replay_buffer, record, fused)
+                    elif fused:
+                        self._fused_pass(replay_buffer, record)
                     else:
                         self._pass(replay_buffer, record)
                 passes += batch

@@ -87,8 +87,9 @@ class FusedSACTrainer(TorchTrainer):
         # Default: whenever world > 1; split_update=True forces it on one rank too (the all-reduce then runs
         # over a world-size-1 group: the same code path as N ranks, an identity on the values)
         self.split = (self.world > 1) if split_update is None else bool(split_update)
-        # hip backend: the grad step as one persistent launch (libsacfused step_kernel 1) or five launches
-        self.persistent_kernel = True if persistent_kernel is None else bool(persistent_kernel)
+        # hip backend: the grad step as five graph-replayed launches (default) or one persistent launch with
+        # grid barriers (libsacfused step_kernel 1; same results, slower on MI355X — DESIGN.md §7c)
+        self.persistent_kernel = False if persistent_kernel is None else bool(persistent_kernel)
 
         self.pi_params = ([self.log_alpha] if use_automatic_entropy_tuning else []) + list(policy.parameters())
         self.q_params = list(qf1.parameters()) + list(qf2.parameters())
@@ -523,3 +524,8 @@ class DevicePolicy:
                             counter=self.counter, eps_out=eps_out)
         if not self.deterministic:
             self.counter.add_(1)
+
+    def weights(self):
+        """(params_ptr, w2t_ptr, obs_dim, hidden) of the trainer's live policy: what ShipSim.run_policy
+        (the decision stream with this policy in the loop) reads; stable for the trainer's lifetime."""
+        return self._sf.policy_weights()

@@ -1127,9 +1127,76 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
 struct PArgs {
   MArgs m;
   WgArgs w;
-  unsigned* bar;  // [arrive, generation]: a sense-reversing grid barrier, both back at rest after a launch
-  int* err;       // set when a barrier wait exceeds its bound (blocks not co-resident): results invalid
+  unsigned* bar;  // barrier state (16 words, all back at rest after a launch), see grid_barrier_*
+  int* err;       // set when a barrier wait exceeds its bound (blocks not co-resident) or a block is not
+                  // on the XCD the tile map assumes: results invalid
+  int xcd_local;  // 1: the passes' row data never leave an XCD (B % 256 == 0), see grid_barrier_xcd
 };
+
+// bounded wait until *w != old (relaxed agent-scope loads); false (and *err set) when the bound is hit
+__device__ __forceinline__ bool wait_change(unsigned* w, unsigned old, int* err) {
+  unsigned spins = 0;
+  while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == old) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 25)) {
+      atomicOr(err, 1);
+      return false;
+    }
+  }
+  return true;
+}
+
+// everyone arrived: count on bar[c], the last arrival resets it and advances bar[c + 1]
+__device__ __forceinline__ void arrive_and_wait(unsigned* bar, int c, unsigned n, int* err) {
+  const unsigned gen = __hip_atomic_load(bar + c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned prev = __hip_atomic_fetch_add(bar + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev == n - 1) {
+    __hip_atomic_store(bar + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(bar + c + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    wait_change(bar + c + 1, gen, err);
+  }
+}
+
+// Grid barrier for passes whose data stay on one XCD (the tile map puts row tile r of every pass on XCD
+// r % 8, so every row a tile reads was written through the same L2): every wave's stores have completed
+// to the L2 (s_waitcnt), the blocks meet on device-coherent counters, and each CU drops its L1 lines
+// before reading what its XCD's other CUs wrote. No L2 write-back or invalidation is needed.
+__device__ __forceinline__ void grid_barrier_xcd(unsigned* bar, int* err, unsigned nblocks) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) arrive_and_wait(bar, 0, nblocks, err);
+  __syncthreads();
+  asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1
+}
+
+// Grid barrier before the weight-gradient pass, which reads every row from every XCD: after everyone
+// arrived, one block per XCD writes its L2 back (an agent-scope release), and once all eight have, every
+// block invalidates its L1 / L2 (agent-scope acquire) before reading.
+__device__ __forceinline__ void grid_barrier_dev(unsigned* bar, int* err, unsigned nblocks) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // (read before arriving: bar[3] cannot advance until every block has arrived)
+    const unsigned gen = __hip_atomic_load(bar + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    arrive_and_wait(bar, 0, nblocks, err);
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7;  // HW_REG_XCC_ID
+    if (__hip_atomic_fetch_add(bar + 8 + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this XCD's L2 written back
+      if (__hip_atomic_fetch_add(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 7) {
+        for (int x = 0; x < 8; ++x) __hip_atomic_store(bar + 8 + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(bar + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(bar + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        wait_change(bar + 3, gen, err);
+      }
+    } else {
+      wait_change(bar + 3, gen, err);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
 
 // Every block arrives once per barrier; the last one to arrive resets the count and advances the
 // generation the others wait on. Writes before the barrier are released device-wide (the L2 of every
@@ -1176,6 +1243,18 @@ __global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg
   float* lds = reinterpret_cast<float*>(raw);
   const int G = gridDim.x, ct = H / kTile2;
   const int B = persist_args().m.L.B;
+  const bool local = persist_args().xcd_local;
+  if (local && threadIdx.x == 0) {  // the tile map's assumption: blocks congruent mod 8 share an XCD
+    const unsigned xcc = (__builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15) + 1;  // HW_REG_XCC_ID
+    const unsigned seen = atomicCAS(persist_args().bar + 24 + blockIdx.x % 8, 0u, xcc);
+    if (seen != 0u && seen != xcc) atomicOr(persist_args().err, 2 | (int)(xcc << 8) | (int)(seen << 16));
+  }
+  auto barrier = [&](bool last) __attribute__((always_inline)) {
+    const PArgs& pa = persist_args();
+    if (!local) grid_barrier(pa.bar + 4, pa.err, G);
+    else if (last) grid_barrier_dev(pa.bar, pa.err, G);
+    else grid_barrier_xcd(pa.bar, pa.err, G);
+  };
   {  // actor_fwd
     const int gx = 2 * B / kTile2, nt = gx * ct;
     for (int t = blockIdx.x; t < nt; t += G) {
@@ -1183,7 +1262,7 @@ __global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg
       __syncthreads();
     }
   }
-  grid_barrier(persist_args().bar, persist_args().err, G);
+  barrier(false);
   {  // critic_fwd
     const int gx = 6 * B / kTile2, nt = gx * ct;
     for (int t = blockIdx.x; t < nt; t += G) {
@@ -1191,7 +1270,7 @@ __global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg
       __syncthreads();
     }
   }
-  grid_barrier(persist_args().bar, persist_args().err, G);
+  barrier(false);
   {  // critic_bwd
     const int gx = 4 * B / kTile2 + 8, nt = gx * ct;
     for (int t = blockIdx.x; t < nt; t += G) {
@@ -1199,7 +1278,7 @@ __global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg
       __syncthreads();
     }
   }
-  grid_barrier(persist_args().bar, persist_args().err, G);
+  barrier(false);
   {  // actor_bwd
     const int gx = B / kTile2, nt = gx * ct;
     for (int t = blockIdx.x; t < nt; t += G) {
@@ -1207,7 +1286,7 @@ __global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg
       __syncthreads();
     }
   }
-  grid_barrier(persist_args().bar, persist_args().err, G);
+  barrier(true);
   {  // weight gradients (+ Adam / soft update / W2T when fused)
     WgLds& S = *reinterpret_cast<WgLds*>(raw);
     const int nb = persist_args().w.n_blocks;
@@ -1640,8 +1719,10 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     wg.hp = h->hp;
   }
   if (cfg->step_kernel == 1) {  // persistent single-launch step: barrier state and a co-resident grid
-    e = hipMalloc(&h->bar, 4 * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemset(h->bar, 0, 4 * sizeof(unsigned));
+    // [0..3] XCD-local / dev barriers, [4..5] full, [8..15] XCD election, [16] error flag, [24..31] the
+    // XCD of each block residue mod 8 (+1, 0 = not seen yet)
+    e = hipMalloc(&h->bar, 32 * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(h->bar, 0, 32 * sizeof(unsigned));
     int per_cu = 0, cus = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = persistent_occupancy(H, &per_cu);
@@ -1689,10 +1770,11 @@ int sacf_step_kernel_status(sacf_handle* h) {
   if (!h->bar) return SACF_OK;
   SDev g(h->device);
   int flag = 0;
-  hipError_t e = hipMemcpy(&flag, h->bar + 2, sizeof(int), hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpy(&flag, h->bar + 16, sizeof(int), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return sfail(h, SACF_EHIP, "sacf_step_kernel_status: %s", hipGetErrorString(e));
-  return flag ? sfail(h, SACF_ESTATE, "persistent step kernel: a grid barrier wait timed out (results invalid)")
-              : SACF_OK;
+  if (!flag) return SACF_OK;
+  return sfail(h, SACF_ESTATE, "persistent step kernel: %s (flag 0x%x; results invalid)",
+               (flag & 1) ? "a grid barrier wait timed out" : "blocks congruent mod 8 ran on different XCDs", flag);
 }
 int64_t sacf_param_count(const sacf_handle* h) { return h ? h->L.n_params : -1; }
 int64_t sacf_target_count(const sacf_handle* h) { return h ? h->L.n_targets : -1; }
@@ -1815,7 +1897,8 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
     p.m = a;
     p.w = w;
     p.bar = h->bar;
-    p.err = reinterpret_cast<int*>(h->bar + 2);
+    p.err = reinterpret_cast<int*>(h->bar + 16);
+    p.xcd_local = (h->L.B % 256 == 0 && !getenv("SACF_FULL_BARRIER")) ? 1 : 0;
     switch (h->L.H) {
       case 32: launch_persistent<32>(p, h->grid, h->stream); break;
       case 64: launch_persistent<64>(p, h->grid, h->stream); break;
@@ -1890,6 +1973,16 @@ int sacf_policy_act(sacf_handle* h, const float* obs, int64_t n, int32_t obs_str
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_policy_act: %s", hipGetErrorString(e));
+}
+
+int sacf_policy_weights(const sacf_handle* h, const float** params, const float** w2t, int32_t* obs_dim,
+                        int32_t* hidden) {
+  if (!h || !h->params || !h->T) return SACF_ESTATE;
+  if (params) *params = h->params + h->L.p_w1;
+  if (w2t) *w2t = h->T;  // the actor's W2ᵀ leads the transposed copies (kept current by every update)
+  if (obs_dim) *obs_dim = h->L.O;
+  if (hidden) *hidden = h->L.H;
+  return SACF_OK;
 }
 
 }  // extern "C"

@@ -58,8 +58,12 @@ struct DevState {
   __host__ __device__ double* legacy_states() const { return (double*)ev(14); }  // [env][4] legacy self.states
   __host__ __device__ int32_t* legacy_flags() const { return (int32_t*)ev(15); }  // 1: still the f32 initial_states
   __host__ __device__ int32_t* dec_ticks() const { return (int32_t*)ev(16); }  // ticks of the decision in progress
+  // the decision in progress as the stream logs it (SHIPSIM_DL_ACTION / _OBS0): its action, the observation it
+  // was chosen from
+  __host__ __device__ float* dec_action() const { return (float*)ev(17); }
+  __host__ __device__ float* dec_obs0() const { return (float*)ev(18); }  // [env][8]
   int32_t* nonfinite;  // device counter: envs flagged SHIPSIM_EV_NONFINITE (read by shipsim_synchronize)
-  static constexpr int kEnvArrays = 17;
+  static constexpr int kEnvArrays = 19;
   static constexpr int kShipArrays = 22;
 };
 #ifdef SHIPSIM_PHASE_TIMING
@@ -918,7 +922,15 @@ struct ChainArgs {
   double* log;         // [env][log_cap][SHIPSIM_DECLOG_COLS] per-decision record (may be null)
   int32_t* log_len;    // [env] records written (counts on past log_cap)
   int32_t log_cap;
+  int32_t log_stop;    // an env whose log is full stops for the launch, its next decision pending
+  // shipsim_run_policy: actions from the policy instead of the table (policy != null)
+  const float* policy;  // TanhGaussianPolicy parameters, torch order (shipsim_policy.params)
+  const float* w2t;     // its fc1 weight transposed, [H][H] (shipsim_policy.w2t)
+  int32_t pol_obs, pol_hidden, pol_det;
+  uint64_t pol_seed;
+  const int64_t* pol_counter;
 };
+
 
 // A copy of the state table whose base pointer the compiler cannot see through: addresses derived
 // from it are recomputed where they are used (a few SALU) instead of being hoisted out of the tick
@@ -927,6 +939,143 @@ __device__ __forceinline__ DevState opaque(const DevState& S) {
   DevState o = S;
   asm volatile("" : "+s"(o.base));
   return o;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The collector's policy inside the decision stream (shipsim_run_policy): TanhGaussianPolicy.forward
+// + TanhNormal.sample (gaussian_policy.py:105-118, distributions.py:394-425) or MakeDeterministic's
+// tanh(mean) (policies/base.py:54-64) on the observation of every env of the wave that needs its next
+// action, evaluated by the whole wave (wave-uniform control flow): up to 8 envs per pass share every
+// weight load; lane l computes hidden units l, l + 64, ... (fmaf chains from the bias in input order,
+// h1 staged in LDS); the heads are reduced across the wave. fp32 as the policy.
+// ---------------------------------------------------------------------------------------------
+constexpr int kPolMaxRows = 8;
+constexpr int kPolMaxHidden = 256;
+
+__device__ inline void philox_env(uint32_t c[4], uint32_t k0, uint32_t k1) {  // Philox4x32-10
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ float wave_sum_f(float x) {  // butterfly: every lane gets the same bits
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// Must be called by every lane of the wave. want: this lane's env needs its next action (all lanes of an
+// env agree); ns: its observation; seq: the env's decisions completed in this call (noise stream index).
+// Returns the normalized action a in (-1, 1) for lanes whose env wanted one.
+__device__ float policy_actions(bool want, const float ns[8], int env, bool env_leader, int env_lane0, int seq,
+                                const ChainArgs& CH, float* lds_h1) {
+  uint64_t req = __ballot(want && env_leader);
+  float act = 0.0f;
+  const int lane = threadIdx.x & 63;
+  const int H = CH.pol_hidden, O = CH.pol_obs, nj = H / 64;
+  const float* W1 = CH.policy;
+  const float* b1 = W1 + (size_t)H * O;
+  const float* b2 = b1 + H + (size_t)H * H;
+  const float* wm = b2 + H;
+  const float* ws = wm + H + 1;
+  while (req) {
+    int src[kPolMaxRows];
+    int E = 0;
+    while (req && E < kPolMaxRows) {
+      src[E++] = __ffsll((unsigned long long)req) - 1;
+      req &= req - 1;
+    }
+    // fc0 + relu for every row, into LDS
+    for (int e = 0; e < E; ++e) {
+      float x[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) x[m] = __shfl(ns[m], src[e], 64);
+      for (int j = 0; j < nj; ++j) {
+        const int u = lane + 64 * j;
+        float h = b1[u];
+        for (int m = 0; m < O; ++m) h = fmaf(W1[(size_t)u * O + m], x[m], h);
+        lds_h1[e * kPolMaxHidden + u] = fmaxf(h, 0.0f);
+      }
+    }
+    __syncthreads();  // (one wave per block)
+    // fc1 + relu: acc[e][j] = b2[u] + sum_k W2[u][k] h1[e][k], k ascending; W2T rows are coalesced
+    float acc[kPolMaxRows][kPolMaxHidden / 64];
+#pragma unroll
+    for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+      const float bj = j < nj ? b2[lane + 64 * j] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < kPolMaxRows; ++e) acc[e][j] = bj;
+    }
+    for (int k = 0; k < H; k += 4) {
+      float w[4][kPolMaxHidden / 64];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int j = 0; j < kPolMaxHidden / 64; ++j) w[kk][j] = j < nj ? CH.w2t[(size_t)(k + kk) * H + lane + 64 * j] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < kPolMaxRows; ++e) {
+        if (e >= E) break;
+        const float4 h4 = *reinterpret_cast<const float4*>(lds_h1 + e * kPolMaxHidden + k);
+#pragma unroll
+        for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+          acc[e][j] = fmaf(w[0][j], h4.x, acc[e][j]);
+          acc[e][j] = fmaf(w[1][j], h4.y, acc[e][j]);
+          acc[e][j] = fmaf(w[2][j], h4.z, acc[e][j]);
+          acc[e][j] = fmaf(w[3][j], h4.w, acc[e][j]);
+        }
+      }
+    }
+    // heads (mean, log_std) reduced across the wave, the sample, and the hand-over to the env's lanes
+    float wmj[kPolMaxHidden / 64], wsj[kPolMaxHidden / 64];
+#pragma unroll
+    for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+      wmj[j] = j < nj ? wm[lane + 64 * j] : 0.0f;
+      wsj[j] = j < nj ? ws[lane + 64 * j] : 0.0f;
+    }
+    const float bm = wm[H], bs = ws[H];
+    const uint64_t ctr = CH.pol_counter ? (uint64_t)*CH.pol_counter : 0;
+#pragma unroll
+    for (int e = 0; e < kPolMaxRows; ++e) {
+      if (e >= E) break;
+      float pm = 0.0f, ps = 0.0f;
+#pragma unroll
+      for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+        const float y = fmaxf(acc[e][j], 0.0f);
+        pm = fmaf(wmj[j], y, pm);
+        ps = fmaf(wsj[j], y, ps);
+      }
+      const float mean = wave_sum_f(pm) + bm;
+      const float log_std = fminf(fmaxf(wave_sum_f(ps) + bs, -20.0f), 2.0f);
+      float z = mean;
+      if (!CH.pol_det) {
+        const int e_env = __shfl(env, src[e], 64), e_seq = __shfl(seq, src[e], 64);
+        uint32_t c[4] = {(uint32_t)e_env, (uint32_t)ctr, (uint32_t)(ctr >> 32), 0x5A100000u ^ (uint32_t)e_seq};
+        philox_env(c, (uint32_t)CH.pol_seed, (uint32_t)(CH.pol_seed >> 32));
+        const float u1 = ((float)c[0] + 1.0f) * 2.3283064365386963e-10f;
+        const float u2 = (float)c[1] * 2.3283064365386963e-10f;
+        z = mean + expf(log_std) * (sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2));
+      }
+      const float a = tanhf(z);
+      if (env_lane0 == src[e]) act = a;
+    }
+    __syncthreads();  // lds_h1 free for the next pass
+  }
+  return act;
+}
+
+// NormalizedBoxEnv's float32 rule (normalized_box_env.py:48-51): lb + (a + 1) * 0.5 * (ub - lb), clipped
+__device__ __forceinline__ float denormalize_f32(float a, float lb, float ub) {
+  const float x = lb + ((a + 1.0f) * 0.5f) * (ub - lb);
+  return fminf(fmaxf(x, lb), ub);
 }
 
 // lanes of the env: value of lane k of the env (LPE 16: the env is one DPP row)
@@ -1045,6 +1194,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
+  __shared__ float lds_pol[CHAIN ? kPolMaxRows * kPolMaxHidden : 1];  // shipsim_run_policy: h1 rows
 #ifdef SHIPSIM_POISON_LDS
   // diagnostics build (scripts, not the product): every LDS word gets a pattern before staging, so a
   // read of LDS the kernel did not write sees the pattern instead of another kernel's leftovers
@@ -1132,10 +1282,15 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
            sampling_count, n_base, phase);
 #endif
   // ---- intermediate waypoint sampling (env.py:659-696) for an env that waits for a decision ----
-  auto decision_prologue = [&](float sa) __attribute__((always_inline)) {
+  auto decision_prologue = [&](float sa, float a_log) __attribute__((always_inline)) {
     const StepArgs& A = step_args();
     const Params& P = A.P;
     const ConstBuf& K = A.K;
+    if (CHAIN && lie == 0) {  // what the decision record will report: the action and the observation it saw
+      const DevState So = opaque(A.S);
+      So.dec_action()[envc] = a_log;
+      for (int i = 0; i < 8; ++i) So.dec_obs0()[envc * 8 + i] = ns[i];
+    }
     if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
     phase = 0;
     have_iw = false;
@@ -1188,6 +1343,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     ep_i = CH.ep_idx[envc];
     dec_i = CH.dec_idx[envc];
     log_n = CH.log_len ? CH.log_len[envc] : 0;
+    if (running && CH.log_stop && log_n >= CH.log_cap) {  // log already full: sit this launch out
+      running = false;
+      stalled = (dflags & DF_AWAITING) != 0;
+    }
   }
   auto table_action = [&]() __attribute__((always_inline)) -> float {
     const StepArgs& A = step_args();
@@ -1229,41 +1388,84 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   // recorded and the next one pending (DF_AWAITING): the wave keeps ticking its other envs and the
   // next launch resumes exactly there, so results do not depend on the burst bound.
   constexpr int kChainBurst = 8;
+  // the next action of every env of the wave that needs one (want): the table entry, or the policy's
+  // sample (wave-cooperative, shipsim_run_policy). Wave-uniform. sa: the scoping angle to run, a_log:
+  // the action as the decision record reports it (the table's angle / the policy's normalized action).
+  auto chain_action = [&](bool want, float& a_log) __attribute__((always_inline)) -> float {
+    const StepArgs& A = step_args();
+    const ChainArgs& CH = A.CH;
+#ifndef SHIPSIM_NO_POLICY_STREAM  // (A/B builds only: the open-loop stream without the policy code)
+    if (CH.policy == nullptr)
+#endif
+    {
+      a_log = want ? table_action() : 0.0f;
+      return a_log;
+    }
+    a_log = policy_actions(want, ns, envc, lie == 0, env_lane0, n_decided, CH, lds_pol);
+    const Params& P = A.P;
+    const float lb = P.normalize_action ? -1.0f : P.action_low, ub = P.normalize_action ? 1.0f : P.action_high;
+    return denormalize_f32(a_log, lb, ub);  // NormalizedBoxEnv in front of the env
+  };
+  // Decisions of the wave just completed (ready): record them, reset envs whose episode ended (done, or
+  // n_dec decisions = the rollout's max_path_length), start each env's next decision. A sampling failure
+  // completes the new decision at once (no tick), hence the loop; after kChainBurst such back-to-back
+  // decisions (actions that all fail their sampling) the env stops for this launch with the last decision
+  // recorded and the next one pending (DF_AWAITING): the wave keeps ticking its other envs and the next
+  // launch resumes exactly there, so results do not depend on the burst bound. Wave-uniform (the policy
+  // is evaluated by the whole wave).
   auto chain_next = [&]() __attribute__((always_inline)) {
-    for (int burst = 0; ready; ++burst) {
-      const ChainArgs& CH = step_args().CH;
-      if (CH.log && lie == 0 && log_n < CH.log_cap) {
-        double* rec = CH.log + ((size_t)env * CH.log_cap + log_n) * SHIPSIM_DECLOG_COLS;
-        rec[SHIPSIM_DL_REWARD] = out_r; rec[SHIPSIM_DL_EVENTS] = (double)out_bits;
-        rec[SHIPSIM_DL_DONE] = out_done ? 1.0 : 0.0; rec[SHIPSIM_DL_EPISODE] = (double)ep_i;
-        rec[SHIPSIM_DL_DECISION] = (double)dec_i; rec[SHIPSIM_DL_TICKS] = (double)out_ticks;
-        for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS + i] = (double)ns[i];
+    for (int burst = 0; __any(ready && running); ++burst) {
+      bool want = false;
+      if (ready && running) {
+        const ChainArgs& CH = step_args().CH;
+        if (CH.log && lie == 0 && log_n < CH.log_cap) {
+          double* rec = CH.log + ((size_t)env * CH.log_cap + log_n) * SHIPSIM_DECLOG_COLS;
+          rec[SHIPSIM_DL_REWARD] = out_r; rec[SHIPSIM_DL_EVENTS] = (double)out_bits;
+          rec[SHIPSIM_DL_DONE] = out_done ? 1.0 : 0.0; rec[SHIPSIM_DL_EPISODE] = (double)ep_i;
+          rec[SHIPSIM_DL_DECISION] = (double)dec_i; rec[SHIPSIM_DL_TICKS] = (double)out_ticks;
+          for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS + i] = (double)ns[i];
+          const DevState So = opaque(step_args().S);
+          rec[SHIPSIM_DL_ACTION] = (double)So.dec_action()[envc];
+          for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS0 + i] = (double)So.dec_obs0()[envc * 8 + i];
+        }
+        log_n += 1;
+        n_decided += 1;
+        if (out_done || dec_i + 1 >= CH.n_dec) {
+          reset_env();
+          ep_i += 1;
+          dec_i = 0;
+        } else {
+          dec_i += 1;
+        }
+        if (lie == 0) {
+          const DevState So = opaque(step_args().S);
+          for (int i = 0; i < 8; ++i) So.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
+        }
+        ready = false;
+        out_done = false;
+        if (burst + 1 >= kChainBurst || (CH.log_stop && log_n >= CH.log_cap)) {
+          stalled = true;  // next decision pending: resumed by the next launch
+          running = false;
+        } else {
+          want = true;
+        }
       }
-      log_n += 1;
-      n_decided += 1;
-      if (out_done || dec_i + 1 >= CH.n_dec) {
-        reset_env();
-        ep_i += 1;
-        dec_i = 0;
-      } else {
-        dec_i += 1;
-      }
-      if (lie == 0) {
-        const DevState So = opaque(step_args().S);
-        for (int i = 0; i < 8; ++i) So.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
-      }
-      ready = false;
-      out_done = false;
-      if (burst + 1 >= kChainBurst) {
-        stalled = true;  // next decision pending: resumed by the next launch
-        running = false;
-        break;
-      }
-      decision_prologue(table_action());
+      float a_log;
+      const float sa = chain_action(want, a_log);
+      if (want) decision_prologue(sa, a_log);
     }
   };
 
-  if (running && (dflags & DF_AWAITING)) decision_prologue(CHAIN ? table_action() : A0.action[envc]);
+  {
+    const bool want = running && (dflags & DF_AWAITING);
+    if (CHAIN) {
+      float a_log;
+      const float sa = chain_action(want, a_log);
+      if (want) decision_prologue(sa, a_log);
+    } else if (want) {
+      decision_prologue(A0.action[envc], A0.action[envc]);
+    }
+  }
 
   bool going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
 #ifdef SHIPSIM_PHASE_TIMING
@@ -1640,7 +1842,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     PT_MARK(3);
   }
   if (!CHAIN) break;
-  if (ready && running) chain_next();
+  chain_next();  // (wave-uniform: a no-op unless a decision of the wave completed)
   going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
   if (!__any(going)) break;
   }
@@ -2663,18 +2865,9 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
   return SHIPSIM_OK;
 }
 
-int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
-                      int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
-                      int32_t log_cap, int32_t* log_len) {
-  if (!h || !h->dev_block || !table || !ep_idx || !dec_idx || n_eps < 1 || n_dec < 1 || max_ticks < 1 ||
-      (log && (!log_len || log_cap < 1)))
-    return SHIPSIM_EINVAL;
-  if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "run_table: AST kind only");
-  if (h->T.ship) return fail(h, SHIPSIM_EINVAL, "run_table: trajectory recording is on (use shipsim_step)");
+// the decision-stream launch shared by shipsim_run_table and shipsim_run_policy
+static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, int32_t* ticks_out) {
   DeviceGuard g(h->device);
-  ChainArgs ch;
-  ch.table = table; ch.n_eps = n_eps; ch.n_dec = n_dec; ch.ep_idx = ep_idx; ch.dec_idx = dec_idx;
-  ch.decisions = decisions_out; ch.log = log; ch.log_len = log_len; ch.log_cap = log_cap;
   // lanes per env: 16 (default) or 8 / 4 (more envs per wave when the handle holds more envs than
   // the chip has SIMD slots at 16; identical results)
   const int lpe = (h->lpe == 8 || h->lpe == 4) ? h->lpe : (h->lpe == 2 ? 4 : 16);
@@ -2715,6 +2908,42 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
 #undef CHAINED_L
   HIPCHK(h, hipGetLastError());
   return SHIPSIM_OK;
+}
+
+int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
+                      int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
+                      int32_t log_cap, int32_t* log_len) {
+  if (!h || !h->dev_block || !table || !ep_idx || !dec_idx || n_eps < 1 || n_dec < 1 || max_ticks < 1 ||
+      (log && (!log_len || log_cap < 1)))
+    return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "run_table: AST kind only");
+  if (h->T.ship) return fail(h, SHIPSIM_EINVAL, "run_table: trajectory recording is on (use shipsim_step)");
+  ChainArgs ch = {};
+  ch.table = table; ch.n_eps = n_eps; ch.n_dec = n_dec; ch.ep_idx = ep_idx; ch.dec_idx = dec_idx;
+  ch.decisions = decisions_out; ch.log = log; ch.log_len = log_len; ch.log_cap = log_cap;
+  return run_chain(h, ch, max_ticks, ticks_out);
+}
+
+int shipsim_run_policy(shipsim_handle* h, const float* policy, const float* w2t, int32_t obs_dim, int32_t hidden,
+                       int32_t deterministic, uint64_t seed, const int64_t* counter, int32_t n_dec,
+                       int32_t max_ticks, int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out,
+                       int32_t* decisions_out, double* log, int32_t log_cap, int32_t* log_len) {
+  if (!h || !h->dev_block || !policy || !w2t || !ep_idx || !dec_idx || n_dec < 1 || max_ticks < 1 ||
+      (log && (!log_len || log_cap < 1)) || (!deterministic && !counter))
+    return SHIPSIM_EINVAL;
+  if (h->P.kind != SHIPSIM_KIND_AST) return fail(h, SHIPSIM_EINVAL, "run_policy: AST kind only");
+  if (h->T.ship) return fail(h, SHIPSIM_EINVAL, "run_policy: trajectory recording is on (use shipsim_step)");
+  if (obs_dim != 8) return fail(h, SHIPSIM_EINVAL, "run_policy: observation dim %d (the AST observation has 8)", obs_dim);
+  if (hidden < 64 || hidden > kPolMaxHidden || hidden % 64)
+    return fail(h, SHIPSIM_EINVAL, "run_policy: hidden %d (64, 128, 192 or 256)", hidden);
+  if (ship_slots(h) > 2) return fail(h, SHIPSIM_EINVAL, "run_policy: one obstacle ship only");
+  ChainArgs ch = {};
+  ch.n_eps = 1; ch.n_dec = n_dec; ch.ep_idx = ep_idx; ch.dec_idx = dec_idx;
+  ch.decisions = decisions_out; ch.log = log; ch.log_len = log_len; ch.log_cap = log_cap;
+  ch.log_stop = log ? 1 : 0;
+  ch.policy = policy; ch.w2t = w2t; ch.pol_obs = obs_dim; ch.pol_hidden = hidden; ch.pol_det = deterministic ? 1 : 0;
+  ch.pol_seed = seed; ch.pol_counter = counter;
+  return run_chain(h, ch, max_ticks, ticks_out);
 }
 
 int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_t* done_out, uint32_t* status_out) {

@@ -13,7 +13,7 @@ ABI_VERSION = 1
 EXPORTED_SYMBOLS = ("sacf_abi_version", "sacf_build_info", "sacf_create", "sacf_destroy", "sacf_last_error", "sacf_set_stream",
                     "sacf_param_count", "sacf_target_count", "sacf_stats_count", "sacf_bind", "sacf_sync_params",
                     "sacf_set_replay", "sacf_grads", "sacf_apply", "sacf_policy_reserve", "sacf_policy_act",
-                    "sacf_step_kernel_status")
+                    "sacf_step_kernel_status", "sacf_policy_weights")
 _lib = None
 
 
@@ -55,6 +55,7 @@ def load_library(path=LIB_PATH):
     L.sacf_policy_reserve.argtypes = [P, C.c_int64]
     L.sacf_step_kernel_status.argtypes = [P]
     L.sacf_policy_act.argtypes = [P, P, C.c_int64, C.c_int32, P, C.c_int32, C.c_uint64, P, P, P]
+    L.sacf_policy_weights.argtypes = [P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     if L.sacf_abi_version() != ABI_VERSION:
         raise SacFusedError("libsacfused ABI mismatch")
     L.sacf_build_info.restype = C.c_char_p
@@ -141,6 +142,14 @@ class SacFused:
         self._check(self.L.sacf_policy_act(self.h, _p(obs), n, stride, _p(mask), int(bool(deterministic)),
                                            int(seed) & ((1 << 64) - 1), _p(counter), _p(act), _p(eps_out)),
                     "sacf_policy_act")
+
+    def policy_weights(self):
+        """(params_ptr, w2t_ptr, obs_dim, hidden): the device policy parameters and the library's current
+        W2ᵀ copy (sacf_policy_weights), for shipsim_run_policy."""
+        p, t, o, hdn = C.c_void_p(), C.c_void_p(), C.c_int32(), C.c_int32()
+        self._check(self.L.sacf_policy_weights(self.h, C.byref(p), C.byref(t), C.byref(o), C.byref(hdn)),
+                    "sacf_policy_weights")
+        return p.value, t.value, o.value, hdn.value
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

@@ -58,6 +58,8 @@ def load_library(path=LIB_PATH):
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
+    L.shipsim_run_policy.argtypes = [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, P, C.c_int32, C.c_int32,
+                                     P, P, P, P, P, C.c_int32, P]
     if L.shipsim_abi_version() != abi.ABI_VERSION:
         raise ShipSimError(f"ABI mismatch: library {L.shipsim_abi_version()} vs binding {abi.ABI_VERSION}")
     from .build_hash import check_library
@@ -73,7 +75,8 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
                     "shipsim_destroy", "shipsim_last_error", "shipsim_num_envs", "shipsim_reset", "shipsim_step",
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
                     "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
-                    "shipsim_nonfinite_count", "shipsim_lanes_per_env", "shipsim_set_stream")
+                    "shipsim_nonfinite_count", "shipsim_lanes_per_env", "shipsim_set_stream",
+                    "shipsim_run_policy")
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):
@@ -200,6 +203,30 @@ class ShipSim:
                                              _ptr(ep_idx), _ptr(dec_idx), _ptr(out["ticks"]), _ptr(out["decisions"]),
                                              _ptr(log), cap, _ptr(log_len)), "shipsim_run_table")
         self._keep_table = t
+        return out
+
+    def run_policy(self, policy, max_ticks, n_dec, ep_idx, dec_idx, deterministic=False, seed=0, counter=None,
+                   out=None, log=None, log_len=None):
+        """The decision stream with the policy in the loop (shipsim_run_policy). policy: (params_ptr, w2t_ptr,
+        obs_dim, hidden) as SacFused.policy_weights() returns; counter: (1,) int64 device tensor read by the
+        launch (the caller advances it between calls); n_dec: decisions per episode (max_path_length).
+        Other arguments and the result as run_table."""
+        params, w2t, obs_dim, hidden = policy
+        for x in (ep_idx, dec_idx):
+            if x.dtype != torch.int32 or x.device != self.device or x.numel() != self.n_envs:
+                raise ValueError("ep_idx / dec_idx must be int32 device tensors of n_envs elements")
+        if counter is not None and (counter.dtype != torch.int64 or counter.device != self.device):
+            raise ValueError("counter must be an int64 device tensor")
+        if out is None:
+            out = dict(ticks=torch.zeros(self.n_envs, dtype=torch.int32, device=self.device),
+                       decisions=torch.zeros(self.n_envs, dtype=torch.int32, device=self.device))
+        cap = int(log.shape[1]) if log is not None else 0
+        self._follow_stream()
+        self._check(self.L.shipsim_run_policy(self.h, C.c_void_p(params), C.c_void_p(w2t), int(obs_dim), int(hidden),
+                                              int(bool(deterministic)), int(seed) & ((1 << 64) - 1), _ptr(counter),
+                                              int(n_dec), int(max_ticks), _ptr(ep_idx), _ptr(dec_idx),
+                                              _ptr(out["ticks"]), _ptr(out["decisions"]), _ptr(log), cap,
+                                              _ptr(log_len)), "shipsim_run_policy")
         return out
 
     def legacy_step(self, k=1, out=None):

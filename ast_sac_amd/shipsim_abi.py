@@ -13,7 +13,7 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 ENONFINITE = -5  # shipsim_synchronize status (include/shipsim.h)
 MAX_ROUTE = 16
 MAX_POLYS = 16
@@ -28,8 +28,9 @@ MACH_SIMPLIFIED, MACH_DETAILED = 0, 1
 SG_GEN, SG_MOTOR, SG_OFF = 0, 1, 2
 
 # shipsim_run_table per-decision record columns
-DECLOG_COLS = 14
+DECLOG_COLS = 23
 DL_REWARD, DL_EVENTS, DL_DONE, DL_EPISODE, DL_DECISION, DL_TICKS, DL_OBS = 0, 1, 2, 3, 4, 5, 6
+DL_ACTION, DL_OBS0 = 14, 15
 
 # legacy MultiShipEnv termination_conditions bits (shipsim_legacy_step, termination_flags.py:66-68)
 LT_TEST_REACHED = 1 << 0

@@ -114,6 +114,10 @@ int sacf_step_kernel_status(sacf_handle* h);
 int sacf_policy_reserve(sacf_handle* h, int64_t n);
 int sacf_policy_act(sacf_handle* h, const float* obs, int64_t n, int32_t obs_stride, const uint8_t* mask,
                     int32_t deterministic, uint64_t seed, const int64_t* counter, float* act, float* eps_out);
+/* The policy's device parameters (torch order, at the bound params) and the library's current W2ᵀ copy,
+ * with obs_dim and hidden: what shipsim_run_policy reads (each output may be NULL). */
+int sacf_policy_weights(const sacf_handle* h, const float** params, const float** w2t, int32_t* obs_dim,
+                        int32_t* hidden);
 
 #ifdef __cplusplus
 }

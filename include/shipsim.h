@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 6
+#define SHIPSIM_ABI_VERSION 7
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -372,7 +372,7 @@ int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double
  *   decisions_out    N int32: decisions completed in this call (may be NULL)
  *   log              N x log_cap x SHIPSIM_DECLOG_COLS doubles: one record per completed decision
  *                    (may be NULL); log_len N int32 (in/out) counts records (past log_cap too). */
-#define SHIPSIM_DECLOG_COLS 14
+#define SHIPSIM_DECLOG_COLS 23
 #define SHIPSIM_DL_REWARD 0   /* accumulated (un-scaled) reward of the decision */
 #define SHIPSIM_DL_EVENTS 1   /* SHIPSIM_EV_* bits */
 #define SHIPSIM_DL_DONE 2     /* combined_done */
@@ -380,9 +380,35 @@ int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double
 #define SHIPSIM_DL_DECISION 4 /* dec_idx of the decision */
 #define SHIPSIM_DL_TICKS 5    /* _step ticks of the decision (across launches; 0 for a sampling failure) */
 #define SHIPSIM_DL_OBS 6      /* 8 columns: the observation returned */
+#define SHIPSIM_DL_ACTION 14  /* the decision's action: the table's scoping angle / the policy's normalized a */
+#define SHIPSIM_DL_OBS0 15    /* 8 columns: the observation the action was chosen from */
 int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
                       int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
                       int32_t log_cap, int32_t* log_len);
+
+/* The same decision stream with the collector's policy in the loop (ABI 7; also new in 7: the 23-column decision record): every decision's action is
+ * sampled inside the launch from the observation the env returned, by the TanhGaussianPolicy
+ * (gaussian_policy.py:105-118: fc0, relu, fc1, relu, mean / clamped log_std heads) then TanhNormal.sample
+ * (distributions.py:394-425: tanh(mean + std * eps), eps ~ N(0, 1)) or, deterministic != 0,
+ * MakeDeterministic's tanh(mean) (policies/base.py:54-64), and denormalized as NormalizedBoxEnv does
+ * (normalized_box_env.py:48-51) — the rollout loop of rollout_functions.py:53-91 for every env at once,
+ * without a host round trip. fp32 as the policy; the env in fp64.
+ *   policy   the policy's parameters in torch order (fcs[0].weight [H][obs_dim], .bias, fcs[1].weight
+ *            [H][H], .bias, last_fc.weight [1][H], .bias, last_fc_log_std.weight, .bias), device
+ *   w2t      fcs[1].weight transposed ([H][H], w2t[k][u] = W2[u][k]), device (sacf_policy_weights)
+ *   obs_dim  8; hidden 64, 128, 192 or 256
+ *   seed, counter  the noise: eps of env i's s-th decision of a call is Philox4x32-10 keyed by seed on
+ *            {i, *counter (64 bits), 0x5A100000 ^ s} then Box-Muller; *counter is read, not changed —
+ *            advance it between calls (ignored when deterministic; counter may then be NULL)
+ *   n_dec    decisions per episode (max_path_length); other arguments as shipsim_run_table, and the
+ *            decision record's SHIPSIM_DL_ACTION column holds the normalized action a in (-1, 1).
+ *            With a log, an env stops for the launch once it holds log_cap records (log_len starts where
+ *            the caller left it), its next decision pending for the next call: no record is lost.
+ * One obstacle ship only (SHIPSIM_EINVAL otherwise, as for a bad obs_dim / hidden). */
+int shipsim_run_policy(shipsim_handle* h, const float* policy, const float* w2t, int32_t obs_dim, int32_t hidden,
+                       int32_t deterministic, uint64_t seed, const int64_t* counter, int32_t n_dec,
+                       int32_t max_ticks, int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out,
+                       int32_t* decisions_out, double* log, int32_t log_cap, int32_t* log_len);
 
 /* ---- legacy per-tick MultiShipEnv (rl_env/ship_in_transit/env.py:783-1181) ----
  * AST kind. Each of the k ticks is one MultiShipEnv.step() (:1104-1173) of every env: test_step

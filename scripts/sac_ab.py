@@ -29,9 +29,14 @@ def main():
     rb.add_batch(torch.randn(n, 8, device=dev, generator=g) * 1000, torch.rand(n, 1, device=dev, generator=g) * 2 - 1,
                  torch.randn(n, 1, device=dev, generator=g), torch.randn(n, 8, device=dev, generator=g) * 1000,
                  (torch.rand(n, 1, device=dev, generator=g) < 0.1).float())
-    res = {}
+    res, status = {}, {}
     for B in (256, 64, 1024):
-        for persistent in (False, True, False, True):
+        for variant in ("five_launches", "persistent", "persistent_full_barrier", "five_launches", "persistent"):
+            persistent = variant != "five_launches"
+            if variant == "persistent_full_barrier":
+                os.environ["SACF_FULL_BARRIER"] = "1"
+            else:
+                os.environ.pop("SACF_FULL_BARRIER", None)
             torch.manual_seed(0)
             q = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[256, 256]).to(dev) for _ in range(4)]
             pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[256, 256]).to(dev)
@@ -45,10 +50,14 @@ def main():
             tr.train_from_buffer(rb, steps)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            tr._sf.step_kernel_status()
-            key = f"B{B}_{'persistent' if persistent else 'five_launches'}"
+            key = f"B{B}_{variant}"
+            try:
+                tr._sf.step_kernel_status()
+            except Exception as e:  # noqa: BLE001  (reported, the timing kept)
+                status[key] = str(e)
             res.setdefault(key, []).append(steps / dt)
-    print(json.dumps({k: dict(grad_steps_per_s=max(v), runs=v, us_per_step=1e6 / max(v)) for k, v in res.items()}))
+    print(json.dumps({k: dict(grad_steps_per_s=max(v), runs=v, us_per_step=1e6 / max(v), status=status.get(k, "ok"))
+                      for k, v in res.items()}))
 
 
 if __name__ == "__main__":

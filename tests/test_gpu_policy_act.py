@@ -81,9 +81,11 @@ def test_device_policy_matches_torch_policy(H, n):
     assert (act3[~keep] - ref3[~keep]).abs().max().item() < 5e-6
 
 
-def test_graph_replayed_collector_equals_eager_collector():
+@pytest.mark.parametrize("fused", [False, True])
+def test_graph_replayed_collector_equals_eager_collector(fused):
     """A deterministic device-policy collector: the HIP-graph pass and the eager pass produce the same
-    transitions in the same replay rows and the same epoch paths."""
+    transitions in the same replay rows and the same epoch paths (sliced passes, and fused ones with the
+    policy inside the env launch)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from ast_sac_amd.rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, default_args
@@ -95,7 +97,8 @@ def test_graph_replayed_collector_equals_eager_collector():
     for use_graph in (True, False):
         env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), 512), 0.75)
         coll = BatchedPathCollector(env, pol, max_path_length=9, max_ticks=128, deterministic=True,
-                                    device_policy=tr.device_policy(True), use_graph=use_graph)
+                                    device_policy=tr.device_policy(True), use_graph=use_graph, fused=fused)
+        assert coll.fused == fused
         rb = DeviceReplayBuffer(40000, 8, 1, "cuda")
         got = coll.collect(6500, rb, record_paths=True)  # ~15 passes of 128 ticks: episodes end
         torch.cuda.synchronize()
@@ -111,3 +114,79 @@ def test_graph_replayed_collector_equals_eager_collector():
     for (r1, a1), (r2, a2) in zip(p1, p2):
         np.testing.assert_array_equal(r1, r2)
         np.testing.assert_array_equal(a1, a2)
+
+
+def test_fused_collector_rows_and_paths_follow_the_decision_log():
+    """The fused collector's bookkeeping: its replay rows are the policy stream's decision records (good ones,
+    pass by pass, env by env, record by record) with the reward scaled, and its epoch paths are the episodes
+    those records form (rollout_functions.py:161-181) — checked against run_policy driven by hand on a second
+    env with the same policy, slice and log capacity."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from ast_sac_amd import shipsim_abi as abi
+    from ast_sac_amd.rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, default_args
+    from ast_sac_amd.ast_sac.env_wrapper.normalized_box_env import BatchedNormalizedBoxEnv
+    from ast_sac_amd.ast_sac.samplers.data_collector.batched_collector import BatchedPathCollector
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    tr, pol = _trainer(128)
+    N, T, ticks, P, scale = 256, 9, 160, 12, 0.75
+    env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), N), scale)
+    dp = tr.device_policy(True)
+    coll = BatchedPathCollector(env, pol, max_path_length=T, max_ticks=ticks, deterministic=True, device_policy=dp,
+                                use_graph=False)
+    assert coll.fused
+    rb = DeviceReplayBuffer(200000, 8, 1, "cuda")
+    coll._take_over()
+    coll._enter("fused")
+    for _ in range(P):
+        coll._fused_pass(rb, True)
+    coll._drain_ring()
+    torch.cuda.synchronize()
+    # by hand
+    env2 = BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), N)
+    sim = env2.sim
+    sim.reset()
+    cap = coll._log_cap()
+    ep = torch.zeros(N, dtype=torch.int32, device="cuda")
+    dec = torch.zeros(N, dtype=torch.int32, device="cuda")
+    log = torch.zeros((N, cap, abi.DECLOG_COLS), dtype=torch.float64, device="cuda")
+    ln = torch.zeros(N, dtype=torch.int32, device="cuda")
+    rows, paths, cur = [], [], [[] for _ in range(N)]
+    for _ in range(P):
+        ln.zero_()
+        sim.run_policy(dp.weights(), ticks, T, ep, dec, deterministic=True, log=log, log_len=ln)
+        L, n = log.cpu().numpy(), ln.cpu().numpy()
+        assert n.max() <= cap
+        for i in range(N):
+            for r in L[i, :n[i]]:
+                ev = int(r[abi.DL_EVENTS])
+                if not ev & abi.EV_NONFINITE:
+                    rows.append((r[abi.DL_OBS0:abi.DL_OBS0 + 8].astype(np.float32), np.float32(r[abi.DL_ACTION]),
+                                 np.float32(r[abi.DL_REWARD] * scale), r[abi.DL_OBS:abi.DL_OBS + 8].astype(np.float32),
+                                 np.float32(bool(ev & abi.EV_TERMINAL))))
+        for j in range(cap):
+            for i in range(N):
+                if j >= n[i]:
+                    continue
+                r = L[i, j]
+                ev = int(r[abi.DL_EVENTS])
+                if not ev & abi.EV_NONFINITE:
+                    cur[i].append((r[abi.DL_REWARD] * scale, np.float32(r[abi.DL_ACTION])))
+                if r[abi.DL_DONE] or ev & abi.EV_NONFINITE or r[abi.DL_DECISION] + 1 >= T:
+                    if cur[i]:
+                        paths.append(cur[i])
+                    cur[i] = []
+    n_rows = rb.num_steps_can_sample()
+    assert n_rows == len(rows) > 4 * N
+    st = {k: v[:n_rows].cpu().numpy() for k, v in rb._store.items()}
+    np.testing.assert_array_equal(st["observations"], np.stack([r[0] for r in rows]))
+    np.testing.assert_array_equal(st["actions"][:, 0], np.array([r[1] for r in rows]))
+    np.testing.assert_array_equal(st["rewards"][:, 0], np.array([r[2] for r in rows]))
+    np.testing.assert_array_equal(st["next_observations"], np.stack([r[3] for r in rows]))
+    np.testing.assert_array_equal(st["terminals"][:, 0], np.array([r[4] for r in rows]))
+    got = list(coll.get_epoch_paths())
+    assert len(got) == len(paths) > N // 2
+    for g, p in zip(got, paths):
+        np.testing.assert_array_equal(g["rewards"][:, 0], np.array([x[0] for x in p]))
+        np.testing.assert_array_equal(g["actions"][:, 0], np.array([x[1] for x in p]))
+    assert coll.get_diagnostics()["num steps total"] == len(rows)
