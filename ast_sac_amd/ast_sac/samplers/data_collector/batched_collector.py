@@ -218,7 +218,9 @@ class BatchedPathCollector:
             self._act.index_copy_(0, idx, self._actions(self._obs.index_select(0, idx)).to(torch.float32))
 
     def _log_cap(self):
-        return max(4, self.max_ticks // 16)
+        """Decision records per env per fused pass: a decision takes ~100 ticks (RoA + the turn), so a third
+        of that leaves room; an env whose log fills just waits for the next pass (no record is lost)."""
+        return max(4, -(-self.max_ticks // 32))
 
     @torch.no_grad()
     def _fused_pass(self, replay_buffer, record):
@@ -248,12 +250,16 @@ class BatchedPathCollector:
         dec = log[:, :, abi.DL_DECISION].to(torch.int64)
         end = valid & ((log[:, :, abi.DL_DONE] != 0) | nonfinite | (dec + 1 >= T))
         act = log[:, :, abi.DL_ACTION].to(torch.float32)
-        if replay_buffer is not None:
-            replay_buffer.add_batch(log[:, :, abi.DL_OBS0:abi.DL_OBS0 + 8].reshape(N * cap, 8).to(torch.float32),
-                                    act.reshape(N * cap, 1), rew.reshape(N * cap, 1).to(torch.float32),
-                                    log[:, :, abi.DL_OBS:abi.DL_OBS + 8].reshape(N * cap, 8).to(torch.float32),
-                                    ((ev & abi.EV_TERMINAL) != 0).reshape(N * cap, 1).to(torch.float32),
-                                    mask=good.reshape(-1))
+        if replay_buffer is not None:  # env-major, in env chunks no larger than the buffer
+            step = max(1, replay_buffer._max // cap)
+            for a in range(0, N, step):
+                b = min(N, a + step)
+                n = (b - a) * cap
+                replay_buffer.add_batch(log[a:b, :, abi.DL_OBS0:abi.DL_OBS0 + 8].reshape(n, 8).to(torch.float32),
+                                        act[a:b].reshape(n, 1), rew[a:b].reshape(n, 1).to(torch.float32),
+                                        log[a:b, :, abi.DL_OBS:abi.DL_OBS + 8].reshape(n, 8).to(torch.float32),
+                                        ((ev[a:b] & abi.EV_TERMINAL) != 0).reshape(n, 1).to(torch.float32),
+                                        mask=good[a:b].reshape(-1))
         if record:  # record by record, in each env's order: the episode buffers, ended episodes -> the ring
             evi = ev.to(torch.int32)
             for j in range(cap):

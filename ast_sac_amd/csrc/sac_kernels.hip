@@ -1158,44 +1158,78 @@ __device__ __forceinline__ void arrive_and_wait(unsigned* bar, int c, unsigned n
   }
 }
 
-// Grid barrier for passes whose data stay on one XCD (the tile map puts row tile r of every pass on XCD
-// r % 8, so every row a tile reads was written through the same L2): every wave's stores have completed
-// to the L2 (s_waitcnt), the blocks meet on device-coherent counters, and each CU drops its L1 lines
-// before reading what its XCD's other CUs wrote. No L2 write-back or invalidation is needed.
+// L2-resident counters of one XCD: atomics without the device-scope bit execute in the issuing XCD's L2,
+// which every CU of that XCD shares, so the blocks of one XCD can count and poll there (polling by RMW:
+// an atomic never hits the CU's L1) without a trip to memory. Slots: bar[32 + 4x] count, bar[33 + 4x]
+// generation, for XCD x (one 16-byte group per XCD).
+__device__ __forceinline__ unsigned l2_add(unsigned* p, unsigned v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool l2_wait_change(unsigned* w, unsigned old, int* err) {
+  unsigned spins = 0;
+  while (l2_add(w, 0u) == old) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 25)) {
+      atomicOr(err, 1);
+      return false;
+    }
+  }
+  return true;
+}
+__device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7; }  // HW_REG_XCC_ID
+
+// Grid barrier for passes whose data stay on one XCD (the tile map puts row tile r of every pass on the XCD
+// of block class r mod 8, so every row a tile reads was written through the same L2): a pass on XCD x only
+// waits for the other blocks of XCD x. Every wave's stores have completed to the L2 (s_waitcnt), the XCD's
+// blocks meet on counters in that L2, and each CU drops its L1 lines before reading what its XCD's other
+// CUs wrote. No L2 write-back or invalidation, no memory-side atomics.
 __device__ __forceinline__ void grid_barrier_xcd(unsigned* bar, int* err, unsigned nblocks) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (threadIdx.x == 0) arrive_and_wait(bar, 0, nblocks, err);
+  if (threadIdx.x == 0) {
+    unsigned* xb = bar + 32 + 4 * xcc_id();
+    const unsigned per_xcd = nblocks / 8;
+    const unsigned gen = l2_add(xb + 1, 0u);
+    if (l2_add(xb, 1u) == per_xcd - 1) {
+      __hip_atomic_store(xb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      l2_add(xb + 1, 1u);
+    } else {
+      l2_wait_change(xb + 1, gen, err);
+    }
+  }
   __syncthreads();
   asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1
 }
 
-// Grid barrier before the weight-gradient pass, which reads every row from every XCD: after everyone
-// arrived, one block per XCD writes its L2 back (an agent-scope release), and once all eight have, every
-// block invalidates its L1 / L2 (agent-scope acquire) before reading.
+// Grid barrier before the weight-gradient pass, which reads every row from every XCD. The blocks of each
+// XCD meet in its L2 as above; the last one to arrive writes that L2 back (an agent-scope release), counts
+// on the device-wide counter and, once all eight XCDs have, invalidates its XCD's L2 (agent-scope acquire)
+// and releases its XCD's blocks, which drop their L1 lines.
 __device__ __forceinline__ void grid_barrier_dev(unsigned* bar, int* err, unsigned nblocks) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    // (read before arriving: bar[3] cannot advance until every block has arrived)
-    const unsigned gen = __hip_atomic_load(bar + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    arrive_and_wait(bar, 0, nblocks, err);
-    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7;  // HW_REG_XCC_ID
-    if (__hip_atomic_fetch_add(bar + 8 + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+    unsigned* xb = bar + 32 + 4 * xcc_id();
+    const unsigned per_xcd = nblocks / 8;
+    const unsigned gen = l2_add(xb + 1, 0u);
+    if (l2_add(xb, 1u) == per_xcd - 1) {
+      __hip_atomic_store(xb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned dgen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this XCD's L2 written back
-      if (__hip_atomic_fetch_add(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 7) {
-        for (int x = 0; x < 8; ++x) __hip_atomic_store(bar + 8 + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(bar + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(bar + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 7) {
+        __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        wait_change(bar + 3, gen, err);
+        wait_change(bar + 1, dgen, err);
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this XCD's L2 (and L1) invalidated
+      l2_add(xb + 1, 1u);
     } else {
-      wait_change(bar + 3, gen, err);
+      l2_wait_change(xb + 1, gen, err);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
+  asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1
 }
 
 // Every block arrives once per barrier; the last one to arrive resets the count and advances the
@@ -1245,7 +1279,7 @@ __global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg
   const int B = persist_args().m.L.B;
   const bool local = persist_args().xcd_local;
   if (local && threadIdx.x == 0) {  // the tile map's assumption: blocks congruent mod 8 share an XCD
-    const unsigned xcc = (__builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15) + 1;  // HW_REG_XCC_ID
+    const unsigned xcc = xcc_id() + 1;
     const unsigned seen = atomicCAS(persist_args().bar + 24 + blockIdx.x % 8, 0u, xcc);
     if (seen != 0u && seen != xcc) atomicOr(persist_args().err, 2 | (int)(xcc << 8) | (int)(seen << 16));
   }
@@ -1719,10 +1753,11 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     wg.hp = h->hp;
   }
   if (cfg->step_kernel == 1) {  // persistent single-launch step: barrier state and a co-resident grid
-    // [0..3] XCD-local / dev barriers, [4..5] full, [8..15] XCD election, [16] error flag, [24..31] the
-    // XCD of each block residue mod 8 (+1, 0 = not seen yet)
-    e = hipMalloc(&h->bar, 32 * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemset(h->bar, 0, 32 * sizeof(unsigned));
+    // [0..1] device-wide count / generation of grid_barrier_dev, [4..5] grid_barrier, [16] error flag,
+    // [24..31] the XCD of each block residue mod 8 (+1, 0 = not seen yet), [32 + 4x, 33 + 4x] XCD x's
+    // L2-resident count / generation
+    e = hipMalloc(&h->bar, 64 * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(h->bar, 0, 64 * sizeof(unsigned));
     int per_cu = 0, cus = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = persistent_occupancy(H, &per_cu);

@@ -976,7 +976,7 @@ __device__ __forceinline__ float wave_sum_f(float x) {  // butterfly: every lane
 // Must be called by every lane of the wave. want: this lane's env needs its next action (all lanes of an
 // env agree); ns: its observation; seq: the env's decisions completed in this call (noise stream index).
 // Returns the normalized action a in (-1, 1) for lanes whose env wanted one.
-__device__ float policy_actions(bool want, const float ns[8], int env, bool env_leader, int env_lane0, int seq,
+__device__ __forceinline__ float policy_actions(bool want, const float ns[8], int env, bool env_leader, int env_lane0, int seq,
                                 const ChainArgs& CH, float* lds_h1) {
   uint64_t req = __ballot(want && env_leader);
   float act = 0.0f;
@@ -988,22 +988,28 @@ __device__ float policy_actions(bool want, const float ns[8], int env, bool env_
   const float* wm = b2 + H;
   const float* ws = wm + H + 1;
   while (req) {
-    int src[kPolMaxRows];
+    // the next (up to) kPolMaxRows requesting envs: the lowest set bits of req (no indexed arrays: row e's
+    // source lane is recomputed from the mask, so nothing lands in scratch)
+    uint64_t rows = req;
     int E = 0;
-    while (req && E < kPolMaxRows) {
-      src[E++] = __ffsll((unsigned long long)req) - 1;
-      req &= req - 1;
-    }
+    for (uint64_t m = req; m && E < kPolMaxRows; m &= m - 1) ++E;
+    for (int e = 0; e < E; ++e) req &= req - 1;
     // fc0 + relu for every row, into LDS
-    for (int e = 0; e < E; ++e) {
-      float x[8];
+    {
+      uint64_t m = rows;
+      for (int e = 0; e < E; ++e, m &= m - 1) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        float x[8];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) x[m] = __shfl(ns[m], src[e], 64);
-      for (int j = 0; j < nj; ++j) {
-        const int u = lane + 64 * j;
-        float h = b1[u];
-        for (int m = 0; m < O; ++m) h = fmaf(W1[(size_t)u * O + m], x[m], h);
-        lds_h1[e * kPolMaxHidden + u] = fmaxf(h, 0.0f);
+        for (int i = 0; i < 8; ++i) x[i] = __shfl(ns[i], src, 64);
+        for (int j = 0; j < nj; ++j) {
+          const int u = lane + 64 * j;
+          float h = b1[u];
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (i < O) h = fmaf(W1[(size_t)u * O + i], x[i], h);  // (O == 8: checked by the host)
+          lds_h1[e * kPolMaxHidden + u] = fmaxf(h, 0.0f);
+        }
       }
     }
     __syncthreads();  // (one wave per block)
@@ -1023,14 +1029,15 @@ __device__ float policy_actions(bool want, const float ns[8], int env, bool env_
         for (int j = 0; j < kPolMaxHidden / 64; ++j) w[kk][j] = j < nj ? CH.w2t[(size_t)(k + kk) * H + lane + 64 * j] : 0.0f;
 #pragma unroll
       for (int e = 0; e < kPolMaxRows; ++e) {
-        if (e >= E) break;
-        const float4 h4 = *reinterpret_cast<const float4*>(lds_h1 + e * kPolMaxHidden + k);
+        if (e < E) {
+          const float4 h4 = *reinterpret_cast<const float4*>(lds_h1 + e * kPolMaxHidden + k);
 #pragma unroll
-        for (int j = 0; j < kPolMaxHidden / 64; ++j) {
-          acc[e][j] = fmaf(w[0][j], h4.x, acc[e][j]);
-          acc[e][j] = fmaf(w[1][j], h4.y, acc[e][j]);
-          acc[e][j] = fmaf(w[2][j], h4.z, acc[e][j]);
-          acc[e][j] = fmaf(w[3][j], h4.w, acc[e][j]);
+          for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+            acc[e][j] = fmaf(w[0][j], h4.x, acc[e][j]);
+            acc[e][j] = fmaf(w[1][j], h4.y, acc[e][j]);
+            acc[e][j] = fmaf(w[2][j], h4.z, acc[e][j]);
+            acc[e][j] = fmaf(w[3][j], h4.w, acc[e][j]);
+          }
         }
       }
     }
@@ -1043,29 +1050,33 @@ __device__ float policy_actions(bool want, const float ns[8], int env, bool env_
     }
     const float bm = wm[H], bs = ws[H];
     const uint64_t ctr = CH.pol_counter ? (uint64_t)*CH.pol_counter : 0;
+    uint64_t m = rows;
 #pragma unroll
     for (int e = 0; e < kPolMaxRows; ++e) {
-      if (e >= E) break;
-      float pm = 0.0f, ps = 0.0f;
+      if (e < E) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        float pm = 0.0f, ps = 0.0f;
 #pragma unroll
-      for (int j = 0; j < kPolMaxHidden / 64; ++j) {
-        const float y = fmaxf(acc[e][j], 0.0f);
-        pm = fmaf(wmj[j], y, pm);
-        ps = fmaf(wsj[j], y, ps);
+        for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+          const float y = fmaxf(acc[e][j], 0.0f);
+          pm = fmaf(wmj[j], y, pm);
+          ps = fmaf(wsj[j], y, ps);
+        }
+        const float mean = wave_sum_f(pm) + bm;
+        const float log_std = fminf(fmaxf(wave_sum_f(ps) + bs, -20.0f), 2.0f);
+        float z = mean;
+        if (!CH.pol_det) {
+          const int e_env = __shfl(env, src, 64), e_seq = __shfl(seq, src, 64);
+          uint32_t c[4] = {(uint32_t)e_env, (uint32_t)ctr, (uint32_t)(ctr >> 32), 0x5A100000u ^ (uint32_t)e_seq};
+          philox_env(c, (uint32_t)CH.pol_seed, (uint32_t)(CH.pol_seed >> 32));
+          const float u1 = ((float)c[0] + 1.0f) * 2.3283064365386963e-10f;
+          const float u2 = (float)c[1] * 2.3283064365386963e-10f;
+          z = mean + expf(log_std) * (sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2));
+        }
+        const float a = tanhf(z);
+        if (env_lane0 == src) act = a;
       }
-      const float mean = wave_sum_f(pm) + bm;
-      const float log_std = fminf(fmaxf(wave_sum_f(ps) + bs, -20.0f), 2.0f);
-      float z = mean;
-      if (!CH.pol_det) {
-        const int e_env = __shfl(env, src[e], 64), e_seq = __shfl(seq, src[e], 64);
-        uint32_t c[4] = {(uint32_t)e_env, (uint32_t)ctr, (uint32_t)(ctr >> 32), 0x5A100000u ^ (uint32_t)e_seq};
-        philox_env(c, (uint32_t)CH.pol_seed, (uint32_t)(CH.pol_seed >> 32));
-        const float u1 = ((float)c[0] + 1.0f) * 2.3283064365386963e-10f;
-        const float u2 = (float)c[1] * 2.3283064365386963e-10f;
-        z = mean + expf(log_std) * (sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2));
-      }
-      const float a = tanhf(z);
-      if (env_lane0 == src[e]) act = a;
     }
     __syncthreads();  // lds_h1 free for the next pass
   }
@@ -1897,7 +1908,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     if (AE.ready_out) AE.ready_out[env] = ready ? 1 : 0;
   }
   if (ready && AE.obs_out && sub == 0 && ship < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
-    for (int i = 0; i < 4; ++i) AE.obs_out[env * 8 + ship * 4 + i] = ns[ship * 4 + i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) AE.obs_out[env * 8 + ship * 4 + i] = ship ? ns[4 + i] : ns[i];  // (no indexed ns)
   }
 }
 

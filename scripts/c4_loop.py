@@ -54,13 +54,22 @@ def main():
     s1, k1 = counters()
     res["collect"] = dict(decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
                           env_ticks_per_s=(k1 - k0) / t)
-    for sl in (32, 64, 128, 256, 512):  # slice length: envs idle after their decision until the pass ends
-        coll.max_ticks = sl
-        s0, k0 = counters()
-        _, t = timed(lambda: coll.collect(32 * n_envs, rb))
-        s1, k1 = counters()
-        res[f"collect_slice{sl}"] = dict(decisions=s1 - s0, env_ticks=k1 - k0, seconds=t,
-                                         decisions_per_s=(s1 - s0) / t, env_ticks_per_s=(k1 - k0) / t)
+    res["collect"]["fused"] = coll.fused
+    fused0 = coll.fused
+    # sliced passes (policy launch + env slice; an env idles after its decision until the pass ends) and,
+    # when the env library can run the policy, fused passes (policy inside the env launch)
+    for fused in ([False, True] if fused0 else [False]):
+        coll.fused = fused
+        for sl in ((128, 256, 512, 1024, 2048) if fused else (32, 64, 128, 256, 512)):
+            coll.max_ticks = sl
+            coll.collect(4 * n_envs, rb)  # warm-up (graph capture of this slice length)
+            s0, k0 = counters()
+            _, t = timed(lambda: coll.collect(32 * n_envs, rb))
+            s1, k1 = counters()
+            res[f"collect_{'fused' if fused else 'sliced'}{sl}"] = dict(
+                decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
+                env_ticks_per_s=(k1 - k0) / t)
+    coll.fused = fused0
     coll.max_ticks = args.slice_ticks
     # SAC alone
     n_sac = 2400
