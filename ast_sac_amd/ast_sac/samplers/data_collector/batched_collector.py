@@ -113,7 +113,7 @@ class BatchedPathCollector:
         wrapper's action bounds equal to the env's (so the in-kernel NormalizedBoxEnv mapping is the
         wrapper's)."""
         dp = self._device_policy
-        if dp is None or not hasattr(dp, "weights") or self.device.type != "cuda":
+        if dp is None or not hasattr(dp, "weights"):
             return False
         base = self._base_env()
         sim = getattr(base, "sim", None)

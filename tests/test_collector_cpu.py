@@ -289,3 +289,132 @@ def test_shared_env_eval_then_expl_resets_and_restarts_episodes():
     # after the takeover the eval collector's episodes all restarted at decision 0
     paths = ev.get_epoch_paths()
     assert all(len(p["actions"]) >= 1 for p in paths)
+
+
+class _PolicySim:
+    """Stands in for ShipSim.run_policy (shipsim_run_policy's contract, include/shipsim.h): env i
+    completes (i + call) % 4 decisions per call (at most the room left in its log), decision d of an
+    episode returns obs (i, d + 1, ep, ...), the episode ends by done after 2 + i % 5 decisions or by the
+    n_dec cut, env 3's second decision ends non-finite (EV_NONFINITE, done)."""
+    n_ships = 2
+
+    def __init__(self, n):
+        self.n, self.calls = n, 0
+        self.obs = torch.zeros((n, 8), dtype=torch.float64)
+        self.obs[:, 0] = torch.arange(n)
+        self.cfg = abi.Config()
+        self.cfg.normalize_action = 0
+        self.cfg.action_low, self.cfg.action_high = float(np.float32(-np.deg2rad(30))), float(np.float32(np.deg2rad(30)))
+
+    def synchronize(self):
+        pass
+
+    def run_policy(self, weights, max_ticks, n_dec, ep, dec, deterministic=False, seed=0, counter=None, out=None,
+                   log=None, log_len=None):
+        cap = log.shape[1]
+        for i in range(self.n):
+            k = min((i + self.calls) % 4, cap - int(log_len[i]))
+            for _ in range(k):
+                d, e = int(dec[i]), int(ep[i])
+                nonfinite = i == 3 and d == 1
+                done = nonfinite or d + 1 >= 2 + i % 5
+                rec = log[i, int(log_len[i])]
+                rec.zero_()
+                rec[abi.DL_OBS0:abi.DL_OBS0 + 8] = self.obs[i]
+                rec[abi.DL_ACTION] = float(np.float32(np.tanh(0.01 * i + 0.1 * d - 0.05 * e)))
+                rec[abi.DL_REWARD] = 10.0 * i + d
+                ev = (abi.EV_TERMINAL | abi.EV_TEST_STOP) if done else 0
+                rec[abi.DL_EVENTS] = ev | (abi.EV_NONFINITE | abi.EV_TERMINAL if nonfinite else 0)
+                rec[abi.DL_DONE] = float(done)
+                rec[abi.DL_EPISODE], rec[abi.DL_DECISION], rec[abi.DL_TICKS] = e, d, 37
+                nxt = torch.tensor([i, d + 1, e, 0, 0, 0, 0, 0], dtype=torch.float64)
+                rec[abi.DL_OBS:abi.DL_OBS + 8] = nxt
+                log_len[i] += 1
+                if done or d + 1 >= n_dec:
+                    ep[i] += 1
+                    dec[i] = 0
+                    self.obs[i] = torch.tensor([i, 0, e + 1, 0, 0, 0, 0, 0], dtype=torch.float64)
+                else:
+                    dec[i] += 1
+                    self.obs[i] = nxt
+            out["ticks"][i] = 37 * k
+            out["decisions"][i] = k
+        self.calls += 1
+        return out
+
+
+class _PolicyEnv(_ScriptedEnv):
+    def __init__(self, n):
+        super().__init__(n)
+        self.sim = _PolicySim(n)
+        self._lb, self._ub = self.sim.cfg.action_low, self.sim.cfg.action_high
+
+
+class _DevicePolicy:
+    deterministic, seed = True, 5
+
+    def __init__(self):
+        self.counter = torch.zeros(1, dtype=torch.int64)
+
+    def reserve(self, n):
+        pass
+
+    def weights(self):
+        return (0, 0, 8, 64)
+
+
+def test_fused_pass_rows_and_paths_follow_the_decision_log():
+    """Fused collection (the policy inside the env launch, shipsim_run_policy): the decision log becomes
+    replay rows (good records, env by env) and reference-shaped epoch paths (records in each env's order;
+    a non-finite record ends its episode without a transition), with the counters the sliced pass keeps."""
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    N, T = 12, 4
+    env = _PolicyEnv(N)
+    coll = BatchedPathCollector(env, _Policy(), max_path_length=T, max_ticks=64, deterministic=True,
+                                device_policy=_DevicePolicy(), use_graph=False)
+    assert coll.fused and coll._log_cap() == 4
+    rb = DeviceReplayBuffer(1000, 8, 1, "cpu")
+    got = coll.collect(60, rb, record_paths=True)
+    # expected, from the same log by hand: re-run the scripted sim for the same number of calls
+    ref, calls = _PolicySim(N), env.sim.calls
+    ep = torch.zeros(N, dtype=torch.int32)
+    dec = torch.zeros(N, dtype=torch.int32)
+    cap = 4
+    log = torch.zeros((N, cap, abi.DECLOG_COLS), dtype=torch.float64)
+    ln = torch.zeros(N, dtype=torch.int32)
+    rows, paths, cur = [], [], [[] for _ in range(N)]
+    for _ in range(calls):
+        ln.zero_()
+        ref.run_policy(None, 64, T, ep, dec, log=log, log_len=ln,
+                       out=dict(ticks=torch.zeros(N, dtype=torch.int32), decisions=torch.zeros(N, dtype=torch.int32)))
+        for i in range(N):
+            for r in log[i, :int(ln[i])]:
+                if not int(r[abi.DL_EVENTS]) & abi.EV_NONFINITE:
+                    rows.append((r[abi.DL_OBS0:abi.DL_OBS0 + 8].float(), float(np.float32(r[abi.DL_ACTION])),
+                                 float(np.float32(r[abi.DL_REWARD] * 0.5)), float(bool(int(r[abi.DL_EVENTS]) & abi.EV_TERMINAL))))
+        for j in range(cap):
+            for i in range(N):
+                if j >= int(ln[i]):
+                    continue
+                r = log[i, j]
+                nf = int(r[abi.DL_EVENTS]) & abi.EV_NONFINITE
+                if not nf:
+                    cur[i].append(float(r[abi.DL_REWARD]) * 0.5)
+                if r[abi.DL_DONE] or nf or r[abi.DL_DECISION] + 1 >= T:
+                    if cur[i]:
+                        paths.append(cur[i])
+                    cur[i] = []
+    n = rb.num_steps_can_sample()
+    assert got == n == len(rows) >= 60
+    st = rb._store
+    for k, (o, a, r, t) in enumerate(rows):
+        assert torch.equal(st["observations"][k], o)
+        assert float(st["actions"][k, 0]) == a and float(st["rewards"][k, 0]) == r and float(st["terminals"][k, 0]) == t
+    got_paths = list(coll.get_epoch_paths())
+    assert len(got_paths) == len(paths) > N
+    for g, p in zip(got_paths, paths):
+        np.testing.assert_array_equal(g["rewards"][:, 0], np.array(p))
+    assert any(len(p) == T for p in paths) and any(len(p) < T for p in paths)
+    d = coll.device_diagnostics()
+    assert d["num nonfinite decisions dropped"] >= 1 and d["num env ticks total"] > 0
+    assert coll.get_diagnostics()["num steps total"] == got
