@@ -125,8 +125,8 @@ class BatchedPathCollector:
         cfg = sim.cfg
         lb, ub = (-1.0, 1.0) if cfg.normalize_action else (cfg.action_low, cfg.action_high)
         w = self._env
-        return (np.float32(getattr(w, "_lb", np.nan)) == np.float32(lb) and
-                np.float32(getattr(w, "_ub", np.nan)) == np.float32(ub))
+        return bool(np.float32(getattr(w, "_lb", np.nan)) == np.float32(lb) and
+                    np.float32(getattr(w, "_ub", np.nan)) == np.float32(ub))
 
     def _base_env(self):
         e = self._env

@@ -1186,8 +1186,9 @@ __device__ __forceinline__ const StepArgs& step_args() {
 // SLOTS (2, 4, 8): ship slots per env. 2 is the reference's two-ship env (lane & 1 = ship); with
 // K > 1 obstacle ships (shipsim_create) ship k sits on the lanes of index k mod SLOTS, and slots past
 // the env's last ship repeat that ship (ghost lanes: same state and arithmetic, never stored).
-template <bool DETAILED, int COLLAV, int LPE, bool REC, bool CHAIN = false, int SLOTS = 2>
+template <bool DETAILED, int COLLAV, int LPE, bool REC, int CHAIN = 0, int SLOTS = 2>
 __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
+  constexpr bool POLICY = CHAIN == 2;  // CHAIN: 0 shipsim_step, 1 shipsim_run_table, 2 shipsim_run_policy
   (void)A_arg;  // read through step_args() only (see StepArgs)
   const StepArgs& A0 = step_args();
   const Params& P = A0.P;
@@ -1205,7 +1206,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
-  __shared__ float lds_pol[CHAIN ? kPolMaxRows * kPolMaxHidden : 1];  // shipsim_run_policy: h1 rows
+  __shared__ float lds_pol[POLICY ? kPolMaxRows * kPolMaxHidden : 1];  // shipsim_run_policy: h1 rows
 #ifdef SHIPSIM_POISON_LDS
   // diagnostics build (scripts, not the product): every LDS word gets a pattern before staging, so a
   // read of LDS the kernel did not write sees the pattern instead of another kernel's leftovers
@@ -1403,29 +1404,26 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   // sample (wave-cooperative, shipsim_run_policy). Wave-uniform. sa: the scoping angle to run, a_log:
   // the action as the decision record reports it (the table's angle / the policy's normalized action).
   auto chain_action = [&](bool want, float& a_log) __attribute__((always_inline)) -> float {
-    const StepArgs& A = step_args();
-    const ChainArgs& CH = A.CH;
-#ifndef SHIPSIM_NO_POLICY_STREAM  // (A/B builds only: the open-loop stream without the policy code)
-    if (CH.policy == nullptr)
-#endif
-    {
+    if constexpr (!POLICY) {
       a_log = want ? table_action() : 0.0f;
       return a_log;
+    } else {
+      const StepArgs& A = step_args();
+      a_log = policy_actions(want, ns, envc, lie == 0, env_lane0, n_decided, A.CH, lds_pol);
+      const Params& P = A.P;
+      const float lb = P.normalize_action ? -1.0f : P.action_low, ub = P.normalize_action ? 1.0f : P.action_high;
+      return denormalize_f32(a_log, lb, ub);  // NormalizedBoxEnv in front of the env
     }
-    a_log = policy_actions(want, ns, envc, lie == 0, env_lane0, n_decided, CH, lds_pol);
-    const Params& P = A.P;
-    const float lb = P.normalize_action ? -1.0f : P.action_low, ub = P.normalize_action ? 1.0f : P.action_high;
-    return denormalize_f32(a_log, lb, ub);  // NormalizedBoxEnv in front of the env
   };
   // Decisions of the wave just completed (ready): record them, reset envs whose episode ended (done, or
   // n_dec decisions = the rollout's max_path_length), start each env's next decision. A sampling failure
   // completes the new decision at once (no tick), hence the loop; after kChainBurst such back-to-back
   // decisions (actions that all fail their sampling) the env stops for this launch with the last decision
   // recorded and the next one pending (DF_AWAITING): the wave keeps ticking its other envs and the next
-  // launch resumes exactly there, so results do not depend on the burst bound. Wave-uniform (the policy
-  // is evaluated by the whole wave).
+  // launch resumes exactly there, so results do not depend on the burst bound. With the policy the loop is
+  // wave-uniform (the policy is evaluated by the whole wave); with the table each env loops on its own.
   auto chain_next = [&]() __attribute__((always_inline)) {
-    for (int burst = 0; __any(ready && running); ++burst) {
+    for (int burst = 0; POLICY ? __any(ready && running) : (ready && running); ++burst) {
       bool want = false;
       if (ready && running) {
         const ChainArgs& CH = step_args().CH;
@@ -1853,7 +1851,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     PT_MARK(3);
   }
   if (!CHAIN) break;
-  chain_next();  // (wave-uniform: a no-op unless a decision of the wave completed)
+  if (POLICY || (ready && running)) chain_next();  // (policy: wave-uniform, a no-op unless a decision completed)
   going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
   if (!__any(going)) break;
   }
@@ -2281,7 +2279,7 @@ static void launch_step(shipsim_handle* h, int lpe, const float* action, const u
 // K > 1 obstacle ships (detailed machinery, collav none / sbmpc): 16 lanes per env in 4 or 8 ship slots
 static int ship_slots(const shipsim_handle* h) { return h->P.n_ships <= 2 ? 2 : (h->P.n_ships <= 4 ? 4 : 8); }
 
-template <int CA, bool CHAIN>
+template <int CA, int CHAIN>
 static void launch_multi(shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks,
                          float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
                          int32_t* ticks_out, uint8_t* ready_out, const ChainArgs& ch) {
@@ -2842,10 +2840,10 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
 #else
   if (ship_slots(h) > 2) {
     if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
-      launch_multi<SHIPSIM_COLLAV_SBMPC, false>(h, action, active, max_ticks, obs_out, reward_out, done_out,
+      launch_multi<SHIPSIM_COLLAV_SBMPC, 0>(h, action, active, max_ticks, obs_out, reward_out, done_out,
                                                 events_out, ticks_out, ready_out, ChainArgs{});
     else
-      launch_multi<SHIPSIM_COLLAV_NONE, false>(h, action, active, max_ticks, obs_out, reward_out, done_out,
+      launch_multi<SHIPSIM_COLLAV_NONE, 0>(h, action, active, max_ticks, obs_out, reward_out, done_out,
                                                events_out, ticks_out, ready_out, ChainArgs{});
     HIPCHK(h, hipGetLastError());
     return SHIPSIM_OK;
@@ -2877,7 +2875,10 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
   return SHIPSIM_OK;
 }
 
-// the decision-stream launch shared by shipsim_run_table and shipsim_run_policy
+}  // extern "C"
+
+// the decision-stream launch shared by shipsim_run_table (MODE 1) and shipsim_run_policy (MODE 2)
+template <int MODE>
 static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, int32_t* ticks_out) {
   DeviceGuard g(h->device);
   // lanes per env: 16 (default) or 8 / 4 (more envs per wave when the handle holds more envs than
@@ -2885,7 +2886,7 @@ static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, 
   const int lpe = (h->lpe == 8 || h->lpe == 4) ? h->lpe : (h->lpe == 2 ? 4 : 16);
   const int threads = 64, blocks = (h->P.n_envs * lpe + threads - 1) / threads;
 #define CHAINED_L(D, CA, LPE)                                                                                          \
-  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, true>), dim3(blocks), dim3(threads), 0, h->stream,        \
+  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, MODE>), dim3(blocks), dim3(threads), 0, h->stream,        \
                      step_args_of(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out,     \
                                   nullptr, ch))
 #define CHAINED(D, CA)                              \
@@ -2900,13 +2901,13 @@ static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, 
   else CHAINED_L(true, SHIPSIM_COLLAV_NONE, 16);
   (void)det;
 #else
-  if (ship_slots(h) > 2) {
+  if (MODE == 1 && ship_slots(h) > 2) {  // (run_policy refuses K > 1 before it gets here)
     if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
-      launch_multi<SHIPSIM_COLLAV_SBMPC, true>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr,
-                                               ticks_out, nullptr, ch);
+      launch_multi<SHIPSIM_COLLAV_SBMPC, 1>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr,
+                                            ticks_out, nullptr, ch);
     else
-      launch_multi<SHIPSIM_COLLAV_NONE, true>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr,
-                                              ticks_out, nullptr, ch);
+      launch_multi<SHIPSIM_COLLAV_NONE, 1>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr,
+                                           ticks_out, nullptr, ch);
     HIPCHK(h, hipGetLastError());
     return SHIPSIM_OK;
   }
@@ -2922,6 +2923,8 @@ static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, 
   return SHIPSIM_OK;
 }
 
+extern "C" {
+
 int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
                       int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
                       int32_t log_cap, int32_t* log_len) {
@@ -2933,7 +2936,7 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
   ChainArgs ch = {};
   ch.table = table; ch.n_eps = n_eps; ch.n_dec = n_dec; ch.ep_idx = ep_idx; ch.dec_idx = dec_idx;
   ch.decisions = decisions_out; ch.log = log; ch.log_len = log_len; ch.log_cap = log_cap;
-  return run_chain(h, ch, max_ticks, ticks_out);
+  return run_chain<1>(h, ch, max_ticks, ticks_out);
 }
 
 int shipsim_run_policy(shipsim_handle* h, const float* policy, const float* w2t, int32_t obs_dim, int32_t hidden,
@@ -2955,7 +2958,7 @@ int shipsim_run_policy(shipsim_handle* h, const float* policy, const float* w2t,
   ch.log_stop = log ? 1 : 0;
   ch.policy = policy; ch.w2t = w2t; ch.pol_obs = obs_dim; ch.pol_hidden = hidden; ch.pol_det = deterministic ? 1 : 0;
   ch.pol_seed = seed; ch.pol_counter = counter;
-  return run_chain(h, ch, max_ticks, ticks_out);
+  return run_chain<2>(h, ch, max_ticks, ticks_out);
 }
 
 int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_t* done_out, uint32_t* status_out) {

@@ -4,6 +4,6 @@ set -eu
 R=$(cd "$(dirname "$0")/.." && pwd); D=$R/ast_sac_amd/lib/abl; mkdir -p $D
 F="-O3 --offload-arch=gfx950 -ffp-contract=off -fPIC -shared -std=c++17 -I$R/include -I$R/ast_sac_amd/csrc"
 S=$R/ast_sac_amd/csrc/shipsim_kernels.hip
-/opt/rocm/bin/hipcc $F -DSHIPSIM_SRC_HASH='"abl-nopol"' -DSHIPSIM_NO_POLICY_STREAM $S -o $D/lib_nopol.so &
+
 /opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=iterative-ilp -DSHIPSIM_SRC_HASH='"abl-ilp"' $S -o $D/lib_ilp.so &
 wait
