@@ -1127,135 +1127,58 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
 struct PArgs {
   MArgs m;
   WgArgs w;
-  unsigned* bar;  // barrier state (16 words, all back at rest after a launch), see grid_barrier_*
-  int* err;       // set when a barrier wait exceeds its bound (blocks not co-resident) or a block is not
-                  // on the XCD the tile map assumes: results invalid
-  int xcd_local;  // 1: the passes' row data never leave an XCD (B % 256 == 0), see grid_barrier_xcd
+  unsigned* bar;  // barrier words (kBarWords, zeroed before every launch), see grid_barrier
+  int* err;       // set when a barrier wait exceeds its bound (blocks not co-resident, or not dealt evenly over
+                  // the XCDs): results invalid
 };
 
-// bounded wait until *w != old (relaxed agent-scope loads); false (and *err set) when the bound is hit
-__device__ __forceinline__ bool wait_change(unsigned* w, unsigned old, int* err) {
-  unsigned spins = 0;
-  while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == old) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 25)) {
-      atomicOr(err, 1);
-      return false;
-    }
-  }
-  return true;
-}
+// Barrier words, each counter on a 128-byte line of its own: [0] arrivals of the XCD leaders, [32] the top
+// generation, [64 + 64x] arrivals on XCD x, [96 + 64x] XCD x's generation. Zeroed by a memset node ahead of
+// every launch, so counts and generations run from 0 within the launch (barrier b waits for b + 1).
+constexpr int kBarWords = 64 + 64 * 8;
 
-// everyone arrived: count on bar[c], the last arrival resets it and advances bar[c + 1]
-__device__ __forceinline__ void arrive_and_wait(unsigned* bar, int c, unsigned n, int* err) {
-  const unsigned gen = __hip_atomic_load(bar + c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned prev = __hip_atomic_fetch_add(bar + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (prev == n - 1) {
-    __hip_atomic_store(bar + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(bar + c + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    wait_change(bar + c + 1, gen, err);
-  }
-}
-
-// L2-resident counters of one XCD: atomics without the device-scope bit execute in the issuing XCD's L2,
-// which every CU of that XCD shares, so the blocks of one XCD can count and poll there (polling by RMW:
-// an atomic never hits the CU's L1) without a trip to memory. Slots: bar[32 + 4x] count, bar[33 + 4x]
-// generation, for XCD x (one 16-byte group per XCD).
-__device__ __forceinline__ unsigned l2_add(unsigned* p, unsigned v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ bool l2_wait_change(unsigned* w, unsigned old, int* err) {
-  unsigned spins = 0;
-  while (l2_add(w, 0u) == old) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 25)) {
-      atomicOr(err, 1);
-      return false;
-    }
-  }
-  return true;
-}
 __device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7; }  // HW_REG_XCC_ID
 
-// Grid barrier for passes whose data stay on one XCD (the tile map puts row tile r of every pass on the XCD
-// of block class r mod 8, so every row a tile reads was written through the same L2): a pass on XCD x only
-// waits for the other blocks of XCD x. Every wave's stores have completed to the L2 (s_waitcnt), the XCD's
-// blocks meet on counters in that L2, and each CU drops its L1 lines before reading what its XCD's other
-// CUs wrote. No L2 write-back or invalidation, no memory-side atomics.
-__device__ __forceinline__ void grid_barrier_xcd(unsigned* bar, int* err, unsigned nblocks) {
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* xb = bar + 32 + 4 * xcc_id();
-    const unsigned per_xcd = nblocks / 8;
-    const unsigned gen = l2_add(xb + 1, 0u);
-    if (l2_add(xb, 1u) == per_xcd - 1) {
-      __hip_atomic_store(xb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      l2_add(xb + 1, 1u);
-    } else {
-      l2_wait_change(xb + 1, gen, err);
+// bounded relaxed agent-scope poll (global_load sc1: L1 bypassed) until *w >= want; false (and *err set)
+// when the bound is hit
+__device__ __forceinline__ bool poll_ge(unsigned* w, unsigned want, int* err) {
+  for (unsigned spins = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want;) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 20)) {  // (a legitimate wait is microseconds)
+      atomicOr(err, 1);
+      return false;
     }
   }
-  __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1
+  return true;
 }
 
-// Grid barrier before the weight-gradient pass, which reads every row from every XCD. The blocks of each
-// XCD meet in its L2 as above; the last one to arrive writes that L2 back (an agent-scope release), counts
-// on the device-wide counter and, once all eight XCDs have, invalidates its XCD's L2 (agent-scope acquire)
-// and releases its XCD's blocks, which drop their L1 lines.
-__device__ __forceinline__ void grid_barrier_dev(unsigned* bar, int* err, unsigned nblocks) {
-  __builtin_amdgcn_s_waitcnt(0);
+// Grid barrier b of a launch, XCD-hierarchical (MI355X_MICROARCH.md "barrier-xcd", cdna_hip_programming.md
+// §6 Guideline 16): every wave's stores drained (vmcnt 0); one lane per block arrives on its XCD's counter;
+// the XCD's last arrival writes that XCD's L2 back (agent release), arrives on the top counter and waits for
+// all eight XCDs, then bumps its XCD's generation; every block then takes an agent-scope acquire (drops its
+// CU's L1) before the next pass reads. Placement-independent for correctness: the XCD only groups the
+// counting (nblocks / 8 per XCD, as the round-robin deal gives for a grid that is a multiple of 8; an
+// uneven deal times out into *err instead of hanging).
+__device__ __forceinline__ void grid_barrier(unsigned* bar, int* err, unsigned nblocks, unsigned b) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned* xb = bar + 32 + 4 * xcc_id();
-    const unsigned per_xcd = nblocks / 8;
-    const unsigned gen = l2_add(xb + 1, 0u);
-    if (l2_add(xb, 1u) == per_xcd - 1) {
-      __hip_atomic_store(xb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const unsigned dgen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this XCD's L2 written back
-      if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 7) {
-        __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        wait_change(bar + 1, dgen, err);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this XCD's L2 (and L1) invalidated
-      l2_add(xb + 1, 1u);
+    const unsigned x = xcc_id(), per_xcd = nblocks / 8, epoch = b + 1;
+    unsigned* xcnt = bar + 64 + 64 * x;
+    unsigned* xgen = xcnt + 32;
+    const unsigned old = __hip_atomic_fetch_add(xcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == epoch * per_xcd - 1) {  // this XCD's last arrival
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (kept: the fence's own wait can be dropped)
+      const unsigned t = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == epoch * 8 - 1) __hip_atomic_store(bar + 32, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else poll_ge(bar + 32, epoch, err);
+      __hip_atomic_store(xgen, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      l2_wait_change(xb + 1, gen, err);
+      poll_ge(xgen, epoch, err);
     }
-  }
-  __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1
-}
-
-// Every block arrives once per barrier; the last one to arrive resets the count and advances the
-// generation the others wait on. Writes before the barrier are released device-wide (the L2 of every
-// XCD) and acquired after it. The wait is bounded: a launch whose blocks are not all resident (which
-// the host sizing rules out) ends with *err set instead of hanging the device.
-__device__ __forceinline__ void grid_barrier(unsigned* bar, int* err, unsigned nblocks) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();
-    const unsigned prev = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == nblocks - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      unsigned spins = 0;
-      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) {
-          atomicOr(err, 1);
-          break;
-        }
-      }
-    }
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate done before the block goes on
   }
   __syncthreads();
 }
@@ -1277,17 +1200,16 @@ __global__ __launch_bounds__(256, 2) void sac_step_persistent_kernel(PArgs p_arg
   float* lds = reinterpret_cast<float*>(raw);
   const int G = gridDim.x, ct = H / kTile2;
   const int B = persist_args().m.L.B;
-  const bool local = persist_args().xcd_local;
-  if (local && threadIdx.x == 0) {  // the tile map's assumption: blocks congruent mod 8 share an XCD
+  if (threadIdx.x == 0) {  // diagnostics: blocks congruent mod 8 share an XCD (the deal the counting assumes)
     const unsigned xcc = xcc_id() + 1;
-    const unsigned seen = atomicCAS(persist_args().bar + 24 + blockIdx.x % 8, 0u, xcc);
+    unsigned* seen_at = persist_args().bar + kBarWords + 8 + blockIdx.x % 8;  // (not zeroed per launch)
+    const unsigned seen = atomicCAS(seen_at, 0u, xcc);
     if (seen != 0u && seen != xcc) atomicOr(persist_args().err, 2 | (int)(xcc << 8) | (int)(seen << 16));
   }
-  auto barrier = [&](bool last) __attribute__((always_inline)) {
+  unsigned nb = 0;  // barriers passed in this launch
+  auto barrier = [&](bool) __attribute__((always_inline)) {
     const PArgs& pa = persist_args();
-    if (!local) grid_barrier(pa.bar + 4, pa.err, G);
-    else if (last) grid_barrier_dev(pa.bar, pa.err, G);
-    else grid_barrier_xcd(pa.bar, pa.err, G);
+    grid_barrier(pa.bar, pa.err, G, nb++);
   };
   {  // actor_fwd
     const int gx = 2 * B / kTile2, nt = gx * ct;
@@ -1753,11 +1675,10 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     wg.hp = h->hp;
   }
   if (cfg->step_kernel == 1) {  // persistent single-launch step: barrier state and a co-resident grid
-    // [0..1] device-wide count / generation of grid_barrier_dev, [4..5] grid_barrier, [16] error flag,
-    // [24..31] the XCD of each block residue mod 8 (+1, 0 = not seen yet), [32 + 4x, 33 + 4x] XCD x's
-    // L2-resident count / generation
-    e = hipMalloc(&h->bar, 64 * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemset(h->bar, 0, 64 * sizeof(unsigned));
+    // [0, kBarWords) barrier words (zeroed before every launch), [kBarWords] error flag, [kBarWords + 8 + r]
+    // the XCD of block residue r mod 8 (+1, 0 = not seen yet)
+    e = hipMalloc(&h->bar, (kBarWords + 16) * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(h->bar, 0, (kBarWords + 16) * sizeof(unsigned));
     int per_cu = 0, cus = 0;
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = persistent_occupancy(H, &per_cu);
@@ -1805,7 +1726,7 @@ int sacf_step_kernel_status(sacf_handle* h) {
   if (!h->bar) return SACF_OK;
   SDev g(h->device);
   int flag = 0;
-  hipError_t e = hipMemcpy(&flag, h->bar + 16, sizeof(int), hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpy(&flag, h->bar + kBarWords, sizeof(int), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return sfail(h, SACF_EHIP, "sacf_step_kernel_status: %s", hipGetErrorString(e));
   if (!flag) return SACF_OK;
   return sfail(h, SACF_ESTATE, "persistent step kernel: %s (flag 0x%x; results invalid)",
@@ -1932,8 +1853,11 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
     p.m = a;
     p.w = w;
     p.bar = h->bar;
-    p.err = reinterpret_cast<int*>(h->bar + 16);
-    p.xcd_local = (h->L.B % 256 == 0 && !getenv("SACF_FULL_BARRIER")) ? 1 : 0;
+    p.err = reinterpret_cast<int*>(h->bar + kBarWords);
+    // the barrier words from 0 for this launch (a memset node under graph capture; 2,304 bytes from the
+    // allocation's start, a multiple of 16)
+    hipError_t me = hipMemsetAsync(h->bar, 0, kBarWords * sizeof(unsigned), h->stream);
+    if (me != hipSuccess) return sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(me));
     switch (h->L.H) {
       case 32: launch_persistent<32>(p, h->grid, h->stream); break;
       case 64: launch_persistent<64>(p, h->grid, h->stream); break;

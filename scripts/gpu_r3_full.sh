@@ -2,7 +2,7 @@
 # Usage: bash scripts/gpu_r3_full.sh TAG
 set -u
 TAG=${1:-r3full}; R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O; cd $R
-timeout -k 10 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/pytest_$TAG.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 200 --timeout-method thread > $O/pytest_$TAG.log 2>&1
 rc=$?; tail -6 $O/pytest_$TAG.log
 case $rc in 0|1) ;; *) echo "STOP pytest rc=$rc"; exit $rc;; esac
 timeout -k 10 300 python scripts/sac_ab.py 3000 > $O/sac_ab_$TAG.json 2> $O/sac_ab_$TAG.err || { echo "sac_ab FAIL"; tail -5 $O/sac_ab_$TAG.err; exit 1; }
