@@ -48,12 +48,14 @@ from ...core.eval_util import create_stats_ordered_dict
 
 
 class BatchedPathCollector:
-    def __init__(self, env, policy, max_path_length=9, max_ticks=64, deterministic=False,
+    SLICED_TICKS = 128   # sliced passes: an env idles after its decision until the pass ends
+    FUSED_TICKS = 1024   # fused passes: envs chain decisions inside the launch; longer passes amortise its tail
+    def __init__(self, env, policy, max_path_length=9, max_ticks=None, deterministic=False,
                  max_num_epoch_paths_saved=None, device_policy=None, use_graph=None, path_ring=None, fused=None):
         self._env = env                       # BatchedNormalizedBoxEnv
         self._policy = policy
         self.max_path_length = int(max_path_length)
-        self.max_ticks = int(max_ticks)
+        self.max_ticks = int(max_ticks) if max_ticks is not None else None  # None: by pass kind, below
         self.deterministic = deterministic
         N = env.n_envs
         dev = env.device
@@ -100,6 +102,8 @@ class BatchedPathCollector:
         self.fused = self._fused_supported() if fused is None else bool(fused)
         if self.fused and not self._fused_supported():
             raise ValueError("fused collection needs a device policy the env library can run (see _fused_supported)")
+        if self.max_ticks is None:  # ticks per pass: the measured best of each kind (DESIGN.md §9, C4 shard)
+            self.max_ticks = self.FUSED_TICKS if self.fused else self.SLICED_TICKS
         self._mode = None                                         # "fused" / "sliced": the last pass's kind
         self._ep_idx = torch.zeros(N, dtype=torch.int32, device=dev)   # fused: episodes started per env
         self._dec_idx = torch.zeros(N, dtype=torch.int32, device=dev)  # fused: decisions of the current episode

@@ -63,7 +63,11 @@ def build_parser():
     p.add_argument("--eval_envs", type=int, default=0,
                    help="0 (default): evaluation on the exploration envs, one env object as the reference (Q10); "
                         "N > 0: a separate evaluation shard of N envs")
-    p.add_argument("--slice_ticks", type=int, default=128)  # collector slice: best of 64/128/256/512
+    p.add_argument("--slice_ticks", type=int, default=0,
+                   help="env ticks per collector pass; 0: the collector's measured best for its pass kind "
+                        "(1024 with the policy inside the env launch, 128 for sliced passes; DESIGN §9)")
+    p.add_argument("--fused_collect", type=_bool, default=True,
+                   help="the policy inside the env launch (shipsim_run_policy) where the networks allow it")
     p.add_argument("--match_update_ratio", type=_bool, default=True,
                    help="grad steps per train loop = collected decisions (all ranks) x num_trains / num_expl_steps "
                         "(the reference's ratio); false: num_trains_per_train_loop per loop")
@@ -168,11 +172,13 @@ def experiment_device(variant, args, device, process_group=None):
     trainer.broadcast_parameters(0)
     # the collectors sample the trainer's current policy on the matrix cores (sacf_policy_act) and replay
     # each slice pass as a HIP graph (batched_collector.py); the torch modules stay their snapshot surface
+    ticks = args.slice_ticks or None
+    fused = None if args.fused_collect else False
     expl_coll = BatchedPathCollector(expl_env, policy, max_path_length=ak["max_path_length"],
-                                     max_ticks=args.slice_ticks, device_policy=trainer.device_policy(False))
+                                     max_ticks=ticks, device_policy=trainer.device_policy(False), fused=fused)
     eval_coll = BatchedPathCollector(eval_env, MakeDeterministic(policy), max_path_length=ak["max_path_length"],
-                                     max_ticks=args.slice_ticks, deterministic=True,
-                                     device_policy=trainer.device_policy(True))
+                                     max_ticks=ticks, deterministic=True,
+                                     device_policy=trainer.device_policy(True), fused=fused)
     return DeviceBatchRLAlgorithm(trainer=trainer, exploration_env=expl_env, evaluation_env=eval_env,
                                   exploration_data_collector=expl_coll, evaluation_data_collector=eval_coll,
                                   replay_buffer=rb, match_update_ratio=variant.get("match_update_ratio", True), **ak)

@@ -69,8 +69,10 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c2", action="store_true", help="skip the configs[1] single-ship secondary line")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round2_pmc_traffic.json"))
-    p.add_argument("--pmc-fp64-json", default=os.path.join(ROOT, "profiles", "round2_pmc_fp64.json"))
+    p.add_argument("--no-policy-stream", action="store_true",
+                   help="skip the secondary line of the same envs with the policy in the loop (shipsim_run_policy)")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round3_pmc_traffic.json"))
+    p.add_argument("--pmc-fp64-json", default=os.path.join(ROOT, "profiles", "round3_pmc_fp64.json"))
     p.add_argument("--sac-steps", type=int, default=300, help="timed SAC grad steps (0 = skip the SAC line)")
     p.add_argument("--sac-global-batch", type=int, default=256,
                    help="SAC batch summed over all ranks (runner: 256); each rank samples global / N rows "
@@ -222,6 +224,67 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
                 ref.train_from_torch(rb.random_batch(batch))
         eager(3)
         res["reference_order_eager_grad_steps_per_s"] = eager_steps / timed(eager, eager_steps)
+    return res
+
+
+def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1):
+    """The C3 envs with the policy in the loop (secondary line): shipsim_run_policy, every decision's action
+    sampled inside the launch from a TanhGaussianPolicy (runner networks 2x256, random init, stochastic) held
+    by a FusedSACTrainer — the collector's fused pass without the replay bookkeeping. env-ticks/s over
+    `launches` launches of `slice_ticks` ticks (HIP events on the launch stream)."""
+    import torch
+    from ast_sac_amd.ast_sac.torch.networks.mlp import ConcatMlp
+    from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
+    from ast_sac_amd.ast_sac.torch.sac.sac_fused import FusedSACTrainer
+    from ast_sac_amd.shipsim import ShipSim
+    from ast_sac_amd import shipsim_abi as abi
+
+    class _Env:
+        class action_space:
+            shape = (1,)
+
+    torch.manual_seed(0)
+    q = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[256, 256]).to(dev) for _ in range(4)]
+    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[256, 256]).to(dev)
+    tr = FusedSACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3],
+                         discount=0.965, soft_target_tau=1e-3, policy_lr=8e-5, qf_lr=8e-5, reward_scale=0.75,
+                         batch_size=256, backend="hip")
+    dp = tr.device_policy(deterministic=False, seed=20251017)
+    sim = ShipSim(cfg, n_envs, device=dev)
+    sim.reset()
+    n_dec = cfg.max_sampling_frequency
+    ep = torch.zeros(n_envs, dtype=torch.int32, device=dev)
+    dec = torch.zeros(n_envs, dtype=torch.int32, device=dev)
+    out = dict(ticks=torch.zeros(n_envs, dtype=torch.int32, device=dev),
+               decisions=torch.zeros(n_envs, dtype=torch.int32, device=dev))
+    ticks = torch.zeros((), dtype=torch.int64, device=dev)
+    decs = torch.zeros((), dtype=torch.int64, device=dev)
+    e0 = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
+    e1 = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
+    for i in range(warmup + launches):
+        if i == warmup:
+            torch.cuda.synchronize()
+            ticks.zero_()
+            decs.zero_()
+            t0 = time.perf_counter()
+        if i >= warmup:
+            e0[i - warmup].record()
+        sim.run_policy(dp.weights(), slice_ticks, n_dec, ep, dec, deterministic=False, seed=dp.seed,
+                       counter=dp.counter, out=out)
+        if i >= warmup:
+            e1[i - warmup].record()
+        dp.counter.add_(1)
+        ticks.add_(out["ticks"].sum())
+        decs.add_(out["decisions"].sum())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kms = sum(a.elapsed_time(b) for a, b in zip(e0, e1)) / launches
+    res = {"env_ticks_per_s": float(ticks.item()) / dt, "decisions_per_s": float(decs.item()) / dt,
+           "kernel_ms": kms, "envs": n_envs, "slice_ticks": slice_ticks, "launches": launches,
+           "lanes_per_env": sim.lanes_per_env,
+           "impl": "shipsim_run_policy (ast_step_kernel CHAIN 2: TanhGaussianPolicy sample per decision in-kernel, "
+                   "NormalizedBoxEnv mapping, in-place episode resets)"}
+    sim.close()
     return res
 
 
@@ -475,6 +538,8 @@ def main():
                                  "kernel issues; 'distinct' counts each ship's chain once (its LPE/2 sub-lanes "
                                  "repeat it)"}
     c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
+    pstream = (bench_policy_stream(dev, cfg, N, args.slice if args.mode == "table" else 4096)
+               if (rank == 0 and not args.no_policy_stream and args.obs_ships == 1) else None)
     sac = None
     if args.sac_steps > 0:
         if args.sac_global_batch % world:
@@ -521,6 +586,7 @@ def main():
             "cpu_baseline": cpu,
             "sac": sac,
             "c2_single_ship": c2,
+            "policy_stream": pstream,
         }
         print(json.dumps(line))
     if world > 1:

@@ -43,8 +43,9 @@ def main():
         torch.cuda.synchronize()
         return r, time.perf_counter() - t0
 
-    res = dict(workload=f"C4 shard: {n_envs} envs/GPU, collav sbmpc, PTI, dt 4, slice {args.slice_ticks}, "
-                        f"SAC B={args.batch_size} 2x{args.layer_size}")
+    ticks0 = coll.max_ticks
+    res = dict(workload=f"C4 shard: {n_envs} envs/GPU, collav sbmpc, PTI, dt 4, {ticks0}-tick "
+                        f"{'fused' if coll.fused else 'sliced'} passes, SAC B={args.batch_size} 2x{args.layer_size}")
     # epoch-0 initial exploration (min_num_steps_before_training) fills the buffer; also warms up
     coll.collect(args.min_num_steps_before_training, rb)
     tr.train_from_buffer(rb, 20)
@@ -70,7 +71,7 @@ def main():
                 decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
                 env_ticks_per_s=(k1 - k0) / t)
     coll.fused = fused0
-    coll.max_ticks = args.slice_ticks
+    coll.max_ticks = ticks0
     # SAC alone
     n_sac = 2400
     _, t = timed(lambda: tr.train_from_buffer(rb, n_sac))

@@ -6,7 +6,7 @@ for round in 1 2; do
   for v in "$@"; do
     if [ $v = new ]; then unset SHIPSIM_LIB; else export SHIPSIM_LIB=$R/ast_sac_amd/lib/abl/lib_$v.so; fi
     for CA in sbmpc none; do
-      timeout -k 10 150 python bench.py --collav $CA --no-cpu-baseline --sac-steps 0 --no-c2 > $O/ab_${TAG}_${v}_${CA}_$round.log 2>&1 || { echo "FAIL $v $CA"; tail -3 $O/ab_${TAG}_${v}_${CA}_$round.log; exit 1; }
+      timeout -k 10 150 python bench.py --collav $CA --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream > $O/ab_${TAG}_${v}_${CA}_$round.log 2>&1 || { echo "FAIL $v $CA"; tail -3 $O/ab_${TAG}_${v}_${CA}_$round.log; exit 1; }
       tail -1 $O/ab_${TAG}_${v}_${CA}_$round.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$round $v $CA', round(d['value']/1e6,1), 'M', round(d['roofline']['kernel_ms_timed'],3), 'ms')"
     done
   done

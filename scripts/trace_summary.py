@@ -5,13 +5,18 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
+
+# the decision-stream (CHAIN 1, shipsim_run_table) instantiations the headline times; the bench's secondary
+# policy-stream line (CHAIN 2) runs the same kernel template with the policy in the loop
+TABLE = re.compile(r"ast_step_kernel<[^>]*,\s*1,\s*\d+>")
 
 d, bench_log, out = sys.argv[1:4]
 rows = []
 for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if "ast_step_kernel" in r["Kernel_Name"]:
+        if TABLE.search(r["Kernel_Name"]):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     os.remove(f)
 rows.sort()
