@@ -21,6 +21,40 @@
 #include "shipsim.h"
 #include "shipsim_device.hpp"
 
+// ---------------------------------------------------------------------------------------------
+// Diagnostics build (-DSHIPSIM_LANECHECK; scripts/build_abl.sh lib_lanecheck.so): every cross-lane exchange
+// checks that all lanes it reads are active (the env's LPE lanes for the DPP / shuffle helpers, the whole
+// wave for the wave-cooperative SBMPC and policy passes), and the data-dependent indices of the decision
+// path are range-checked. A violation is counted (first site and exec mask kept) and read back with
+// shipsim_diag_lane_faults; the default build compiles all of it out.
+// ---------------------------------------------------------------------------------------------
+#ifdef SHIPSIM_LANECHECK
+__device__ unsigned g_lane_diag[4];  // [0] violations, [1] first site, [2] / [3] its exec mask lo / hi
+__device__ __noinline__ void lane_fault(int site) {
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  if (atomicAdd(&g_lane_diag[0], 1u) == 0u) {
+    atomicExch(&g_lane_diag[1], (unsigned)site);
+    atomicExch(&g_lane_diag[2], (unsigned)ex);
+    atomicExch(&g_lane_diag[3], (unsigned)(ex >> 32));
+  }
+}
+template <int LPE>
+__device__ __forceinline__ void lane_check(int site) {  // all LPE lanes of this lane's group active
+  const int l0 = (int)(threadIdx.x & 63) & ~(LPE - 1);
+  const uint64_t need = LPE >= 64 ? ~0ull : (((1ull << LPE) - 1) << l0);
+  if ((__builtin_amdgcn_read_exec() & need) != need) lane_fault(site);
+}
+#define SHIPSIM_LANE_CHECK(LPE_, site) lane_check<LPE_>(site)
+#define SHIPSIM_INDEX_CHECK(cond, site) \
+  do {                                  \
+    if (!(cond)) lane_fault(site);      \
+  } while (0)
+#else
+#define SHIPSIM_LANE_CHECK(LPE_, site) ((void)0)
+#define SHIPSIM_INDEX_CHECK(cond, site) ((void)0)
+#endif
+
+
 using namespace shipsim;
 
 // ---------------------------------------------------------------------------------------------
@@ -618,6 +652,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
 // request an optimisation with inputs `in`; they receive (P_best, Chi_best).
 __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double DT, double& p_best,
                                   double& chi_best) {
+  SHIPSIM_LANE_CHECK(64, 4);
   const int lane = opaque_v(threadIdx.x) & 63;  // (opaque: no lane masks held across the caller's loop)
   const int half = lane >> 5;
   const int scen = lane & 31;
@@ -680,6 +715,7 @@ struct SbMulti {
 template <int NOB>
 __device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n_obs, int n_samp, double DT,
                                         double& p_best, double& chi_best) {
+  SHIPSIM_LANE_CHECK(64, 4);
   const int lane = opaque_v(threadIdx.x) & 63;
   const int half = lane >> 5;
   const int scen = lane & 31;
@@ -978,6 +1014,7 @@ __device__ __forceinline__ float wave_sum_f(float x) {  // butterfly: every lane
 // Returns the normalized action a in (-1, 1) for lanes whose env wanted one.
 __device__ __forceinline__ float policy_actions(bool want, const float ns[8], int env, bool env_leader, int env_lane0, int seq,
                                 const ChainArgs& CH, float* lds_h1) {
+  SHIPSIM_LANE_CHECK(64, 5);
   uint64_t req = __ballot(want && env_leader);
   float act = 0.0f;
   const int lane = threadIdx.x & 63;
@@ -1092,11 +1129,13 @@ __device__ __forceinline__ float denormalize_f32(float a, float lb, float ub) {
 // lanes of the env: value of lane k of the env (LPE 16: the env is one DPP row)
 template <int LPE, int K>
 __device__ __forceinline__ double env_lane_d(double x, int env_lane0) {
+  SHIPSIM_LANE_CHECK(LPE, 1);
   if constexpr (LPE == 16) return dpp_d<kDppRowBcast + K>(x);
   else return shfl_d(x, env_lane0 + K);
 }
 template <int LPE, int K>
 __device__ __forceinline__ int env_lane_i(int x, int env_lane0) {
+  SHIPSIM_LANE_CHECK(LPE, 2);
   if constexpr (LPE == 16) return dpp_i<kDppRowBcast + K>(x);
   else return __shfl(x, env_lane0 + K, 64);
 }
@@ -1105,6 +1144,7 @@ __device__ __forceinline__ int env_lane_i(int x, int env_lane0) {
 // quad_perm [2,3,0,1], row_ror 4, row_ror 8 (parity-preserving) — DPP only, no LDS permute
 template <int LPE, int SLOTS = 2>
 __device__ __forceinline__ void ship_reduce(double& d2, int& gri) {
+  SHIPSIM_LANE_CHECK(LPE, 3);
   if constexpr (LPE == 16) {  // sub-lanes of a ship are the lanes of equal index mod SLOTS
     if constexpr (SLOTS == 2) {
       d2 = py_min(d2, dpp_d<kDppQuadXor2>(d2));
@@ -1364,6 +1404,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     const StepArgs& A = step_args();
     const Params& P = A.P;
     const ChainArgs& CH = A.CH;
+    SHIPSIM_INDEX_CHECK(ep_i >= 0 && dec_i >= 0 && dec_i < CH.n_dec && envc < P.n_envs, 10);
     return CH.table[((size_t)(ep_i % CH.n_eps) * CH.n_dec + dec_i) * P.n_envs + envc];
   };
   auto reset_env = [&]() __attribute__((always_inline)) {
@@ -1371,6 +1412,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     const Params& P = A.P;
     const ConstBuf& K = A.K;
     const ShipConst& c = lds_sc[opaque_v(shipc)];
+    SHIPSIM_INDEX_CHECK(c.n_route >= 2 && c.n_route <= kMaxRoute, 11);
     s.n = c.init_n; s.e = c.init_e; s.yaw = c.init_yaw; s.u = c.init_u; s.v = c.init_v; s.r = c.init_r;
     s.omega = c.init_omega; s.time = 0.0;
     s.e_ct = 0; s.e_ct_int = 0; s.hdg_ei = 0; s.hdg_prev = 0;
@@ -1600,6 +1642,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
           float dn = st4[0] - st4[2], de = st4[1] - st4[3];
           imminent = (dn * dn + de * de) < 9000000.0f;
         }
+        SHIPSIM_LANE_CHECK(LPE, 6);
         control_and_integrate_sc<DETAILED, REC>(c, P, s, rn, re, -off, sf, mach_dt, (SIMPLE && is_test) ? 1 : 0,
                                                 imminent, (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel,
                                                 sy, cy);
@@ -3081,5 +3124,19 @@ int shipsim_synchronize(shipsim_handle* h) {
 }
 
 int32_t shipsim_nonfinite_count(const shipsim_handle* h) { return h ? h->nonfinite_seen : -1; }
+
+int shipsim_diag_lane_faults(uint32_t* out4) {
+  if (!out4) return SHIPSIM_EINVAL;
+  for (int i = 0; i < 4; ++i) out4[i] = 0;
+#ifdef SHIPSIM_LANECHECK
+  if (hipDeviceSynchronize() != hipSuccess) return SHIPSIM_EHIP;
+  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_lane_diag), 4 * sizeof(uint32_t)) != hipSuccess) return SHIPSIM_EHIP;
+  const uint32_t zero[4] = {0, 0, 0, 0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_lane_diag), zero, sizeof(zero)) != hipSuccess) return SHIPSIM_EHIP;
+  return SHIPSIM_OK;
+#else
+  return SHIPSIM_EINVAL;  // not a diagnostics build
+#endif
+}
 
 }  // extern "C"

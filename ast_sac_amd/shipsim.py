@@ -58,6 +58,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
+    L.shipsim_diag_lane_faults.argtypes = [P]
     L.shipsim_run_policy.argtypes = [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, P, C.c_int32, C.c_int32,
                                      P, P, P, P, P, C.c_int32, P]
     if L.shipsim_abi_version() != abi.ABI_VERSION:
@@ -76,7 +77,16 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
                     "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
                     "shipsim_nonfinite_count", "shipsim_lanes_per_env", "shipsim_set_stream",
-                    "shipsim_run_policy")
+                    "shipsim_run_policy", "shipsim_diag_lane_faults")
+
+
+def diag_lane_faults():
+    """Lane / index check violations of a diagnostics build (-DSHIPSIM_LANECHECK) since the last call:
+    dict(violations, site, exec), or None for the default build."""
+    out = (C.c_uint32 * 4)()
+    if load_library().shipsim_diag_lane_faults(out) != 0:
+        return None
+    return dict(violations=int(out[0]), site=int(out[1]), exec=(int(out[3]) << 32) | int(out[2]))
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):

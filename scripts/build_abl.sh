@@ -7,3 +7,7 @@ S=$R/ast_sac_amd/csrc/shipsim_kernels.hip
 
 /opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=iterative-ilp -DSHIPSIM_SRC_HASH='"abl-ilp"' $S -o $D/lib_ilp.so &
 wait
+# lane / index checks compiled in (shipsim_diag_lane_faults), default scheduler and the ILP-first one
+/opt/rocm/bin/hipcc $F -DSHIPSIM_LANECHECK -DSHIPSIM_SRC_HASH='"abl-lanecheck"' $S -o $D/lib_lanecheck.so &
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=iterative-ilp -DSHIPSIM_LANECHECK -DSHIPSIM_SRC_HASH='"abl-ilp-lanecheck"' $S -o $D/lib_ilp_lanecheck.so &
+wait
