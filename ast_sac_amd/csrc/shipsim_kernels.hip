@@ -1011,27 +1011,30 @@ __device__ __forceinline__ float wave_sum_f(float x) {  // butterfly: every lane
 
 // Must be called by every lane of the wave. want: this lane's env needs its next action (all lanes of an
 // env agree); ns: its observation; seq: the env's decisions completed in this call (noise stream index).
-// Returns the normalized action a in (-1, 1) for lanes whose env wanted one.
-__device__ __forceinline__ float policy_actions(bool want, const float ns[8], int env, bool env_leader, int env_lane0, int seq,
-                                const ChainArgs& CH, float* lds_h1) {
+// Returns the normalized action a in (-1, 1) for lanes whose env wanted one. Lane l owns the nj = H / 64
+// consecutive hidden units [l·nj, l·nj + nj): one row of the transposed fc1 weight is one coalesced load
+// per lane (a float4 at H = 256), and the h1 rows in LDS are read as broadcast float4s.
+__device__ __forceinline__ float policy_actions(bool want, const float ns[8], int env, bool env_leader, int env_lane0,
+                                                int seq, const ChainArgs& CH, float* lds_h1) {
   SHIPSIM_LANE_CHECK(64, 5);
   uint64_t req = __ballot(want && env_leader);
   float act = 0.0f;
   const int lane = threadIdx.x & 63;
-  const int H = CH.pol_hidden, O = CH.pol_obs, nj = H / 64;
-  const float* W1 = CH.policy;
-  const float* b1 = W1 + (size_t)H * O;
+  const int H = CH.pol_hidden, nj = H / 64, u0 = lane * nj;
+  const float* W1 = CH.policy;  // [H][8] (obs_dim 8: checked by the host)
+  const float* b1 = W1 + (size_t)H * 8;
   const float* b2 = b1 + H + (size_t)H * H;
   const float* wm = b2 + H;
   const float* ws = wm + H + 1;
+  constexpr int kJ = kPolMaxHidden / 64;
   while (req) {
     // the next (up to) kPolMaxRows requesting envs: the lowest set bits of req (no indexed arrays: row e's
     // source lane is recomputed from the mask, so nothing lands in scratch)
-    uint64_t rows = req;
+    const uint64_t rows = req;
     int E = 0;
     for (uint64_t m = req; m && E < kPolMaxRows; m &= m - 1) ++E;
     for (int e = 0; e < E; ++e) req &= req - 1;
-    // fc0 + relu for every row, into LDS
+    // fc0 + relu for every row, into LDS: unit u = b1[u] + sum_i W1[u][i] x[i], i ascending
     {
       uint64_t m = rows;
       for (int e = 0; e < E; ++e, m &= m - 1) {
@@ -1039,37 +1042,47 @@ __device__ __forceinline__ float policy_actions(bool want, const float ns[8], in
         float x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = __shfl(ns[i], src, 64);
-        for (int j = 0; j < nj; ++j) {
-          const int u = lane + 64 * j;
-          float h = b1[u];
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (i < O) h = fmaf(W1[(size_t)u * O + i], x[i], h);  // (O == 8: checked by the host)
-          lds_h1[e * kPolMaxHidden + u] = fmaxf(h, 0.0f);
+        for (int j = 0; j < kJ; ++j) {
+          if (j < nj) {
+            const int u = u0 + j;
+            float h = b1[u];  // (the parameters are 4-byte aligned only: log α leads them)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) h = fmaf(W1[(size_t)u * 8 + i], x[i], h);
+            lds_h1[e * kPolMaxHidden + u] = fmaxf(h, 0.0f);
+          }
         }
       }
     }
     __syncthreads();  // (one wave per block)
-    // fc1 + relu: acc[e][j] = b2[u] + sum_k W2[u][k] h1[e][k], k ascending; W2T rows are coalesced
-    float acc[kPolMaxRows][kPolMaxHidden / 64];
+    // fc1 + relu: acc[e][j] = b2[u] + sum_k W2[u][k] h1[e][k], k ascending; W2T row k is [H] contiguous
+    float acc[kPolMaxRows][kJ];
 #pragma unroll
-    for (int j = 0; j < kPolMaxHidden / 64; ++j) {
-      const float bj = j < nj ? b2[lane + 64 * j] : 0.0f;
+    for (int j = 0; j < kJ; ++j) {
+      const float bj = j < nj ? b2[u0 + j] : 0.0f;
 #pragma unroll
       for (int e = 0; e < kPolMaxRows; ++e) acc[e][j] = bj;
     }
     for (int k = 0; k < H; k += 4) {
-      float w[4][kPolMaxHidden / 64];
+      float w[4][kJ];
+      if (nj == 4) {  // H = 256: one float4 per row
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
+        for (int kk = 0; kk < 4; ++kk) {
+          const float4 v = *reinterpret_cast<const float4*>(CH.w2t + (size_t)(k + kk) * H + u0);
+          w[kk][0] = v.x; w[kk][1] = v.y; w[kk][2] = v.z; w[kk][3] = v.w;
+        }
+      } else {
 #pragma unroll
-        for (int j = 0; j < kPolMaxHidden / 64; ++j) w[kk][j] = j < nj ? CH.w2t[(size_t)(k + kk) * H + lane + 64 * j] : 0.0f;
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int j = 0; j < kJ; ++j) w[kk][j] = j < nj ? CH.w2t[(size_t)(k + kk) * H + u0 + j] : 0.0f;
+      }
 #pragma unroll
       for (int e = 0; e < kPolMaxRows; ++e) {
         if (e < E) {
           const float4 h4 = *reinterpret_cast<const float4*>(lds_h1 + e * kPolMaxHidden + k);
 #pragma unroll
-          for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+          for (int j = 0; j < kJ; ++j) {
             acc[e][j] = fmaf(w[0][j], h4.x, acc[e][j]);
             acc[e][j] = fmaf(w[1][j], h4.y, acc[e][j]);
             acc[e][j] = fmaf(w[2][j], h4.z, acc[e][j]);
@@ -1079,11 +1092,11 @@ __device__ __forceinline__ float policy_actions(bool want, const float ns[8], in
       }
     }
     // heads (mean, log_std) reduced across the wave, the sample, and the hand-over to the env's lanes
-    float wmj[kPolMaxHidden / 64], wsj[kPolMaxHidden / 64];
+    float wmj[kJ], wsj[kJ];
 #pragma unroll
-    for (int j = 0; j < kPolMaxHidden / 64; ++j) {
-      wmj[j] = j < nj ? wm[lane + 64 * j] : 0.0f;
-      wsj[j] = j < nj ? ws[lane + 64 * j] : 0.0f;
+    for (int j = 0; j < kJ; ++j) {
+      wmj[j] = j < nj ? wm[u0 + j] : 0.0f;
+      wsj[j] = j < nj ? ws[u0 + j] : 0.0f;
     }
     const float bm = wm[H], bs = ws[H];
     const uint64_t ctr = CH.pol_counter ? (uint64_t)*CH.pol_counter : 0;
@@ -1095,7 +1108,7 @@ __device__ __forceinline__ float policy_actions(bool want, const float ns[8], in
         m &= m - 1;
         float pm = 0.0f, ps = 0.0f;
 #pragma unroll
-        for (int j = 0; j < kPolMaxHidden / 64; ++j) {
+        for (int j = 0; j < kJ; ++j) {
           const float y = fmaxf(acc[e][j], 0.0f);
           pm = fmaf(wmj[j], y, pm);
           ps = fmaf(wsj[j], y, ps);
