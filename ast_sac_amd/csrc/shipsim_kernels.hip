@@ -29,9 +29,11 @@
 // shipsim_diag_lane_faults; the default build compiles all of it out.
 // ---------------------------------------------------------------------------------------------
 #ifdef SHIPSIM_LANECHECK
-__device__ unsigned g_lane_diag[4];  // [0] violations, [1] first site, [2] / [3] its exec mask lo / hi
+// [0] violations, [1] first site, [2] / [3] its exec mask lo / hi, [8 + site] violations per site
+__device__ unsigned g_lane_diag[32];
 __device__ __noinline__ void lane_fault(int site) {
   const uint64_t ex = __builtin_amdgcn_read_exec();
+  atomicAdd(&g_lane_diag[8 + (site & 15)], 1u);
   if (atomicAdd(&g_lane_diag[0], 1u) == 0u) {
     atomicExch(&g_lane_diag[1], (unsigned)site);
     atomicExch(&g_lane_diag[2], (unsigned)ex);
@@ -44,13 +46,23 @@ __device__ __forceinline__ void lane_check(int site) {  // all LPE lanes of this
   const uint64_t need = LPE >= 64 ? ~0ull : (((1ull << LPE) - 1) << l0);
   if ((__builtin_amdgcn_read_exec() & need) != need) lane_fault(site);
 }
+template <int LPE, int SLOTS>
+__device__ __forceinline__ void ship_check(int site) {  // the lanes of this lane's ship within its env
+  const int lane = (int)(threadIdx.x & 63), l0 = lane & ~(LPE - 1);
+  uint64_t pat = 0;
+  for (int k = lane % SLOTS; k < LPE; k += SLOTS) pat |= 1ull << k;
+  const uint64_t need = pat << l0;
+  if ((__builtin_amdgcn_read_exec() & need) != need) lane_fault(site);
+}
 #define SHIPSIM_LANE_CHECK(LPE_, site) lane_check<LPE_>(site)
+#define SHIPSIM_SHIP_CHECK(LPE_, SLOTS_, site) ship_check<LPE_, SLOTS_>(site)
 #define SHIPSIM_INDEX_CHECK(cond, site) \
   do {                                  \
     if (!(cond)) lane_fault(site);      \
   } while (0)
 #else
 #define SHIPSIM_LANE_CHECK(LPE_, site) ((void)0)
+#define SHIPSIM_SHIP_CHECK(LPE_, SLOTS_, site) ((void)0)
 #define SHIPSIM_INDEX_CHECK(cond, site) ((void)0)
 #endif
 
@@ -1546,6 +1558,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     const ConstBuf& K = A.K;
     const Traj& T = A.T;
     // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
+    SHIPSIM_LANE_CHECK(LPE, 7);
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
     const double psy = pair_swap(sy), pcy = pair_swap(cy);  // sin/cos(pyaw), carried by the partner
@@ -1655,7 +1668,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
           float dn = st4[0] - st4[2], de = st4[1] - st4[3];
           imminent = (dn * dn + de * de) < 9000000.0f;
         }
-        SHIPSIM_LANE_CHECK(LPE, 6);
+        SHIPSIM_SHIP_CHECK(LPE, SLOTS, 6);  // (its DPP exchanges pair sub-lanes of one ship)
         control_and_integrate_sc<DETAILED, REC>(c, P, s, rn, re, -off, sf, mach_dt, (SIMPLE && is_test) ? 1 : 0,
                                                 imminent, (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel,
                                                 sy, cy);
@@ -1736,6 +1749,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     int Tf, Of;
     bool any_nf;
     if constexpr (SLOTS == 2) {  // the partner lane (lane ^ 1) holds the other ship
+      SHIPSIM_LANE_CHECK(LPE, 8);
       const int o_flags = pair_swap_i(my_flags);
       const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
       const double o_ect = pair_swap(s.log_ect), o_ground = pair_swap(my_ground);
@@ -3138,13 +3152,13 @@ int shipsim_synchronize(shipsim_handle* h) {
 
 int32_t shipsim_nonfinite_count(const shipsim_handle* h) { return h ? h->nonfinite_seen : -1; }
 
-int shipsim_diag_lane_faults(uint32_t* out4) {
-  if (!out4) return SHIPSIM_EINVAL;
-  for (int i = 0; i < 4; ++i) out4[i] = 0;
+int shipsim_diag_lane_faults(uint32_t* out32) {
+  if (!out32) return SHIPSIM_EINVAL;
+  for (int i = 0; i < 32; ++i) out32[i] = 0;
 #ifdef SHIPSIM_LANECHECK
   if (hipDeviceSynchronize() != hipSuccess) return SHIPSIM_EHIP;
-  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_lane_diag), 4 * sizeof(uint32_t)) != hipSuccess) return SHIPSIM_EHIP;
-  const uint32_t zero[4] = {0, 0, 0, 0};
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_lane_diag), 32 * sizeof(uint32_t)) != hipSuccess) return SHIPSIM_EHIP;
+  const uint32_t zero[32] = {};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_lane_diag), zero, sizeof(zero)) != hipSuccess) return SHIPSIM_EHIP;
   return SHIPSIM_OK;
 #else

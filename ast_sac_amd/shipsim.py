@@ -83,10 +83,11 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
 def diag_lane_faults():
     """Lane / index check violations of a diagnostics build (-DSHIPSIM_LANECHECK) since the last call:
     dict(violations, site, exec), or None for the default build."""
-    out = (C.c_uint32 * 4)()
+    out = (C.c_uint32 * 32)()
     if load_library().shipsim_diag_lane_faults(out) != 0:
         return None
-    return dict(violations=int(out[0]), site=int(out[1]), exec=(int(out[3]) << 32) | int(out[2]))
+    return dict(violations=int(out[0]), site=int(out[1]), exec=(int(out[3]) << 32) | int(out[2]),
+                per_site={i: int(out[8 + i]) for i in range(16) if out[8 + i]})
 
 
 def default_config(kind=abi.KIND_AST, machinery=abi.MACH_DETAILED, collav=abi.COLLAV_SBMPC, time_step=4.0):

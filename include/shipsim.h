@@ -439,10 +439,11 @@ int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_
 int shipsim_synchronize(shipsim_handle* h);
 /* Decisions flagged SHIPSIM_EV_NONFINITE since create, as of the last shipsim_synchronize. */
 int32_t shipsim_nonfinite_count(const shipsim_handle* h);
-/* Diagnostics builds only (-DSHIPSIM_LANECHECK): out4 = {violations, first site, its exec mask lo, hi} of
- * the cross-lane / index checks since the last call (then cleared; synchronizes the current device).
- * SHIPSIM_EINVAL (out4 zeroed) in the default build, which compiles the checks out. */
-int shipsim_diag_lane_faults(uint32_t* out4);
+/* Diagnostics builds only (-DSHIPSIM_LANECHECK): out32 = {violations, first site, its exec mask lo, hi,
+ * 0 x 4, violations of site 0..15 x 16, 0 x 8} of the cross-lane / index checks since the last call (then
+ * cleared; synchronizes the current device). SHIPSIM_EINVAL (out32 zeroed) in the default build, which
+ * compiles the checks out. */
+int shipsim_diag_lane_faults(uint32_t* out32);
 
 #ifdef __cplusplus
 }
