@@ -1359,15 +1359,28 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
            sampling_count, n_base, phase);
 #endif
   // ---- intermediate waypoint sampling (env.py:659-696) for an env that waits for a decision ----
+  // CHAIN: episode / decision counters, decisions completed and records written in this call
+  int ep_i = 0, dec_i = 0, n_decided = 0, log_n = 0;
+  bool started_here = false;  // POLICY: the decision in progress started in this launch (its record row holds
+                              // its action and observation-of-choice already)
   auto decision_prologue = [&](float sa, float a_log) __attribute__((always_inline)) {
     const StepArgs& A = step_args();
     const Params& P = A.P;
     const ConstBuf& K = A.K;
-    if (CHAIN && lie == 0) {  // what the decision record will report: the action and the observation it saw
+    if (POLICY && lie == 0) {  // what the decision record will report: the action and the observation it saw,
+                               // into the record row it will complete in (stores only) and, for a decision
+                               // that completes in a later launch, the state
       const DevState So = opaque(A.S);
       So.dec_action()[envc] = a_log;
       for (int i = 0; i < 8; ++i) So.dec_obs0()[envc * 8 + i] = ns[i];
+      const ChainArgs& CH = A.CH;
+      if (CH.log && log_n < CH.log_cap) {
+        double* rec = CH.log + ((size_t)env * CH.log_cap + log_n) * SHIPSIM_DECLOG_COLS;
+        rec[SHIPSIM_DL_ACTION] = (double)a_log;
+        for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS0 + i] = (double)ns[i];
+      }
     }
+    started_here = true;
     if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
     phase = 0;
     have_iw = false;
@@ -1414,7 +1427,6 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   };
 
   // ---- CHAIN: in-place reset (env.py:238-342, as reset_kernel) and the next decision ----
-  int ep_i = 0, dec_i = 0, n_decided = 0, log_n = 0;
   if (CHAIN) {
     const ChainArgs& CH = A0.CH;
     ep_i = CH.ep_idx[envc];
@@ -1500,12 +1512,15 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
           rec[SHIPSIM_DL_DONE] = out_done ? 1.0 : 0.0; rec[SHIPSIM_DL_EPISODE] = (double)ep_i;
           rec[SHIPSIM_DL_DECISION] = (double)dec_i; rec[SHIPSIM_DL_TICKS] = (double)out_ticks;
           for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS + i] = (double)ns[i];
-          const DevState So = opaque(step_args().S);
-          rec[SHIPSIM_DL_ACTION] = (double)So.dec_action()[envc];
-          for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS0 + i] = (double)So.dec_obs0()[envc * 8 + i];
+          if (POLICY && !started_here) {  // started in an earlier launch: from the state
+            const DevState So = opaque(step_args().S);
+            rec[SHIPSIM_DL_ACTION] = (double)So.dec_action()[envc];
+            for (int i = 0; i < 8; ++i) rec[SHIPSIM_DL_OBS0 + i] = (double)So.dec_obs0()[envc * 8 + i];
+          }
         }
         log_n += 1;
         n_decided += 1;
+        started_here = false;
         if (out_done || dec_i + 1 >= CH.n_dec) {
           reset_env();
           ep_i += 1;

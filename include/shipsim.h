@@ -380,8 +380,9 @@ int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double
 #define SHIPSIM_DL_DECISION 4 /* dec_idx of the decision */
 #define SHIPSIM_DL_TICKS 5    /* _step ticks of the decision (across launches; 0 for a sampling failure) */
 #define SHIPSIM_DL_OBS 6      /* 8 columns: the observation returned */
-#define SHIPSIM_DL_ACTION 14  /* the decision's action: the table's scoping angle / the policy's normalized a */
-#define SHIPSIM_DL_OBS0 15    /* 8 columns: the observation the action was chosen from */
+#define SHIPSIM_DL_ACTION 14  /* shipsim_run_policy only: the policy's normalized action a */
+#define SHIPSIM_DL_OBS0 15    /* shipsim_run_policy only, 8 columns: the observation a was chosen from */
+/* (shipsim_run_table leaves columns 14..22 as they were: its actions are the caller's table) */
 int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int32_t n_dec, int32_t max_ticks,
                       int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out, int32_t* decisions_out, double* log,
                       int32_t log_cap, int32_t* log_len);

@@ -112,8 +112,6 @@ def test_policy_stream_deterministic(collav, H):
         k = len(recs[i])
         assert len(rep[i]) >= k
         np.testing.assert_array_equal(rep[i][:k][:, _KEEP], recs[i][:, _KEEP], err_msg=f"{collav} env {i}")
-        np.testing.assert_array_equal(rep[i][:k][:, abi.DL_ACTION], table[recs[i][:, abi.DL_EPISODE].astype(int),
-                                                                          recs[i][:, abi.DL_DECISION].astype(int), i])
 
 
 def test_policy_stream_stochastic_noise():
