@@ -57,7 +57,8 @@ struct ShipConst {
 
 struct Params {
   int32_t kind, machinery, collav, n_ships;
-  int32_t max_sampling, n_envs, n_polys, pad_;
+  int32_t max_sampling, n_envs, n_polys;
+  int32_t epw;  // envs per wave of the AST step / stream kernels (0: 64 / lanes per env; fewer leave lanes idle)
   double dt, sim_time, mach_dt_reset, mach_dt_init;
   double vc_n, vc_e, wind_dir, wind_speed;
   double roa2;                       // args.radius_of_acceptance ** 2

@@ -1252,7 +1252,11 @@ __device__ __forceinline__ const StepArgs& step_args() {
 // K > 1 obstacle ships (shipsim_create) ship k sits on the lanes of index k mod SLOTS, and slots past
 // the env's last ship repeat that ship (ghost lanes: same state and arithmetic, never stored).
 template <bool DETAILED, int COLLAV, int LPE, bool REC, int CHAIN = 0, int SLOTS = 2>
+#ifdef SHIPSIM_OCC2  // diagnostics build: two waves per SIMD (<= 256 VGPR + AGPR per wave)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ast_step_kernel(const StepArgs A_arg) {
+#else
 __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
+#endif
   constexpr bool POLICY = CHAIN == 2;  // CHAIN: 0 shipsim_step, 1 shipsim_run_table, 2 shipsim_run_policy
   (void)A_arg;  // read through step_args() only (see StepArgs)
   const StepArgs& A0 = step_args();
@@ -1298,9 +1302,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   for (int i = threadIdx.x; i < P.n_polys; i += blockDim.x) lds_boxes[i] = K.boxes()[i];
   __syncthreads();
 
-  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
-  const int env = gl / LPE;
-  const int lie = gl % LPE;
+  // one wave per block: envs [blockIdx.x * epw, + epw) on lanes [0, epw * LPE); lanes past them idle
+  const int epw = P.epw > 0 ? P.epw : 64 / LPE;
+  const int eslot = (int)(threadIdx.x & 63) / LPE;
+  const int env = (int)blockIdx.x * epw + eslot;
+  const int lie = (int)(threadIdx.x & 63) % LPE;
   const int ship = lie % SLOTS;
   const int sub = lie / SLOTS;
   const bool is_test = ship == 0;
@@ -1310,7 +1316,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   const bool is_obs1 = shipc == 1;            // "the" obstacle ship (sampling, decisions, observation)
   const int lane = threadIdx.x & 63;
   const int env_lane0 = lane - lie;
-  const bool valid = env < P.n_envs;
+  const bool valid = eslot < epw && env < P.n_envs;
   const int envc = valid ? env : 0;
   const int qc = envc * nsh + shipc;
   const ShipConst& c = SC[shipc];
@@ -1992,7 +1998,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   }
   if (ready && AE.obs_out && sub == 0 && ship < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
 #pragma unroll
-    for (int i = 0; i < 4; ++i) AE.obs_out[env * 8 + ship * 4 + i] = ship ? ns[4 + i] : ns[i];  // (no indexed ns)
+    for (int i = 0; i < 4; ++i) {  // (values in registers first: a select of two ns elements would become
+      float a = ns[i], b = ns[4 + i];  // an indexed ns, i.e. the whole array in scratch)
+      asm volatile("" : "+v"(a), "+v"(b));
+      AE.obs_out[env * 8 + ship * 4 + i] = ship ? b : a;
+    }
   }
 }
 
@@ -2325,6 +2335,12 @@ static int lanes_per_env(const shipsim_config* cfg, int n_envs, int device) {
   return lpe;
 }
 
+// blocks (one wave each) of an AST step / stream launch at lpe lanes per env
+static int step_blocks(const shipsim_handle* h, int lpe) {
+  const int epw = h->P.epw > 0 && h->P.epw <= 64 / lpe ? h->P.epw : 64 / lpe;
+  return (h->P.n_envs + epw - 1) / epw;
+}
+
 static StepArgs step_args_of(const shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks,
                             float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
                             int32_t* ticks_out, uint8_t* ready_out, const ChainArgs& ch) {
@@ -2343,7 +2359,7 @@ static void launch_step(shipsim_handle* h, int lpe, const float* action, const u
                         int32_t* ticks_out, uint8_t* ready_out) {
   const int threads = 64;
   if (h->T.ship) lpe = 16;  // recording kernels are built for the default layout only
-  const int lanes = h->P.n_envs * lpe, blocks = (lanes + threads - 1) / threads;
+  const int blocks = step_blocks(h, lpe);
 #define L(LPE, REC)                                                                                              \
   hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, REC>), dim3(blocks), dim3(threads), 0, h->stream,            \
                      step_args_of(h, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, \
@@ -2368,7 +2384,7 @@ template <int CA, int CHAIN>
 static void launch_multi(shipsim_handle* h, const float* action, const uint8_t* active, int32_t max_ticks,
                          float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
                          int32_t* ticks_out, uint8_t* ready_out, const ChainArgs& ch) {
-  const int threads = 64, blocks = (h->P.n_envs * 16 + threads - 1) / threads;
+  const int threads = 64, blocks = step_blocks(h, 16);
 #define LM(SL)                                                                                                         \
   hipLaunchKernelGGL((ast_step_kernel<true, CA, 16, false, CHAIN, SL>), dim3(blocks), dim3(threads), 0, h->stream,  \
                      step_args_of(h, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, \
@@ -2691,6 +2707,7 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
   h->lpe = cfg->n_ships > 2 ? 16 : lanes_per_env(cfg, n_envs, device);  // K > 1: 16 lanes in ship slots
   Params& P = h->P;
   memset(&P, 0, sizeof(P));
+  if (const char* e = getenv("SHIPSIM_EPW")) P.epw = atoi(e);  // envs per wave (timing experiments; 0 = full waves)
   const int ns = cfg->n_ships;
   ShipConst sc[SHIPSIM_MAX_SHIPS];
   memset(sc, 0, sizeof(sc));
@@ -2969,7 +2986,7 @@ static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, 
   // lanes per env: 16 (default) or 8 / 4 (more envs per wave when the handle holds more envs than
   // the chip has SIMD slots at 16; identical results)
   const int lpe = (h->lpe == 8 || h->lpe == 4) ? h->lpe : (h->lpe == 2 ? 4 : 16);
-  const int threads = 64, blocks = (h->P.n_envs * lpe + threads - 1) / threads;
+  const int threads = 64, blocks = step_blocks(h, lpe);
 #define CHAINED_L(D, CA, LPE)                                                                                          \
   hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, MODE>), dim3(blocks), dim3(threads), 0, h->stream,        \
                      step_args_of(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out,     \
