@@ -509,6 +509,36 @@ __device__ __forceinline__ bool sbmpc_far(const SbIn& in, int n_samp, double DT)
   return ex * ex + ey * ey > lim * lim;
 }
 
+// running state of a scenario's horizon: best (s1 at time t1, squared distance q1) and runner-up s2 of the
+// ranking t·d², and whether any in-range sample sat within a rounding band of a decision (unc)
+struct HzBest {
+  double s1, s2, t1, q1;
+  bool unc;
+};
+struct HzConst {
+  double so, co, ovr2, ot2, ah2, cl2;  // obstacle heading sin/cos, squared thresholds
+  bool ovr;                            // the overtaking override of d_safe_i holds for every sample
+};
+// one horizon sample (time tt, offset (d0, d1), d2s = |.|²) into the running state; inr: the sample is within
+// max_d_safe (one beyond it contributes nothing and flags nothing). Branch-free (& | on bools).
+__device__ __forceinline__ void hz_sample(HzBest& h, const HzConst c, double tt, double d0, double d1, double d2s,
+                                          bool inr) {
+  constexpr double kEps = 1e-12;
+  // sector of phi_o (see sbmpc_sample_cost): overtaking sector iff cr >= 0 and ey > 0
+  const double ex = c.so * (-d0) - c.co * (-d1), ey = c.co * (-d0) + c.so * (-d1);
+  const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
+  const bool sec_ok = (cr * cr > 1e-18 * d2s) & (ey * ey > 1e-18 * d2s);
+  const double D2 = c.ovr ? c.ovr2 : (((cr >= 0) & (ey > 0)) ? c.ot2 : c.ah2);
+  const bool member = inr & (d2s < D2 * (1.0 - kEps)) & (d2s < c.cl2 * (1.0 - kEps));
+  h.unc = h.unc | (inr & (((!c.ovr) & (!sec_ok)) | (fabs(d2s - D2) <= kEps * D2) | (fabs(d2s - c.cl2) <= kEps * c.cl2)));
+  const double sc = member ? tt * d2s * d2s : INFINITY;
+  const bool lt1 = sc < h.s1;
+  h.s2 = fmin(h.s2, fmax(h.s1, sc));  // runner-up: the old best if sc takes the lead, else min(s2, sc)
+  h.t1 = lt1 ? tt : h.t1;
+  h.q1 = lt1 ? d2s : h.q1;
+  h.s1 = fmin(h.s1, sc);
+}
+
 __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
 #ifdef SHIPSIM_PHASE_TIMING
   SbTimer sb_timer;
@@ -548,6 +578,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   if (psi_w != psi_d) sincos(psi_w, &sp0, &cp0);
   const double H2 = sbmpc_h2(in, ichi, jp);
   int i_last = n_samp - 1;  // (set by the skip test below)
+  int i_past = n_samp + 1;  // first sample past the closest approach, with a one-sample margin (ditto)
   // Exact skip of the horizon loop: H0 can only be non-zero at samples with dist < max_d_safe.
   // After sample 0 both predictions are straight lines (the own ship's sway is zeroed after the
   // first step), so the relative position is P1 + k·W, k = 0..n_samp-2; if its continuous minimum
@@ -573,6 +604,11 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     const double disc = b * b - ww * cq;
     const double j2 = (ww > 0 && disc >= 0) ? (-b + sqrt(disc)) / ww : (double)n_samp;
     i_last = (j2 < (double)(n_samp - 2)) ? (int)floor(j2) + 2 : n_samp - 1;
+    // Past the continuous minimum k of |P1 + j·W| both t and the distance grow, so the ranking t·d⁴ grows
+    // sample by sample: once a sample there ranks beyond the best so far by more than the runner-up band,
+    // no later sample can win or tie (and a later sample's flags cannot change the result). Sample i = j + 1;
+    // k is clamped to the horizon, so a minimum at its end never stops the loop.
+    i_past = (int)ceil(k) + 3;
   }
   const double lim2 = (max_d_safe * (1.0 + 1e-9)) * (max_d_safe * (1.0 + 1e-9));
   // Sample 0 (own ship at wrap(psi_d) with its current sway) exactly as the reference.
@@ -607,13 +643,18 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   double ox = in.ob_x, oy = in.ob_y;
   double sx = in.os_x + DT * (q11 * ud + q12 * in.os_v), sy = in.os_y + DT * (q21 * ud + q22 * in.os_v);
   double t = DT;
-  double s1 = INFINITY, s2 = INFINITY, t1 = 0.0, q1 = 0.0;
-  bool unc = false;
 #ifdef SHIPSIM_ABL_NO_SBLOOP
   n_samp = 1;  // ablation build only: no horizon samples after sample 0
 #endif
+  HzBest hb{INFINITY, INFINITY, 0.0, 0.0, false};
+  const HzConst hc{so, co, ovr2, ot2, ah2, cl2, ovr};
+  auto sample = [&](double tt, double d0, double d1, double d2s, bool inr) __attribute__((always_inline)) {
+    hz_sample(hb, hc, tt, d0, d1, d2s, inr);
+  };
+#ifdef SHIPSIM_SB_ROLLED  // diagnostics build: one sample per iteration
+  bool done = false;  // past the minimum and beyond the best (see i_past)
   for (int i = 1; i < n_samp; ++i) {
-    if (!__any(i <= i_last)) break;  // every lane of the wave is past its last reachable sample
+    if (!__any((i <= i_last) & !done)) break;  // every lane of the wave is past its last useful sample
     ox = ox + dox;
     oy = oy + doy;
     if (i > 1) {
@@ -623,26 +664,51 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     t += DT;
     const double d0 = ox - sx, d1 = oy - sy;
     const double d2s = d0 * d0 + d1 * d1;
-    if (d2s < lim2) {  // samples beyond max_d_safe contribute nothing
-      // sector of phi_o (see sbmpc_sample_cost): overtaking sector iff cr >= 0 and ey > 0.
-      // Non-short-circuit boolean algebra (& | on bools): no exec-mask branches inside the body.
-      // (The in-range branch itself stays: most samples of an env's requests are out of range, and
-      // a branch-free body measured 193 M vs 237 M env-ticks/s in the sbmpc bench.)
-      const double ex = so * (-d0) - co * (-d1), ey = co * (-d0) + so * (-d1);
-      const double cr = kCosPhiAh * ey - kSinPhiAh * ex;
-      const bool sec_ok = (cr * cr > 1e-18 * d2s) & (ey * ey > 1e-18 * d2s);
-      const double D2 = ovr ? ovr2 : (((cr >= 0) & (ey > 0)) ? ot2 : ah2);
-      const bool member = (d2s < D2 * (1.0 - kEps)) & (d2s < cl2 * (1.0 - kEps));
-      unc = unc | ((!ovr) & (!sec_ok)) | (fabs(d2s - D2) <= kEps * D2) | (fabs(d2s - cl2) <= kEps * cl2);
-      const double sc = member ? t * d2s * d2s : INFINITY;
-      const bool lt1 = sc < s1;
-      s2 = fmin(s2, fmax(s1, sc));  // runner-up: the old best if sc takes the lead, else min(s2, sc)
-      t1 = lt1 ? t : t1;
-      q1 = lt1 ? d2s : q1;
-      s1 = fmin(s1, sc);
-    }
+    // (The in-range branch stays: most samples of an env's requests are out of range, and a branch-free
+    // body measured 193 M vs 237 M env-ticks/s in the sbmpc bench.)
+    if (d2s < lim2) sample(t, d0, d1, d2s, true);
+    done = done | ((i >= i_past) & (hb.s1 < INFINITY) & (t * d2s * d2s > hb.s1 * (1.0 + 2e-10)));
   }
-  if (unc)
+#else
+  // two samples per iteration (i, i + 1): their bodies are independent chains the one wave of the SIMD
+  // can interleave; the positions are the same incremental sums as one per iteration, and the samples
+  // enter the running best in order (ties keep the earlier sample)
+  int i = 1;
+  bool done = false;  // past the minimum and beyond the best (see i_past)
+  for (; i + 1 < n_samp; i += 2) {
+    if (!__any((i <= i_last) & !done)) break;  // every lane of the wave is past its last useful sample
+    const double oxa = ox + dox, oya = oy + doy;
+    const double sxa = (i > 1) ? sx + dsx : sx, sya = (i > 1) ? sy + dsy : sy;
+    const double ta = t + DT;
+    ox = oxa + dox;
+    oy = oya + doy;
+    sx = sxa + dsx;
+    sy = sya + dsy;
+    t = ta + DT;
+    const double d0a = oxa - sxa, d1a = oya - sya, d0b = ox - sx, d1b = oy - sy;
+    const double d2a = d0a * d0a + d1a * d1a, d2b = d0b * d0b + d1b * d1b;
+    const bool ia = d2a < lim2, ib = d2b < lim2;
+    if (ia | ib) {
+      sample(ta, d0a, d1a, d2a, ia);
+      sample(t, d0b, d1b, d2b, ib);
+    }
+    done = done | ((i + 1 >= i_past) & (hb.s1 < INFINITY) & (t * d2b * d2b > hb.s1 * (1.0 + 2e-10)));
+  }
+  if (i < n_samp && __any((i <= i_last) & !done)) {  // the last sample of an odd count
+    ox = ox + dox;
+    oy = oy + doy;
+    if (i > 1) {
+      sx = sx + dsx;
+      sy = sy + dsy;
+    }
+    t += DT;
+    const double d0 = ox - sx, d1 = oy - sy;
+    const double d2s = d0 * d0 + d1 * d1;
+    if (d2s < lim2) sample(t, d0, d1, d2s, true);
+  }
+#endif
+  const double s1 = hb.s1, s2 = hb.s2, t1 = hb.t1, q1 = hb.q1;
+  if (hb.unc)
     return sbmpc_scenario_cost_direct(in, n_samp, DT, ud, sp, cp, sp0, cp0, so, co, vo0, vo1, no, max_d_safe, lim2,
                                       cos_ot, H2);
   SB_MARK(2);
