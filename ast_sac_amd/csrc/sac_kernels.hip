@@ -192,9 +192,10 @@ struct MScratch {
   float *dg1pi[2];                         // critic input gradient on (obs, ã) rows [B][H]
   // per-row dot products of a layer output with a head weight vector, one partial per 32-column
   // block (the epilogue of the tile that produced those columns), summed in block order by the consumer
-  float *hpart;  // actor heads: [mean | log_std][H/32][2B] over the obs and next_obs rows
-  float *qpart;  // critic heads g2 · w3: [Q1 | Q2 | T1 | T2][H/32][2B] (targets: rows [0, B))
-  float *apart;  // dg1 · (fc0 action column) on the (obs, ã) rows: [Q1 | Q2][H/32][B]
+  // (row-major per row: a consumer's CB parts of one row are contiguous, float4 loads when CB % 4 == 0)
+  float *hpart;  // actor heads: [2B][mean | log_std][H/32] over the obs and next_obs rows
+  float *qpart;  // critic heads g2 · w3: [Q1 | Q2 | T1 | T2][2B][H/32] (targets: rows [0, B))
+  float *apart;  // dg1 · (fc0 action column) on the (obs, ã) rows: [Q1 | Q2][B][H/32]
 };
 enum { HD_MEAN, HD_LSRAW, HD_STD, HD_Z, HD_A, HD_LOGP };
 
@@ -280,6 +281,22 @@ __device__ __forceinline__ float sum_parts(const float* part, int64_t stride, in
   return s;
 }
 
+// n (compile-time) contiguous floats from p, 16-byte aligned when n % 4 == 0: float4 loads then (fewer
+// vector-memory instructions in flight: a wave stalls issuing its 64th outstanding load)
+template <int N>
+__device__ __forceinline__ void load_run(const float* p, float (&v)[N]) {
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) {
+      const float4 x = reinterpret_cast<const float4*>(p)[q];
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = p[i];
+  }
+}
+
 // a contiguous run of n floats of the parameters into LDS (the block's first-layer weights)
 __device__ __forceinline__ void stage(float* dst, const float* src, int n) {
   for (int e = threadIdx.x; e < n; e += kThreads) dst[e] = src[e];
@@ -344,7 +361,7 @@ constexpr int kLdsXOff = kLdsA + kLdsW1;
 constexpr int kLdsTileOff = kLdsA;
 constexpr int kLdsHeadWOff = kLdsA + kLdsTile;
 
-// 32 consecutive rows of a row-major [*][H] activation matrix <-> an LDS tile of pitch H + 4, in
+// 32 consecutive rows of a row-major [*][H] activation matrix -> an LDS tile of pitch H + 4, in
 // float4 pieces (coalesced: a wave moves whole 1 KiB rows). The MFMA A operand wants one row per lane
 // (lane & 31), which read straight from the matrix would touch 32 rows per instruction.
 template <int H>
@@ -365,27 +382,18 @@ __device__ __forceinline__ void tile_load(float* t, const float* src) {
     if (kFull || e < 32 * C4) *reinterpret_cast<float4*>(t + r * (H + 4) + 4 * c) = make_float4(vx[i], vy[i], vz[i], vw[i]);
   }
 }
-template <int H>
-__device__ __forceinline__ void tile_store(float* dst, const float* t) {
-  constexpr int C4 = H / 4, kIt = (32 * C4 + kThreads - 1) / kThreads;
-#pragma unroll
-  for (int i = 0; i < kIt; ++i) {
-    const int e = threadIdx.x + i * kThreads, r = e / C4, c = e % C4;
-    if (e < 32 * C4)
-      *reinterpret_cast<float4*>(dst + (int64_t)r * H + 4 * c) = *reinterpret_cast<const float4*>(t + r * (H + 4) + 4 * c);
-  }
-}
-// this lane's operands (row lane & 31, columns kb .. kb + H/8) into the tile, then the tile to memory
-template <int H>
-__device__ __forceinline__ void store_operands(float* dst, float* t, const float (&av)[kMaxN2], int kb) {
-  const int rr = threadIdx.x & 31;
-#pragma unroll
-  for (int i = 0; i < H / 8; ++i) t[rr * (H + 4) + kb + i] = av[i];
-  __syncthreads();
-  tile_store<H>(dst, t);
-  __syncthreads();
-}
 
+// this lane's operands (row lane & 31, columns kb .. kb + H/8) straight to its row of the matrix, by the
+// column block whose columns they are (kb / 32 == by): float4 stores, no LDS staging or block barrier,
+// and the rows' stores spread over the column blocks instead of delaying block column 0
+template <int H>
+__device__ __forceinline__ void store_slice(float* base, int r0, int by, const float (&av)[kMaxN2], int kb) {
+  constexpr int n2 = H / 8;
+  if (kb / kTile2 != by) return;
+  float4* d = reinterpret_cast<float4*>(base + (int64_t)(r0 + (threadIdx.x & 31)) * H + kb);
+#pragma unroll
+  for (int q = 0; q < n2 / 4; ++q) d[q] = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+}
 // one batch item (replay sample or given batch) and its two reparameterisation normals
 __device__ __forceinline__ int64_t batch_item(const MArgs& a, int r, float& e0, float& e1) {
   int64_t idx = r;
@@ -461,7 +469,7 @@ __device__ __forceinline__ void actor_fwd_tile(const MArgs& a, int bx, int by, f
   SAC_T(0, 2);
   // h1 for this lane's k (fmaf chain from the bias, as fc0 computes it)
   first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O, kb, av);
-  if (by == 0 && r0 < B) store_operands<H>(a.sc.a_h1 + (int64_t)r0 * H, lds, av, kb);  // block-uniform
+  if (r0 < B) store_slice<H>(a.sc.a_h1, r0, by, av, kb);
   SAC_T(0, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
@@ -475,8 +483,8 @@ __device__ __forceinline__ void actor_fwd_tile(const MArgs& a, int bx, int by, f
     // this column block's part of the mean / log_std heads of row r (rows [0, 2B))
     const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
     if (cc == 0) {
-      a.ms.hpart[(int64_t)by * 2 * B + r] = pm;
-      a.ms.hpart[(int64_t)(CB + by) * 2 * B + r] = ps;
+      a.ms.hpart[(int64_t)r * 2 * CB + by] = pm;
+      a.ms.hpart[(int64_t)r * 2 * CB + CB + by] = ps;
     }
   });
   SAC_T(0, 5);
@@ -533,15 +541,11 @@ __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, 
   // addresses are valid for either row kind) so no branch splits the batch of loads.
   const float* xr = (is_t ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
   float xin[kXLd];
-#pragma unroll
-  for (int m = 0; m < kXLd; ++m) xin[m] = xr[m];
+  load_run<kXLd>(xr, xin);
   const int64_t hr = (is_t ? B : 0) + item;
   float pm[CB], pls[CB];
-#pragma unroll
-  for (int cb = 0; cb < CB; ++cb) {
-    pm[cb] = a.ms.hpart[cb * (int64_t)(2 * B) + hr];
-    pls[cb] = a.ms.hpart[(CB + cb) * (int64_t)(2 * B) + hr];
-  }
+  load_run<CB>(a.ms.hpart + hr * 2 * CB, pm);
+  load_run<CB>(a.ms.hpart + hr * 2 * CB + CB, pls);
   const float bm = P[L.p_bm], bs = P[L.p_bs];
   const float ev = a.ms.eps[(is_t ? B : 0) + item];
   const float act_data = a.ms.act[item];
@@ -586,11 +590,11 @@ __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, 
   }
   __syncthreads();
   first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O + 1, kb, av);
-  if (by == 0 && !is_t) {  // block-uniform
-    if (data && w == 0 && h == 0)
+  if (!is_t) {  // block-uniform
+    if (by == 0 && data && w == 0 && h == 0)
 #pragma unroll
       for (int m = 0; m < kXLd; ++m) a.sc.q_x[net][(int64_t)item * kXLd + m] = m < O ? xin[m] : (m == O ? act : 0.0f);
-    store_operands<H>((data ? a.sc.q_g1[net] + (int64_t)(r0 - B) * H : a.ms.g1pi[net] + (int64_t)r0 * H), lds, av, kb);
+    store_slice<H>(data ? a.sc.q_g1[net] : a.ms.g1pi[net], data ? r0 - B : r0, by, av, kb);
   }
   SAC_T(1, 3);
   f32x16 acc = zero16();
@@ -603,7 +607,7 @@ __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, 
     else if (r >= B) a.sc.q_g2[net][(int64_t)(r - B) * H + col] = y;
     else a.ms.g2pi[net][(int64_t)r * H + col] = y;
     const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
-    if (cc == 0) a.ms.qpart[((int64_t)net * CB + by) * 2 * B + r] = pq;
+    if (cc == 0) a.ms.qpart[((int64_t)net * 2 * B + r) * CB + by] = pq;
   });
   SAC_T(1, 5);
   SAC_SPAN_END(1);
@@ -654,13 +658,10 @@ __device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, 
   const int64_t qs = (int64_t)CB * 2 * B;  // one net's parts
   const int64_t qrow = data ? B + item : item;
   float q1p[CB], q2p[CB], t1p[CB], t2p[CB];
-#pragma unroll
-  for (int cb = 0; cb < CB; ++cb) {
-    q1p[cb] = qp[cb * (int64_t)(2 * B) + qrow];
-    q2p[cb] = qp[qs + cb * (int64_t)(2 * B) + qrow];
-    t1p[cb] = qp[2 * qs + cb * (int64_t)(2 * B) + item];
-    t2p[cb] = qp[3 * qs + cb * (int64_t)(2 * B) + item];
-  }
+  load_run<CB>(qp + qrow * CB, q1p);
+  load_run<CB>(qp + qs + qrow * CB, q2p);
+  load_run<CB>(qp + 2 * qs + (int64_t)item * CB, t1p);
+  load_run<CB>(qp + 3 * qs + (int64_t)item * CB, t2p);
   const float bq1 = P[L.q_base[0] + L.c_b3], bq2 = P[L.q_base[1] + L.c_b3];
   const float bt1 = TG[L.c_b3], bt2 = TG[L.q_size + L.c_b3];
   const float logp_n = a.ms.hdn[HD_LOGP * B + item], rew_i = a.ms.rew[item], term_i = a.ms.term[item];
@@ -739,7 +740,7 @@ __device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, 
     const int j = kb + i;
     av[i] = tg[(lane & 31) * (H + 4) + j] > 0.0f ? dq * lw3[j] : 0.0f;
   }
-  if (data && by == 0) store_operands<H>(a.sc.q_dg2[net] + (int64_t)ib * H, tg, av, kb);  // block-uniform
+  if (data) store_slice<H>(a.sc.q_dg2[net], ib, by, av, kb);
   SAC_T(2, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);
@@ -754,7 +755,7 @@ __device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, 
       const float d = g1m[q] > 0.0f ? v : 0.0f;
       a.ms.dg1pi[net][o] = d;
       const float pa = halfwave_sum(d * wa);  // this column block's part of dQ/dã for row r
-      if (cc == 0) a.ms.apart[((int64_t)net * CB + by) * B + r] = pa;
+      if (cc == 0) a.ms.apart[((int64_t)net * B + r) * CB + by] = pa;
     }
   });
   SAC_T(2, 5);
@@ -785,11 +786,8 @@ __device__ __forceinline__ void actor_bwd_tile(const MArgs& a, int bx, int by, f
   // the row's dQ/dã partials, head and noise first (the prologue's longest chain; vector loads complete
   // in issue order, so the staging loads below queue behind them)
   float ap1[CB], ap2[CB];
-#pragma unroll
-  for (int cb = 0; cb < CB; ++cb) {
-    ap1[cb] = a.ms.apart[cb * (int64_t)B + item];
-    ap2[cb] = a.ms.apart[(int64_t)CB * B + cb * (int64_t)B + item];
-  }
+  load_run<CB>(a.ms.apart + (int64_t)item * CB, ap1);
+  load_run<CB>(a.ms.apart + ((int64_t)B + item) * CB, ap2);
   const float act = a.ms.hd[HD_A * B + item], z = a.ms.hd[HD_Z * B + item], mean = a.ms.hd[HD_MEAN * B + item];
   const float std = a.ms.hd[HD_STD * B + item], ls_raw = a.ms.hd[HD_LSRAW * B + item];
   const float eps_i = a.ms.eps[item];
@@ -836,7 +834,7 @@ __device__ __forceinline__ void actor_bwd_tile(const MArgs& a, int bx, int by, f
     const int j = kb + i;
     av[i] = th[(lane & 31) * (H + 4) + j] > 0.0f ? (lwh[j] * dmean + lwh[H + j] * dls) : 0.0f;
   }
-  if (by == 0) store_operands<H>(a.sc.a_dh2 + (int64_t)r0 * H, th, av, kb);
+  store_slice<H>(a.sc.a_dh2, r0, by, av, kb);
   SAC_T(3, 3);
   f32x16 acc = zero16();
   mfma_chain(acc, av, bv, n2);

@@ -591,7 +591,8 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     const double p1y = (in.ob_y + voy * DT) - (in.os_y + DT * (q21 * ud + q22 * in.os_v));
     const double wx = (vox - q11 * ud) * DT, wy = (voy - q21 * ud) * DT;
     const double ww = wx * wx + wy * wy;
-    double k = ww > 0 ? -(p1x * wx + p1y * wy) / ww : 0.0;
+    const double iww = ww > 0 ? 1.0 / ww : 0.0;  // (k and j2 below only place bounds with margins)
+    double k = ww > 0 ? -(p1x * wx + p1y * wy) * iww : 0.0;
     k = k < 0 ? 0 : (k > n_samp - 2 ? n_samp - 2 : k);
     const double mx = p1x + k * wx, my = p1y + k * wy;
     const double lim = max_d_safe + 1e-3;
@@ -602,7 +603,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     // below differ from this closed form by ~1e-10 m, far inside the 1e-3 m of lim). Sample i = j + 1.
     const double b = p1x * wx + p1y * wy, cq = p1x * p1x + p1y * p1y - lim * lim;
     const double disc = b * b - ww * cq;
-    const double j2 = (ww > 0 && disc >= 0) ? (-b + sqrt(disc)) / ww : (double)n_samp;
+    const double j2 = (ww > 0 && disc >= 0) ? (-b + sqrt(disc)) * iww : (double)n_samp;
     i_last = (j2 < (double)(n_samp - 2)) ? (int)floor(j2) + 2 : n_samp - 1;
     // Past the continuous minimum k of |P1 + j·W| both t and the distance grow, so the ranking t·d⁴ grows
     // sample by sample: once a sample there ranks beyond the best so far by more than the runner-up band,
@@ -727,7 +728,10 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
 }
 
 // Must be called by every lane of the wave (wave-uniform control flow). `need` marks lanes that
-// request an optimisation with inputs `in`; they receive (P_best, Chi_best).
+// request an optimisation with inputs `in`; they receive (P_best, Chi_best). SHIP_UNIFORM: u_d, obs_l and
+// obs_w are the same for every request and set in every lane's `in` (the AST kernels: the ships'
+// configured desired speed and obstacle size), so they are not gathered from the requesting lane.
+template <bool SHIP_UNIFORM = false>
 __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double DT, double& p_best,
                                   double& chi_best) {
   SHIPSIM_LANE_CHECK(64, 4);
@@ -746,11 +750,15 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
     int src = half ? src1 : src0;
     int srcc = src < 0 ? src0 : src;
     SbIn g;
-    g.u_d = shfl_d(in.u_d, srcc); g.chi_d = shfl_d(in.chi_d, srcc);
+    if constexpr (SHIP_UNIFORM) {
+      g.u_d = in.u_d; g.obs_l = in.obs_l; g.obs_w = in.obs_w;
+    } else {
+      g.u_d = shfl_d(in.u_d, srcc); g.obs_l = shfl_d(in.obs_l, srcc); g.obs_w = shfl_d(in.obs_w, srcc);
+    }
+    g.chi_d = shfl_d(in.chi_d, srcc);
     g.os_x = shfl_d(in.os_x, srcc); g.os_y = shfl_d(in.os_y, srcc); g.os_v = shfl_d(in.os_v, srcc);
     g.ob_x = shfl_d(in.ob_x, srcc); g.ob_y = shfl_d(in.ob_y, srcc); g.ob_psi = shfl_d(in.ob_psi, srcc);
     g.ob_u = shfl_d(in.ob_u, srcc); g.ob_v = shfl_d(in.ob_v, srcc);
-    g.obs_l = shfl_d(in.obs_l, srcc); g.obs_w = shfl_d(in.obs_w, srcc);
     g.p_last = shfl_d(in.p_last, srcc); g.chi_last = shfl_d(in.chi_last, srcc);
     g.ob_so = shfl_d(in.ob_so, srcc); g.ob_co = shfl_d(in.ob_co, srcc);
     double cost = INFINITY;
@@ -1706,6 +1714,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     } else if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
       bool need = false;
       SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      in.u_d = SC[0].desired_speed;  // the same in every lane (sbmpc_cooperative<true>)
+      in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
       if (going && is_test) {
         // env.py:362-363: next_wpt result discarded; los_guidance integrates e_ct_int (Q3). The
         // course (atan) only feeds the optimisation, so it is evaluated for requesting envs only.
@@ -1718,15 +1728,13 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         need = false;
 #endif
         if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
-        in.u_d = c.desired_speed;
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
         in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
         in.ob_so = -psy; in.ob_co = pcy;  // sin(-yaw) = -sin(yaw), cos(-yaw) = cos(yaw)
-        in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
         in.p_last = p_last; in.chi_last = chi_last;
       }
       double pb = 1.0, cb = 0.0;
-      sbmpc_cooperative(need && sub == 0, in, P.sbmpc_nsamp, P.sbmpc_dt, pb, cb);
+      sbmpc_cooperative<true>(need && sub == 0, in, P.sbmpc_nsamp, P.sbmpc_dt, pb, cb);
       pb = env_lane_d<LPE, 0>(pb, env_lane0);
       cb = env_lane_d<LPE, 0>(cb, env_lane0);
       const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
@@ -2140,6 +2148,8 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevStat
     if (COLLAV == SHIPSIM_COLLAV_SBMPC) {  // test_step :938-963 (obstacle ship before it moves)
       bool need = false;
       SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      in.u_d = SC[0].desired_speed;  // the same in every lane (sbmpc_cooperative<true>)
+      in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
       if (going && is_test) {
         const double los_arg = los_update(c, s, s.n, s.e);
         const double d0 = pe - s.e, d1 = pn - s.n;
@@ -2150,15 +2160,13 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevStat
         need = false;
 #endif
         if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
-        in.u_d = c.desired_speed;
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
         in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
         sb_set_heading_trig(in);
-        in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
         in.p_last = p_last; in.chi_last = chi_last;
       }
       double pb = 1.0, cb = 0.0;
-      sbmpc_cooperative(need, in, n_samp, P.sbmpc_dt, pb, cb);
+      sbmpc_cooperative<true>(need, in, n_samp, P.sbmpc_dt, pb, cb);
       if (going && is_test) {
         if (need) { p_last = pb; chi_last = cb; sf = pb; off = cb; }
         else { p_last = 1; chi_last = 0; }
