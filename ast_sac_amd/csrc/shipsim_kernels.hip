@@ -335,6 +335,13 @@ __device__ __forceinline__ int opaque_v(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// opaque_v where OPQ (the kernels whose allocation otherwise spills the lane masks derived from x), x as is
+// elsewhere (there the recomputation costs more than the held mask)
+template <bool OPQ>
+__device__ __forceinline__ int opaque_if(int x) {
+  if constexpr (OPQ) return opaque_v(x);
+  return x;
+}
 
 __device__ __forceinline__ double shfl_d(double x, int src) {
   int lo = __double2loint(x), hi = __double2hiint(x);
@@ -799,7 +806,7 @@ struct SbMulti {
 };
 
 template <int NOB>
-__device__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n_obs, int n_samp, double DT,
+__device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti<NOB>& in, int n_obs, int n_samp, double DT,
                                         double& p_best, double& chi_best) {
   SHIPSIM_LANE_CHECK(64, 4);
   const int lane = opaque_v(threadIdx.x) & 63;
@@ -1108,6 +1115,7 @@ __device__ __forceinline__ float policy_actions(bool want, const float ns[8], in
   const int lane = threadIdx.x & 63;
   const int H = CH.pol_hidden, nj = H / 64, u0 = lane * nj;
   const float* W1 = CH.policy;  // [H][8] (obs_dim 8: checked by the host)
+  asm volatile("" : "+s"(W1));  // (the weight addresses below derived per call, not held across the tick loop)
   const float* b1 = W1 + (size_t)H * 8;
   const float* b2 = b1 + H + (size_t)H * H;
   const float* wm = b2 + H;
@@ -1345,6 +1353,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   static_assert(NSUB >= 1 && 8 % NSUB == 0, "sub-lanes per ship must divide 8 (grid_part shares)");
   static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 16, "LPE must be a power of two in [2, 16]");
   constexpr bool SIMPLE = COLLAV == SHIPSIM_COLLAV_SIMPLE;
+  constexpr bool OPQ = LPE != 16 || POLICY;  // see opaque_if (measured: LPE-16 table kernels hold no spills without)
   __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
   __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
@@ -1398,7 +1407,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   double* re = S.route_e() + (size_t)qc * kMaxRoute;
 
   bool running = valid && (A0.active_mask == nullptr || A0.active_mask[envc]) && S.was_reset()[envc];
-  const bool touched = running;
+  // (ints in VGPRs read by the epilogue: not lane masks held in SGPRs for the whole launch)
+  const int touched = opaque_v(running && valid ? 1 : 0);
 
   Ship s;
   load_ship(S, qc, s);
@@ -1802,7 +1812,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         // 8 sub-lanes for 4 corners: sub-lanes k and k + 4 split corner k's ring edges (every other
         // edge) and combine the crossing parity (XOR) and the boundary flag (OR) per polygon — the
         // same boolean as corner_inside (the partner lane is 4·SLOTS lanes away, same env and ship)
-        const int k = sub & 3, half = sub >> 2;
+        const int sv = opaque_if<OPQ>(sub);  // (recomputed in the loop: no lane masks kept across it)
+        const int k = sv & 3, half = sv >> 2;
         const double cn = (k < 2) ? s.n - margin : s.n + margin;
         const double ce = (k & 1) ? s.e + margin : s.e - margin;
         const int c = K.cell(cn, ce);
@@ -1813,7 +1824,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         const uint32_t bnd_o = (uint32_t)__shfl_xor((int)bnd, 4 * SLOTS, 64);
         if (f == GRID_MIXED ? (((par ^ par_o) & ~(bnd | bnd_o)) != 0) : (f == GRID_IN)) gr = true;
       } else {
-        for (int k = sub; k < 4; k += NSUB) {
+        for (int k = opaque_if<OPQ>(sub); k < 4; k += NSUB) {  // (opaque: no lane masks kept across the loop)
           const double cn = (k < 2) ? s.n - margin : s.n + margin;
           const double ce = (k & 1) ? s.e + margin : s.e - margin;
           if (corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) gr = true;
@@ -1910,7 +1921,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       const double of[5] = {200000000.0, 175000.0, 1250000.0, 50000.0, 12500.0};
       double ex[5];
       if (LPE >= 8) {
-        const int j = lie & 7;
+        const int j = opaque_if<OPQ>(lie) & 7;  // (recomputed in the loop: no lane masks kept across it)
         const double xj = (j == 0) ? xv[0] : (j == 1) ? xv[1] : (j == 2) ? xv[2] : (j == 3) ? xv[3] : xv[4];
         const double tj = (j == 2) ? tg[2] : (j == 4) ? tg[4] : 0.0;
         const double oj = (j == 0) ? of[0] : (j == 1) ? of[1] : (j == 2) ? of[2] : (j == 3) ? of[3] : of[4];
@@ -2025,7 +2036,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     for (int k = 0; k < 4; ++k) atomicAdd(&g_phase_cycles[k], pt_acc[k]);
 #endif
 
-  if (!valid || !touched) return;
+  if (touched == 0) return;  // (!valid || !touched)
   const StepArgs& AE = step_args();  // not the values loaded before the loop (no live range across it)
   const ChainArgs& CH = AE.CH;
   const Traj& TE = AE.T;
@@ -2035,20 +2046,23 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
            ticks, sampling_count, n_base, phase, (int)have_iw);
 #endif
   const DevState So = opaque(AE.S);  // addresses recomputed here, not carried through the loop
-  if (sub == 0 && !ghost) store_ship(So, qc, s);
+  // the lane's role re-derived here (opaque), not lane masks carried through the loop
+  const int lie_e = opaque_v(lie), sub_e = lie_e / SLOTS, ship_e = lie_e % SLOTS;
+  const bool ghost_e = (SLOTS > 2) && ship_e >= nsh;
+  if (sub_e == 0 && !ghost_e) store_ship(So, qc, s);
   if (REC) {
-    if (sub == 0)
+    if (sub_e == 0)
       for (int k = 0; k < 3; ++k) TE.fuel[(size_t)qc * 3 + k] = fuel[k];
-    if (lie == 0) TE.len[env] = rec_t;
+    if (lie_e == 0) TE.len[env] = rec_t;
   }
-  if (CHAIN && lie == 0) {
+  if (CHAIN && lie_e == 0) {
     CH.ep_idx[env] = ep_i;
     CH.dec_idx[env] = dec_i;
     if (CH.decisions) CH.decisions[env] = n_decided;
     if (CH.log_len) CH.log_len[env] = log_n;
     So.mach_dt()[env] = mach_dt;
   }
-  if (lie == 0) {
+  if (lie_e == 0) {
     So.sampling_count()[env] = sampling_count;
     So.travel_dist()[env] = travel_dist; So.travel_time()[env] = travel_time; So.acc()[env] = acc;
     So.n_base()[env] = n_base; So.e_base()[env] = e_base;
@@ -2070,12 +2084,12 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     if (AE.ticks_out) AE.ticks_out[env] = ticks;
     if (AE.ready_out) AE.ready_out[env] = ready ? 1 : 0;
   }
-  if (ready && AE.obs_out && sub == 0 && ship < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
+  if (ready && AE.obs_out && sub_e == 0 && ship_e < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // (values in registers first: a select of two ns elements would become
       float a = ns[i], b = ns[4 + i];  // an indexed ns, i.e. the whole array in scratch)
       asm volatile("" : "+v"(a), "+v"(b));
-      AE.obs_out[env * 8 + ship * 4 + i] = ship ? b : a;
+      AE.obs_out[env * 8 + ship_e * 4 + i] = ship_e ? b : a;
     }
   }
 }
