@@ -1386,7 +1386,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   __syncthreads();
 
   // one wave per block: envs [blockIdx.x * epw, + epw) on lanes [0, epw * LPE); lanes past them idle
-  const int epw = P.epw > 0 ? P.epw : 64 / LPE;
+  const int epw = P.epw > 0 && P.epw <= 64 / LPE ? P.epw : 64 / LPE;  // (as step_blocks)
   const int eslot = (int)(threadIdx.x & 63) / LPE;
   const int env = (int)blockIdx.x * epw + eslot;
   const int lie = (int)(threadIdx.x & 63) % LPE;

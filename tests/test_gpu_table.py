@@ -103,3 +103,20 @@ def test_stream_lanes_per_env_bitwise(collav, lpe):
     assert t_got == t_ref
     for i in range(N):
         np.testing.assert_array_equal(got[i], ref[i], err_msg=f"{collav} lpe {lpe} env {i}")
+
+
+@pytest.mark.parametrize("collav,epw", [("sbmpc", 1), ("sbmpc", 3), ("none", 2)])
+def test_stream_envs_per_wave_bitwise(collav, epw, monkeypatch):
+    """Waves launched with fewer envs than they hold (SHIPSIM_EPW: the idle lanes of each wave take no
+    part; the wave-cooperative SBMPC pass serves the envs it has) give bitwise the full-wave records."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    cfg = abi.ast_config(collav)
+    N = 96
+    table = _table(2, cfg.max_sampling_frequency, N, seed=7)
+    ref, t_ref = _chained(cfg, N, table, 200, 6)
+    monkeypatch.setenv("SHIPSIM_EPW", str(epw))  # read by shipsim_create
+    got, t_got = _chained(cfg, N, table, 200, 6)
+    assert t_got == t_ref
+    for i in range(N):
+        np.testing.assert_array_equal(got[i], ref[i], err_msg=f"{collav} epw {epw} env {i}")
