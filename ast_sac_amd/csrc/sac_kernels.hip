@@ -882,11 +882,12 @@ struct AdamElem {
   bool q;
 };
 
-__device__ __forceinline__ AdamElem adam_ld(const ApplyArgs& a, int64_t e) {
+// (with_g false: the caller has the gradient in hand — the fused weight-gradient pass)
+__device__ __forceinline__ AdamElem adam_ld(const ApplyArgs& a, int64_t e, bool with_g = true) {
   const Layout& L = a.L;
   AdamElem x;
   x.q = e >= L.q_base[0];
-  x.g = a.grads[e];
+  x.g = with_g ? a.grads[e] : 0.0f;
   x.m = a.m[e];
   x.v = a.v[e];
   x.p = a.params[e];
@@ -939,6 +940,7 @@ struct WgArgs {
   float* stats;
   Hyper hp;
   int n_blocks;  // grid
+  int blk0;      // (timing experiments, $SACF_WG_MODE) this launch's first block / block rotation
   int fuse;      // single process: each block also applies Adam / soft update / W2ᵀ to the elements it finished
   ApplyArgs ap;  // (fuse) parameters, optimizer state, targets, transposed copies
 };
@@ -1015,12 +1017,15 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
     int s = 0;
     int64_t l = 0;
     const GMat* m = nullptr;
+    AdamElem xv;
     if (e < a.n_small) {
       const WgTable& tb = tab;
       while (s + 1 < tb.n_small_mats && e >= tb.small_start[s + 1]) ++s;
       m = &tb.mats[tb.small_mat[s]];
       l = e - tb.small_start[s];
       const int j = (int)(l / m->N), k = (int)(l % m->N);
+      // the optimizer state of this output (the lane of wave 0 that finishes it), in flight with the row sums
+      if (a.fuse && w == 0) xv = adam_ld(a.ap, m->out_off + l, false);
       const int rq = a.B / 4, rb = w * rq;
       const gptr dy = as_global(m->dY) + (int64_t)rb * m->ldY + j;
       const gptr x = m->X ? as_global(m->X) + (int64_t)rb * m->ldX + k : nullptr;
@@ -1043,8 +1048,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
     if (w == 0 && m) {
       const int c = tid & 63;
       const int64_t e = m->out_off + l;
-      AdamElem x;
-      if (a.fuse) x = adam_ld(a.ap, e);  // (in flight while the partials are added)
+      AdamElem x = xv;
       x.g = ((part[c] + part[64 + c]) + part[128 + c]) + part[192 + c];
       a.grads[e] = x.g;
       if (a.fuse) adam_st(a.ap, sst, e, x);
@@ -1063,9 +1067,6 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
   const int w = tid >> 6, lane = tid & 63, h = lane >> 5;
   const int mat = tb.big_slot[bx / tiles];  // 0: actor W2, 1 / 2: Q1 / Q2 W2
   AdamElem x[4];
-  if (a.fuse)  // the optimizer state of the four outputs this lane finishes, in flight during the GEMM
-#pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = adam_ld(a.ap, m.out_off + (int64_t)(j0 + finish_row(q)) * m.N + k0 + (lane & 31));
   const int rows_w = a.B / 4;  // this wave's rows, in chunks of up to 64 (32 MFMAs)
   f32x16 acc = zero16();
   for (int rc = 0; rc < rows_w; rc += 2 * kMaxN2) {
@@ -1078,6 +1079,13 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
       av[i] = as_global(m.dY)[r * m.ldY + j0 + (lane & 31)];
       bv[i] = as_global(m.X)[r * m.ldX + k0 + (lane & 31)];
     }
+    // the optimizer state of the four outputs this lane finishes, in flight during the GEMM: issued after the
+    // first chunk's operands (vector loads complete in issue order, so operands first lets the MFMA chain
+    // start without waiting for these)
+    if (rc == 0 && a.fuse)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        x[q] = adam_ld(a.ap, m.out_off + (int64_t)(j0 + finish_row(q)) * m.N + k0 + (lane & 31), false);
     SAC_T(4, 1);
     mfma_chain(acc, av, bv, n2);
   }
@@ -1111,7 +1119,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
 __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
   __shared__ WgLds S;
   wgrad_stage(a, S);
-  wgrad_tile(a, blockIdx.x, S);
+  wgrad_tile(a, ((int)blockIdx.x + a.blk0) % a.n_blocks, S);
 }
 
 
@@ -1872,7 +1880,18 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   }
   if (!launch_hidden(h->L.H, a, h->stream, 0)) return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);
   launch_hidden(h->L.H, a, h->stream, 1);
-  hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_blocks), dim3(256), 0, h->stream, w);
+  static const int wg_mode = getenv("SACF_WG_MODE") ? atoi(getenv("SACF_WG_MODE")) : 0;  // timing experiments
+  if (wg_mode == 1) {  // two launches: the MFMA tiles, then the VALU elements and the scalars
+    WgArgs w1 = w;
+    w1.blk0 = 0;
+    hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_mfma), dim3(256), 0, h->stream, w1);
+    w1.blk0 = w.n_mfma;
+    hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_blocks - w.n_mfma), dim3(256), 0, h->stream, w1);
+  } else {
+    WgArgs w1 = w;
+    w1.blk0 = wg_mode == 2 ? w.n_mfma : 0;  // 2: the VALU / scalar blocks dispatched first
+    hipLaunchKernelGGL(sac_wgrad_mfma_kernel, dim3(w.n_blocks), dim3(256), 0, h->stream, w1);
+  }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
 }
