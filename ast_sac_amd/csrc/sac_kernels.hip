@@ -42,6 +42,15 @@ constexpr int kThreads = 256;
 // timing build only (scripts/build_timing.sh): wall-clock stamps of block (0, 0) thread 0 at phase
 // boundaries, each after waiting for that wave's outstanding memory operations
 __device__ unsigned long long g_sac_stamp[64];
+__device__ unsigned long long g_wg_blk[3 * 1024];  // weight-gradient pass: per block start, end, XCC id
+__device__ unsigned long long g_wg_wave[1024 * 4 * 4];  // ... per block, wave, stage (MFMA tiles)
+#define SAC_WAVE(bx, k)                                                                              \
+  do {                                                                                              \
+    if ((threadIdx.x & 63) == 0 && (bx) < 1024) {                                                   \
+      __builtin_amdgcn_s_waitcnt(0);                                                                \
+      g_wg_wave[((bx) * 4 + (threadIdx.x >> 6)) * 4 + (k)] = wall_clock64();                         \
+    }                                                                                               \
+  } while (0)
 #define SAC_TB(kern, k, cond)                                    \
   do {                                                           \
     if ((cond) && threadIdx.x == 0) {                            \
@@ -52,6 +61,11 @@ __device__ unsigned long long g_sac_stamp[64];
 #else
 #define SAC_TB(kern, k, cond) \
   do {                        \
+  } while (0)
+#endif
+#ifndef SACF_PHASE_TIMING
+#define SAC_WAVE(bx, k) \
+  do {                  \
   } while (0)
 #endif
 #define SAC_T(kern, k) SAC_TB(kern, k, blockIdx.x == 0 && blockIdx.y == 0)
@@ -394,6 +408,23 @@ __device__ __forceinline__ void store_slice(float* base, int r0, int by, const f
 #pragma unroll
   for (int q = 0; q < n2 / 4; ++q) d[q] = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
 }
+// XCD-aware block -> tile map of the forward/backward grids (gx row tiles x H/32 column tiles). The hardware
+// deals consecutive blocks round-robin over the 8 XCDs, each with its own L2; every block of one column tile
+// reads that column's 32 KB weight slice. With 8 column tiles (H = 256), column tile = linear block id mod 8
+// puts them all on one XCD, which then brings only its slice into its L2 instead of all eight (fabric
+// traffic / 8). Any placement gives the same results (the map is a bijection of the same grid).
+template <int H>
+__device__ __forceinline__ void xcd_tile(int& bx, int& by) {
+  if constexpr (H / kTile2 == 8) {
+    const int L = (int)(blockIdx.x + blockIdx.y * gridDim.x);
+    by = L & 7;
+    bx = L >> 3;
+  } else {
+    bx = (int)blockIdx.x;
+    by = (int)blockIdx.y;
+  }
+}
+
 // one batch item (replay sample or given batch) and its two reparameterisation normals
 __device__ __forceinline__ int64_t batch_item(const MArgs& a, int r, float& e0, float& e1) {
   int64_t idx = r;
@@ -495,7 +526,9 @@ __device__ __forceinline__ void actor_fwd_tile(const MArgs& a, int bx, int by, f
 template <int H>
 __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   __shared__ float lds[kLdsFloats];
-  actor_fwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
+  int bx, by;
+  xcd_tile<H>(bx, by);
+  actor_fwd_tile<H>(a, bx, by, lds);
 }
 
 // TanhNormal.rsample_and_logprob (distributions.py:346-392) of one row's head
@@ -617,7 +650,9 @@ __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, 
 template <int H>
 __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   __shared__ float lds[kLdsFloats];
-  critic_fwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
+  int bx, by;
+  xcd_tile<H>(bx, by);
+  critic_fwd_tile<H>(a, bx, by, lds);
 }
 
 // grid (2 critics x 2B / 32 row tiles, H / 32): losses and dq (sac.py:170-247), dg2, dg1 = (dg2 W2) ⊙ [g1 > 0]
@@ -766,7 +801,9 @@ __device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, 
 template <int H>
 __global__ __launch_bounds__(256) void sac_critic_bwd_kernel(MArgs a) {
   __shared__ float lds[kLdsFloats];
-  critic_bwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
+  int bx, by;
+  xcd_tile<H>(bx, by);
+  critic_bwd_tile<H>(a, bx, by, lds);
 }
 
 // grid (B / 32, H / 32): policy backward through the action (obs rows)
@@ -851,7 +888,9 @@ __device__ __forceinline__ void actor_bwd_tile(const MArgs& a, int bx, int by, f
 template <int H>
 __global__ __launch_bounds__(256) void sac_actor_bwd_kernel(MArgs a) {
   __shared__ float lds[kLdsFloats];
-  actor_bwd_tile<H>(a, blockIdx.x, blockIdx.y, lds);
+  int bx, by;
+  xcd_tile<H>(bx, by);
+  actor_bwd_tile<H>(a, bx, by, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1061,11 +1100,20 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
   const WgTable& tb = tab;
   const int H = tb.mats[tb.big[0]].M;
   const int tiles = (H / kTile2) * (H / kTile2);
-  const GMat m = tb.mats[tb.big[bx / tiles]];
-  const int t = bx % tiles;
+  // XCD-aware tile map (H = 256: 64 tiles per matrix, 24 per XCD): XCD x = bx mod 8 takes, of each matrix, the
+  // 2 x 4 tiles of row blocks 2(x / 2) + {0, 1} and column blocks 4(x mod 2) + {0..3}, so its L2 fetches a quarter
+  // of dYᵀ's columns and half of X's instead of all of both (the fabric traffic of the pass / 2.7; any placement
+  // gives the same results)
+  int bm = bx / tiles, t = bx % tiles;
+  if (H == 256 && a.n_mfma == 3 * tiles) {
+    const int x = bx & 7, sl = bx >> 3, tt = sl & 7;
+    bm = sl >> 3;
+    t = ((x >> 1) * 2 + (tt >> 2)) * 8 + (x & 1) * 4 + (tt & 3);
+  }
+  const GMat m = tb.mats[tb.big[bm]];
   const int j0 = (t / (H / kTile2)) * kTile2, k0 = (t % (H / kTile2)) * kTile2;
   const int w = tid >> 6, lane = tid & 63, h = lane >> 5;
-  const int mat = tb.big_slot[bx / tiles];  // 0: actor W2, 1 / 2: Q1 / Q2 W2
+  const int mat = tb.big_slot[bm];  // 0: actor W2, 1 / 2: Q1 / Q2 W2
   AdamElem x[4];
   const int rows_w = a.B / 4;  // this wave's rows, in chunks of up to 64 (32 MFMAs)
   f32x16 acc = zero16();
@@ -1082,6 +1130,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
     // the optimizer state of the four outputs this lane finishes, in flight during the GEMM: issued after the
     // first chunk's operands (vector loads complete in issue order, so operands first lets the MFMA chain
     // start without waiting for these)
+    if (rc == 0) SAC_WAVE(bx, 0);  // (timing build: operands only)
     if (rc == 0 && a.fuse)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -1090,8 +1139,10 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
     mfma_chain(acc, av, bv, n2);
   }
   SAC_T(4, 2);
+  SAC_WAVE(bx, 1);
   auto& tt = S.tt;  // (fuse) updated parameters / targets, transposed
   splitk_finish_q(acc, lds, [&](int q, int rr, int cc, float v) {
+    if (q == 0) SAC_WAVE(bx, 2);
     const int64_t e = m.out_off + (int64_t)(j0 + rr) * m.N + k0 + cc;
     a.grads[e] = v;
     if (a.fuse) {
@@ -1111,6 +1162,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
       if (mat > 0) a.ap.T[(size_t)(2 + mat) * HH + o] = tt[1][cc][tc];
     }
   }
+  SAC_WAVE(bx, 3);
   SAC_T(4, 3);
   SAC_SPAN_END(4);
 }
@@ -1118,8 +1170,20 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
 
 __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
   __shared__ WgLds S;
+  const int bx = ((int)blockIdx.x + a.blk0) % a.n_blocks;
+#ifdef SACF_PHASE_TIMING
+  if (threadIdx.x == 0 && bx < 1024) {
+    g_wg_blk[3 * bx] = wall_clock64();
+    g_wg_blk[3 * bx + 2] = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7;  // HW_REG_XCC_ID
+  }
+#endif
   wgrad_stage(a, S);
-  wgrad_tile(a, ((int)blockIdx.x + a.blk0) % a.n_blocks, S);
+  wgrad_tile(a, bx, S);
+#ifdef SACF_PHASE_TIMING
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0 && bx < 1024) g_wg_blk[3 * bx + 1] = wall_clock64();
+#endif
 }
 
 
@@ -1722,6 +1786,15 @@ int sacf_debug_reset(void) {
 }
 int sacf_debug_stamps(unsigned long long* out64) {
   return hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_sac_stamp), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+}
+// weight-gradient pass, per block: start, end (wall clock), XCC id; and the pass's block classes; per MFMA-tile
+// block and wave: operands loaded, MFMA chain issued, split-K sum read, done (each after the wave's memory drained)
+int sacf_debug_wg_blocks(const sacf_handle* h, unsigned long long* out, int* n_mfma, int* n_blocks,
+                         unsigned long long* waves) {
+  *n_mfma = h->wg[0].n_mfma;
+  *n_blocks = h->wg[0].n_blocks;
+  if (hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_wg_wave), sizeof(unsigned long long) * 1024 * 16) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_blk), sizeof(unsigned long long) * 3 * 1024) == hipSuccess ? 0 : -1;
 }
 #endif
 
