@@ -27,6 +27,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <type_traits>
 #include <string.h>
 
 #include <new>
@@ -1070,11 +1071,27 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
       const gptr x = m->X ? as_global(m->X) + (int64_t)rb * m->ldX + k : nullptr;
       for (int r0 = 0; r0 < rq; r0 += 32) {  // 32 rows' loads in flight, then the fmaf chain in row order
         float yv[32], xv[32];
+        if (r0 + 32 <= rq) {  // a full batch: straight-line loads, no per-load guard (see the MFMA tiles)
+          if (x) {
 #pragma unroll
-        for (int u = 0; u < 32; ++u) {
-          const bool ok = r0 + u < rq;
-          yv[u] = ok ? dy[(int64_t)(r0 + u) * m->ldY] : 0.0f;
-          xv[u] = ok ? (x ? x[(int64_t)(r0 + u) * m->ldX] : 1.0f) : 0.0f;
+            for (int u = 0; u < 32; ++u) {
+              yv[u] = dy[(int64_t)(r0 + u) * m->ldY];
+              xv[u] = x[(int64_t)(r0 + u) * m->ldX];
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 32; ++u) {
+              yv[u] = dy[(int64_t)(r0 + u) * m->ldY];
+              xv[u] = 1.0f;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 32; ++u) {
+            const bool ok = r0 + u < rq;
+            yv[u] = ok ? dy[(int64_t)(r0 + u) * m->ldY] : 0.0f;
+            xv[u] = ok ? (x ? x[(int64_t)(r0 + u) * m->ldX] : 1.0f) : 0.0f;
+          }
         }
 #pragma unroll
         for (int u = 0; u < 32; ++u) acc = fmaf(yv[u], xv[u], acc);
@@ -1120,12 +1137,30 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
   for (int rc = 0; rc < rows_w; rc += 2 * kMaxN2) {
     const int n2 = min(kMaxN2, (rows_w - rc) / 2), rb = w * rows_w + rc + h * n2;
     float av[kMaxN2], bv[kMaxN2];
+    // the chunk's operands as one straight-line batch of loads, all in flight together (a run-time guard per
+    // load would make a chain of branches with a wait after every load): n2 = 32 for B >= 256, 16 / 8 / 4 for
+    // B = 128 / 64 / 32
+    auto load_chunk = [&](auto n_tag) __attribute__((always_inline)) {
+      constexpr int N = decltype(n_tag)::value;
 #pragma unroll
-    for (int i = 0; i < kMaxN2; ++i) {
-      if (i >= n2) continue;  // (continue, not break: the constant trip count keeps the loop unrolled)
-      const int64_t r = rb + i;
-      av[i] = as_global(m.dY)[r * m.ldY + j0 + (lane & 31)];
-      bv[i] = as_global(m.X)[r * m.ldX + k0 + (lane & 31)];
+      for (int i = 0; i < N; ++i) {
+        const int64_t r = rb + i;
+        av[i] = as_global(m.dY)[r * m.ldY + j0 + (lane & 31)];
+        bv[i] = as_global(m.X)[r * m.ldX + k0 + (lane & 31)];
+      }
+    };
+    if (n2 == 32) load_chunk(std::integral_constant<int, 32>{});
+    else if (n2 == 16) load_chunk(std::integral_constant<int, 16>{});
+    else if (n2 == 8) load_chunk(std::integral_constant<int, 8>{});
+    else if (n2 == 4) load_chunk(std::integral_constant<int, 4>{});
+    else {
+#pragma unroll
+      for (int i = 0; i < kMaxN2; ++i) {
+        if (i >= n2) continue;  // (continue, not break: the constant trip count keeps the loop unrolled)
+        const int64_t r = rb + i;
+        av[i] = as_global(m.dY)[r * m.ldY + j0 + (lane & 31)];
+        bv[i] = as_global(m.X)[r * m.ldX + k0 + (lane & 31)];
+      }
     }
     // the optimizer state of the four outputs this lane finishes, in flight during the GEMM: issued after the
     // first chunk's operands (vector loads complete in issue order, so operands first lets the MFMA chain
