@@ -524,12 +524,28 @@ __device__ __forceinline__ void actor_fwd_tile(const MArgs& a, int bx, int by, f
 }
 
 
+template <int H, bool kGather = false>
+__device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, float* lds);
+
+// SACF_EARLY_DATA (default): the critics' (obs, a) row tiles need nothing from the actor forward pass, so they
+// run in this launch beside the actor tiles (row tiles [2B/32, 4B/32) of the grid: Q1 then Q2 data rows), and
+// the critic_fwd launch keeps only the rows that need the actor head — 2 x 128 blocks at B = 256 instead of
+// 128 + 384 (one block per CU in both passes)
+#ifndef SACF_EARLY_DATA
+#define SACF_EARLY_DATA 1
+#endif
 template <int H>
 __global__ __launch_bounds__(256) void sac_actor_fwd_kernel(MArgs a) {
   __shared__ float lds[kLdsFloats];
   int bx, by;
   xcd_tile<H>(bx, by);
-  actor_fwd_tile<H>(a, bx, by, lds);
+  const int at = 2 * a.L.B / kTile2;
+  if (!SACF_EARLY_DATA || bx < at) {
+    actor_fwd_tile<H>(a, bx, by, lds);
+  } else {
+    const int d = bx - at, dt = a.L.B / kTile2;  // data row tile d % dt of critic d / dt
+    critic_fwd_tile<H, true>(a, (d / dt) * 2 * dt + dt + d % dt, by, lds);
+  }
 }
 
 // TanhNormal.rsample_and_logprob (distributions.py:346-392) of one row's head
@@ -547,7 +563,10 @@ __device__ __forceinline__ void tanh_normal(float mean, float ls_raw, float eps,
 }
 
 // grid (row tiles of [Q1: 2B | Q2: 2B | T1: B | T2: B], H / 32). Q rows [0, B): (obs, ã), [B, 2B): (obs, a)
-template <int H>
+// kGather (a data-row tile run in the actor_fwd launch, SACF_EARLY_DATA): the row's observation and replayed
+// action come straight from the replay buffer (the same Philox draw as actor_fwd's gather, so the same values
+// as the gathered copies), since the gathered batch is being written by that same launch
+template <int H, bool kGather>
 __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, float* lds) {
   SAC_T(1, 0);
   SAC_SPAN_BEGIN(1);
@@ -573,16 +592,28 @@ __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, 
   // they end the prologue's longest chain; vector loads complete in issue order, so the staging loads
   // below queue behind them instead of delaying them. Every load is issued unconditionally (the
   // addresses are valid for either row kind) so no branch splits the batch of loads.
-  const float* xr = (is_t ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
   float xin[kXLd];
-  load_run<kXLd>(xr, xin);
-  const int64_t hr = (is_t ? B : 0) + item;
   float pm[CB], pls[CB];
-  load_run<CB>(a.ms.hpart + hr * 2 * CB, pm);
-  load_run<CB>(a.ms.hpart + hr * 2 * CB + CB, pls);
-  const float bm = P[L.p_bm], bs = P[L.p_bs];
-  const float ev = a.ms.eps[(is_t ? B : 0) + item];
-  const float act_data = a.ms.act[item];
+  float bm = 0.0f, bs = 0.0f, ev = 0.0f, act_data;
+  if constexpr (kGather) {  // (data rows only: no actor head)
+    float e0, e1;
+    const int64_t idx = batch_item(a, item, e0, e1);
+#pragma unroll
+    for (int m = 0; m < kXLd; ++m) xin[m] = m < O ? a.obs[idx * O + m] : 0.0f;
+    act_data = a.act[idx];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) pm[cb] = pls[cb] = 0.0f;
+  } else {
+    const float* xr = (is_t ? a.ms.xn : a.ms.x) + (int64_t)item * kXLd;
+    load_run<kXLd>(xr, xin);
+    const int64_t hr = (is_t ? B : 0) + item;
+    load_run<CB>(a.ms.hpart + hr * 2 * CB, pm);
+    load_run<CB>(a.ms.hpart + hr * 2 * CB + CB, pls);
+    bm = P[L.p_bm];
+    bs = P[L.p_bs];
+    ev = a.ms.eps[(is_t ? B : 0) + item];
+    act_data = a.ms.act[item];
+  }
   float av[kMaxN2], bv[kMaxN2];
   const float* WT = a.T + (int64_t)(1 + net) * H * H;  // [q1 | q2 | t1 | t2] W2ᵀ
 #pragma unroll
@@ -594,7 +625,7 @@ __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, 
   stage_w1t<H>(lw1, C + L.c_w1, C + L.c_b1, O + 1);
   SAC_T(1, 7);
   float act;
-  if (data) {
+  if (kGather || data) {
     act = act_data;
   } else {  // actor head of the row (the column-block parts of actor_fwd's epilogue, summed in block
             // order as sum_parts does) and its sample
@@ -653,6 +684,10 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   __shared__ float lds[kLdsFloats];
   int bx, by;
   xcd_tile<H>(bx, by);
+  if (SACF_EARLY_DATA) {  // row tiles: Q1 (obs, ã) | Q2 (obs, ã) | T1 | T2 (the data rows ran with the actor)
+    const int dt = a.L.B / kTile2;
+    bx = bx < 2 * dt ? (bx / dt) * 2 * dt + bx % dt : bx + 2 * dt;
+  }
   critic_fwd_tile<H>(a, bx, by, lds);
 }
 
@@ -1522,8 +1557,8 @@ template <int H>
 void launch_passes(const MArgs& a, hipStream_t st, int part) {
   const int B = a.L.B, ct = H / kTile2;
   if (part == 0) {
-    hipLaunchKernelGGL(sac_actor_fwd_kernel<H>, dim3(2 * B / kTile2, ct), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(sac_critic_fwd_kernel<H>, dim3(6 * B / kTile2, ct), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sac_actor_fwd_kernel<H>, dim3((SACF_EARLY_DATA ? 4 : 2) * B / kTile2, ct), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sac_critic_fwd_kernel<H>, dim3((SACF_EARLY_DATA ? 4 : 6) * B / kTile2, ct), dim3(256), 0, st, a);
     // (grid x a multiple of 8 everywhere: block i runs on XCD i % 8, so row tile r of every kernel
     //  lands on XCD r % 8, the L2 that holds what the previous kernel wrote for those rows)
     hipLaunchKernelGGL(sac_critic_bwd_kernel<H>, dim3(4 * B / kTile2 + 8, ct), dim3(256), 0, st, a);
