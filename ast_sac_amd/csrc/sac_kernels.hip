@@ -185,7 +185,8 @@ constexpr int kMaxMats = 24;
 // lane l holds A[l & 31][k] and B[k][l & 31] with k = kb + (l >> 5)·K/8 + i for MFMA i of the wave's
 // K/4-slice (a permuted k order: the sum is the same, the loads stay contiguous per lane / per half
 // wave); C/D: col = l & 31, row = (reg & 3) + 8·(reg >> 2) + 4·(l >> 5).
-//   sac_actor_fwd_kernel  : batch gather (replay sampling), h1 (VALU), h2 = relu(h1 W2ᵀ + b2) on 2B rows
+//   sac_actor_fwd_kernel  : batch gather (replay sampling), h1 (VALU), h2 = relu(h1 W2ᵀ + b2) on 2B rows;
+//                           beside them the critics' (obs, a) row tiles of critic_fwd (SACF_EARLY_DATA)
 //   sac_critic_fwd_kernel : actor heads + TanhNormal sample per row, g1 (VALU), g2 = relu(g1 W2ᵀ + b2) for
 //                           Q1, Q2 on [(obs, ã); (obs, a)] and T1, T2 on (next_obs, ã')
 //   sac_critic_bwd_kernel : q heads, losses, dq, dg2 = dq·w3 ⊙ [g2 > 0], dg1 = (dg2 W2) ⊙ [g1 > 0]
