@@ -25,7 +25,7 @@ H x H weight gradients as batched fp32 GEMMs on the matrix cores (v_mfma_f32_32x
 Adam, the soft target update and the transposed-weight refresh fused into the weight-gradient
 kernel when there is no all-reduce — five launches per step inside the HIP graph. It raises
 ValueError for networks it does not cover (two equal hidden layers <= 256 and a multiple of 32,
-act_dim 1, obs_dim <= 15, per-rank batch a multiple of 32 up to 1024). backend="torch" runs the same
+act_dim 1, obs_dim <= 15, per-rank batch a multiple of 32 up to 8192). backend="torch" runs the same
 step with PyTorch ops (any shape).
 
 Numerics: fp32 like the reference; results equal SACTrainer's up to GEMM accumulation order
@@ -125,7 +125,7 @@ class FusedSACTrainer(TorchTrainer):
         if backend == "hip":
             if not self._hip_shapes_ok():
                 raise ValueError("FusedSACTrainer hip backend: needs 2 equal hidden layers (<= 256, multiple of 32), "
-                                 "act_dim 1, obs_dim <= 15 and a per-rank batch_size that is a multiple of 32 and <= 1024; pass backend='torch' to run "
+                                 "act_dim 1, obs_dim <= 15 and a per-rank batch_size that is a multiple of 32 and <= 8192; pass backend='torch' to run "
                                  "these networks with PyTorch ops")
             self._init_hip(policy_lr, qf_lr)
         self._n_train_steps_total = 0
@@ -140,7 +140,7 @@ class FusedSACTrainer(TorchTrainer):
             obs = pol.fcs[0].weight.shape[1]
             ok = (len(pol.fcs) == 2 and pol.fcs[1].weight.shape == (H, H) and pol.last_fc.weight.shape == (1, H)
                   and getattr(pol, "last_fc_log_std", None) is not None and H % 32 == 0 and H <= 256
-                  and obs <= 15 and self.batch_size % 32 == 0 and 32 <= self.batch_size <= 1024)
+                  and obs <= 15 and self.batch_size % 32 == 0 and 32 <= self.batch_size <= 8192)
             for n in nets:
                 ok = ok and len(n.fcs) == 2 and n.fcs[0].weight.shape == (H, obs + 1) \
                     and n.fcs[1].weight.shape == (H, H) and n.last_fc.weight.shape == (1, H)

@@ -1654,7 +1654,7 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   *out = nullptr;
   if (!cfg || cfg->abi_version != SACF_ABI_VERSION) return SACF_EINVAL;
   const int O = cfg->obs_dim, H = cfg->hidden, B = cfg->batch;
-  if (O < 1 || O + 1 > kXLd || H < 32 || H > SACF_MAX_HIDDEN || H % 32 || B < kTile2 || B % kTile2 || B > 1024 ||
+  if (O < 1 || O + 1 > kXLd || H < 32 || H > SACF_MAX_HIDDEN || H % 32 || B < kTile2 || B % kTile2 || B > SACF_MAX_BATCH ||
       cfg->world_size < 1)
     return SACF_EINVAL;
   sacf_handle* h = new (std::nothrow) sacf_handle();

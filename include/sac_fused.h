@@ -42,12 +42,13 @@ extern "C" {
 #define SACF_ESTATE -3
 #define SACF_MAX_OBS 16
 #define SACF_MAX_HIDDEN 256
+#define SACF_MAX_BATCH 8192 /* per-rank batch bound of the hip SAC kernels (any multiple of 32 up to it) */
 
 typedef struct sacf_config {
   int32_t abi_version;   /* = SACF_ABI_VERSION */
   int32_t obs_dim;       /* <= SACF_MAX_OBS (8 for the AST env) */
   int32_t hidden;        /* H, multiple of 32, <= SACF_MAX_HIDDEN (runner: 256) */
-  int32_t batch;         /* B per call (per rank), multiple of 32, <= 1024 */
+  int32_t batch;         /* B per call (per rank), multiple of 32, <= SACF_MAX_BATCH */
   float discount;        /* sac.py:31  γ */
   float reward_scale;    /* sac.py:32 */
   float soft_target_tau; /* sac.py:37  τ */

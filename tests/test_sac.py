@@ -202,7 +202,8 @@ def _assert_grads_close(g_hip, g_ref, tr, what):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,B", [(32, 64), (64, 96), (96, 64), (160, 128), (224, 32), (256, 32), (256, 256), (256, 1024)])
+@pytest.mark.parametrize("H,B", [(32, 64), (64, 96), (96, 64), (160, 128), (224, 32), (256, 32), (256, 256), (256, 1024),
+                                 (256, 4096), (128, 8192)])
 def test_hip_sac_gradients_match_torch_autograd(H, B):
     """One update's flat gradient (α | π | Q1 | Q2) from the fused kernels == torch autograd's."""
     batch, eps = _rand_batch(B, "cuda")
@@ -272,7 +273,8 @@ def test_hip_sac_graph_replay_equals_eager_launches():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,B,split", [(256, 256, False), (256, 256, True), (64, 96, False), (256, 1024, False)])
+@pytest.mark.parametrize("H,B,split", [(256, 256, False), (256, 256, True), (64, 96, False), (256, 1024, False),
+                                           (256, 4096, False)])
 def test_hip_sac_persistent_step_equals_five_launches(H, B, split):
     """libsacfused step_kernel 1 (the whole grad step in one persistent launch, grid barriers between the
     passes) runs the five-launch kernels' own tiles in the same order: 20 graph-replayed steps from the
