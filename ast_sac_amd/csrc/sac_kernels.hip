@@ -692,6 +692,11 @@ __global__ __launch_bounds__(256) void sac_critic_fwd_kernel(MArgs a) {
   critic_fwd_tile<H>(a, bx, by, lds);
 }
 
+// SACF_DIRECT_BWD (default): the backward passes read each lane's activation-row segment and head weights straight
+// from memory (float4 runs) instead of staging a 32-row tile and the head vectors in LDS behind a block barrier
+#ifndef SACF_DIRECT_BWD
+#define SACF_DIRECT_BWD 1
+#endif
 // grid (2 critics x 2B / 32 row tiles, H / 32): losses and dq (sac.py:170-247), dg2, dg1 = (dg2 W2) ⊙ [g1 > 0]
 template <int H>
 __device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, float* lds) {
@@ -755,10 +760,19 @@ __device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, 
   const float invB = 1.0f / (float)B;
   float dq;
   const int ib = data ? r0 - B : r0;  // first batch item of the tile (tiles never straddle B)
+  // this lane's g2 row segment and w3 entries (columns kb .. kb + H/8), straight from memory: no LDS staging
+  // and no block barrier before the dg2 operand (SACF_DIRECT_BWD)
+  float g2v[n2], w3v[n2];
+#if SACF_DIRECT_BWD
+  load_run<n2>((data ? a.sc.q_g2[net] : a.ms.g2pi[net]) + (int64_t)(ib + (lane & 31)) * H + kb, g2v);
+#pragma unroll
+  for (int i = 0; i < n2; ++i) w3v[i] = C[L.c_w3 + kb + i];
+#else
   float* tg = lds + kLdsTileOff;      // this critic's g2 rows of the tile
   float* lw3 = lds + kLdsHeadWOff;    // this critic's w3
   tile_load<H>(tg, (data ? a.sc.q_g2[net] : a.ms.g2pi[net]) + (int64_t)ib * H);
   stage(lw3, C + L.c_w3, H);
+#endif
   // Σ of the column-block parts in block order (sum_parts), then the head bias
   float s_q1 = q1p[0], s_q2 = q2p[0], s_t1 = t1p[0], s_t2 = t2p[0];
 #pragma unroll
@@ -806,11 +820,17 @@ __device__ __forceinline__ void critic_bwd_tile(const MArgs& a, int bx, int by, 
     }
   }
   SAC_T(2, 1);
+#if !SACF_DIRECT_BWD
   __syncthreads();  // g2 tile and w3 staged
 #pragma unroll
   for (int i = 0; i < n2; ++i) {
-    const int j = kb + i;
-    av[i] = tg[(lane & 31) * (H + 4) + j] > 0.0f ? dq * lw3[j] : 0.0f;
+    g2v[i] = tg[(lane & 31) * (H + 4) + kb + i];
+    w3v[i] = lw3[kb + i];
+  }
+#endif
+#pragma unroll
+  for (int i = 0; i < n2; ++i) {
+    av[i] = g2v[i] > 0.0f ? dq * w3v[i] : 0.0f;
   }
   if (data) store_slice<H>(a.sc.q_dg2[net], ib, by, av, kb);
   SAC_T(2, 3);
@@ -874,11 +894,22 @@ __device__ __forceinline__ void actor_bwd_tile(const MArgs& a, int bx, int by, f
   const float log_alpha = P[0];
   const float alpha = a.hp.auto_ent ? expf(log_alpha) : 1.0f;
   const float invB = 1.0f / (float)B;
+  // this lane's h2 row segment and head weights (columns kb .. kb + H/8), straight from memory (SACF_DIRECT_BWD)
+  float h2v[n2], wmv[n2], wsv[n2];
+#if SACF_DIRECT_BWD
+  load_run<n2>(a.sc.a_h2 + (int64_t)(r0 + (lane & 31)) * H + kb, h2v);
+#pragma unroll
+  for (int i = 0; i < n2; ++i) {
+    wmv[i] = P[L.p_wm + kb + i];
+    wsv[i] = P[L.p_ws + kb + i];
+  }
+#else
   float* th = lds + kLdsTileOff;     // actor h2 rows of the tile
   float* lwh = lds + kLdsHeadWOff;   // wm | ws
   tile_load<H>(th, a.sc.a_h2 + (int64_t)r0 * H);
   stage(lwh, P + L.p_wm, H);
   stage(lwh + H, P + L.p_ws, H);
+#endif
   // dA = Σ_m wa1[m] dg1_Q1[m] + Σ_m wa2[m] dg1_Q2[m] (wa: the action column of each critic's fc0), each
   // sum over the column-block parts in block order (sum_parts)
   float s1 = ap1[0], s2 = ap2[0];
@@ -902,12 +933,17 @@ __device__ __forceinline__ void actor_bwd_tile(const MArgs& a, int bx, int by, f
     a.sc.a_dhead[(int64_t)item * 2 + 1] = dls;
   }
   SAC_T(3, 2);
+#if !SACF_DIRECT_BWD
   __syncthreads();  // h2 tile and head weights staged
 #pragma unroll
   for (int i = 0; i < n2; ++i) {
-    const int j = kb + i;
-    av[i] = th[(lane & 31) * (H + 4) + j] > 0.0f ? (lwh[j] * dmean + lwh[H + j] * dls) : 0.0f;
+    h2v[i] = th[(lane & 31) * (H + 4) + kb + i];
+    wmv[i] = lwh[kb + i];
+    wsv[i] = lwh[H + kb + i];
   }
+#endif
+#pragma unroll
+  for (int i = 0; i < n2; ++i) av[i] = h2v[i] > 0.0f ? (wmv[i] * dmean + wsv[i] * dls) : 0.0f;
   store_slice<H>(a.sc.a_dh2, r0, by, av, kb);
   SAC_T(3, 3);
   f32x16 acc = zero16();
