@@ -646,15 +646,15 @@ __device__ __forceinline__ void critic_fwd_tile(const MArgs& a, int bx, int by, 
       for (int q = 0; q < 6; ++q) (is_t ? a.ms.hdn : a.ms.hd)[q * B + item] = hd[q];
   }
   SAC_T(1, 1);
-  __syncthreads();  // lw1 staged (also when the tile computed no heads)
-  SAC_T(1, 2);
+  // the tile's input rows next to W1ᵀ | b1, both behind one barrier
   if (w == 0 && h == 0) {
 #pragma unroll
     for (int m = 0; m < kXLd; ++m)
       if (m < O) lx[(lane & 31) * (kXLd + 1) + m] = xin[m];
     lx[(lane & 31) * (kXLd + 1) + O] = act;
   }
-  __syncthreads();
+  __syncthreads();  // lw1 and the input rows staged (also when the tile computed no heads)
+  SAC_T(1, 2);
   first_layer<H>(lw1, lx + (lane & 31) * (kXLd + 1), O + 1, kb, av);
   if (!is_t) {  // block-uniform
     if (by == 0 && data && w == 0 && h == 0)
