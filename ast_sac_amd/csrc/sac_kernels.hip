@@ -1055,8 +1055,6 @@ struct WgArgs {
   int blk0;      // (timing experiments, $SACF_WG_MODE) this launch's first block / block rotation
   int fuse;      // single process: each block also applies Adam / soft update / W2ᵀ to the elements it finished
   ApplyArgs ap;  // (fuse) parameters, optimizer state, targets, transposed copies
-  GMat bigm[3];  // the H x H matrices (= tab->mats[tab->big[k]]) and their W2ᵀ slots, for the MFMA tiles of the
-  int bigslot[3];  // weight-gradient launch: read from the kernel arguments, no table staging (SACF_WG_KARG)
 };
 
 // the weight-gradient kernel's LDS (also one region of the persistent step kernel's)
@@ -1085,7 +1083,6 @@ __device__ __forceinline__ void wgrad_stage(const WgArgs& a, WgLds& S) {
 }
 
 // block bx of the weight-gradient pass (see above); S staged by wgrad_stage
-template <bool kKarg = false>
 __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
   float* lds = S.lds;
   const WgTable& tab = S.tab;
@@ -1190,12 +1187,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
   }
   // MFMA tile of an H x H matrix: A[j][r] = dY[r][j], B[r][k] = X[r][k]
   const WgTable& tb = tab;
-  // (kKarg: the matrix from the kernel arguments — block-uniform selects, no indexed argument array — and this
-  // step's Adam bias corrections from the stats critic_bwd wrote, as scalar loads issued here, used at the end)
-  AdamStep sst_k;
-  if constexpr (kKarg) sst_k = AdamStep{a.stats[5], a.stats[6], a.stats[7]};
-  const AdamStep& sstm = kKarg ? sst_k : sst;
-  const int H = kKarg ? a.bigm[0].M : tb.mats[tb.big[0]].M;
+  const int H = tb.mats[tb.big[0]].M;
   const int tiles = (H / kTile2) * (H / kTile2);
   // XCD-aware tile map (H = 256: 64 tiles per matrix, 24 per XCD): XCD x = bx mod 8 takes, of each matrix, the
   // 2 x 4 tiles of row blocks 2(x / 2) + {0, 1} and column blocks 4(x mod 2) + {0..3}, so its L2 fetches a quarter
@@ -1207,17 +1199,10 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
     bm = sl >> 3;
     t = ((x >> 1) * 2 + (tt >> 2)) * 8 + (x & 1) * 4 + (tt & 3);
   }
-  GMat m;
-  int mat;  // 0: actor W2, 1 / 2: Q1 / Q2 W2
-  if constexpr (kKarg) {
-    m = bm == 0 ? a.bigm[0] : (bm == 1 ? a.bigm[1] : a.bigm[2]);
-    mat = bm == 0 ? a.bigslot[0] : (bm == 1 ? a.bigslot[1] : a.bigslot[2]);
-  } else {
-    m = tb.mats[tb.big[bm]];
-    mat = tb.big_slot[bm];
-  }
+  const GMat m = tb.mats[tb.big[bm]];
   const int j0 = (t / (H / kTile2)) * kTile2, k0 = (t % (H / kTile2)) * kTile2;
   const int w = tid >> 6, lane = tid & 63, h = lane >> 5;
+  const int mat = tb.big_slot[bm];  // 0: actor W2, 1 / 2: Q1 / Q2 W2
   AdamElem x[4];
   const int rows_w = a.B / 4;  // this wave's rows, in chunks of up to 64 (32 MFMAs)
   f32x16 acc = zero16();
@@ -1269,7 +1254,7 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
     a.grads[e] = v;
     if (a.fuse) {
       x[q].g = v;
-      adam_st(a.ap, sstm, e, x[q]);
+      adam_st(a.ap, sst, e, x[q]);
       tt[0][cc][rr] = x[q].p;
       tt[1][cc][rr] = x[q].t;
     }
@@ -1290,9 +1275,6 @@ __device__ __forceinline__ void wgrad_tile(const WgArgs& a, int bx, WgLds& S) {
 }
 
 
-#ifndef SACF_WG_KARG
-#define SACF_WG_KARG 1
-#endif
 __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
   __shared__ WgLds S;
   const int bx = ((int)blockIdx.x + a.blk0) % a.n_blocks;
@@ -1302,12 +1284,8 @@ __global__ __launch_bounds__(256) void sac_wgrad_mfma_kernel(WgArgs a) {
     g_wg_blk[3 * bx + 2] = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7;  // HW_REG_XCC_ID
   }
 #endif
-  if (SACF_WG_KARG && bx < a.n_mfma) {  // MFMA tile: its matrix from the kernel arguments, no table staging
-    wgrad_tile<true>(a, bx, S);
-  } else {
-    wgrad_stage(a, S);
-    wgrad_tile(a, bx, S);
-  }
+  wgrad_stage(a, S);
+  wgrad_tile(a, bx, S);
 #ifdef SACF_PHASE_TIMING
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -1868,10 +1846,6 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     }
     wg.tab = h->wtab[part];
     wg.n_mfma = nb * (H / kTile2) * (H / kTile2);
-    for (int k = 0; k < nb && k < 3; ++k) {
-      wg.bigm[k] = tab.mats[tab.big[k]];
-      wg.bigslot[k] = tab.big_slot[k];
-    }
     wg.n_blocks = wg.n_mfma + (wg.n_small + 63) / 64 + tab.has_scalar;
     wg.B = B;
     wg.sc = sc;
