@@ -1,8 +1,9 @@
 """DeviceBatchRLAlgorithm — BatchRLAlgorithm's epoch shape (batch_rl_algorithm.py:58-106) on
 device-resident envs, replay buffer and a graph-captured SAC update.
 
-Per epoch (rank-local counts; with R ranks the job does R× the decisions and every grad step
-averages R local batches of batch_size, i.e. a global batch of R·batch_size):
+Per epoch (rank-local counts; with R ranks the job does R× the decisions; the grad steps either run
+replicated on every rank over the union of all ranks' transitions — a ReplicatedReplayBuffer, synced after
+every collect — or average R local batches with a gradient all-reduce):
   epoch 0: collect ≥ min_num_steps_before_training exploration decisions into the buffer;
   every epoch: ≥ num_eval_steps_per_epoch decisions with the deterministic policy (eval env),
   then per train loop ≥ num_expl_steps_per_train_loop exploration decisions + grad steps, each on a
@@ -67,6 +68,7 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
     def _train(self):
         if self.epoch == 0 and self.min_num_steps_before_training > 0:
             self.expl_data_collector.collect(self.min_num_steps_before_training, self.replay_buffer)
+            self._sync_buffer()
             self.expl_data_collector.end_epoch(-1)  # (unstamped, as in the reference: counts as evaluation sampling)
         if self.num_eval_steps_per_epoch > 0:
             self.eval_data_collector.collect(self.num_eval_steps_per_epoch, None, record_paths=True)
@@ -75,7 +77,8 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
             got = self.expl_data_collector.collect(self.num_expl_steps_per_train_loop, self.replay_buffer,
                                                    record_paths=True)
             self.timer.stamp("exploration sampling")
-            self.timer.stamp("data storing")  # the collector already wrote the buffer on the device
+            self._sync_buffer()
+            self.timer.stamp("data storing")  # the collector wrote the buffer on the device (+ the replicas' sync)
             self.training_mode(True)
             self.num_loop_expl_steps_total += got
             k = self._n_grad_steps(got)
@@ -85,6 +88,12 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
             self.timer.stamp("sac training")  # the reference stamps it in SACTrainer.train_from_torch (sac.py:142)
             self.timer.stamp("training")
             self.training_mode(False)
+
+    def _sync_buffer(self):
+        """Replicated data parallel: every rank's new rows into every rank's ring (one all-gather per collect)."""
+        sync = getattr(self.replay_buffer, "sync", None)
+        if sync is not None:
+            sync()
 
     def to(self, device):
         for net in self.trainer.networks:

@@ -212,3 +212,58 @@ class DeviceReplayBuffer(ReplayBuffer):
 
     def get_diagnostics(self):
         return OrderedDict([("size", self.num_steps_can_sample())])
+
+
+class ReplicatedReplayBuffer(DeviceReplayBuffer):
+    """The union of every rank's transitions, held identically by every rank of `process_group` — the
+    replicated-trainer data-parallel shape. `add_batch` (the collector's, graph-capturable)
+    stages this rank's rows; `sync()` all-gathers every rank's staged rows — one collective per train loop,
+    76 B per row, instead of one gradient all-reduce per grad step — and appends them in rank order, so
+    every rank's ring holds the same rows in the same slots. Every rank then runs the same SAC step on the
+    same global batch (the reference's uniform sample over all collected transitions, replay_buffer.py /
+    simple_replay_buffer.py:72-76) with the same seed, and the replicas stay bitwise equal without any
+    per-step exchange."""
+
+    def __init__(self, max_replay_buffer_size, observation_dim, action_dim, device, process_group, stage_size,
+                 generator=None):
+        super().__init__(max_replay_buffer_size, observation_dim, action_dim, device, generator)
+        self.pg = process_group
+        self._stage = DeviceReplayBuffer(int(stage_size), observation_dim, action_dim, device)
+        self._staged_t = torch.zeros((), dtype=torch.int64, device=self.device)  # rows added since the last sync
+        self._dims = (observation_dim, action_dim)
+
+    def add_batch(self, obs, action, reward, next_obs, terminal, mask=None):
+        n = obs.shape[0]
+        self._stage.add_batch(obs, action, reward, next_obs, terminal, mask)
+        self._staged_t += n if mask is None else mask.reshape(-1).to(torch.int64).sum()
+
+    def sync(self):
+        """Append every rank's staged rows (rank order) to the shared ring; returns the rows appended."""
+        import torch.distributed as dist
+        od, ad = self._dims
+        world = dist.get_world_size(self.pg)
+        comm_dev = self.device if dist.get_backend(self.pg) == "nccl" else torch.device("cpu")
+        cnt = self._staged_t.reshape(1).to(comm_dev)
+        counts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(counts, cnt, group=self.pg)
+        counts = [int(c.item()) for c in counts]
+        if max(counts) > self._stage._max:
+            raise RuntimeError(f"ReplicatedReplayBuffer: a rank staged {max(counts)} rows between syncs, more than "
+                               f"the staging ring's {self._stage._max}; sync after every collect or enlarge stage_size")
+        m = max(counts)
+        if m:
+            st = self._stage._store
+            rows = torch.cat([st["observations"][:m], st["actions"][:m], st["rewards"][:m], st["next_observations"][:m],
+                              st["terminals"][:m]], 1).to(comm_dev).contiguous()
+            got = [torch.empty_like(rows) for _ in range(world)]
+            dist.all_gather(got, rows, group=self.pg)
+            for r, c in enumerate(counts):
+                if not c:
+                    continue
+                x = got[r][:c].to(self.device)
+                DeviceReplayBuffer.add_batch(self, x[:, :od], x[:, od:od + ad], x[:, od + ad:od + ad + 1],
+                                             x[:, od + ad + 1:2 * od + ad + 1], x[:, 2 * od + ad + 1:])
+        self._stage._top_t.zero_()
+        self._stage._size_t.zero_()
+        self._staged_t.zero_()
+        return sum(counts)

@@ -153,16 +153,18 @@ class BatchedPathCollector:
         self._mode = None
 
     def _enter(self, mode):
-        """Switching from fused to sliced passes: the sliced pass keeps the pending observations and the
-        awaiting flags on the host side, which fused passes do not maintain — start every episode afresh
-        (as _take_over). Sliced -> fused continues the episodes (the env holds everything it needs)."""
-        if self._mode == "fused" and mode == "sliced":
+        """A switch between pass kinds starts every episode afresh (as _take_over), in either direction:
+        fused -> sliced because the sliced pass keeps the pending observations and awaiting flags on the
+        host side, which fused passes do not maintain; sliced -> fused because a decision a sliced pass
+        began is still in flight in the env, and only the policy stream's own decision prologue stores the
+        action and observation its log record (and so its replay row) is built from."""
+        if self._mode is not None and self._mode != mode:
             self._obs.copy_(self._env.reset())
             self._awaiting.fill_(True)
             self._path_len.zero_()
             self._ret.zero_()
             self._n_awaiting = self.N
-        elif mode == "fused" and self._mode != "fused":
+        if mode == "fused" and self._mode != "fused":
             self._dec_idx.copy_(self._path_len)
         self._mode = mode
 
@@ -330,7 +332,8 @@ class BatchedPathCollector:
             self._ring_ev.index_copy_(0, idx, self._path_ev)
             self._ring_top += k64.sum()
         self._obs.copy_(torch.where(ready.unsqueeze(1), out["obs"], self._obs))
-        self._awaiting.copy_(ready)
+        self._awaiting.copy_(ready)  # (non-finite decisions included: those envs were reset and wait too)
+        self._n_ready = ready.sum()
         n_ready = good.sum()
         self._steps_total += n_ready
         self._paths_total += end.sum()
@@ -385,8 +388,8 @@ class BatchedPathCollector:
             got = 0
             while got < num_steps:
                 n = self._pass(replay_buffer, record)
-                self._n_awaiting = int(n.item())
-                got += self._n_awaiting
+                got += int(n.item())                      # transitions (non-finite decisions left out)
+                self._n_awaiting = int(self._n_ready.item())  # envs that wait for an action
         else:
             start = int(self._steps_total.item())
             got, passes, batch = 0, 0, 1
@@ -415,6 +418,10 @@ class BatchedPathCollector:
         n = min(top, self._ring_cap)
         if n == 0:
             return
+        if top > self._ring_cap:
+            warnings.warn(f"BatchedPathCollector: {top} episodes ended during this collect but the path ring holds "
+                          f"{self._ring_cap}; the epoch paths keep the newest {self._ring_cap} (construct the "
+                          f"collector with a larger path_ring)", RuntimeWarning, stacklevel=2)
         order = [(top - n + j) % self._ring_cap for j in range(n)]  # oldest first
         sel = torch.as_tensor(order, dtype=torch.long, device=self.device)
         lens = self._ring_len[sel].cpu().numpy()

@@ -23,10 +23,12 @@ Two backends run this restructured step. backend="hip" (the default on a GPU; th
 libsacfused (include/sac_fused.h, csrc/sac_kernels.hip): the forward / backward passes and the
 H x H weight gradients as batched fp32 GEMMs on the matrix cores (v_mfma_f32_32x32x2_f32), with
 Adam, the soft target update and the transposed-weight refresh fused into the weight-gradient
-kernel when there is no all-reduce — five launches per step inside the HIP graph. It raises
-ValueError for networks it does not cover (two equal hidden layers <= 256 and a multiple of 32,
-act_dim 1, obs_dim <= 15, per-rank batch a multiple of 32 up to 8192). backend="torch" runs the same
-step with PyTorch ops (any shape).
+kernel when there is no all-reduce — three launches per step inside the HIP graph (the critics'
+action gradient is a forward-mode tangent and the backward factors of layer 2 are formed beside the
+forward pass, so no separate backward pass is launched). It raises ValueError for networks it does
+not cover (two equal hidden layers of a width libsacfused compiles — every multiple of 32 up to 256,
+and 320 / 384 / 448 / 512 —, act_dim 1, obs_dim <= 15, per-rank batch 1..8192). backend="torch" runs
+the same step with PyTorch ops (any shape).
 
 Numerics: fp32 like the reference; results equal SACTrainer's up to GEMM accumulation order
 (tests/test_sac.py checks both against the captured reference step, tests/golden/sac_step.npz,
@@ -58,7 +60,7 @@ class FusedSACTrainer(TorchTrainer):
                  policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None, soft_target_tau=1e-2, target_update_period=1,
                  plotter=None, render_eval_paths=False, use_automatic_entropy_tuning=True, target_entropy=None,
                  action_reg_coeff=None, clip_val=np.inf, batch_size=256, use_graph=None, process_group=None,
-                 backend=None, split_update=None, persistent_kernel=None):
+                 backend=None, split_update=None, replicated=False, capture_collective=None):
         super().__init__()
         if target_update_period != 1:
             raise NotImplementedError("FusedSACTrainer soft-updates every step (runner: target_update_period=1)")
@@ -82,14 +84,22 @@ class FusedSACTrainer(TorchTrainer):
             self.target_entropy = 0.0
         self.log_alpha = torch.zeros(1, requires_grad=use_automatic_entropy_tuning, device=dev)
         self.pg = process_group
-        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
-        # the data-parallel step shape: grads | all-reduce over process_group | update (two graph halves).
-        # Default: whenever world > 1; split_update=True forces it on one rank too (the all-reduce then runs
-        # over a world-size-1 group: the same code path as N ranks, an identity on the values)
+        # data-parallel shapes. replicated: every rank of process_group runs this same step on the
+        # same global batch from a ReplicatedReplayBuffer (the union of all ranks' transitions) with the same seed,
+        # so the replicas stay equal with no per-step exchange (parameters and the sampling seed are broadcast
+        # once). Otherwise (gradient all-reduce): each rank takes its batch_size rows from its own buffer and the
+        # flat gradient is all-reduced every step.
+        self.replicated = bool(replicated) and process_group is not None
+        self.world = (torch.distributed.get_world_size(process_group)
+                      if process_group is not None and not self.replicated else 1)
+        # the all-reduce step shape: grads | all-reduce over process_group | update. Default: whenever world > 1;
+        # split_update=True forces it on one rank too (the all-reduce then runs over a world-size-1 group: the
+        # same code path as N ranks, an identity on the values)
         self.split = (self.world > 1) if split_update is None else bool(split_update)
-        # hip backend: the grad step as five graph-replayed launches (default) or one persistent launch with
-        # grid barriers (libsacfused step_kernel 1; same results, slower on MI355X — DESIGN.md §7c)
-        self.persistent_kernel = False if persistent_kernel is None else bool(persistent_kernel)
+        # the all-reduce inside the one captured HIP graph of the step (RCCL kernels are capturable) instead of
+        # an eager call between two graph halves; default with an RCCL ("nccl") group
+        nccl = process_group is not None and torch.distributed.get_backend(process_group) == "nccl"
+        self.capture_collective = (self.split and nccl) if capture_collective is None else bool(capture_collective)
 
         self.pi_params = ([self.log_alpha] if use_automatic_entropy_tuning else []) + list(policy.parameters())
         self.q_params = list(qf1.parameters()) + list(qf2.parameters())
@@ -124,9 +134,9 @@ class FusedSACTrainer(TorchTrainer):
         self.backend = backend
         if backend == "hip":
             if not self._hip_shapes_ok():
-                raise ValueError("FusedSACTrainer hip backend: needs 2 equal hidden layers (<= 256, multiple of 32), "
-                                 "act_dim 1, obs_dim <= 15 and a per-rank batch_size that is a multiple of 32 and <= 8192; pass backend='torch' to run "
-                                 "these networks with PyTorch ops")
+                raise ValueError("FusedSACTrainer hip backend: needs 2 equal hidden layers of a compiled width (multiples "
+                                 "of 32 up to 256, 320, 384, 448, 512), act_dim 1, obs_dim <= 15 and a per-rank batch_size "
+                                 "of 1..8192; pass backend='torch' to run these networks with PyTorch ops")
             self._init_hip(policy_lr, qf_lr)
         self._n_train_steps_total = 0
         self._need_to_update_eval_statistics = True
@@ -134,13 +144,14 @@ class FusedSACTrainer(TorchTrainer):
 
     # ---------------------------------------------------------------- hip backend
     def _hip_shapes_ok(self):
+        from ....sacfused import hidden_supported
         pol, nets = self.policy, (self.qf1, self.qf2, self.target_qf1, self.target_qf2)
         try:
             H = pol.fcs[0].weight.shape[0]
             obs = pol.fcs[0].weight.shape[1]
             ok = (len(pol.fcs) == 2 and pol.fcs[1].weight.shape == (H, H) and pol.last_fc.weight.shape == (1, H)
-                  and getattr(pol, "last_fc_log_std", None) is not None and H % 32 == 0 and H <= 256
-                  and obs <= 15 and self.batch_size % 32 == 0 and 32 <= self.batch_size <= 8192)
+                  and getattr(pol, "last_fc_log_std", None) is not None and hidden_supported(H)
+                  and obs <= 15 and 1 <= self.batch_size <= 8192)
             for n in nets:
                 ok = ok and len(n.fcs) == 2 and n.fcs[0].weight.shape == (H, obs + 1) \
                     and n.fcs[1].weight.shape == (H, H) and n.last_fc.weight.shape == (1, H)
@@ -180,12 +191,13 @@ class FusedSACTrainer(TorchTrainer):
         self._sf = SacFused(obs_dim, H, self.batch_size, dev, self.discount, self.reward_scale, self.soft_target_tau,
                             self.action_reg_coeff, self.clip_val, float(self.target_entropy), policy_lr, qf_lr,
                             auto_entropy=self.use_automatic_entropy_tuning, world_size=self.world,
-                            split_update=self.split, persistent=self.persistent_kernel)
+                            split_update=self.split)
         if self._sf.n_params != flat.numel() or self._sf.n_targets != tflat.numel():
             raise RuntimeError("hip backend: flat layout mismatch")
         self._stats_t = torch.zeros(self._sf.n_stats, device=dev)
         self._sf.bind(flat, tflat, self.flat_grad, self._adam_m, self._adam_v, self._step_t, self._stats_t)
         self._seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self._collective_warm = False
         self._eps_static = None
         self._replay_key = None
 
@@ -222,14 +234,26 @@ class FusedSACTrainer(TorchTrainer):
             return
         if self._graphs is None or self._graphs[0] != key:
             torch.cuda.synchronize(self.device)
-            parts = ("a", "b") if self.split else ("ab",)
             graphs = []
-            for part in parts:
+            if self.split and self.capture_collective:  # grads | all-reduce | update in one graph
+                if not self._collective_warm:  # the communicator's first collective runs eagerly (set-up)
+                    torch.distributed.all_reduce(torch.zeros(1, device=self.device), group=self.pg)
+                    torch.cuda.synchronize(self.device)
+                    self._collective_warm = True
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     sf.set_stream()
-                    self._hip_launch(replay_buffer, part)
+                    self._hip_launch(replay_buffer, "a")
+                    torch.distributed.all_reduce(self.flat_grad, group=self.pg)
+                    self._hip_launch(replay_buffer, "b")
                 graphs.append(g)
+            else:
+                for part in (("a", "b") if self.split else ("ab",)):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        sf.set_stream()
+                        self._hip_launch(replay_buffer, part)
+                    graphs.append(g)
             sf.set_stream()
             self._graphs = (key, graphs)
         graphs = self._graphs[1]
@@ -459,16 +483,24 @@ class FusedSACTrainer(TorchTrainer):
         return st
 
     def broadcast_parameters(self, src=0):
-        """Make every rank start from rank `src`'s networks."""
-        if self.world > 1:
-            with torch.no_grad():
-                if self.backend == "hip":
-                    torch.distributed.broadcast(self.flat_param, src, group=self.pg)
-                    torch.distributed.broadcast(self.flat_target, src, group=self.pg)
-                    self._sf.sync_params()
-                    return
-                for p in self.pi_params + self.q_params + self.t_params:
-                    torch.distributed.broadcast(p.data, src, group=self.pg)
+        """Make every rank start from rank `src`'s networks; replicated: also its batch-
+        sampling / noise seed, so every rank draws the same batches."""
+        if self.pg is None or torch.distributed.get_world_size(self.pg) == 1:
+            return
+        with torch.no_grad():
+            if self.backend == "hip":
+                torch.distributed.broadcast(self.flat_param, src, group=self.pg)
+                torch.distributed.broadcast(self.flat_target, src, group=self.pg)
+                self._sf.sync_params()
+                if self.replicated:
+                    dev = self.device if torch.distributed.get_backend(self.pg) == "nccl" else "cpu"
+                    t = torch.tensor([self._seed], dtype=torch.int64, device=dev)
+                    torch.distributed.broadcast(t, src, group=self.pg)
+                    self._seed = int(t.item())
+                    self._replay_key = None  # (re-bind the replay ring with the common seed)
+                return
+            for p in self.pi_params + self.q_params + self.t_params:
+                torch.distributed.broadcast(p.data, src, group=self.pg)
 
     def device_policy(self, deterministic=False, seed=None):
         """The collector's policy on the matrix cores (hip backend): DevicePolicy.act(obs, mask, out) writes

@@ -2795,7 +2795,7 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
   h->lpe = cfg->n_ships > 2 ? 16 : lanes_per_env(cfg, n_envs, device);  // K > 1: 16 lanes in ship slots
   Params& P = h->P;
   memset(&P, 0, sizeof(P));
-  if (const char* e = getenv("SHIPSIM_EPW")) P.epw = atoi(e);  // envs per wave (timing experiments; 0 = full waves)
+  P.epw = cfg->envs_per_wave;  // performance knob (0 = full waves; results identical)
   const int ns = cfg->n_ships;
   ShipConst sc[SHIPSIM_MAX_SHIPS];
   memset(sc, 0, sizeof(sc));
@@ -2861,8 +2861,7 @@ int shipsim_create(const shipsim_config* cfg_in, int32_t n_envs, int32_t n_obs_s
   P.min_east = mn_e; P.max_east = mx_e; P.min_north = mn_n; P.max_north = mx_n;
 
   // constant block: edges | boxes | config routes | grid (ConstBuf layout)
-  const char* no_grid = getenv("SHIPSIM_NO_GRID");
-  const bool use_grid = nv <= 64 && nv > 0 && !(no_grid && no_grid[0] == '1');
+  const bool use_grid = nv <= 64 && nv > 0 && cfg->map_query == SHIPSIM_MAP_GRID;
   const int gnx = use_grid ? (int)ceil((mx_e - mn_e + 2 * kGridPad) / kGridCell) : 0;
   const int gny = use_grid ? (int)ceil((mx_n - mn_n + 2 * kGridPad) / kGridCell) : 0;
   const size_t gcells = (size_t)gnx * gny;

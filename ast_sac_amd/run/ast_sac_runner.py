@@ -7,8 +7,11 @@ Same CLI and variant as the reference. Two execution shapes:
   TorchBatchRLAlgorithm — for drop-in use and side-by-side comparison.
 * `--n_envs N` (default 4096): the MI355X shape — N device-resident envs per GPU stepped in
   slices, transitions written straight into a DeviceReplayBuffer, FusedSACTrainer (HIP-graph
-  step) and DeviceBatchRLAlgorithm. Under torch.distributed.run every rank owns N envs and a
-  local buffer; SAC gradients are averaged with one RCCL all-reduce per grad step.
+  step) and DeviceBatchRLAlgorithm. Under torch.distributed.run every rank owns N envs. With
+  --dp_mode replicated (default) every rank keeps the union of all ranks' transitions (one RCCL
+  all-gather of the new rows per train loop) and runs the same global-batch SAC step, so no
+  collective runs per grad step; --dp_mode allreduce gives each rank a local buffer and averages
+  the SAC gradients with one RCCL all-reduce per grad step.
 
     python -m ast_sac_amd.run.ast_sac_runner --num_epochs 2
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m ast_sac_amd.run.ast_sac_runner
@@ -71,6 +74,10 @@ def build_parser():
     p.add_argument("--match_update_ratio", type=_bool, default=True,
                    help="grad steps per train loop = collected decisions (all ranks) x num_trains / num_expl_steps "
                         "(the reference's ratio); false: num_trains_per_train_loop per loop")
+    p.add_argument("--dp_mode", type=str, default="replicated", choices=["replicated", "allreduce"],
+                   help="multi-rank SAC: replicated = every rank trains on the union of all ranks' transitions (one "
+                        "all-gather per train loop, no per-step collective); allreduce = local buffers, one gradient "
+                        "all-reduce per grad step")
     p.add_argument("--machinery", type=str, default="detailed", choices=["detailed", "simplified"])
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--log_dir", type=str, default=None)
@@ -96,7 +103,7 @@ def make_variant(args):
                             use_automatic_entropy_tuning=args.use_automatic_entropy_tuning,
                             action_reg_coeff=args.action_reg_coeff, clip_val=args.clip_val),
         n_envs=args.n_envs, slice_ticks=args.slice_ticks, machinery=args.machinery,
-        match_update_ratio=args.match_update_ratio)
+        match_update_ratio=args.match_update_ratio, dp_mode=args.dp_mode)
 
 
 def _networks(obs_dim, act_dim, M, device):
@@ -139,7 +146,7 @@ def experiment_reference(variant, args, device):
 def experiment_device(variant, args, device, process_group=None):
     from ..rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, config_from_args
     from ..ast_sac.env_wrapper.normalized_box_env import BatchedNormalizedBoxEnv
-    from ..ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    from ..ast_sac.data_management.replay_buffer import DeviceReplayBuffer, ReplicatedReplayBuffer
     from ..ast_sac.samplers.data_collector.batched_collector import BatchedPathCollector
     from ..ast_sac.torch.sac.policies.base import MakeDeterministic
     from ..ast_sac.torch.sac.sac_fused import FusedSACTrainer
@@ -159,15 +166,21 @@ def experiment_device(variant, args, device, process_group=None):
     act_dim = expl_env.action_space.low.size
     policy, (qf1, qf2, tq1, tq2) = _networks(obs_dim, act_dim, variant["layer_size"], device)
     ak = variant["algorithm_kwargs"]
-    rb = DeviceReplayBuffer(variant["replay_buffer_size"], obs_dim, act_dim, device)
-    # --batch_size is the GLOBAL batch (the reference's 256, run/ast-sac_runner.py:55): each of the
-    # `world` ranks samples batch_size / world rows from its own buffer shard and the averaged
-    # gradient equals the single-GPU B-row gradient in expectation
+    # --batch_size is the GLOBAL batch (the reference's 256, run/ast-sac_runner.py:55)
     world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
-    if ak["batch_size"] % world:
-        raise ValueError(f"--batch_size {ak['batch_size']} must be a multiple of the {world} ranks")
+    replicated = world > 1 and variant.get("dp_mode", "replicated") == "replicated"
+    if replicated:  # every rank: the union of all ranks' rows, the whole global batch, the same seed
+        stage = max(65536, args.n_envs * 64)  # rows one collect can stage (fused passes: <= 32 per env per pass)
+        rb = ReplicatedReplayBuffer(variant["replay_buffer_size"], obs_dim, act_dim, device, process_group, stage)
+        per_rank_batch = ak["batch_size"]
+    else:  # each rank samples batch_size / world rows from its own shard; the averaged gradient equals the
+        # single-GPU B-row gradient in expectation
+        rb = DeviceReplayBuffer(variant["replay_buffer_size"], obs_dim, act_dim, device)
+        if ak["batch_size"] % world:
+            raise ValueError(f"--batch_size {ak['batch_size']} must be a multiple of the {world} ranks")
+        per_rank_batch = ak["batch_size"] // world
     trainer = FusedSACTrainer(env=eval_env, policy=policy, qf1=qf1, qf2=qf2, target_qf1=tq1, target_qf2=tq2,
-                              batch_size=ak["batch_size"] // world, process_group=process_group,
+                              batch_size=per_rank_batch, process_group=process_group, replicated=replicated,
                               backend="hip", **variant["trainer_kwargs"])
     trainer.broadcast_parameters(0)
     # the collectors sample the trainer's current policy on the matrix cores (sacf_policy_act) and replay

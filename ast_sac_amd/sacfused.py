@@ -9,11 +9,11 @@ import torch  # noqa: F401  (HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACFUSED_LIB") or os.path.join(_HERE, "lib", "libsacfused.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 EXPORTED_SYMBOLS = ("sacf_abi_version", "sacf_build_info", "sacf_create", "sacf_destroy", "sacf_last_error", "sacf_set_stream",
                     "sacf_param_count", "sacf_target_count", "sacf_stats_count", "sacf_bind", "sacf_sync_params",
                     "sacf_set_replay", "sacf_grads", "sacf_apply", "sacf_policy_reserve", "sacf_policy_act",
-                    "sacf_step_kernel_status", "sacf_policy_weights")
+                    "sacf_policy_weights", "sacf_hidden_supported")
 _lib = None
 
 
@@ -27,7 +27,7 @@ class Config(C.Structure):
                 ("action_reg_coeff", C.c_float), ("clip_val", C.c_float), ("target_entropy", C.c_float),
                 ("policy_lr", C.c_float), ("qf_lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
                 ("adam_eps", C.c_float), ("auto_entropy", C.c_int32), ("world_size", C.c_int32),
-                ("split_update", C.c_int32), ("step_kernel", C.c_int32), ("reserved", C.c_int32 * 4)]
+                ("split_update", C.c_int32), ("reserved", C.c_int32 * 5)]
 
 
 def load_library(path=LIB_PATH):
@@ -53,7 +53,7 @@ def load_library(path=LIB_PATH):
     L.sacf_grads.argtypes = [P] * 7
     L.sacf_apply.argtypes = [P]
     L.sacf_policy_reserve.argtypes = [P, C.c_int64]
-    L.sacf_step_kernel_status.argtypes = [P]
+    L.sacf_hidden_supported.argtypes = [C.c_int32]
     L.sacf_policy_act.argtypes = [P, P, C.c_int64, C.c_int32, P, C.c_int32, C.c_uint64, P, P, P]
     L.sacf_policy_weights.argtypes = [P, C.POINTER(P), C.POINTER(P), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     if L.sacf_abi_version() != ABI_VERSION:
@@ -68,6 +68,11 @@ def load_library(path=LIB_PATH):
     return L
 
 
+def hidden_supported(hidden):
+    """True if libsacfused has kernels for this hidden width (sacf_hidden_supported)."""
+    return bool(load_library().sacf_hidden_supported(int(hidden)))
+
+
 def _p(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -77,14 +82,13 @@ class SacFused:
 
     def __init__(self, obs_dim, hidden, batch, device, discount, reward_scale, tau, action_reg, clip_val,
                  target_entropy, policy_lr, qf_lr, auto_entropy=True, world_size=1, betas=(0.9, 0.999), eps=1e-8,
-                 split_update=False, persistent=False):
+                 split_update=False):
         self.L = load_library()
         cfg = Config(abi_version=ABI_VERSION, obs_dim=obs_dim, hidden=hidden, batch=batch, discount=discount,
                      reward_scale=reward_scale, soft_target_tau=tau, action_reg_coeff=action_reg or 0.0,
                      clip_val=clip_val, target_entropy=target_entropy, policy_lr=policy_lr, qf_lr=qf_lr,
                      beta1=betas[0], beta2=betas[1], adam_eps=eps, auto_entropy=int(bool(auto_entropy)),
-                     world_size=world_size, split_update=int(bool(split_update)),
-                     step_kernel=1 if persistent else 0)
+                     world_size=world_size, split_update=int(bool(split_update)))
         self.device = torch.device(device)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
@@ -127,10 +131,6 @@ class SacFused:
 
     def apply(self):
         self._check(self.L.sacf_apply(self.h), "sacf_apply")
-
-    def step_kernel_status(self):
-        """Raise if a persistent step launch ever hit its grid-barrier wait bound (synchronizes)."""
-        self._check(self.L.sacf_step_kernel_status(self.h), "sacf_step_kernel_status")
 
     def policy_reserve(self, n):
         self._check(self.L.sacf_policy_reserve(self.h, int(n)), "sacf_policy_reserve")

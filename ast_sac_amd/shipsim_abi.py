@@ -13,7 +13,8 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 7
+ABI_VERSION = 8
+MAP_GRID, MAP_ALL_EDGES = 0, 1  # shipsim_config.map_query (results identical)
 ENONFINITE = -5  # shipsim_synchronize status (include/shipsim.h)
 MAX_ROUTE = 16
 MAX_POLYS = 16
@@ -137,7 +138,8 @@ class Config(C.Structure):
         ("action_low", C.c_float), ("action_high", C.c_float), ("ship", ShipConfig * MAX_SHIPS),
         ("n_polys", C.c_int32), ("poly_start", C.c_int32 * (MAX_POLYS + 1)),
         ("poly_east", C.c_double * MAX_VERTS), ("poly_north", C.c_double * MAX_VERTS),
-        ("lanes_per_env", C.c_int32), ("reserved", C.c_int32 * 7)]
+        ("lanes_per_env", C.c_int32), ("envs_per_wave", C.c_int32), ("map_query", C.c_int32),
+        ("reserved", C.c_int32 * 5)]
 
 
 # ------------------------------------------------------------------------------------------

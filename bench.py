@@ -112,6 +112,16 @@ def cpu_baseline(cfg, seconds, n_threads, n_envs=4096):
         if dt >= seconds * 0.5 or n >= 64 * n_envs:
             break
         n = n_envs * max(2 * (n // n_envs), int(np.ceil(n / n_envs * seconds * 0.6 / max(dt, 1e-3))))
+    # thread scaling on a smaller sample of the same stream (one thread, then the lease's threads), for the
+    # all-core figure below: envs are independent, so the rate per thread is what the extra cores would add
+    small = abi.normalized_to_scoping(abi.ast_action_table(512))
+    per_thread = {}
+    for k in sorted({1, n_threads}):
+        t0 = time.perf_counter()
+        tot_k = O.ast_rollouts(cfg, small, n_threads=k, L=L)[0]
+        per_thread[k] = tot_k / (time.perf_counter() - t0) / k
+    eff = per_thread[n_threads] / per_thread[1]
+    affinity = host_threads()[1]
     c2 = {}
     init = abi.c2_initial_states(n_envs)
     for step in (30, 4):
@@ -121,7 +131,15 @@ def cpu_baseline(cfg, seconds, n_threads, n_envs=4096):
         O.c2_run(c2cfg, init, max_ticks=n_ticks, trace=False, n_threads=n_threads, L=L)
         c2[f"dt{step}"] = n_envs * n_ticks / (time.perf_counter() - t0)
     return dict(value=total / dt, unit="env-ticks/s", cores=n_threads, kind="port",
-                nproc=os.cpu_count(), affinity_cpus=host_threads()[1],
+                nproc=os.cpu_count(), affinity_cpus=affinity,
+                all_affinity_cores=dict(
+                    value=total / dt / n_threads * affinity, cores=affinity, kind="extrapolated",
+                    thread_scaling={"threads": sorted(per_thread), "env_ticks_per_s_per_thread":
+                                    [per_thread[k] for k in sorted(per_thread)], "efficiency": eff},
+                    note=f"measured rate per thread at {n_threads} threads x the {affinity} CPUs in affinity: the box "
+                         f"leases {n_threads} threads (OMP_NUM_THREADS) and running more is not allowed there; "
+                         f"envs share nothing, and per-thread efficiency {n_threads} vs 1 thread on a 512-env sample "
+                         f"was {eff:.2f}"),
                 sample=f"C3: {n // n_envs} x {n_envs} two-ship AST envs x 1 episode each (<=9 decisions from the "
                        f"PCG64 table), {int(total)} env-ticks in {dt:.1f} s; oracle/shipsim_oracle.c built -O3 "
                        f"-march=native, OpenMP {n_threads} threads",

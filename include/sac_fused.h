@@ -7,17 +7,19 @@
  *   policy  TanhGaussianPolicy(obs_dim -> H -> H -> (mean, log_std)), act_dim = 1
  *   qf1/qf2 ConcatMlp(obs_dim + 1 -> H -> H -> 1), targets likewise
  * as batched fp32 GEMMs on the matrix cores (v_mfma_f32_32x32x2_f32):
- *   sacf_grads : four forward/backward kernels (batch gather/sampling, every layer, losses) and the
- *                weight-gradient kernel (flat fp32 gradient of [log_alpha | policy | qf1 | qf2]);
- *                with world_size == 1 that kernel also applies Adam (torch.optim.Adam semantics,
- *                betas/eps as configured), the soft target update and the refresh of the library's
- *                transposed weight copies to the elements it finishes: five launches per grad step.
- *   sacf_apply : world_size > 1 or split_update only (a no-op otherwise): the same update as a sixth
+ *   sacf_grads : three dependent launches per grad step — the forward pass (batch gather/sampling,
+ *                actor on obs / next_obs, critics on the (obs, a) rows); the critics on (obs, ã) with
+ *                the forward-mode tangent of Q along the action, the target critics, and the backward
+ *                factors of layer 2; the weight-gradient kernel (flat fp32 gradient of
+ *                [log_alpha | policy | qf1 | qf2], losses, d log α). With world_size == 1 that kernel
+ *                also applies Adam (torch.optim.Adam semantics, betas/eps as configured), the soft
+ *                target update and the refresh of the library's transposed weight copies.
+ *   sacf_apply : world_size > 1 or split_update only (a no-op otherwise): the same update as a fourth
  *                launch, after the caller all-reduced the flat gradient; the gradient is divided by
  *                world_size.
  *
  * Memory: the caller owns the flat buffers (torch tensors) bound with sacf_bind; the library owns
- * its scratch (per-row activations, ≈12·B·H floats) and transposed copies of the H×H weights.
+ * its scratch (per-row activations, ≈10·B·H floats) and transposed copies of the H×H weights.
  * Flat layout (fp32, torch parameter order and (out, in) row-major weights):
  *   params : [log_alpha] policy{fc0.w (H×O), fc0.b (H), fc1.w (H×H), fc1.b (H), last_fc.w (H),
  *            last_fc.b (1), last_fc_log_std.w (H), last_fc_log_std.b (1)}
@@ -35,20 +37,20 @@
 extern "C" {
 #endif
 
-#define SACF_ABI_VERSION 1
+#define SACF_ABI_VERSION 2 /* 2: three-pass step, any batch, hidden up to 512, no step_kernel */
 #define SACF_OK 0
 #define SACF_EINVAL -1
 #define SACF_EHIP -2
 #define SACF_ESTATE -3
 #define SACF_MAX_OBS 16
-#define SACF_MAX_HIDDEN 256
-#define SACF_MAX_BATCH 8192 /* per-rank batch bound of the hip SAC kernels (any multiple of 32 up to it) */
+#define SACF_MAX_HIDDEN 512 /* hidden: any multiple of 32 up to 256, or 320 / 384 / 448 / 512 */
+#define SACF_MAX_BATCH 8192 /* per-rank batch bound (any size 1..8192; rows padded to a multiple of 32) */
 
 typedef struct sacf_config {
   int32_t abi_version;   /* = SACF_ABI_VERSION */
   int32_t obs_dim;       /* <= SACF_MAX_OBS (8 for the AST env) */
-  int32_t hidden;        /* H, multiple of 32, <= SACF_MAX_HIDDEN (runner: 256) */
-  int32_t batch;         /* B per call (per rank), multiple of 32, <= SACF_MAX_BATCH */
+  int32_t hidden;        /* H: see SACF_MAX_HIDDEN and sacf_hidden_supported (runner: 256) */
+  int32_t batch;         /* B per call (per rank), 1 ..= SACF_MAX_BATCH */
   float discount;        /* sac.py:31  γ */
   float reward_scale;    /* sac.py:32 */
   float soft_target_tau; /* sac.py:37  τ */
@@ -62,9 +64,7 @@ typedef struct sacf_config {
   int32_t world_size;    /* gradient is divided by this in sacf_apply */
   int32_t split_update;  /* 1: keep the update out of sacf_grads even with world_size 1 (the data-parallel
                             call pattern grads | all-reduce | apply on one rank); 0: fused when world_size 1 */
-  int32_t step_kernel;   /* 0: sacf_grads = five launches; 1: one persistent launch (the same tiles as phases
-                            between grid barriers, bit-identical results; see sacf_step_kernel_status) */
-  int32_t reserved[4];
+  int32_t reserved[5];   /* must be 0 */
 } sacf_config;
 
 typedef struct sacf_handle sacf_handle;
@@ -72,6 +72,8 @@ typedef struct sacf_handle sacf_handle;
 int32_t sacf_abi_version(void);
 /* "sacfused gfx950 HIP src <hash>": the content hash of the sources this library was built from */
 const char* sacf_build_info(void);
+/* 1 if kernels for this hidden width are compiled in, else 0 */
+int sacf_hidden_supported(int32_t hidden);
 int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** out);
 int sacf_destroy(sacf_handle* h);
 const char* sacf_last_error(const sacf_handle* h);
@@ -102,8 +104,6 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
                const float* next_obs, const float* eps);
 /* Adam + soft target update from `grads` (divided by world_size); a no-op when sacf_grads applied it. */
 int sacf_apply(sacf_handle* h);
-/* step_kernel 1: SACF_ESTATE when a launch's grid barrier ever timed out (its results are invalid); syncs. */
-int sacf_step_kernel_status(sacf_handle* h);
 
 /* Collector actions from the CURRENT policy parameters (the bound params and the library's W2ᵀ copy):
  * TanhGaussianPolicy.forward + TanhNormal.sample (gaussian_policy.py:105-118, distributions.py:394-425)

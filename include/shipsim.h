@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 7
+#define SHIPSIM_ABI_VERSION 8
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -186,8 +186,16 @@ typedef struct shipsim_config {
   /* performance knob (no effect on results): device lanes per AST env, 2/4/8/16 (the decision
    * stream runs 4/8/16); 0 = $SHIPSIM_LPE or automatic (shipsim_lanes_per_env) */
   int32_t lanes_per_env;
-  int32_t reserved[7];
+  /* performance knobs (no effect on results; ABI 8): envs per wave (0 = as many as the wave holds, 64 / LPE;
+   * fewer leave idle lanes), and the coastline query (SHIPSIM_MAP_GRID: the candidate edges of the ship's
+   * 200 m grid cell; SHIPSIM_MAP_ALL_EDGES: every edge, the reference's own loop) */
+  int32_t envs_per_wave;
+  int32_t map_query;
+  int32_t reserved[5];
 } shipsim_config;
+
+#define SHIPSIM_MAP_GRID 0
+#define SHIPSIM_MAP_ALL_EDGES 1
 
 /* Per-ship state fields for get/set_state (SoA, double unless noted; [env][ship], n_ships = 1 + K) */
 #define SHIPSIM_F_NORTH 0

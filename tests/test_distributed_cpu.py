@@ -98,3 +98,85 @@ def test_dp_sac_matches_single_process_full_batch(tmp_path):
         cur["eps"] = torch.cat([eps[s][0], eps[s][1]], 0)
         tr.train_from_torch(batches[s])
     np.testing.assert_allclose(r0, _params(tr), rtol=2e-5, atol=2e-6)
+
+
+# ------------------------------------------------------------------------------------------------
+# replicated data parallel: every rank trains on the union of all ranks' transitions
+# ------------------------------------------------------------------------------------------------
+N_ROWS, RB_SEED, BG = 40, 11, 2 * B
+
+
+def _rank_rows(rank):
+    g = torch.Generator().manual_seed(1000 + rank)
+    return (torch.randn(N_ROWS, 8, generator=g) * 100, torch.rand(N_ROWS, 1, generator=g) * 2 - 1,
+            torch.randn(N_ROWS, 1, generator=g), torch.randn(N_ROWS, 8, generator=g) * 100,
+            (torch.rand(N_ROWS, 1, generator=g) < 0.3).float())
+
+
+def _noise():
+    g = torch.Generator().manual_seed(77)
+    return [torch.randn(2 * BG, 1, generator=g) for _ in range(STEPS)]
+
+
+def _replicated_worker(rank, world, port, out_dir):
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import ReplicatedReplayBuffer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pol, qs = _make(seed=100 + rank)
+    from ast_sac_amd.ast_sac.torch.sac.sac_fused import FusedSACTrainer
+    tr = FusedSACTrainer(env=_Env, policy=pol, qf1=qs[0], qf2=qs[1], target_qf1=qs[2], target_qf2=qs[3],
+                         discount=0.965, reward_scale=0.75, policy_lr=3e-3, qf_lr=3e-3, soft_target_tau=0.05,
+                         action_reg_coeff=0.01, clip_val=100.0, batch_size=BG, use_graph=False,
+                         process_group=dist.group.WORLD, replicated=True)
+    assert tr.world == 1 and not tr.split
+    tr.broadcast_parameters(0)
+    rb = ReplicatedReplayBuffer(1000, 8, 1, "cpu", dist.group.WORLD, stage_size=64,
+                                generator=torch.Generator().manual_seed(RB_SEED))
+    o, a, r, no, t = _rank_rows(rank)
+    keep = torch.arange(N_ROWS) % 4 != rank  # a masked add, as the collector's
+    rb.add_batch(o, a, r, no, t, mask=keep)
+    assert rb.num_steps_can_sample() == 0  # staged only
+    n = rb.sync()
+    assert n == rb.num_steps_can_sample() == 2 * int(keep.sum())
+    noise = _noise()
+    cur = {}
+    tr.noise_fn = lambda shape: cur["eps"]
+    for s in range(STEPS):
+        cur["eps"] = noise[s]
+        tr.train_from_buffer(rb, 1)
+    np.save(os.path.join(out_dir, f"rep{rank}.npy"), _params(tr))
+    np.save(os.path.join(out_dir, f"rows{rank}.npy"), rb._observations[:n].numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_replicated_dp_sac_equals_single_process_on_the_union():
+    """Two gloo ranks with different local transitions and different initial networks: after sync() both hold
+    the union (rank order) and, with the broadcast parameters and the common batch seed, their SAC steps give
+    bitwise the parameters of ONE process training on that union with the whole global batch."""
+    import tempfile
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_replicated_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        r0, r1 = np.load(os.path.join(d, "rep0.npy")), np.load(os.path.join(d, "rep1.npy"))
+        rows0, rows1 = np.load(os.path.join(d, "rows0.npy")), np.load(os.path.join(d, "rows1.npy"))
+    np.testing.assert_array_equal(r0, r1)
+    np.testing.assert_array_equal(rows0, rows1)
+    pol, qs = _make(seed=100)
+    from ast_sac_amd.ast_sac.torch.sac.sac_fused import FusedSACTrainer
+    tr = FusedSACTrainer(env=_Env, policy=pol, qf1=qs[0], qf2=qs[1], target_qf1=qs[2], target_qf2=qs[3],
+                         discount=0.965, reward_scale=0.75, policy_lr=3e-3, qf_lr=3e-3, soft_target_tau=0.05,
+                         action_reg_coeff=0.01, clip_val=100.0, batch_size=BG, use_graph=False)
+    rb = DeviceReplayBuffer(1000, 8, 1, "cpu", generator=torch.Generator().manual_seed(RB_SEED))
+    for rank in range(world):
+        o, a, r, no, t = _rank_rows(rank)
+        rb.add_batch(o, a, r, no, t, mask=torch.arange(N_ROWS) % 4 != rank)
+    np.testing.assert_array_equal(rows0, rb._observations[:rb.num_steps_can_sample()].numpy())
+    noise = _noise()
+    cur = {}
+    tr.noise_fn = lambda shape: cur["eps"]
+    for s in range(STEPS):
+        cur["eps"] = noise[s]
+        tr.train_from_buffer(rb, 1)
+    np.testing.assert_array_equal(r0, _params(tr))

@@ -215,7 +215,7 @@ def test_step_inactive_mask_and_errors(torch_cuda):
 
 
 @pytest.mark.parametrize("collav", ["none", "sbmpc"])
-def test_map_grid_is_exact(torch_cuda, collav, monkeypatch):
+def test_map_grid_is_exact(torch_cuda, collav):
     """The map grid (cell edge lists + inside/outside classification) changes no result: 2048 C3 envs
     under random actions give bitwise-identical obs/reward/events/state with and without it."""
     import torch
@@ -223,9 +223,10 @@ def test_map_grid_is_exact(torch_cuda, collav, monkeypatch):
     n = 2048
     tables = abi.normalized_to_scoping(abi.ast_action_table(n, n_dec=9, seed=99)).T  # (9, n)
     res = []
-    for no_grid in ("1", "0"):
-        monkeypatch.setenv("SHIPSIM_NO_GRID", no_grid)
-        sim = ShipSim(abi.ast_config(collav), n)
+    for query in (abi.MAP_ALL_EDGES, abi.MAP_GRID):
+        cfg = abi.ast_config(collav)
+        cfg.map_query = query
+        sim = ShipSim(cfg, n)
         sim.reset()
         outs = []
         dec = torch.zeros(n, dtype=torch.long, device="cuda")

@@ -190,3 +190,37 @@ def test_fused_collector_rows_and_paths_follow_the_decision_log():
         np.testing.assert_array_equal(g["rewards"][:, 0], np.array([x[0] for x in p]))
         np.testing.assert_array_equal(g["actions"][:, 0], np.array([x[1] for x in p]))
     assert coll.get_diagnostics()["num steps total"] == len(rows)
+
+
+def test_sliced_then_fused_collect_rows_match_the_policy():
+    """A collector switched from sliced passes (step()) to fused ones (collect()) starts its episodes afresh:
+    every replay row the fused passes write has a real observation and the deterministic policy's action on
+    it (a decision a sliced pass began and left in flight would have no stored observation / action in the
+    policy stream's log: ADVICE round 3)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from ast_sac_amd.rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, default_args
+    from ast_sac_amd.ast_sac.env_wrapper.normalized_box_env import BatchedNormalizedBoxEnv
+    from ast_sac_amd.ast_sac.samplers.data_collector.batched_collector import BatchedPathCollector
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    tr, pol = _trainer(128)
+    N = 128
+    env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), N), 0.75)
+    dp = tr.device_policy(True)
+    coll = BatchedPathCollector(env, pol, max_path_length=9, max_ticks=40, deterministic=True, device_policy=dp,
+                                use_graph=False)
+    assert coll.fused
+    for _ in range(3):  # sliced passes of 40 ticks: most envs are mid-decision afterwards
+        coll.step()
+    rb = DeviceReplayBuffer(100000, 8, 1, "cuda")
+    coll.max_ticks = 256
+    got = coll.collect(400, rb)
+    torch.cuda.synchronize()
+    n = rb.num_steps_can_sample()
+    assert n == got >= 400
+    obs0, act = rb._observations[:n], rb._actions[:n]
+    assert bool((obs0.abs().sum(1) > 0).all()), "replay row with an all-zero observation"
+    with torch.no_grad():
+        ref = torch.tanh(pol(obs0).normal_mean)
+    err = (act - ref).abs().max().item()
+    assert err < 5e-6, err

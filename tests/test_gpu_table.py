@@ -106,8 +106,8 @@ def test_stream_lanes_per_env_bitwise(collav, lpe):
 
 
 @pytest.mark.parametrize("collav,epw", [("sbmpc", 1), ("sbmpc", 3), ("none", 2)])
-def test_stream_envs_per_wave_bitwise(collav, epw, monkeypatch):
-    """Waves launched with fewer envs than they hold (SHIPSIM_EPW: the idle lanes of each wave take no
+def test_stream_envs_per_wave_bitwise(collav, epw):
+    """Waves launched with fewer envs than they hold (config envs_per_wave: the idle lanes of each wave take no
     part; the wave-cooperative SBMPC pass serves the envs it has) give bitwise the full-wave records."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -115,7 +115,7 @@ def test_stream_envs_per_wave_bitwise(collav, epw, monkeypatch):
     N = 96
     table = _table(2, cfg.max_sampling_frequency, N, seed=7)
     ref, t_ref = _chained(cfg, N, table, 200, 6)
-    monkeypatch.setenv("SHIPSIM_EPW", str(epw))  # read by shipsim_create
+    cfg.envs_per_wave = epw
     got, t_got = _chained(cfg, N, table, 200, 6)
     assert t_got == t_ref
     for i in range(N):

@@ -203,9 +203,11 @@ def _assert_grads_close(g_hip, g_ref, tr, what):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,B", [(32, 64), (64, 96), (96, 64), (160, 128), (224, 32), (256, 32), (256, 256), (256, 1024),
-                                 (256, 4096), (128, 8192)])
+                                 (256, 4096), (128, 8192), (256, 100), (512, 100), (512, 256), (384, 33), (64, 1),
+                                 (320, 300), (448, 64)])
 def test_hip_sac_gradients_match_torch_autograd(H, B):
-    """One update's flat gradient (α | π | Q1 | Q2) from the fused kernels == torch autograd's."""
+    """One update's flat gradient (α | π | Q1 | Q2) from the fused kernels == torch autograd's, including
+    batches that are not a multiple of 32 (padded rows) and hidden widths above 256 (two K chunks)."""
     batch, eps = _rand_batch(B, "cuda")
     ref = _trainer("torch", H, B, "cuda")
     hip = _trainer("hip", H, B, "cuda")
@@ -273,26 +275,37 @@ def test_hip_sac_graph_replay_equals_eager_launches():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,B,split", [(256, 256, False), (256, 256, True), (64, 96, False), (256, 1024, False),
-                                           (256, 4096, False)])
-def test_hip_sac_persistent_step_equals_five_launches(H, B, split):
-    """libsacfused step_kernel 1 (the whole grad step in one persistent launch, grid barriers between the
-    passes) runs the five-launch kernels' own tiles in the same order: 20 graph-replayed steps from the
-    replay ring give bitwise the same parameters, targets and Adam state, fused or split (grads | apply)."""
+@pytest.mark.parametrize("H,B", [(256, 256), (64, 96), (512, 100)])
+def test_hip_sac_split_update_equals_fused(H, B):
+    """The data-parallel call pattern on one rank (sacf_grads | all-reduce over a world-size-1 group |
+    sacf_apply) gives bitwise the fused step's parameters, targets and Adam state over 20 graph-replayed
+    steps from the replay ring (Adam is the same element function in both kernels)."""
     from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
     rb = DeviceReplayBuffer(5000, 8, 1, "cuda")
     b, _ = _rand_batch(3000, "cuda", seed=4)
     rb.add_batch(b["observations"], b["actions"], b["rewards"], b["next_observations"], b["terminals"])
     res = []
-    for persistent in (False, True):
+    for split in (False, True):
         pol, qs = _seeded_nets(H, "cuda", 7)
         tr = FusedSACTrainer(env=_Env, policy=pol, qf1=qs[0], qf2=qs[1], target_qf1=qs[2], target_qf2=qs[3],
                              discount=0.965, reward_scale=0.75, policy_lr=8e-5, qf_lr=8e-5, soft_target_tau=1e-3,
                              action_reg_coeff=0.01, clip_val=100.0, batch_size=B, use_graph=True, backend="hip",
-                             split_update=split, persistent_kernel=persistent)
+                             split_update=split)
         tr._seed = 1234
         tr.train_from_buffer(rb, 20)
         torch.cuda.synchronize()
-        tr._sf.step_kernel_status()
         res.append(torch.cat([tr.flat_param, tr.flat_target, tr._adam_m, tr._adam_v, tr._stats_t]).cpu())
     assert torch.equal(res[0], res[1])
+
+
+def test_hip_backend_shape_rules():
+    """The hip backend takes every batch size 1..8192 and the compiled hidden widths; other widths raise
+    (no silent fallback). CPU-only: checks the rules the trainer applies before touching the device."""
+    from ast_sac_amd import sacfused
+    try:
+        sacfused.load_library()
+    except sacfused.SacFusedError:
+        pytest.skip("libsacfused not built")
+    ok = [h for h in range(32, 513, 32) if sacfused.hidden_supported(h)]
+    assert ok == [32, 64, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512]
+    assert not sacfused.hidden_supported(288) and not sacfused.hidden_supported(100)
