@@ -335,6 +335,11 @@ __device__ __forceinline__ int opaque_v(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// a wave-uniform value the compiler must re-derive after this point (comparisons on it cannot be hoisted)
+__device__ __forceinline__ int opaque_s(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
 // opaque_v where OPQ (the kernels whose allocation otherwise spills the lane masks derived from x), x as is
 // elsewhere (there the recomputation costs more than the held mask)
 template <bool OPQ>
@@ -814,6 +819,8 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
   const int scen = lane & 31;
   uint64_t req = __ballot(need);
   while (req) {
+    // the counts re-derived per pass: tests on them are not hoisted out of this loop and held across it
+    const int n_obs_p = opaque_s(n_obs), n_samp_p = opaque_s(n_samp);
     int src0 = __ffsll((unsigned long long)req) - 1;
     req &= req - 1;
     int src1 = -1;
@@ -834,16 +841,16 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
     const bool act = src >= 0 && scen < 28;
 #pragma unroll
     for (int k = 0; k < NOB; ++k) {
-      if (k >= n_obs) break;  // (wave-uniform) slots past the env's K obstacles duplicate the last one
+      if (k >= n_obs_p) break;  // (wave-uniform) slots past the env's K obstacles duplicate the last one
       g.ob_x = shfl_d(in.ob_x[k], srcc); g.ob_y = shfl_d(in.ob_y[k], srcc); g.ob_psi = shfl_d(in.ob_psi[k], srcc);
       g.ob_u = shfl_d(in.ob_u[k], srcc); g.ob_v = shfl_d(in.ob_v[k], srcc);
       g.obs_l = shfl_d(in.obs_l[k], srcc); g.obs_w = shfl_d(in.obs_w[k], srcc);
       // an obstacle out of reach costs exactly sbmpc_h2 in every scenario (added once below)
-      const bool far = act && sbmpc_far(g, n_samp, DT);
+      const bool far = act && sbmpc_far(g, n_samp_p, DT);
       any_far = any_far || far;
       if (act && !far) {
         sb_set_heading_trig(g);
-        const double ck = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3);
+        const double ck = sbmpc_scenario_cost(g, opaque_s(n_samp_p), DT, scen >> 2, scen & 3);
         if (ck > worst) worst = ck;
       }
     }
@@ -1353,7 +1360,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   static_assert(NSUB >= 1 && 8 % NSUB == 0, "sub-lanes per ship must divide 8 (grid_part shares)");
   static_assert(LPE >= 2 && (LPE & (LPE - 1)) == 0 && LPE <= 16, "LPE must be a power of two in [2, 16]");
   constexpr bool SIMPLE = COLLAV == SHIPSIM_COLLAV_SIMPLE;
-  constexpr bool OPQ = LPE != 16 || POLICY;  // see opaque_if (measured: LPE-16 table kernels hold no spills without)
+  constexpr bool OPQ = LPE != 16 || POLICY || SLOTS > 2;  // see opaque_if (measured: LPE-16 two-slot table kernels hold no spills without)
   __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
   __shared__ EdgeX lds_edges[SHIPSIM_MAX_VERTS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
@@ -1406,7 +1413,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   double* rn = S.route_n() + (size_t)qc * kMaxRoute;
   double* re = S.route_e() + (size_t)qc * kMaxRoute;
 
-  bool running = valid && (A0.active_mask == nullptr || A0.active_mask[envc]) && S.was_reset()[envc];
+  // (an int laundered where it is set, as have_iw: a bool here stayed a lane mask across the tick loop)
+  int running = opaque_if<OPQ>((valid && (A0.active_mask == nullptr || A0.active_mask[envc]) && S.was_reset()[envc]) ? 1 : 0);
   // (ints in VGPRs read by the epilogue: not lane masks held in SGPRs for the whole launch)
   const int touched = opaque_v(running && valid ? 1 : 0);
 
@@ -1424,7 +1432,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     for (int i = 0; i < 4; ++i) st4[i] = S.states4()[envc * 4 + i];
   uint32_t snap_bits = S.snap_bits()[envc];
   int dflags = S.dec_flags()[envc];
-  bool have_iw = dflags & DF_HAVE_IW;
+  // (an int laundered where it is set and read: a bool here was kept as a lane mask across the tick loop and
+  // spilled in the LPE-8 policy kernels)
+  int have_iw = opaque_if<OPQ>((dflags & DF_HAVE_IW) ? 1 : 0);
   int phase = (dflags >> DF_PHASE_SHIFT) & 3;
   int dec_ticks = S.dec_ticks()[envc];  // ticks of the decision in progress (across calls)
 
@@ -1473,7 +1483,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     started_here = true;
     if (P.normalize_action) sa = (sa + 1.0f) / 2.0f * (P.action_high - P.action_low) + P.action_low;
     phase = 0;
-    have_iw = false;
+    have_iw = opaque_if<OPQ>(0);
     dec_ticks = 0;
     if (sampling_count < P.max_sampling) {
       sampling_count += 1;
@@ -1486,7 +1496,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       double iw_n = n_base + n_s, iw_e = e_base + e_s;
       n_base = iw_n + P.AB_seg_n;
       e_base = iw_e + P.AB_seg_e;
-      if (is_obs1) {  // auto_pilot.update_route: list.insert(-1, IW); every sub-lane writes the same bytes
+      if (opaque_if<OPQ>(shipc) == 1) {  // auto_pilot.update_route: list.insert(-1, IW); every sub-lane writes the same bytes
         int L = s.n_route;
         rn[L] = s.end_n; re[L] = s.end_e;
         rn[L - 1] = iw_n; re[L - 1] = iw_e;
@@ -1499,7 +1509,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       }
       travel_dist = 0;
       travel_time = 0;
-      have_iw = true;
+      have_iw = opaque_if<OPQ>(1);
       bool fail = corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, iw_n, iw_e) ||
                   ((iw_n < P.min_north || iw_n > P.max_north) || (iw_e < P.min_east || iw_e > P.max_east));
       if (fail) {  // env.py:673-693 with obs_ship_IW_sampling_failure_reward (multiplier 2)
@@ -1523,7 +1533,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     dec_i = CH.dec_idx[envc];
     log_n = CH.log_len ? CH.log_len[envc] : 0;
     if (running && CH.log_stop && log_n >= CH.log_cap) {  // log already full: sit this launch out
-      running = false;
+      running = opaque_if<OPQ>(0);
       stalled = (dflags & DF_AWAITING) != 0;
     }
   }
@@ -1560,7 +1570,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     for (int i = 0; i < 8; ++i) ns[i] = P.initial_states[i];
     snap_bits = 0;
     phase = 0;
-    have_iw = false;
+    have_iw = opaque_if<OPQ>(0);
   };
   // A decision just completed (ready): record it, reset if the episode ended (done, or n_dec decisions
   // = the rollout's max_path_length), consume the next table action. A sampling failure completes the
@@ -1596,7 +1606,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       bool want = false;
       if (ready && running) {
         const ChainArgs& CH = step_args().CH;
-        if (CH.log && lie == 0 && log_n < CH.log_cap) {
+        if (CH.log && opaque_if<OPQ>(lie) == 0 && log_n < CH.log_cap) {
           double* rec = CH.log + ((size_t)env * CH.log_cap + log_n) * SHIPSIM_DECLOG_COLS;
           rec[SHIPSIM_DL_REWARD] = out_r; rec[SHIPSIM_DL_EVENTS] = (double)out_bits;
           rec[SHIPSIM_DL_DONE] = out_done ? 1.0 : 0.0; rec[SHIPSIM_DL_EPISODE] = (double)ep_i;
@@ -1618,7 +1628,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         } else {
           dec_i += 1;
         }
-        if (lie == 0) {
+        if (opaque_if<OPQ>(lie) == 0) {
           const DevState So = opaque(step_args().S);
           for (int i = 0; i < 8; ++i) So.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
         }
@@ -1626,7 +1636,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         out_done = false;
         if (burst + 1 >= kChainBurst || (CH.log_stop && log_n >= CH.log_cap)) {
           stalled = true;  // next decision pending: resumed by the next launch
-          running = false;
+          running = opaque_if<OPQ>(0);
         } else {
           want = true;
         }
@@ -1662,6 +1672,17 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     const Params& P = A.P;
     const ConstBuf& K = A.K;
     const Traj& T = A.T;
+    // the lane's roles re-derived per tick where OPQ (shadowing the entry's): the run-time ship count and the
+    // slot tests of the K > 1 kernels otherwise stay lane masks and scalars held across the loop, and spill
+    const int lie_t = opaque_if<OPQ>(lie);
+    const int ship = lie_t % SLOTS;
+    const int sub = lie_t / SLOTS;
+    const bool is_test = ship == 0;
+    const int nsh = (SLOTS == 2) ? 2 : P.n_ships;
+    const bool ghost = (SLOTS > 2) && ship >= nsh;
+    const int shipc = ghost ? nsh - 1 : ship;
+    const bool is_obs1 = shipc == 1;
+    (void)ghost;
     // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
     SHIPSIM_LANE_CHECK(LPE, 7);
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
@@ -1999,7 +2020,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         const bool roa = Of & XF_ROA;
         if (combined_done) finish = true;
         else if (roa) {
-          if (have_iw) phase = 1;
+          if (opaque_if<OPQ>(have_iw) != 0) phase = 1;
           else finish = true;
         }
       } else if (phase == 1) {
@@ -2022,13 +2043,15 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         snap_bits = bits;
         ready = true;
       }
-      going = !ready && (max_ticks <= 0 || ticks < max_ticks);
+      const int mt = OPQ ? step_args().max_ticks : max_ticks;  // (OPQ: its test not held across the loop)
+      going = !ready && (mt <= 0 || ticks < mt);
     }
     PT_MARK(3);
   }
   if (!CHAIN) break;
   if (POLICY || (ready && running)) chain_next();  // (policy: wave-uniform, a no-op unless a decision completed)
-  going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
+  const int mt = OPQ ? step_args().max_ticks : max_ticks;
+  going = running && !ready && (mt <= 0 || ticks < mt);
   if (!__any(going)) break;
   }
 #ifdef SHIPSIM_PHASE_TIMING
@@ -2119,43 +2142,65 @@ __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevStat
 // Two lanes per env (lane & 1 = ship); the termination flags of get_termination_status
 // (termination_flags.py:5-70) are evaluated in fp64 on the next_states, as the reference does on
 // its Python-float list.
+// Arguments read through the kernarg segment pointer (as step_args): the Params block and the state base
+// addresses are scalar loads where a tick uses them, not argument SGPRs held (and spilled) across the loop.
+struct LegacyArgs {
+  Params P;
+  DevState S;
+  ConstBuf K;
+  int k;
+  double* states_out;
+  uint8_t* done_out;
+  uint32_t* status_out;
+};
+typedef const __attribute__((address_space(4))) LegacyArgs* LegacyArgsPtr;
+__device__ __forceinline__ const LegacyArgs& legacy_args() {
+  LegacyArgsPtr q = (LegacyArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return *(const LegacyArgs*)q;
+}
+
 template <bool DETAILED, int COLLAV>
-__global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevState S, ConstBuf K, int k,
-                                                         double* __restrict__ states_out, uint8_t* __restrict__ done_out,
-                                                         uint32_t* __restrict__ status_out) {
+__global__ __launch_bounds__(64) void legacy_step_kernel(LegacyArgs a_arg) {
+  (void)a_arg;  // read through legacy_args()
   __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
-  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
-  for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) lds_edges_raw[i] = K.edges()[i];
-  for (int i = threadIdx.x; i < P.n_polys; i += blockDim.x) lds_boxes[i] = K.boxes()[i];
+  const LegacyArgs& A0 = legacy_args();
+  const ShipConst* SC = stage_consts(A0.K, lds_sc, A0.P.n_ships);
+  for (int i = threadIdx.x; i < A0.K.n_edges; i += blockDim.x) lds_edges_raw[i] = A0.K.edges()[i];
+  for (int i = threadIdx.x; i < A0.P.n_polys; i += blockDim.x) lds_boxes[i] = A0.K.boxes()[i];
   __syncthreads();
 
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const int env = gl >> 1;
   const int ship = gl & 1;
   const bool is_test = ship == 0;
-  const bool valid = env < P.n_envs;
+  const bool valid = env < A0.P.n_envs;
   const int envc = valid ? env : 0;
   const int qc = envc * 2 + ship;
   const ShipConst& c = SC[ship];
-  const double* rn = S.route_n() + (size_t)qc * kMaxRoute;
-  const double* re = S.route_e() + (size_t)qc * kMaxRoute;
+  const double* rn = A0.S.route_n() + (size_t)qc * kMaxRoute;
+  const double* re = A0.S.route_e() + (size_t)qc * kMaxRoute;
   Ship s;
-  load_ship(S, qc, s);
-  double p_last = S.p_last()[envc], chi_last = S.chi_last()[envc];
-  const double mach_dt = S.mach_dt()[envc];
-  double* lst = S.legacy_states() + (size_t)envc * 4;  // self.states [test n, e, obs n, e]
+  load_ship(A0.S, qc, s);
+  double p_last = A0.S.p_last()[envc], chi_last = A0.S.chi_last()[envc];
+  const double mach_dt = A0.S.mach_dt()[envc];
+  const double* lst = A0.S.legacy_states() + (size_t)envc * 4;  // self.states [test n, e, obs n, e]
   double st[4] = {lst[0], lst[1], lst[2], lst[3]};
-  bool st_f32 = S.legacy_flags()[envc] & 1;
-  const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
+  bool st_f32 = A0.S.legacy_flags()[envc] & 1;
+  const int n_samp = (int)(A0.P.sbmpc_tf / A0.P.sbmpc_dt);
 
   double out8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t status = 0;
   bool done = false, ticked = false;
   bool going = valid;
-  for (int it = 0; it < k; ++it) {
+  for (int it = 0; it < legacy_args().k; ++it) {
     if (!__any(going)) break;
+    // this tick's constants: re-read through the kernarg pointer rather than kept in registers across ticks
+    const LegacyArgs& A = legacy_args();
+    const Params& P = A.P;
+    const ConstBuf& K = A.K;
     const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
     const double pu = pair_swap(s.u), pv = pair_swap(s.v);
     double sf = 1.0, off = 0.0;
@@ -2246,16 +2291,19 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(const Params P, DevStat
     }
   }
   if (!valid) return;
+  const LegacyArgs& A = legacy_args();
+  const DevState S = opaque(A.S);
   store_ship(S, qc, s);
   if (is_test) {
     S.p_last()[env] = p_last; S.chi_last()[env] = chi_last;
-    for (int i = 0; i < 4; ++i) lst[i] = st[i];
+    double* lsto = S.legacy_states() + (size_t)env * 4;
+    for (int i = 0; i < 4; ++i) lsto[i] = st[i];
     S.legacy_flags()[env] = st_f32 ? 1 : 0;
     if (ticked) {
-      if (states_out)
-        for (int i = 0; i < 8; ++i) states_out[(size_t)env * 8 + i] = out8[i];
-      if (done_out) done_out[env] = done ? 1 : 0;
-      if (status_out) status_out[env] = status;
+      if (A.states_out)
+        for (int i = 0; i < 8; ++i) A.states_out[(size_t)env * 8 + i] = out8[i];
+      if (A.done_out) A.done_out[env] = done ? 1 : 0;
+      if (A.status_out) A.status_out[env] = status;
     }
   }
 }
@@ -3025,6 +3073,14 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
 #define LAUNCH(D, CA) launch_step<D, CA>(h, lpe, action, active, max_ticks, obs_out, reward_out, done_out, events_out, ticks_out, ready_out)
 #ifdef SHIPSIM_REGCHECK  // register-usage inspection builds (scripts/regcheck.sh): headline kernels only
   (void)lpe; (void)det;
+#if SHIPSIM_REGCHECK == 3  // the multi-obstacle (K > 1) kernels
+  if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
+    launch_multi<SHIPSIM_COLLAV_SBMPC, 0>(h, action, active, max_ticks, obs_out, reward_out, done_out, events_out,
+                                          ticks_out, ready_out, ChainArgs{});
+  else
+    launch_multi<SHIPSIM_COLLAV_NONE, 0>(h, action, active, max_ticks, obs_out, reward_out, done_out, events_out,
+                                         ticks_out, ready_out, ChainArgs{});
+#endif
   return fail(h, SHIPSIM_EINVAL, "REGCHECK build");
 #else
   if (ship_slots(h) > 2) {
@@ -3086,9 +3142,19 @@ static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, 
   } while (0)
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
 #ifdef SHIPSIM_REGCHECK
+#if SHIPSIM_REGCHECK == 2  // the LPE-8 stream kernels (the C4 shard's collector)
+  if (det) CHAINED_L(true, SHIPSIM_COLLAV_SBMPC, 8);
+  else CHAINED_L(false, SHIPSIM_COLLAV_SBMPC, 8);
+#elif SHIPSIM_REGCHECK == 3  // the multi-obstacle decision stream
+  (void)det;
+  if (MODE == 1)
+    launch_multi<SHIPSIM_COLLAV_SBMPC, 1>(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out,
+                                          nullptr, ch);
+#else
   if (h->P.collav == SHIPSIM_COLLAV_SBMPC) CHAINED_L(true, SHIPSIM_COLLAV_SBMPC, 16);
   else CHAINED_L(true, SHIPSIM_COLLAV_NONE, 16);
   (void)det;
+#endif
 #else
   if (MODE == 1 && ship_slots(h) > 2) {  // (run_policy refuses K > 1 before it gets here)
     if (h->P.collav == SHIPSIM_COLLAV_SBMPC)
@@ -3157,9 +3223,8 @@ int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_
   if (k == 0) return SHIPSIM_OK;
   DeviceGuard g(h->device);
   const int threads = 64, blocks = (2 * h->P.n_envs + threads - 1) / threads;
-#define LEGACY(D, CA)                                                                                      \
-  hipLaunchKernelGGL((legacy_step_kernel<D, CA>), dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k, \
-                     states_out, done_out, status_out)
+  const LegacyArgs la{h->P, h->S, h->K, k, states_out, done_out, status_out};
+#define LEGACY(D, CA) hipLaunchKernelGGL((legacy_step_kernel<D, CA>), dim3(blocks), dim3(threads), 0, h->stream, la)
   const bool det = h->P.machinery == SHIPSIM_MACH_DETAILED;
 #ifdef SHIPSIM_REGCHECK
   (void)det;
