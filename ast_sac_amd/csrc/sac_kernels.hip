@@ -88,7 +88,12 @@ struct Scr {
   float *hpart;              // [2Bp][2][CB] actor head parts (mean | log_std) of the obs and next_obs rows
   float *part;               // [PS_N][Bp][CB]
   float *loss;               // [5][Bp] per-row loss terms (scalar block)
+  // the parameters P3 reads, as they were before this step's update (P3 updates them in place with fused Adam,
+  // so its blocks must not read the live values): [log α, b3 Q1, b3 Q2, b3 T1, b3 T2, -, -, -] then
+  // wm [H], ws [H], w3 Q1 [H], w3 Q2 [H]
+  float *snap;
 };
+enum { SN_LOGA, SN_BQ1, SN_BQ2, SN_BT1, SN_BT2, SN_HEAD = 8 };
 
 struct MArgs {
   const float* params;
@@ -669,13 +674,29 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
 template <int H>
 __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   __shared__ float lds[FwdLds<H>::kFloats];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
-    const int64_t t = *a.step + 1;
-    *a.step = t;
-    const AdamStep st = adam_step(a.hp, t);
-    a.stats[5] = st.step_pi;
-    a.stats[6] = st.step_q;
-    a.stats[7] = st.bc2_sqrt;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
+      const int64_t t = *a.step + 1;
+      *a.step = t;
+      const AdamStep st = adam_step(a.hp, t);
+      a.stats[5] = st.step_pi;
+      a.stats[6] = st.step_q;
+      a.stats[7] = st.bc2_sqrt;
+    }
+    // the parameters P3 reads (it updates them in place), before this step's update
+    const Layout& L = a.L;
+    const float* P = a.params;
+    float* sn = a.s.snap;
+    if (threadIdx.x < 5) {
+      const int i = threadIdx.x;
+      sn[i] = i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3];
+    }
+    for (int j = threadIdx.x; j < L.H; j += kThreads) {
+      sn[SN_HEAD + j] = P[L.p_wm + j];
+      sn[SN_HEAD + L.H + j] = P[L.p_ws + j];
+      sn[SN_HEAD + 2 * L.H + j] = P[L.q_base[0] + L.c_w3 + j];
+      sn[SN_HEAD + 3 * L.H + j] = P[L.q_base[1] + L.c_w3 + j];
+    }
   }
   int bx, by;
   tile_of<H>(bx, by);
@@ -703,13 +724,12 @@ __device__ __forceinline__ CriticRow critic_row(const MArgs& a, int r, float alp
   load_run<CB>(pt + ((int64_t)PS_Q2D * Bp + r) * CB, p1);
   load_run<CB>(pt + ((int64_t)PS_T1 * Bp + r) * CB, p2);
   load_run<CB>(pt + ((int64_t)PS_T2 * Bp + r) * CB, p3);
-  const float* P = a.params;
-  const float* TG = a.targets;
+  const float* sn = a.s.snap;  // (the pre-update biases: P3 updates the live ones)
   const float logpn = a.s.logpn[r], rw = a.s.rew[r], tm = a.s.term[r];
   CriticRow o;
-  o.q1 = fold(p0) + P[L.q_base[0] + L.c_b3];
-  o.q2 = fold(p1) + P[L.q_base[1] + L.c_b3];
-  const float t1 = fold(p2) + TG[L.c_b3], t2 = fold(p3) + TG[L.q_size + L.c_b3];
+  o.q1 = fold(p0) + sn[SN_BQ1];
+  o.q2 = fold(p1) + sn[SN_BQ2];
+  const float t1 = fold(p2) + sn[SN_BT1], t2 = fold(p3) + sn[SN_BT2];
   const float tq = fminf(t1, t2) - alpha * logpn;
   float y = a.hp.rscale * rw + ((1.0f - tm) * a.hp.gamma) * tq;
   o.y = fminf(fmaxf(y, -a.hp.clip), a.hp.clip);
@@ -737,9 +757,9 @@ __device__ __forceinline__ ActorRow actor_row(const MArgs& a, int r, float alpha
   const float mean = hd[HD_MEAN * Bp + r], ls_raw = hd[HD_LSRAW * Bp + r], std = hd[HD_STD * Bp + r];
   const float z = hd[HD_Z * Bp + r], act = hd[HD_A * Bp + r], logp = hd[HD_LOGP * Bp + r];
   const float eps_i = a.s.eps[r];
-  const float* P = a.params;
-  const float q1a = fold(p4) + P[L.q_base[0] + L.c_b3];
-  const float q2a = fold(p5) + P[L.q_base[1] + L.c_b3];
+  const float* sn = a.s.snap;
+  const float q1a = fold(p4) + sn[SN_BQ1];
+  const float q2a = fold(p5) + sn[SN_BQ2];
   const float invB = 1.0f / (float)L.B;
   // d min(Q1, Q2): all to the smaller, split evenly on a tie (torch.min's backward)
   const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
@@ -840,7 +860,7 @@ struct WLds {
 };
 
 __device__ __forceinline__ float alpha_of(const MArgs& a) {
-  return a.hp.auto_ent ? expf(a.params[0]) : 1.0f;
+  return a.hp.auto_ent ? expf(a.s.snap[SN_LOGA]) : 1.0f;
 }
 
 // MFMA tile of dW2 for matrix mat (0 actor, 1 / 2 Q1 / Q2): out[j][k] = Σ_r dY[r][j] X[r][k] with
@@ -864,14 +884,13 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   const int j0 = (t / CB) * kTile2, k0 = (t % CB) * kTile2;
   const bool actor = mat == 0;
   const int net = actor ? 0 : mat - 1;
-  const float* P = m.params;
-  const float* C = P + L.q_base[net];
+  const float* hw = m.s.snap + SN_HEAD;  // pre-update head weights: wm | ws | w3 Q1 | w3 Q2
   const gptr Y = as_global(actor ? m.s.h2 : m.s.g2[net]);
   const gptr X = as_global(actor ? m.s.h1 : m.s.g1[net]);
   const int jc = j0 + rl;
-  const float c1 = actor ? P[L.p_wm + jc] : C[L.c_w3 + jc];
-  const float c2 = actor ? P[L.p_ws + jc] : 0.0f;
-  const float alpha = alpha_of(m), log_alpha = P[0];
+  const float c1 = actor ? hw[jc] : hw[(2 + net) * H + jc];
+  const float c2 = actor ? hw[H + jc] : 0.0f;
+  const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
   const int64_t out_off = actor ? L.p_w2 : L.q_base[net] + L.c_w2;
   AdamElem xe[4];
   f32x16 acc = zero16();
@@ -970,16 +989,15 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
   const bool actor = net == 0, jok = j < H;
   const int jj = jok ? j : H - 1;
   const int cn = actor ? 0 : net - 1;
-  const float* P = m.params;
-  const float* C = P + L.q_base[cn];
+  const float* hw = m.s.snap + SN_HEAD;  // pre-update head weights: wm | ws | w3 Q1 | w3 Q2
   const int nin = actor ? L.O : L.O + 1;
   const float* U1 = actor ? m.s.um : m.s.uq[cn];
   const float* U2 = m.s.us;
   const float* A2 = actor ? m.s.h2 : m.s.g2[cn];
   const float* XR = actor ? m.s.x : m.s.qx;
-  const float c1 = actor ? P[L.p_wm + jj] : C[L.c_w3 + jj];
-  const float c2 = actor ? P[L.p_ws + jj] : 0.0f;
-  const float alpha = alpha_of(m), log_alpha = P[0];
+  const float c1 = actor ? hw[jj] : hw[(2 + cn) * H + jj];
+  const float c2 = actor ? hw[H + jj] : 0.0f;
+  const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
   float w1a[kXLd], b1a = 0.0f, b2a = 0.0f, ha1 = 0.0f, ha2 = 0.0f;
 #pragma unroll
   for (int i = 0; i < kXLd; ++i) w1a[i] = 0.0f;
@@ -1063,8 +1081,7 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   const MArgs& m = a.m;
   const Layout& L = m.L;
   const int B = L.B, Bp = L.Bp, tid = threadIdx.x;
-  const float* P = m.params;
-  const float alpha = alpha_of(m), log_alpha = P[0];
+  const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
   const float invB = 1.0f / (float)B;
   float v[9];
 #pragma unroll
@@ -1441,7 +1458,7 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   SDev g(device);
   const int64_t Bp = L.Bp, BH = Bp * H, CB = H / kTile2;
   // rows 3·16 + 5 + 2, activations 10·H, heads 7, parts (2 + 8)·CB, losses 5
-  const int64_t n_scr = Bp * (3 * kXLd + 5) + 10 * BH + 7 * Bp + 2 * Bp * 2 * CB + PS_N * Bp * CB + 5 * Bp;
+  const int64_t n_scr = Bp * (3 * kXLd + 5) + 10 * BH + 7 * Bp + 2 * Bp * 2 * CB + PS_N * Bp * CB + 5 * Bp + SN_HEAD + 4 * H;
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
     *out = h;
@@ -1471,6 +1488,7 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   sc.hpart = s; s += 2 * Bp * 2 * CB;
   sc.part = s; s += PS_N * Bp * CB;
   sc.loss = s; s += 5 * Bp;
+  sc.snap = s; s += SN_HEAD + 4 * H;
   e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);
   if (e != hipSuccess) {
     *out = h;
