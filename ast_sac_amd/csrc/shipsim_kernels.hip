@@ -1059,6 +1059,11 @@ struct ChainArgs {
   int32_t* log_len;    // [env] records written (counts on past log_cap)
   int32_t log_cap;
   int32_t log_stop;    // an env whose log is full stops for the launch, its next decision pending
+  // work-conserving launch tail (shipsim_set_stream_tail): a wave whose envs met max_ticks keeps ticking in chunks
+  // of kTailChunk while tail_ctr (waves that met it, zeroed per launch) < the grid, up to tail_extra more ticks
+  int32_t* tail_ctr;
+  int32_t tail_extra;
+  int32_t tail_waves;  // waves of the launch (the grid: one wave per block)
   // shipsim_run_policy: actions from the policy instead of the table (policy != null)
   const float* policy;  // TanhGaussianPolicy parameters, torch order (shipsim_policy.params)
   const float* w2t;     // its fc1 weight transposed, [H][H] (shipsim_policy.w2t)
@@ -1451,6 +1456,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   uint32_t out_bits = 0;
   int out_ticks = 0;
   int ticks = 0;
+  int budget = opaque_v(max_ticks);  // this launch's tick quota per env (CHAIN: extended in the launch tail; a VGPR)
+  int tail_arrived = 0;  // this wave counted itself on the tail counter (an int: no lane mask held)
   int n_nonfinite = 0;
 
 #ifdef SHIPSIM_DEBUG_ENV
@@ -1579,6 +1586,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   // recorded and the next one pending (DF_AWAITING): the wave keeps ticking its other envs and the
   // next launch resumes exactly there, so results do not depend on the burst bound.
   constexpr int kChainBurst = 8;
+  constexpr int kTailChunk = 32;  // launch tail: ticks per extension
   // the next action of every env of the wave that needs one (want): the table entry, or the policy's
   // sample (wave-cooperative, shipsim_run_policy). Wave-uniform. sa: the scoping angle to run, a_log:
   // the action as the decision record reports it (the table's angle / the policy's normalized action).
@@ -1658,7 +1666,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     }
   }
 
-  bool going = running && !ready && (max_ticks <= 0 || ticks < max_ticks);
+  bool going = running && !ready && (budget <= 0 || ticks < budget);
 #ifdef SHIPSIM_PHASE_TIMING
   unsigned long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long pt_last = wall_clock64();
@@ -1942,7 +1950,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       const double of[5] = {200000000.0, 175000.0, 1250000.0, 50000.0, 12500.0};
       double ex[5];
       if (LPE >= 8) {
-        const int j = opaque_if<OPQ>(lie) & 7;  // (recomputed in the loop: no lane masks kept across it)
+        const int j = opaque_v(lie) & 7;  // (recomputed in the loop: no lane masks kept across it)
         const double xj = (j == 0) ? xv[0] : (j == 1) ? xv[1] : (j == 2) ? xv[2] : (j == 3) ? xv[3] : xv[4];
         const double tj = (j == 2) ? tg[2] : (j == 4) ? tg[4] : 0.0;
         const double oj = (j == 0) ? of[0] : (j == 1) ? of[1] : (j == 2) ? of[2] : (j == 3) ? of[3] : of[4];
@@ -2043,16 +2051,37 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         snap_bits = bits;
         ready = true;
       }
-      const int mt = OPQ ? step_args().max_ticks : max_ticks;  // (OPQ: its test not held across the loop)
+      const int mt = OPQ ? opaque_v(budget) : budget;  // (OPQ: its test not held across the loop)
       going = !ready && (mt <= 0 || ticks < mt);
     }
     PT_MARK(3);
   }
   if (!CHAIN) break;
   if (POLICY || (ready && running)) chain_next();  // (policy: wave-uniform, a no-op unless a decision completed)
-  const int mt = OPQ ? step_args().max_ticks : max_ticks;
-  going = running && !ready && (mt <= 0 || ticks < mt);
-  if (!__any(going)) break;
+  {
+    const int mt = OPQ ? opaque_v(budget) : budget;
+    going = running && !ready && (mt <= 0 || ticks < mt);
+  }
+  if (!__any(going)) {
+    // Launch tail: this wave's envs met the quota. While any wave of the launch has not, keep ticking in chunks
+    // instead of idling the SIMD until the slowest wave ends (an env's results do not depend on where a launch
+    // ends: slicing is exact). Bounded by tail_extra, so a wave that is not co-resident delays nothing forever.
+    // (One exit, every test wave-uniform: no flow masks held across the loop.)
+    const ChainArgs& CT = step_args().CH;
+    if (SLOTS == 2 && CT.tail_ctr && budget < step_args().max_ticks + CT.tail_extra) {  // (two-ship envs)
+      const bool lead = (opaque_v(threadIdx.x) & 63) == 0;  // (re-derived here: no lane mask held across the loop)
+      if (lead && opaque_v(tail_arrived) == 0)
+        __hip_atomic_fetch_add(CT.tail_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tail_arrived = opaque_v(1);
+      int n_met = 0;
+      if (lead) n_met = __hip_atomic_load(CT.tail_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_readfirstlane(n_met) < CT.tail_waves) {
+        budget += kTailChunk;
+        going = running && !ready && ticks < budget;
+      }
+    }
+    if (!__any(going)) break;  // (quota met, or every env of the wave stalled)
+  }
   }
 #ifdef SHIPSIM_PHASE_TIMING
   if ((threadIdx.x & 63) == 0)
@@ -2351,6 +2380,8 @@ struct shipsim_handle {
   size_t dev_bytes;
   int ever_reset;
   int lpe;  // lanes per AST env of the step / stream kernels (lanes_per_env)
+  int32_t tail_extra;  // shipsim_set_stream_tail (0: off)
+  int32_t* tail_ctr;   // its device counter (one int, zeroed before every stream launch)
   char err[512];
 };
 
@@ -3025,6 +3056,7 @@ int shipsim_destroy(shipsim_handle* h) {
     if (h->const_block) (void)hipFree(h->const_block);
     if (h->fuel_block) (void)hipFree(h->fuel_block);
     if (h->nonfinite_dev) (void)hipFree(h->nonfinite_dev);
+    if (h->tail_ctr) (void)hipFree(h->tail_ctr);
   }
   delete h;
   return SHIPSIM_OK;
@@ -3122,6 +3154,16 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
 
 }  // extern "C"
 
+// the launch tail is used when it is on and every wave of the launch is resident at once (one 64-thread block per
+// wave): a wave that is not resident yet would only start after the resident ones ran their whole extension
+static bool tail_on(const shipsim_handle* h, const void* kern, int blocks) {
+  if (h->tail_extra <= 0 || !h->tail_ctr) return false;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) return false;
+  return (int64_t)blocks <= (int64_t)per_cu * cus;
+}
+
 // the decision-stream launch shared by shipsim_run_table (MODE 1) and shipsim_run_policy (MODE 2)
 template <int MODE>
 static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, int32_t* ticks_out) {
@@ -3130,10 +3172,20 @@ static int run_chain(shipsim_handle* h, const ChainArgs& ch, int32_t max_ticks, 
   // the chip has SIMD slots at 16; identical results)
   const int lpe = (h->lpe == 8 || h->lpe == 4) ? h->lpe : (h->lpe == 2 ? 4 : 16);
   const int threads = 64, blocks = step_blocks(h, lpe);
-#define CHAINED_L(D, CA, LPE)                                                                                          \
-  hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, MODE>), dim3(blocks), dim3(threads), 0, h->stream,        \
-                     step_args_of(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out,     \
-                                  nullptr, ch))
+#define CHAINED_L(D, CA, LPE)                                                                                      \
+  do {                                                                                                             \
+    const void* kern_ = reinterpret_cast<const void*>(&ast_step_kernel<D, CA, LPE, false, MODE>);                 \
+    ChainArgs c_ = ch;                                                                                             \
+    if (tail_on(h, kern_, blocks)) {                                                                               \
+      (void)hipMemsetAsync(h->tail_ctr, 0, sizeof(int32_t), h->stream);                                            \
+      c_.tail_ctr = h->tail_ctr;                                                                                   \
+      c_.tail_extra = h->tail_extra;                                                                               \
+      c_.tail_waves = blocks;                                                                                      \
+    }                                                                                                              \
+    hipLaunchKernelGGL((ast_step_kernel<D, CA, LPE, false, MODE>), dim3(blocks), dim3(threads), 0, h->stream,    \
+                       step_args_of(h, nullptr, nullptr, max_ticks, nullptr, nullptr, nullptr, nullptr, ticks_out, \
+                                    nullptr, c_));                                                                 \
+  } while (0)
 #define CHAINED(D, CA)                              \
   do {                                              \
     if (lpe == 8) CHAINED_L(D, CA, 8);              \
@@ -3214,6 +3266,16 @@ int shipsim_run_policy(shipsim_handle* h, const float* policy, const float* w2t,
   ch.policy = policy; ch.w2t = w2t; ch.pol_obs = obs_dim; ch.pol_hidden = hidden; ch.pol_det = deterministic ? 1 : 0;
   ch.pol_seed = seed; ch.pol_counter = counter;
   return run_chain<2>(h, ch, max_ticks, ticks_out);
+}
+
+int shipsim_set_stream_tail(shipsim_handle* h, int32_t extra_ticks) {
+  if (!h || extra_ticks < 0) return SHIPSIM_EINVAL;
+  if (extra_ticks > 0 && !h->tail_ctr) {
+    DeviceGuard g(h->device);
+    HIPCHK(h, hipMalloc(&h->tail_ctr, sizeof(int32_t)));
+  }
+  h->tail_extra = extra_ticks;
+  return SHIPSIM_OK;
 }
 
 int shipsim_legacy_step(shipsim_handle* h, int32_t k, double* states_out, uint8_t* done_out, uint32_t* status_out) {

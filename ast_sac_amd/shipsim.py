@@ -58,6 +58,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
+    L.shipsim_set_stream_tail.argtypes = [P, C.c_int32]
     try:
         L.shipsim_diag_lane_faults.argtypes = [P]
         L.shipsim_run_policy.argtypes = [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, P, C.c_int32,
@@ -81,7 +82,7 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
                     "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
                     "shipsim_nonfinite_count", "shipsim_lanes_per_env", "shipsim_set_stream",
-                    "shipsim_run_policy", "shipsim_diag_lane_faults")
+                    "shipsim_run_policy", "shipsim_diag_lane_faults", "shipsim_set_stream_tail")
 
 
 def diag_lane_faults():
@@ -197,6 +198,12 @@ class ShipSim:
     def tick(self, k=1):
         self._follow_stream()
         self._check(self.L.shipsim_tick(self.h, int(k), None), "shipsim_tick")
+
+    def set_stream_tail(self, extra_ticks):
+        """Work-conserving launch tail of run_table / run_policy (shipsim_set_stream_tail): a wave whose envs met
+        max_ticks keeps ticking, 32 ticks at a time, while any wave of the launch has not, up to extra_ticks more
+        (0: off). Per-env results are unchanged; only where launches end moves."""
+        self._check(self.L.shipsim_set_stream_tail(self.h, int(extra_ticks)), "shipsim_set_stream_tail")
 
     def run_table(self, table, max_ticks, ep_idx, dec_idx, out=None, log=None, log_len=None):
         """Open-loop decision stream (shipsim_run_table): table (n_eps, n_dec, N) float32 scoping angles

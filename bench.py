@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--obs-ships", type=int, default=1,
                    help="obstacle ships per env (C5 multi-obstacle generalisation; 1 = the reference env)")
     p.add_argument("--lpe", type=int, default=0, help="device lanes per env (0 = library choice from envs per GPU)")
+    p.add_argument("--tail-ticks", type=int, default=1024,
+                   help="table mode: work-conserving launch tail (shipsim_set_stream_tail): waves that met --slice "
+                        "keep ticking while the launch's slowest wave has not, up to this many more ticks (0 = off)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c2", action="store_true", help="skip the configs[1] single-ship secondary line")
@@ -161,10 +164,13 @@ def sac_flops_per_step(B, H, O):
     return 2 * (mac_fwd + mac_bwd + mac_wg)
 
 
-def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
-    """SAC grad-steps/s (secondary metric): FusedSACTrainer HIP-graph step (runner networks: 2x256
-    hidden, batch `batch` per GPU, on-device uniform sampling from a 300k-row DeviceReplayBuffer,
-    RCCL gradient all-reduce when world > 1), beside the reference-order eager SACTrainer."""
+def bench_sac(dev, world, pg, steps, global_batch, eager_steps=40, graph=True, dp_mode="replicated"):
+    """SAC grad-steps/s (secondary metric): FusedSACTrainer HIP-graph step (runner networks: 2x256 hidden, global
+    batch `global_batch`, on-device uniform sampling from a 300k-row DeviceReplayBuffer), beside the reference-order
+    eager SACTrainer. With world > 1: dp_mode "replicated" (the runner's default) runs the whole
+    global batch on every rank over the same buffer rows (the union a ReplicatedReplayBuffer holds: filled here
+    with the same seed on every rank) with no per-step collective; "allreduce" gives each rank global / world rows
+    and all-reduces the flat gradient every step over RCCL (captured in the step's HIP graph)."""
     import torch
     import torch.distributed as dist
     from ast_sac_amd.ast_sac.torch.networks.mlp import ConcatMlp
@@ -184,8 +190,11 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
 
     hp = dict(discount=0.965, soft_target_tau=1e-3, policy_lr=8e-5, qf_lr=8e-5, reward_scale=0.75,
               action_reg_coeff=0.01, clip_val=100.0)
+    replicated = world > 1 and dp_mode == "replicated"
+    batch = global_batch if (world == 1 or replicated) else global_batch // world
     rb = DeviceReplayBuffer(300000, 8, 1, dev)
-    g = torch.Generator(device=dev).manual_seed(1)
+    # rank-specific rows for the all-reduce shape (own shards); the same rows everywhere when replicated
+    g = torch.Generator(device=dev).manual_seed(1 if replicated or world == 1 else 1 + dist.get_rank())
     n = 65536
     rb.add_batch(torch.randn(n, 8, device=dev, generator=g) * 1000, torch.rand(n, 1, device=dev, generator=g) * 2 - 1,
                  torch.randn(n, 1, device=dev, generator=g), torch.randn(n, 8, device=dev, generator=g) * 1000,
@@ -208,7 +217,8 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
     def fused(backend):
         pol, q = nets()
         tr = FusedSACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3],
-                             batch_size=batch, process_group=pg, backend=backend, use_graph=graph, **hp)
+                             batch_size=batch, process_group=pg, backend=backend, use_graph=graph,
+                             replicated=replicated, **hp)
         tr.broadcast_parameters(0)
         tr.train_from_buffer(rb, 10)  # captures the graph
         return timed(lambda k: tr.train_from_buffer(rb, k), steps)
@@ -218,19 +228,29 @@ def bench_sac(dev, world, pg, steps, batch, eager_steps=40, graph=True):
     backend = dist.get_backend(pg) if world > 1 else None
     ar = {"nccl": "RCCL all-reduce", "gloo": "gloo all-reduce (rehearsal, not RCCL)"}.get(backend, f"{backend} all-reduce")
     flops = sac_flops_per_step(batch, H, O)
+    if world == 1:
+        shape = "single rank"
+    elif replicated:
+        shape = (f"replicated x{world}: every rank runs the global-batch step over the same rows, no per-step "
+                 "collective (the runner's default; its per-loop row all-gather is not in this timing)")
+    else:
+        shape = f"gradient all-reduce x{world}: {batch} rows per rank, {ar} of the flat gradient every step"
     res = {"grad_steps_per_s": steps / dt, "ms_per_grad_step": dt / steps * 1e3, "batch_per_gpu": batch,
-           "global_batch": batch * world, "hidden": [H, H], "dtype": "f32", "dist_backend": backend,
-           "impl": "FusedSACTrainer hip backend (csrc/sac_kernels.hip: four MFMA f32 forward/backward GEMM "
-                   "kernels + the MFMA weight-gradient kernel" +
-                   (f", {ar}, Adam/soft-update kernel; HIP graph halves)" if world > 1 else
-                    " with Adam, soft target update and W2T refresh fused in: five launches, HIP graph)"),
+           "global_batch": global_batch, "hidden": [H, H], "dtype": "f32", "dist_backend": backend,
+           "dp_mode": dp_mode if world > 1 else None, "shape": shape,
+           "impl": "FusedSACTrainer hip backend (csrc/sac_kernels.hip: three launches per grad step — forward, "
+                   "critics on the sampled action with the action tangent + backward factors, weight gradients "
+                   "with Adam / soft update / W2T refresh fused in" +
+                   ("; the gradient all-reduce and a separate Adam launch inside the same HIP graph)"
+                    if (world > 1 and not replicated) else "; one HIP graph)"),
            "roofline": {"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_F32_PEAK_TFLOPS,
                         "flops_per_step": flops,
                         "achieved": flops / (dt / steps) / 1e12,
                         "frac": flops / (dt / steps) / 1e12 / MFMA_F32_PEAK_TFLOPS,
                         "note": "algorithmic matrix flops of one grad step (2 per multiply-add: forward, "
-                                "backward and weight-gradient products of every layer, per rank) / whole-step "
-                                "wall time (every launch of the step); v_mfma_f32_32x32x2_f32 dense f32 peak"}}
+                                "backward and weight-gradient products of every layer of the reference's "
+                                "formulation, per rank) / whole-step wall time (every launch of the step); "
+                                "v_mfma_f32_32x32x2_f32 dense f32 peak"}}
     if world == 1 and eager_steps:
         res["torch_ops_graph_grad_steps_per_s"] = steps / fused("torch")
     if world == 1 and eager_steps:
@@ -455,7 +475,9 @@ def main():
     # written to a per-env record ring, as shipsim_step writes its outputs
     # (sized for every decision of a launch: decisions average ~130 ticks at dt 4 s and the measured
     # maximum is ~slice / 76; the largest per-launch count is reported as decision_log.max_per_launch)
-    dlog_cap = max(8, args.slice // 32 + 16)
+    dlog_cap = max(8, (args.slice + max(args.tail_ticks, 0)) // 32 + 16)
+    if args.tail_ticks > 0:  # launches end on the slowest wave's quota, the others tick on meanwhile
+        sim.set_stream_tail(args.tail_ticks)
     dlog = torch.zeros((N, dlog_cap, abi.DECLOG_COLS), dtype=torch.float64, device=dev)
     dlog_len = torch.zeros(N, dtype=torch.int32, device=dev)
     dlog_max = torch.zeros((), dtype=torch.int32, device=dev)
@@ -558,12 +580,15 @@ def main():
     c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
     pstream = (bench_policy_stream(dev, cfg, N, args.slice if args.mode == "table" else 4096)
                if (rank == 0 and not args.no_policy_stream and args.obs_ships == 1) else None)
-    sac = None
+    sac = sac_ar = None
     if args.sac_steps > 0:
         if args.sac_global_batch % world:
             raise SystemExit(f"--sac-global-batch {args.sac_global_batch} is not a multiple of {world} ranks")
-        sac = bench_sac(dev, world, dist.group.WORLD if world > 1 else None, args.sac_steps,
-                        args.sac_global_batch // world)
+        pgw = dist.group.WORLD if world > 1 else None
+        sac = bench_sac(dev, world, pgw, args.sac_steps, args.sac_global_batch, dp_mode="replicated")
+        if world > 1:  # the alternative data-parallel shape, for DESIGN.md §6's comparison
+            sac_ar = bench_sac(dev, world, pgw, args.sac_steps, args.sac_global_batch, eager_steps=0,
+                               dp_mode="allreduce")
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure
@@ -589,7 +614,7 @@ def main():
                        "obs_ships": args.obs_ships,
                        "envs_per_gpu": N, "global_envs": N * world, "collav": args.collav,
                        "machinery": args.machinery, "slice_ticks": args.slice, "lanes_per_env": sim.lanes_per_env,
-                       "mode": args.mode,
+                       "mode": args.mode, "tail_ticks": args.tail_ticks if args.mode == "table" else 0,
                        "parallelism": f"env-shard x{world}" + (f" on {n_devices} device(s), {args.dist_backend}"
                                                                   if n_devices != world else "")},
             "decisions_per_s": all_dec / elapsed,
@@ -603,6 +628,7 @@ def main():
                          "launches": int(len(all_ms)), "fp64_valu": fp64_valu},
             "cpu_baseline": cpu,
             "sac": sac,
+            "sac_allreduce": sac_ar,
             "c2_single_ship": c2,
             "policy_stream": pstream,
         }

@@ -419,6 +419,14 @@ int shipsim_run_policy(shipsim_handle* h, const float* policy, const float* w2t,
                        int32_t max_ticks, int32_t* ep_idx, int32_t* dec_idx, int32_t* ticks_out,
                        int32_t* decisions_out, double* log, int32_t log_cap, int32_t* log_len);
 
+/* Work-conserving launch tail of the decision streams (shipsim_run_table / shipsim_run_policy; ABI 8): a wave
+ * whose envs all met max_ticks keeps ticking, 32 ticks at a time, while any wave of the same launch has not, up to
+ * extra_ticks more (0, the default: off). Per-env results do not change (a decision stream is exact whatever its
+ * launch boundaries); ticks_out / decisions_out then exceed max_ticks by up to extra_ticks for the envs of the
+ * faster waves. Used only when every wave of the launch is resident at once (otherwise the launch runs as with 0),
+ * and for one obstacle ship per env (the K > 1 streams run as with 0). */
+int shipsim_set_stream_tail(shipsim_handle* h, int32_t extra_ticks);
+
 /* ---- legacy per-tick MultiShipEnv (rl_env/ship_in_transit/env.py:783-1181) ----
  * AST kind. Each of the k ticks is one MultiShipEnv.step() (:1104-1173) of every env: test_step
  * (:923-1023, SBMPC / simple collision avoidance as configured) + obs_step (:1025-1102) +

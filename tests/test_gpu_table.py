@@ -120,3 +120,40 @@ def test_stream_envs_per_wave_bitwise(collav, epw):
     assert t_got == t_ref
     for i in range(N):
         np.testing.assert_array_equal(got[i], ref[i], err_msg=f"{collav} epw {epw} env {i}")
+
+
+@pytest.mark.parametrize("collav", ["sbmpc", "none"])
+def test_stream_launch_tail_keeps_every_record(collav):
+    """The work-conserving launch tail (shipsim_set_stream_tail): waves that met max_ticks tick on while the
+    launch's slowest wave has not. Launch boundaries move, results do not: every env's decision records equal
+    the fixed-length launches' record for record (the common prefix), and no env ticks past max_ticks + extra."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    cfg = abi.ast_config(collav)
+    N, T, X, calls = 512, 200, 256, 5
+    table = _table(2, cfg.max_sampling_frequency, N, seed=5)
+    ref, _ = _chained(cfg, N, table, T, calls, cap=256)
+    sim = ShipSim(cfg, N)
+    sim.reset()
+    sim.set_stream_tail(X)
+    ep = torch.zeros(N, dtype=torch.int32, device="cuda")
+    dec = torch.zeros(N, dtype=torch.int32, device="cuda")
+    log = torch.zeros((N, 256, abi.DECLOG_COLS), dtype=torch.float64, device="cuda")
+    log_len = torch.zeros(N, dtype=torch.int32, device="cuda")
+    over = 0
+    for _ in range(calls):
+        o = sim.run_table(table, T, ep, dec, log=log, log_len=log_len)
+        assert int(o["ticks"].max()) <= T + X
+        over += int((o["ticks"] > T).sum())
+    ln = log_len.cpu().numpy()
+    assert ln.max() <= 256
+    L = log.cpu().numpy()
+    keep = [abi.DL_REWARD, abi.DL_EVENTS, abi.DL_DONE, abi.DL_EPISODE, abi.DL_DECISION] + \
+        list(range(abi.DL_OBS, abi.DL_OBS + 8))
+    sim.close()
+    for i in range(N):
+        got = L[i, :ln[i]][:, keep]
+        n = min(len(got), len(ref[i]))
+        assert len(got) >= len(ref[i]) and n > 0
+        np.testing.assert_array_equal(got[:n], ref[i][:n], err_msg=f"{collav} env {i}")
+    print(f"\n[launch tail {collav}] env-launches past max_ticks: {over} of {N * calls}")

@@ -10,7 +10,6 @@ torch and checked against autograd of the reference losses (sac.py:156-270) — 
 import numpy as np
 import torch
 
-torch.set_default_dtype(torch.float64)
 LOG2 = float(np.log(2.0))
 
 
@@ -126,6 +125,15 @@ def _three_pass(pol, qs, log_alpha, b, eps, hp):
 
 
 def test_three_pass_gradients_equal_autograd():
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)  # (restored below: other tests build float32 buffers)
+    try:
+        _check_three_pass()
+    finally:
+        torch.set_default_dtype(prev)
+
+
+def _check_three_pass():
     gen = torch.Generator().manual_seed(4)
     H, O, B = 48, 8, 37
     pol, qs = _nets(H, O, gen)
