@@ -410,6 +410,11 @@ def rank_layout(args, torch):
     return world, rank, local
 
 
+def progress(msg):
+    """A phase line on stderr (the GPU box takes a run silent for minutes to be hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -511,6 +516,7 @@ def main():
         ep_idx.add_(end.long())
         sim.reset(mask=end.to(torch.uint8), obs_out=obs_reset)
 
+    progress("headline stream: warmup + timed launches")
     sim.reset(obs_out=obs_reset)
     for i in range(args.warmup):
         one_step(args.steps + i)
@@ -577,9 +583,12 @@ def main():
                                  "instructions) per launch / this run's mean launch time: the FP64 VALU rate the "
                                  "kernel issues; 'distinct' counts each ship's chain once (its LPE/2 sub-lanes "
                                  "repeat it)"}
+    progress("c2 single ships")
     c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
+    progress("policy stream")
     pstream = (bench_policy_stream(dev, cfg, N, args.slice if args.mode == "table" else 4096)
                if (rank == 0 and not args.no_policy_stream and args.obs_ships == 1) else None)
+    progress("sac")
     sac = sac_ar = None
     if args.sac_steps > 0:
         if args.sac_global_batch % world:
@@ -592,6 +601,7 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure
+            progress("cpu baseline")
             cpu = cpu_baseline(cfg, args.cpu_baseline_seconds, host_threads()[0], N)
         line = {
             "metric": "batched env-steps/sec (two-ship AST)",

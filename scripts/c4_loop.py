@@ -24,6 +24,10 @@ from ast_sac_amd.ast_sac.torch.utils import pytorch_util as ptu  # noqa: E402
 from ast_sac_amd.run.ast_sac_runner import experiment_device, make_variant, parse_cli_args  # noqa: E402
 
 
+def progress(msg):
+    print(f"[c4 {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     n_envs = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
     args = parse_cli_args(["--n_envs", str(n_envs), "--do_logging", "False", "--seed", "0"])
@@ -67,6 +71,7 @@ def main():
             s0, k0 = counters()
             _, t = timed(lambda: coll.collect(32 * n_envs, rb))
             s1, k1 = counters()
+            progress(f"collect {'fused' if fused else 'sliced'} {sl}")
             res[f"collect_{'fused' if fused else 'sliced'}{sl}"] = dict(
                 decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
                 env_ticks_per_s=(k1 - k0) / t)
@@ -76,6 +81,7 @@ def main():
     n_sac = 2400
     _, t = timed(lambda: tr.train_from_buffer(rb, n_sac))
     res["sac"] = dict(grad_steps=n_sac, seconds=t, grad_steps_per_s=n_sac / t)
+    progress(f"sac {n_sac / t:.0f} grad steps/s")
     # the runner's train loop as configured
     loops = 20
     s0, k0 = counters()
