@@ -69,25 +69,25 @@ struct Hyper {
   float inv_world;
 };
 
-// per-row parts (one per 32-column block, in block order) of the head dot products, [set][Bp][CB]
+// per-row parts (one per 32-column block, in block order) of the head dot products, [Bp][set][CB]: a row's
+// sets are contiguous, so a reader's set offsets are compile-time constants off one row address
 enum { PS_Q1D, PS_Q2D, PS_T1, PS_T2, PS_Q1A, PS_Q2A, PS_D1, PS_D2, PS_N };
-enum { HD_MEAN, HD_LSRAW, HD_STD, HD_Z, HD_A, HD_LOGP };
+// the per-row record [Bp][kRec]: the obs row's actor head (HD_*: mean, ls_raw, std, z, a, logp), its two
+// reparameterisation normals, the replayed reward / terminal / action and log π(ã'|s') of the next_obs row
+enum { HD_MEAN, HD_LSRAW, HD_STD, HD_Z, HD_A, HD_LOGP, R_EPS, R_EPSN, R_REW, R_TERM, R_ACT, R_LOGPN };
+constexpr int kRec = 16;
 
 // library-owned activations, all [Bp][...] (row pitch H unless stated)
 struct Scr {
   float *x, *xn;             // gathered obs / next_obs rows [Bp][kXLd]
   float *qx;                 // critic data rows (obs | a) [Bp][kXLd]
-  float *act, *rew, *term;   // [Bp]
-  float *eps;                // [2][Bp]: obs rows | next_obs rows
   float *h1, *h2;            // actor on the obs rows
   float *g1[2], *g2[2];      // Q1 / Q2 on the (obs, a) rows
   float *um, *us;            // actor backward factors
   float *uq[2];              // critic backward factors (data rows)
-  float *hd;                 // [6][Bp] head of the obs rows: mean, ls_raw, std, z, a, logp
-  float *logpn;              // [Bp] log π(ã'|s') of the next_obs rows
+  float *rec;                // [Bp][kRec] per-row record (HD_* / R_*)
   float *hpart;              // [2Bp][2][CB] actor head parts (mean | log_std) of the obs and next_obs rows
-  float *part;               // [PS_N][Bp][CB]
-  float *loss;               // [5][Bp] per-row loss terms (scalar block)
+  float *part;               // [Bp][PS_N][CB]
   // the parameters P3 reads, as they were before this step's update (P3 updates them in place with fused Adam,
   // so its blocks must not read the live values): [log α, b3 Q1, b3 Q2, b3 T1, b3 T2, -, -, -] then
   // wm [H], ws [H], w3 Q1 [H], w3 Q2 [H]
@@ -325,6 +325,18 @@ __device__ __forceinline__ void store_slice(float* base, int r0, int by, const f
   for (int q = 0; q < CS / 4; ++q) d[q] = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
 }
 
+// a batch row's O inputs, zero past O, branch-free: a clamped index and a compare against O held in a VGPR, so
+// no per-input lane mask is kept live (at H > 256 those masks spilled)
+__device__ __forceinline__ void load_obs_row(const float* src, int64_t idx, int O, float (&x)[kXLd]) {
+  int Ov = O;
+  asm volatile("" : "+v"(Ov));
+#pragma unroll
+  for (int m = 0; m < kXLd; ++m) {
+    const float v = src[idx * O + min(m, Ov - 1)];
+    x[m] = m < Ov ? v : 0.0f;
+  }
+}
+
 // LDS of the forward kernels (P1, P2, policy act): two split-K regions, W1ᵀ | b1, the tile's input rows
 template <int H>
 struct FwdLds {
@@ -410,8 +422,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   const int64_t idx = batch_item(a, item, e0, e1);
   const float* src = nrow ? a.nobs : a.obs;
   float x[kXLd];
-#pragma unroll
-  for (int m = 0; m < kXLd; ++m) x[m] = m < O ? src[idx * O + m] : 0.0f;
+  load_obs_row(src, idx, O, x);
   float bv[CS];
   load_b<CS>(bv, a.T, H, kb, c0 + rl);  // actor W2ᵀ, chunk 0
   const float b2c = P[L.p_b2 + c0 + rl];
@@ -421,19 +432,19 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
   if (w == 0 && h == 0) {
 #pragma unroll
-    for (int m = 0; m < kXLd; ++m)
-      if (m < O) lx[rl * (kXLd + 1) + m] = x[m];
+    for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = x[m];  // (zero past O: no per-m mask kept live)
   }
   if (by == 0 && w == 0 && h == 0) {  // the gathered batch for the later passes
     float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) xd[m] = x[m];
     if (!nrow) {
-      a.s.act[item] = a.act[idx];
-      a.s.rew[item] = a.rew[idx];
-      a.s.term[item] = a.term[idx];
-      a.s.eps[item] = e0;
-      a.s.eps[Bp + item] = e1;
+      float* rc = a.s.rec + (int64_t)item * kRec;
+      rc[R_ACT] = a.act[idx];
+      rc[R_REW] = a.rew[idx];
+      rc[R_TERM] = a.term[idx];
+      rc[R_EPS] = e0;
+      rc[R_EPSN] = e1;
     }
   }
   (void)B;
@@ -477,8 +488,7 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   float e0, e1;
   const int64_t idx = batch_item(a, item, e0, e1);
   float xin[kXLd];
-#pragma unroll
-  for (int m = 0; m < kXLd; ++m) xin[m] = m < O ? a.obs[idx * O + m] : 0.0f;
+  load_obs_row(a.obs, idx, O, xin);
   const float act = a.act[idx];
   float bv[CS];
   const float* WT = a.T + (int64_t)(1 + net) * H * H;
@@ -489,12 +499,11 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   stage_w1t<H>(lw1, C + L.c_w1, C + L.c_b1, O + 1);
   if (w == 0 && h == 0) {
 #pragma unroll
-    for (int m = 0; m < kXLd; ++m)
-      if (m < O) lx[rl * (kXLd + 1) + m] = xin[m];
+    for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
     lx[rl * (kXLd + 1) + O] = act;
     if (net == 0 && by == 0)
 #pragma unroll
-      for (int m = 0; m < kXLd; ++m) a.s.qx[(int64_t)item * kXLd + m] = m < O ? xin[m] : (m == O ? act : 0.0f);
+      for (int m = 0; m < kXLd; ++m) a.s.qx[(int64_t)item * kXLd + m] = m == O ? act : xin[m];
   }
   __syncthreads();
   f32x16 acc = zero16();
@@ -512,7 +521,7 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
     const float y = relu(v + b2c);
     a.s.g2[net][(int64_t)r * H + col] = y;
     const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
-    if (cc == 0) a.s.part[((int64_t)(PS_Q1D + net) * Bp + r) * CB + by] = pq;
+    if (cc == 0) a.s.part[((int64_t)r * PS_N + PS_Q1D + net) * CB + by] = pq;
   });
 }
 
@@ -556,7 +565,7 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   const int item = r0 + rl;
   float xin[kXLd];
   load_run<kXLd>((kTarget ? a.s.xn : a.s.x) + (int64_t)item * kXLd, xin);
-  const float ev = a.s.eps[(kTarget ? Bp : 0) + item];
+  const float ev = a.s.rec[(int64_t)item * kRec + (kTarget ? R_EPSN : R_EPS)];
   float bv[CS];
   const float* WT = a.T + (int64_t)((kTarget ? 3 : 1) + net) * H * H;
   load_b<CS>(bv, WT, H, kb, c0 + rl);
@@ -568,15 +577,15 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   row_head<CB>(a, (kTarget ? Bp : 0) + item, ev, hd);
   if (w == 0 && h == 0) {
 #pragma unroll
-    for (int m = 0; m < kXLd; ++m)
-      if (m < O) lx[rl * (kXLd + 1) + m] = xin[m];
+    for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
     lx[rl * (kXLd + 1) + O] = hd[HD_A];
     if (net == 0 && by == 0) {
+      float* rc = a.s.rec + (int64_t)item * kRec;
       if (kTarget) {
-        a.s.logpn[item] = hd[HD_LOGP];
+        rc[R_LOGPN] = hd[HD_LOGP];
       } else {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) a.s.hd[(int64_t)q * Bp + item] = hd[q];
+        for (int q = 0; q < 6; ++q) rc[q] = hd[q];
       }
     }
   }
@@ -602,13 +611,13 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
     const float y = relu(v + b2c);
     gm[q] = y > 0.0f;
     const float pq = halfwave_sum(y * w3);
-    if (cc == 0) a.s.part[((int64_t)((kTarget ? PS_T1 : PS_Q1A) + net) * Bp + r) * CB + by] = pq;
+    if (cc == 0) a.s.part[((int64_t)r * PS_N + (kTarget ? PS_T1 : PS_Q1A) + net) * CB + by] = pq;
   });
   if constexpr (!kTarget) {
     splitk_finish(act, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v) {
       const int r = r0 + rr;
       const float pd = halfwave_sum(gm[q] ? w3 * v : 0.0f);  // this column block's part of ∂Q/∂ã
-      if (cc == 0) a.s.part[((int64_t)(PS_D1 + net) * Bp + r) * CB + by] = pd;
+      if (cc == 0) a.s.part[((int64_t)r * PS_N + PS_D1 + net) * CB + by] = pd;
     });
   }
 }
@@ -716,16 +725,15 @@ struct CriticRow {
 };
 template <int CB>
 __device__ __forceinline__ CriticRow critic_row(const MArgs& a, int r, float alpha) {
-  const Layout& L = a.L;
-  const int64_t Bp = L.Bp;
-  const float* pt = a.s.part;
+  const float* pt = a.s.part + (int64_t)r * PS_N * CB;
   float p0[CB], p1[CB], p2[CB], p3[CB];
-  load_run<CB>(pt + ((int64_t)PS_Q1D * Bp + r) * CB, p0);
-  load_run<CB>(pt + ((int64_t)PS_Q2D * Bp + r) * CB, p1);
-  load_run<CB>(pt + ((int64_t)PS_T1 * Bp + r) * CB, p2);
-  load_run<CB>(pt + ((int64_t)PS_T2 * Bp + r) * CB, p3);
+  load_run<CB>(pt + PS_Q1D * CB, p0);
+  load_run<CB>(pt + PS_Q2D * CB, p1);
+  load_run<CB>(pt + PS_T1 * CB, p2);
+  load_run<CB>(pt + PS_T2 * CB, p3);
   const float* sn = a.s.snap;  // (the pre-update biases: P3 updates the live ones)
-  const float logpn = a.s.logpn[r], rw = a.s.rew[r], tm = a.s.term[r];
+  const float* rc = a.s.rec + (int64_t)r * kRec;
+  const float logpn = rc[R_LOGPN], rw = rc[R_REW], tm = rc[R_TERM];
   CriticRow o;
   o.q1 = fold(p0) + sn[SN_BQ1];
   o.q2 = fold(p1) + sn[SN_BQ2];
@@ -746,17 +754,17 @@ struct ActorRow {
 template <int CB>
 __device__ __forceinline__ ActorRow actor_row(const MArgs& a, int r, float alpha, float log_alpha) {
   const Layout& L = a.L;
-  const int64_t Bp = L.Bp;
-  const float* pt = a.s.part;
+  const float* pt = a.s.part + (int64_t)r * PS_N * CB;
   float p4[CB], p5[CB], p6[CB], p7[CB];
-  load_run<CB>(pt + ((int64_t)PS_Q1A * Bp + r) * CB, p4);
-  load_run<CB>(pt + ((int64_t)PS_Q2A * Bp + r) * CB, p5);
-  load_run<CB>(pt + ((int64_t)PS_D1 * Bp + r) * CB, p6);
-  load_run<CB>(pt + ((int64_t)PS_D2 * Bp + r) * CB, p7);
-  const float* hd = a.s.hd;
-  const float mean = hd[HD_MEAN * Bp + r], ls_raw = hd[HD_LSRAW * Bp + r], std = hd[HD_STD * Bp + r];
-  const float z = hd[HD_Z * Bp + r], act = hd[HD_A * Bp + r], logp = hd[HD_LOGP * Bp + r];
-  const float eps_i = a.s.eps[r];
+  load_run<CB>(pt + PS_Q1A * CB, p4);
+  load_run<CB>(pt + PS_Q2A * CB, p5);
+  load_run<CB>(pt + PS_D1 * CB, p6);
+  load_run<CB>(pt + PS_D2 * CB, p7);
+  float rc[kRec];
+  load_run<kRec>(a.s.rec + (int64_t)r * kRec, rc);
+  const float mean = rc[HD_MEAN], ls_raw = rc[HD_LSRAW], std = rc[HD_STD];
+  const float z = rc[HD_Z], act = rc[HD_A], logp = rc[HD_LOGP];
+  const float eps_i = rc[R_EPS];
   const float* sn = a.s.snap;
   const float q1a = fold(p4) + sn[SN_BQ1];
   const float q2a = fold(p5) + sn[SN_BQ2];
@@ -798,33 +806,31 @@ struct ApplyArgs {
   int n_tile_blocks;  // blocks [0, n_tile_blocks) take 32x32 tiles of the three H x H W2 matrices
 };
 
-// one element: loads (ld) and update/stores (st) split so several elements' loads are in flight first
+// one element: loads (ld) and update/stores (st) split so several elements' loads are in flight first. q: the
+// element is a critic's (lr_q, and a soft-updated target) — the caller knows it (a block's elements share it)
 struct AdamElem {
   float g, m, v, p, t;
-  bool q;
 };
-__device__ __forceinline__ AdamElem adam_ld(const ApplyArgs& a, int64_t e, bool with_g = true) {
-  const Layout& L = a.L;
+__device__ __forceinline__ AdamElem adam_ld(const ApplyArgs& a, int64_t e, bool q, bool with_g = true) {
   AdamElem x;
-  x.q = e >= L.q_base[0];
   x.g = with_g ? a.grads[e] : 0.0f;
   x.m = a.m[e];
   x.v = a.v[e];
   x.p = a.params[e];
-  x.t = x.q ? a.targets[e - L.q_base[0]] : 0.0f;
+  x.t = q ? a.targets[e - a.L.q_base[0]] : 0.0f;
   return x;
 }
-__device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, int64_t e, AdamElem& x) {
+__device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, int64_t e, AdamElem& x, bool q) {
   const float g = x.g * a.hp.inv_world;
   const float m = x.m + (1.0f - a.hp.beta1) * (g - x.m);              // exp_avg.lerp_(grad, 1 - beta1)
   const float v = x.v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);   // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
   const float denom = sqrtf(v) / st.bc2_sqrt + a.hp.eps;
-  const float p = x.p + (-(x.q ? st.step_q : st.step_pi)) * (m / denom);
+  const float p = x.p + (-(q ? st.step_q : st.step_pi)) * (m / denom);
   a.m[e] = m;
   a.v[e] = v;
   a.params[e] = p;
   x.p = p;
-  if (x.q) {
+  if (q) {
     x.t = x.t * (1.0f - a.hp.tau) + p * a.hp.tau;
     a.targets[e - a.L.q_base[0]] = x.t;
   }
@@ -839,6 +845,12 @@ struct WArgs {
   int fuse;   // single process: each block also applies Adam / soft update / W2ᵀ to the elements it finished
   int n_mfma, n_valu;
   ApplyArgs ap;
+  // per H x H matrix (0 actor, 1 / 2 Q1 / Q2): the MFMA tiles' operands and output offset, indexed (one scalar
+  // load) rather than selected between fields (a live mask and both candidates across the GEMM loop)
+  const float* dy_src[3];  // h2 | g2 Q1 | g2 Q2
+  const float* x_src[3];   // h1 | g1 Q1 | g1 Q2
+  int64_t w2_off[3];       // the W2 block in params (and grads, Adam state)
+  int hw_off[3];           // the first head-weight row in snap's SN_HEAD block: wm | w3 Q1 | w3 Q2
 };
 
 constexpr int kRowChunk = 256;  // rows whose scalars a block holds at once (one per thread)
@@ -866,13 +878,10 @@ __device__ __forceinline__ float alpha_of(const MArgs& a) {
 // MFMA tile of dW2 for matrix mat (0 actor, 1 / 2 Q1 / Q2): out[j][k] = Σ_r dY[r][j] X[r][k] with
 //   actor  dY = [h2 > 0] ⊙ (wm dmean + ws dls), X = h1;   critic  dY = [g2 > 0] ⊙ w3 dq, X = g1
 template <int H>
-__device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
+__device__ __forceinline__ void mfma_tile_of(int bx, int& mat, int& j0, int& k0) {
   constexpr int CB = H / kTile2, tiles = CB * CB;
-  const MArgs& m = a.m;
-  const Layout& L = m.L;
-  const int B = L.B, Bp = L.Bp;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5, rl = lane & 31;
-  int mat = bx / tiles, t = bx % tiles;
+  mat = bx / tiles;
+  int t = bx % tiles;
   if constexpr (CB == 8) {
     // XCD-aware (64 tiles per matrix, 24 per XCD): XCD x = bx mod 8 takes, of each matrix, the 2 x 4 tiles of row
     // blocks 2(x / 2) + {0, 1} and column blocks 4(x mod 2) + {0..3}, so its L2 fetches a quarter of dYᵀ's
@@ -881,18 +890,34 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     mat = sl >> 3;
     t = ((x >> 1) * 2 + (tt >> 2)) * 8 + (x & 1) * 4 + (tt & 3);
   }
-  const int j0 = (t / CB) * kTile2, k0 = (t % CB) * kTile2;
+  j0 = (t / CB) * kTile2;
+  k0 = (t % CB) * kTile2;
+}
+
+template <int H>
+__device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
+  constexpr int CB = H / kTile2;
+  const MArgs& m = a.m;
+  const Layout& L = m.L;
+  const int B = L.B, Bp = L.Bp;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5, rl = lane & 31;
+  int mat, j0, k0;
+  mfma_tile_of<H>(bx, mat, j0, k0);
   const bool actor = mat == 0;
   const int net = actor ? 0 : mat - 1;
   const float* hw = m.s.snap + SN_HEAD;  // pre-update head weights: wm | ws | w3 Q1 | w3 Q2
-  const gptr Y = as_global(actor ? m.s.h2 : m.s.g2[net]);
-  const gptr X = as_global(actor ? m.s.h1 : m.s.g1[net]);
+  const gptr Y = as_global(a.dy_src[mat]);
+  const gptr X = as_global(a.x_src[mat]);
   const int jc = j0 + rl;
-  const float c1 = actor ? hw[jc] : hw[(2 + net) * H + jc];
+  const float c1 = hw[a.hw_off[mat] + jc];
   const float c2 = actor ? hw[H + jc] : 0.0f;
   const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
-  const int64_t out_off = actor ? L.p_w2 : L.q_base[net] + L.c_w2;
-  AdamElem xe[4];
+  const int64_t out_off = a.w2_off[mat];
+  AdamElem xe[4];  // the optimizer state of the four outputs this lane finishes, in flight during the GEMM
+  if (a.fuse)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      xe[q] = adam_ld(a.ap, out_off + (int64_t)(j0 + finish_row(q)) * H + k0 + rl, !actor, false);
   f32x16 acc = zero16();
   for (int rc = 0; rc < Bp; rc += kRowChunk) {
     const int nrow = min(kRowChunk, Bp - rc);
@@ -943,21 +968,22 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
       const float d = actor ? c1 * S.s0[rl0 + i] + c2 * S.s1[rl0 + i] : c1 * S.s0[rl0 + i];
       av[i] = yv[i] > 0.0f ? d : 0.0f;
     }
-    // the optimizer state of the four outputs this lane finishes, in flight during the GEMM
-    if (rc == 0 && a.fuse)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        xe[q] = adam_ld(a.ap, out_off + (int64_t)(j0 + finish_row(q)) * H + k0 + rl, false);
     mfma_chain(acc, av, xv, n2);
     if (rc + kRowChunk < Bp) __syncthreads();  // S.s0 / s1 reused
   }
   auto& tt = S.u.mm.tt;
+  {
+  // the tile's coordinates again, from an opaque block id: recomputed here rather than held across the loop
+  int bxe = (int)blockIdx.x;
+  asm volatile("" : "+s"(bxe));
+  mfma_tile_of<H>(bxe, mat, j0, k0);
+  const int64_t out_off = a.w2_off[mat];
   splitk_finish(acc, S.u.mm.split, [&](int q, int rr, int cc, float v) {
     const int64_t e = out_off + (int64_t)(j0 + rr) * H + k0 + cc;
     a.grads[e] = v;
     if (a.fuse) {
       xe[q].g = v;
-      adam_st(a.ap, S.sst, e, xe[q]);
+      adam_st(a.ap, S.sst, e, xe[q], mat > 0);
       tt[0][cc][rr] = xe[q].p;
       tt[1][cc][rr] = xe[q].t;
     }
@@ -971,6 +997,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
       a.ap.T[(size_t)mat * HH + o] = tt[0][cc][tc];
       if (mat > 0) a.ap.T[(size_t)(2 + mat) * HH + o] = tt[1][cc][tc];
     }
+  }
   }
 }
 
@@ -1060,9 +1087,9 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
   auto emit = [&](int64_t e, float g) {
     a.grads[e] = g;
     if (a.fuse) {
-      AdamElem x = adam_ld(a.ap, e, false);
+      AdamElem x = adam_ld(a.ap, e, !actor, false);
       x.g = g;
-      adam_st(a.ap, S.sst, e, x);
+      adam_st(a.ap, S.sst, e, x, !actor);
     }
   };
   const int64_t base = actor ? 0 : L.q_base[cn];
@@ -1122,9 +1149,9 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   for (int i = 0; i < 5; ++i) {
     a.grads[off[i]] = g[i];
     if (a.fuse && (i > 0 || m.hp.auto_ent)) {
-      AdamElem x = adam_ld(a.ap, off[i], false);
+      AdamElem x = adam_ld(a.ap, off[i], i >= 3, false);
       x.g = g[i];
-      adam_st(a.ap, S.sst, off[i], x);
+      adam_st(a.ap, S.sst, off[i], x, i >= 3);
     }
   }
 }
@@ -1168,11 +1195,11 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
     const int tc = threadIdx.x % kTile2, tr = threadIdx.x / kTile2;  // 8 rows per pass
     AdamElem x[kPer];
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) x[u] = adam_ld(a, w2[mat] + (int64_t)(r0 + tr + u * 8) * H + c0 + tc);
+    for (int u = 0; u < kPer; ++u) x[u] = adam_ld(a, w2[mat] + (int64_t)(r0 + tr + u * 8) * H + c0 + tc, mat > 0);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int rr = tr + u * 8;
-      adam_st(a, st, w2[mat] + (int64_t)(r0 + rr) * H + c0 + tc, x[u]);
+      adam_st(a, st, w2[mat] + (int64_t)(r0 + rr) * H + c0 + tc, x[u], mat > 0);
       tile[0][tc][rr] = x[u].p;
       tile[1][tc][rr] = x[u].t;
     }
@@ -1196,8 +1223,9 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
     if (e >= w2[k]) e += HH;
   if (e >= L.n_params) return;
   if (e == 0 && !a.hp.auto_ent) return;
-  AdamElem x = adam_ld(a, e);
-  adam_st(a, st, e, x);
+  const bool q = e >= L.q_base[0];
+  AdamElem x = adam_ld(a, e, q);
+  adam_st(a, st, e, x, q);
 }
 
 __global__ void sac_transpose_kernel(const float* params, const float* targets, float* T, Layout L) {
@@ -1335,6 +1363,11 @@ void launch_act(const ActArgs& a, hipStream_t st) {
 // F(std::integral_constant<int, H>) for the handle's hidden width; false if none is compiled
 template <class F>
 bool with_hidden(int H, F&& f) {
+#ifdef SACF_REGCHECK_H  // register-report builds of one width (scripts/regcheck.sh sac H)
+  if (H != SACF_REGCHECK_H) return false;
+  f(std::integral_constant<int, SACF_REGCHECK_H>{});
+  return true;
+#else
   switch (H) {
 #define SACF_H(h) \
   case h: f(std::integral_constant<int, h>{}); return true;
@@ -1343,6 +1376,7 @@ bool with_hidden(int H, F&& f) {
 #undef SACF_H
     default: return false;
   }
+#endif
 }
 
 }  // namespace
@@ -1457,8 +1491,8 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
 
   SDev g(device);
   const int64_t Bp = L.Bp, BH = Bp * H, CB = H / kTile2;
-  // rows 3·16 + 5 + 2, activations 10·H, heads 7, parts (2 + 8)·CB, losses 5
-  const int64_t n_scr = Bp * (3 * kXLd + 5) + 10 * BH + 7 * Bp + 2 * Bp * 2 * CB + PS_N * Bp * CB + 5 * Bp + SN_HEAD + 4 * H;
+  // rows 3·16, activations 10·H, the row record, parts (2 + 8)·CB, the snapshot
+  const int64_t n_scr = Bp * 3 * kXLd + 10 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H;
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
     *out = h;
@@ -1470,10 +1504,6 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   sc.x = s; s += Bp * kXLd;
   sc.xn = s; s += Bp * kXLd;
   sc.qx = s; s += Bp * kXLd;
-  sc.act = s; s += Bp;
-  sc.rew = s; s += Bp;
-  sc.term = s; s += Bp;
-  sc.eps = s; s += 2 * Bp;
   sc.h1 = s; s += BH;
   sc.h2 = s; s += BH;
   sc.um = s; s += BH;
@@ -1483,11 +1513,9 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
     sc.g2[k] = s; s += BH;
     sc.uq[k] = s; s += BH;
   }
-  sc.hd = s; s += 6 * Bp;
-  sc.logpn = s; s += Bp;
+  sc.rec = s; s += Bp * kRec;
   sc.hpart = s; s += 2 * Bp * 2 * CB;
   sc.part = s; s += PS_N * Bp * CB;
-  sc.loss = s; s += 5 * Bp;
   sc.snap = s; s += SN_HEAD + 4 * H;
   e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);
   if (e != hipSuccess) {
@@ -1609,6 +1637,13 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   const int CB = h->L.H / kTile2;
   w.n_mfma = 3 * CB * CB;
   w.n_valu = 3 * ((h->L.H + 63) / 64);
+  const Layout& L = h->L;
+  for (int mat = 0; mat < 3; ++mat) {
+    w.dy_src[mat] = mat == 0 ? h->s.h2 : h->s.g2[mat - 1];
+    w.x_src[mat] = mat == 0 ? h->s.h1 : h->s.g1[mat - 1];
+    w.w2_off[mat] = mat == 0 ? L.p_w2 : L.q_base[mat - 1] + L.c_w2;
+    w.hw_off[mat] = mat == 0 ? 0 : (mat + 1) * L.H;
+  }
   SDev g(h->device);
   if (!with_hidden(h->L.H, [&](auto hc) { launch_step<decltype(hc)::value>(a, w, h->stream); }))
     return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);

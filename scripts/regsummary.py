@@ -14,6 +14,6 @@ for line in open(sys.argv[1]):
     if m and cur:
         rows[cur][m.group(1).strip()] = int(m.group(2))
 for k, v in rows.items():
-    dn = subprocess.run(["c++filt", k], capture_output=True, text=True).stdout.strip().split("(")[0]
-    print(f"{dn:58s} VGPR {v.get('VGPRs')} AGPR {v.get('AGPRs')} SGPR {v.get('SGPRs')} sgpr_spill {v.get('SGPRs Spill')} "
+    dn = subprocess.run(["c++filt", k], capture_output=True, text=True).stdout.strip().replace("(anonymous namespace)::", "").split("(")[0]
+    print(f"{dn:58s} VGPR {v.get('VGPRs')} AGPR {v.get('AGPRs')} SGPR {v.get('TotalSGPRs')} sgpr_spill {v.get('SGPRs Spill')} "
           f"vgpr_spill {v.get('VGPRs Spill')} scratch {v.get('ScratchSize [bytes/lane]')} occ {v.get('Occupancy [waves/SIMD]')}")
