@@ -1452,7 +1452,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     for (int k = 0; k < 3; ++k) fuel[k] = T.fuel[(size_t)qc * 3 + k];
   }
   double out_r = 0.0;
-  bool out_done = false, ready = false, stalled = false;
+  bool out_done = false, stalled = false;
+  int ready = 0;  // (an int: OPQ kernels keep it in a VGPR, not a lane mask merged across the tick loop)
   uint32_t out_bits = 0;
   int out_ticks = 0;
   int ticks = 0;
@@ -1526,7 +1527,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         out_bits = snap_bits;
         out_done = true;
         out_ticks = 0;
-        ready = true;
+        ready = opaque_if<OPQ>(1);
       } else {
         acc = 0;
       }
@@ -1640,7 +1641,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
           const DevState So = opaque(step_args().S);
           for (int i = 0; i < 8; ++i) So.next_obs8()[envc * 8 + i] = ns[i];  // self.next_observations
         }
-        ready = false;
+        ready = opaque_if<OPQ>(0);
         out_done = false;
         if (burst + 1 >= kChainBurst || (CH.log_stop && log_n >= CH.log_cap)) {
           stalled = true;  // next decision pending: resumed by the next launch
@@ -1666,7 +1667,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     }
   }
 
-  bool going = running && !ready && (budget <= 0 || ticks < budget);
+  // (an int: OPQ kernels hold it in a VGPR, not as a lane mask live across the whole tick loop)
+  int going = opaque_if<OPQ>((running && !ready && (budget <= 0 || ticks < budget)) ? 1 : 0);
 #ifdef SHIPSIM_PHASE_TIMING
   unsigned long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long pt_last = wall_clock64();
@@ -1674,7 +1676,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   // CHAIN: the tick loop hands over to the (rare) chaining code below whenever a decision of the
   // wave completes, so the loop body itself is the per-decision kernel's.
   for (;;) {
-  while (__any(going) && !(CHAIN && __any(ready && running))) {
+  while (__any(opaque_if<OPQ>(going)) && !(CHAIN && __any(ready && running))) {
     // this tick's constants: re-read (scalar loads, LDS) rather than kept in registers across ticks
     const StepArgs& A = step_args();
     const Params& P = A.P;
@@ -2049,10 +2051,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         out_bits = bits;
         out_ticks = dec_ticks;
         snap_bits = bits;
-        ready = true;
+        ready = opaque_if<OPQ>(1);
       }
       const int mt = OPQ ? opaque_v(budget) : budget;  // (OPQ: its test not held across the loop)
-      going = !ready && (mt <= 0 || ticks < mt);
+      going = opaque_if<OPQ>((!ready && (mt <= 0 || ticks < mt)) ? 1 : 0);
     }
     PT_MARK(3);
   }
@@ -2060,9 +2062,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   if (POLICY || (ready && running)) chain_next();  // (policy: wave-uniform, a no-op unless a decision completed)
   {
     const int mt = OPQ ? opaque_v(budget) : budget;
-    going = running && !ready && (mt <= 0 || ticks < mt);
+    going = opaque_if<OPQ>((running && !ready && (mt <= 0 || ticks < mt)) ? 1 : 0);
   }
-  if (!__any(going)) {
+  if (!__any(opaque_if<OPQ>(going))) {
     // Launch tail: this wave's envs met the quota. While any wave of the launch has not, keep ticking in chunks
     // instead of idling the SIMD until the slowest wave ends (an env's results do not depend on where a launch
     // ends: slicing is exact). Bounded by tail_extra, so a wave that is not co-resident delays nothing forever.
@@ -2077,10 +2079,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       if (lead) n_met = __hip_atomic_load(CT.tail_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__builtin_amdgcn_readfirstlane(n_met) < CT.tail_waves) {
         budget += kTailChunk;
-        going = running && !ready && ticks < budget;
+        going = opaque_if<OPQ>((running && !ready && ticks < budget) ? 1 : 0);
       }
     }
-    if (!__any(going)) break;  // (quota met, or every env of the wave stalled)
+    if (!__any(opaque_if<OPQ>(going))) break;  // (quota met, or every env of the wave stalled)
   }
   }
 #ifdef SHIPSIM_PHASE_TIMING
