@@ -141,6 +141,7 @@ constexpr int kDppRowBcast = 0x150;  // row_newbcast:k (0x150 + k): lane k of th
 constexpr int kDppRowRor4 = 0x124;   // row_ror:4
 constexpr int kDppRowRor8 = 0x128;   // row_ror:8
 constexpr int kDppQuadXor2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int kDppQuadXor1 = 0xB1;   // quad_perm [1,0,3,2]
 
 // swap a double with the partner lane (lane ^ 1) — DPP quad_perm [1,0,3,2]
 __device__ __forceinline__ double pair_swap(double x) {

@@ -739,6 +739,22 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   return H1 + H2;
 }
 
+// Argmin of (cost, index) over each half-wave (its 32 scenario lanes), every lane of the half ending with the
+// result; ties -> the lower index. The order (cost, then index) is a total order on non-NaN costs, so any pairing
+// gives the same result: inside each 16-lane row by DPP (quad xor 1, quad xor 2, row_ror 4, row_ror 8: every lane
+// then holds its row's minimum), then one LDS permute across the half-wave's two rows. Every lane of the wave
+// must be active (the cooperative passes are called wave-uniformly).
+__device__ __forceinline__ void scenario_argmin(double& cost, int& idx, int lane) {
+  auto take = [&](double oc, int oi) __attribute__((always_inline)) {
+    if (oc < cost || (oc == cost && oi < idx)) { cost = oc; idx = oi; }
+  };
+  take(dpp_d<kDppQuadXor1>(cost), dpp_i<kDppQuadXor1>(idx));
+  take(dpp_d<kDppQuadXor2>(cost), dpp_i<kDppQuadXor2>(idx));
+  take(dpp_d<kDppRowRor4>(cost), dpp_i<kDppRowRor4>(idx));
+  take(dpp_d<kDppRowRor8>(cost), dpp_i<kDppRowRor8>(idx));
+  take(shfl_d(cost, lane ^ 16), __shfl(idx, lane ^ 16, 64));
+}
+
 // Must be called by every lane of the wave (wave-uniform control flow). `need` marks lanes that
 // request an optimisation with inputs `in`; they receive (P_best, Chi_best). SHIP_UNIFORM: u_d, obs_l and
 // obs_w are the same for every request and set in every lane's `in` (the AST kernels: the ships'
@@ -781,13 +797,9 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
     }
     // argmin over the half-wave; ties -> lowest scenario index (first strict improvement in the
     // reference's i-major / j-minor loop)
-    for (int off = 16; off >= 1; off >>= 1) {
-      double oc = shfl_d(cost, lane ^ off);
-      int oi = __shfl(idx, lane ^ off, 64);
-      if (oc < cost || (oc == cost && oi < idx)) { cost = oc; idx = oi; }
-    }
-    int best0 = __shfl(idx, 0, 64);
-    int best1 = __shfl(idx, 32, 64);
+    scenario_argmin(cost, idx, lane);
+    const int best0 = __builtin_amdgcn_readlane(idx, 0);
+    const int best1 = __builtin_amdgcn_readlane(idx, 32);
     if (lane == src0) {
       p_best = p_ca_of(best0 & 3);
       chi_best = (-30.0 + 10.0 * (best0 >> 2)) * (kPi / 180.0);
@@ -862,13 +874,9 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
       cost = worst;
       idx = scen;
     }
-    for (int off = 16; off >= 1; off >>= 1) {
-      double oc = shfl_d(cost, lane ^ off);
-      int oi = __shfl(idx, lane ^ off, 64);
-      if (oc < cost || (oc == cost && oi < idx)) { cost = oc; idx = oi; }
-    }
-    int best0 = __shfl(idx, 0, 64);
-    int best1 = __shfl(idx, 32, 64);
+    scenario_argmin(cost, idx, lane);
+    const int best0 = __builtin_amdgcn_readlane(idx, 0);
+    const int best1 = __builtin_amdgcn_readlane(idx, 32);
     if (lane == src0) {
       p_best = p_ca_of(best0 & 3);
       chi_best = (-30.0 + 10.0 * (best0 >> 2)) * (kPi / 180.0);
