@@ -1025,6 +1025,22 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
   const float c1 = actor ? hw[jj] : hw[(2 + cn) * H + jj];
   const float c2 = actor ? hw[H + jj] : 0.0f;
   const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
+  // this unit's outputs: fc0 row (nin), fc0 bias, fc1 bias, head weight(s); wave w finishes outputs w, w + 4, ...
+  // (at most 4 each), their optimizer state in flight during the row loop
+  const int n_el = nin + (actor ? 4 : 3);
+  const int64_t base = actor ? 0 : L.q_base[cn];
+  auto el_off = [&](int k) -> int64_t {
+    if (k < nin) return base + (actor ? L.p_w1 : L.c_w1) + (int64_t)jj * nin + k;
+    if (k == nin) return base + (actor ? L.p_b1 : L.c_b1) + jj;
+    if (k == nin + 1) return base + (actor ? L.p_b2 : L.c_b2) + jj;
+    if (k == nin + 2) return base + (actor ? L.p_wm : L.c_w3) + jj;
+    return L.p_ws + jj;
+  };
+  AdamElem xe[4];
+  if (a.fuse)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (w + 4 * q < n_el) xe[q] = adam_ld(a.ap, el_off(w + 4 * q), !actor, false);
   float w1a[kXLd], b1a = 0.0f, b2a = 0.0f, ha1 = 0.0f, ha2 = 0.0f;
 #pragma unroll
   for (int i = 0; i < kXLd; ++i) w1a[i] = 0.0f;
@@ -1082,22 +1098,20 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
   vr[w][kXLd + 2][lane] = ha1;
   vr[w][kXLd + 3][lane] = ha2;
   __syncthreads();
-  if (w != 0 || !jok) return;
+  if (!jok) return;
   auto total = [&](int i) { return ((vr[0][i][lane] + vr[1][i][lane]) + vr[2][i][lane]) + vr[3][i][lane]; };
-  auto emit = [&](int64_t e, float g) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = w + 4 * q;
+    if (k >= n_el) break;
+    const float g = total(k < nin ? k : kXLd + (k - nin));
+    const int64_t e = el_off(k);
     a.grads[e] = g;
     if (a.fuse) {
-      AdamElem x = adam_ld(a.ap, e, !actor, false);
-      x.g = g;
-      adam_st(a.ap, S.sst, e, x, !actor);
+      xe[q].g = g;
+      adam_st(a.ap, S.sst, e, xe[q], !actor);
     }
-  };
-  const int64_t base = actor ? 0 : L.q_base[cn];
-  for (int i = 0; i < nin; ++i) emit(base + (actor ? L.p_w1 : L.c_w1) + (int64_t)j * nin + i, total(i));
-  emit(base + (actor ? L.p_b1 : L.c_b1) + j, total(kXLd));
-  emit(base + (actor ? L.p_b2 : L.c_b2) + j, total(kXLd + 1));
-  emit(base + (actor ? L.p_wm : L.c_w3) + j, total(kXLd + 2));
-  if (actor) emit(L.p_ws + j, total(kXLd + 3));
+  }
 }
 
 // scalar block: per-row losses and diagnostics, the loss means, the bias gradients of the scalar heads
@@ -1110,6 +1124,11 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   const int B = L.B, Bp = L.Bp, tid = threadIdx.x;
   const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
   const float invB = 1.0f / (float)B;
+  // the five scalar parameters (log α, b_mean, b_log_std, b3 Q1, b3 Q2): thread i < 5 finishes parameter i, its
+  // optimizer state in flight during the row pass
+  const int64_t off = tid == 0 ? 0 : tid == 1 ? L.p_bm : tid == 2 ? L.p_bs : L.q_base[tid >= 4 ? 1 : 0] + L.c_b3;
+  AdamElem xs;
+  if (a.fuse && tid < 5) xs = adam_ld(a.ap, off, tid >= 3, false);
   float v[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) v[i] = 0.0f;
@@ -1137,22 +1156,20 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
     st[5 * B + r] = ar.std;
   }
   block_sum<9>(v, S.red, S.sum);
-  if (tid != 0) return;
   const float* sum = S.sum;
-  m.stats[0] = sum[0] * invB;
-  m.stats[1] = sum[1] * invB;
-  m.stats[2] = sum[2] * invB;
-  m.stats[3] = m.hp.auto_ent ? sum[3] * invB : 0.0f;
-  m.stats[4] = alpha;
-  const int64_t off[5] = {0, L.p_bm, L.p_bs, L.q_base[0] + L.c_b3, L.q_base[1] + L.c_b3};
-  const float g[5] = {m.hp.auto_ent ? sum[4] * invB : 0.0f, sum[5], sum[6], sum[7], sum[8]};
-  for (int i = 0; i < 5; ++i) {
-    a.grads[off[i]] = g[i];
-    if (a.fuse && (i > 0 || m.hp.auto_ent)) {
-      AdamElem x = adam_ld(a.ap, off[i], i >= 3, false);
-      x.g = g[i];
-      adam_st(a.ap, S.sst, off[i], x, i >= 3);
-    }
+  if (tid == 0) {
+    m.stats[0] = sum[0] * invB;
+    m.stats[1] = sum[1] * invB;
+    m.stats[2] = sum[2] * invB;
+    m.stats[3] = m.hp.auto_ent ? sum[3] * invB : 0.0f;
+    m.stats[4] = alpha;
+  }
+  if (tid >= 5) return;
+  const float g = tid == 0 ? (m.hp.auto_ent ? sum[4] * invB : 0.0f) : sum[4 + tid];
+  a.grads[off] = g;
+  if (a.fuse && (tid > 0 || m.hp.auto_ent)) {
+    xs.g = g;
+    adam_st(a.ap, S.sst, off, xs, tid >= 3);
   }
 }
 
