@@ -1,7 +1,6 @@
 """The data-parallel SAC step through RCCL on the hardware: a world-size-1 "nccl"
-process group (RCCL) drives FusedSACTrainer's split path — gradient graph half, torch.distributed
-all_reduce of the flat gradient on the stream, update graph half (libsacfused sacf_grads | RCCL |
-sacf_apply) — the exact code N ranks run, and it must equal the fused single-rank step (where Adam
+process group (RCCL) drives FusedSACTrainer's split path — libsacfused sacf_grads | torch.distributed all_reduce of the flat
+gradient | sacf_apply, captured in one HIP graph (and eagerly, use_graph False) — the exact code N ranks run, and it must equal the fused single-rank step (where Adam
 runs inside the weight-gradient kernel). SURVEY.md §8(e); sac.py:102-154. Needs an MI355X."""
 import os
 import socket
@@ -58,9 +57,11 @@ def _worker(rank, port, out_dir, use_graph):
     tr.broadcast_parameters(0)
     batches, eps = _data(1)
     _run(tr, batches, eps, slice(0, B), dev)
-    if use_graph:
-        assert len(tr._graphs[1]) == 2, "split step = two graph halves"
-    assert len(calls) >= 3 and calls[-1] == tr.flat_grad.numel(), calls
+    if use_graph:  # sacf_grads | all_reduce | sacf_apply captured in ONE HIP graph (replays run no Python)
+        assert tr.capture_collective and len(tr._graphs[1]) == 1, "grads | all-reduce | apply in one graph"
+        assert calls[-1] == tr.flat_grad.numel(), calls
+    else:
+        assert len(calls) >= 3 and calls[-1] == tr.flat_grad.numel(), calls
     np.save(os.path.join(out_dir, "rccl.npy"), _params(tr))
     dist.all_reduce = real
     dist.destroy_process_group()
