@@ -953,6 +953,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     else {
 #pragma unroll
       for (int i = 0; i < kMaxN2; ++i) {
+        yv[i] = xv[i] = 0.0f;
         if (i >= n2) continue;  // (continue, not break: the constant trip count keeps the loop unrolled)
         yv[i] = Y[(int64_t)(rb + i) * H + jc];
         xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
@@ -961,14 +962,17 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     S.s0[tid] = s0;
     S.s1[tid] = s1;
     __syncthreads();
+    // (every LDS read unconditional — rl0 + i < 256 for every chunk shape — and the actor / critic choice a select
+    // of values: a guard or branch per read compiles into a wait per read)
     float av[kMaxN2];
 #pragma unroll
     for (int i = 0; i < kMaxN2; ++i) {
-      if (i >= n2) continue;
-      const float d = actor ? c1 * S.s0[rl0 + i] + c2 * S.s1[rl0 + i] : c1 * S.s0[rl0 + i];
+      const float s0v = S.s0[rl0 + i], s1v = S.s1[rl0 + i];
+      const float d = actor ? c1 * s0v + c2 * s1v : c1 * s0v;
       av[i] = yv[i] > 0.0f ? d : 0.0f;
     }
-    mfma_chain(acc, av, xv, n2);
+    if (n2 == kMaxN2) mfma_n<kMaxN2>(acc, av, xv);  // (full chunks: one straight chain)
+    else mfma_chain(acc, av, xv, n2);
     if (rc + kRowChunk < Bp) __syncthreads();  // S.s0 / s1 reused
   }
   auto& tt = S.u.mm.tt;
@@ -1068,10 +1072,12 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
     for (int q0 = w * rows_w; q0 < (w + 1) * rows_w; q0 += 8) {
       float u1[8], u2[8], x2[8];
 #pragma unroll
+      // (every load and LDS read unconditional — U2 is a valid buffer for a critic too, and the input rows are zero
+      // past nin — with the actor / critic choice a select of values: a guard per read compiled into a wait per read)
       for (int u = 0; u < 8; ++u) {
         const int64_t o = (int64_t)(rc + q0 + u) * H + jj;
         u1[u] = U1[o];
-        u2[u] = actor ? U2[o] : 0.0f;
+        u2[u] = U2[o];
         x2[u] = A2[o];
       }
 #pragma unroll
@@ -1080,8 +1086,7 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
         const float d1 = actor ? a0 * u1[u] + a1 * u2[u] : a0 * u1[u];
         const float d2 = x2[u] > 0.0f ? (actor ? c1 * a0 + c2 * a1 : c1 * a0) : 0.0f;
 #pragma unroll
-        for (int i = 0; i < kXLd; ++i)
-          if (i < nin) w1a[i] = fmaf(d1, S.xs[q0 + u][i], w1a[i]);
+        for (int i = 0; i < kXLd; ++i) w1a[i] = fmaf(d1, S.xs[q0 + u][i], w1a[i]);
         b1a += d1;
         b2a += d2;
         ha1 = fmaf(a0, x2[u], ha1);

@@ -5,7 +5,7 @@
 TAG=${1:-sac}; NOTESTS=${2:-}; SQ=${3:-}
 export TMPDIR=/tmp
 if [ "$NOTESTS" != "notests" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_sac.py tests/test_gpu_distributed.py tests/test_gpu_rccl.py -m gpu -q \
+  timeout -k 10 600 python -u -m pytest tests/test_sac.py tests/test_gpu_distributed.py tests/test_gpu_rccl.py tests/test_gpu_runner_shapes.py -m gpu -q \
     -p no:cacheprovider --timeout 300 --timeout-method thread > "$O/pytest_sac_$TAG.txt" 2>&1
   rc=$?; tail -3 "$O/pytest_sac_$TAG.txt"; soft_pytest $rc pytest_sac
 fi
