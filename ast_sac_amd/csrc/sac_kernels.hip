@@ -112,6 +112,22 @@ struct MArgs {
   Hyper hp;
 };
 
+// Diagnostics build only (-DSACF_PHASE_TIMING, scripts/sac_phase_timing.py): wave 0 of every block of the three
+// step kernels stamps the device wall clock (100 MHz) at entry (0), operands ready (1), products done (2) and exit
+// (3); the product build compiles the stamps out.
+#ifdef SACF_PHASE_TIMING
+constexpr int kStampBlocks = 8192;
+__device__ unsigned long long g_sac_stamps[3][kStampBlocks][4];
+#define SAC_STAMP(K, P)                                                                               \
+  do {                                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) g_sac_stamps[K][blockIdx.x][P] = wall_clock64(); \
+  } while (0)
+#else
+#define SAC_STAMP(K, P) \
+  do {                  \
+  } while (0)
+#endif
+
 // Adam bias corrections of step t (torch.optim.Adam: step_size = lr / (1 - beta1^t), denominator
 // sqrt(v) / sqrt(1 - beta2^t) + eps), in double as torch computes them on the host, then rounded once
 struct AdamStep {
@@ -449,6 +465,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   }
   (void)B;
   __syncthreads();
+  SAC_STAMP(0, 1);
   f32x16 acc = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -459,6 +476,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
     if (!nrow) store_slice<H, CS>(a.s.h1, r0, by, av, k0);
     mfma_n<CS>(acc, av, bv);
   }
+  SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
@@ -506,6 +524,7 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
       for (int m = 0; m < kXLd; ++m) a.s.qx[(int64_t)item * kXLd + m] = m == O ? act : xin[m];
   }
   __syncthreads();
+  SAC_STAMP(0, 1);
   f32x16 acc = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -516,6 +535,7 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
     store_slice<H, CS>(a.s.g1[net], r0, by, av, k0);
     mfma_n<CS>(acc, av, bv);
   }
+  SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
@@ -528,11 +548,13 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
 template <int H>
 __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
   __shared__ float lds[FwdLds<H>::kFloats];
+  SAC_STAMP(0, 0);
   int bx, by;
   tile_of<H>(bx, by);
   const int bt = a.L.Bp / kTile2;
   if (bx < 2 * bt) p1_actor_tile<H>(a, bx, by, lds);
   else p1_data_tile<H>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
+  SAC_STAMP(0, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -590,6 +612,7 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
     }
   }
   __syncthreads();
+  SAC_STAMP(1, 1);
   f32x16 acc = zero16(), act = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -605,6 +628,7 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
       mfma_n<CS>(act, tv, bv);
     }
   }
+  SAC_STAMP(1, 2);
   bool gm[4];
   splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
     const int r = r0 + rr;
@@ -655,6 +679,7 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   if constexpr (kActor)
 #pragma unroll
     for (int i = 0; i < N2; ++i) hw2[i] = HW2[kb + i];
+  SAC_STAMP(1, 1);
   f32x16 acc = zero16(), acc2 = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -669,6 +694,7 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
       mfma_n<CS>(acc2, av, bv);
     }
   }
+  SAC_STAMP(1, 2);
   float* o1 = kActor ? a.s.um : a.s.uq[net];
   splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
     o1[(int64_t)(r0 + rr) * H + j0 + cc] = m1[q] > 0.0f ? v : 0.0f;
@@ -683,6 +709,7 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
 template <int H>
 __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   __shared__ float lds[FwdLds<H>::kFloats];
+  SAC_STAMP(1, 0);
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
       const int64_t t = *a.step + 1;
@@ -714,6 +741,7 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   else if (bx < 3 * bt) p2_factor_tile<H, true>(a, 0, bx - 2 * bt, by, lds);
   else if (bx < 5 * bt) p2_critic_tile<H, true>(a, (bx - 3 * bt) / bt, (bx - 3 * bt) % bt, by, lds);
   else p2_factor_tile<H, false>(a, (bx - 5 * bt) / bt, (bx - 5 * bt) % bt, by, lds);
+  SAC_STAMP(1, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -962,6 +990,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     S.s0[tid] = s0;
     S.s1[tid] = s1;
     __syncthreads();
+    SAC_STAMP(2, 1);
     // (every LDS read unconditional — rl0 + i < 256 for every chunk shape — and the actor / critic choice a select
     // of values: a guard or branch per read compiles into a wait per read)
     float av[kMaxN2];
@@ -975,6 +1004,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     else mfma_chain(acc, av, xv, n2);
     if (rc + kRowChunk < Bp) __syncthreads();  // S.s0 / s1 reused
   }
+  SAC_STAMP(2, 2);
   auto& tt = S.u.mm.tt;
   {
   // the tile's coordinates again, from an opaque block id: recomputed here rather than held across the loop
@@ -1068,6 +1098,7 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
 #pragma unroll
     for (int i = 0; i < kXLd; ++i) S.xs[tid][i] = xr[i];
     __syncthreads();
+    SAC_STAMP(2, 1);
     const int rows_w = nrow / 4;  // a multiple of 8
     for (int q0 = w * rows_w; q0 < (w + 1) * rows_w; q0 += 8) {
       float u1[8], u2[8], x2[8];
@@ -1095,6 +1126,7 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
     }
     __syncthreads();
   }
+  SAC_STAMP(2, 2);
   auto& vr = S.u.vred;
 #pragma unroll
   for (int i = 0; i < kXLd; ++i) vr[w][i][lane] = w1a[i];
@@ -1160,7 +1192,9 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
     st[4 * B + r] = tanhf(ar.mean);
     st[5 * B + r] = ar.std;
   }
+  SAC_STAMP(2, 1);
   block_sum<9>(v, S.red, S.sum);
+  SAC_STAMP(2, 2);
   const float* sum = S.sum;
   if (tid == 0) {
     m.stats[0] = sum[0] * invB;
@@ -1192,12 +1226,14 @@ __global__ __launch_bounds__(256) void sac_wgrad_kernel(WArgs a_arg) {
   (void)a_arg;  // read through wargs()
   __shared__ WLds S;
   const WArgs& a = wargs();
+  SAC_STAMP(2, 0);
   if (threadIdx.x == 0) S.sst = AdamStep{a.m.stats[5], a.m.stats[6], a.m.stats[7]};
   __syncthreads();
   const int bx = (int)blockIdx.x;
   if (bx < a.n_mfma) p3_mfma_tile<H>(a, bx, S);
   else if (bx < a.n_mfma + a.n_valu) p3_valu_block<H>(a, bx - a.n_mfma, S);
   else p3_scalar_block<H>(a, S);
+  SAC_STAMP(2, 3);
 }
 
 // world_size > 1 / split_update: the update from the (all-reduced) flat gradient
@@ -1453,6 +1489,15 @@ int32_t sacf_abi_version(void) { return SACF_ABI_VERSION; }
 #define SACF_SRC_HASH "unknown"
 #endif
 const char* sacf_build_info(void) { return "sacfused gfx950 HIP src " SACF_SRC_HASH; }
+
+#ifdef SACF_PHASE_TIMING
+// diagnostics build: the last step's stamps, [3 kernels][kStampBlocks][4] (not in include/sac_fused.h)
+int sacf_debug_stamps(unsigned long long* out, int n) {
+  const size_t bytes = sizeof(unsigned long long) * 3 * kStampBlocks * 4;
+  if (!out || (size_t)n * sizeof(unsigned long long) < bytes) return kStampBlocks;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sac_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int sacf_hidden_supported(int32_t hidden) { return hidden_ok(hidden) ? 1 : 0; }
 

@@ -1,5 +1,6 @@
 # The SAC update: its GPU tests, grad-step timing at the runner's batch (256) and the per-rank batches of 2 / 8
-# ranks, the per-kernel rocprofv3 stats of one timing run, and (with sq) one SQ counter pass of the SAC kernels.
+# ranks, the per-kernel rocprofv3 stats of one timing run, per-block phase stamps (diagnostics build), and (with sq)
+# one SQ counter pass of the SAC kernels.
 # Usage: bash scripts/gpu/sac.sh TAG [notests] [sq]
 . "$(dirname "$0")/common.sh"
 TAG=${1:-sac}; NOTESTS=${2:-}; SQ=${3:-}
@@ -17,6 +18,12 @@ cd /tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_sac_$TAG" -o run -- \
   python3 "$R/scripts/prof_sac.py" --steps 500 --graph 1 > "$O/prof_sac_$TAG.log" 2>&1; hard $? rocprof_sac
 f=$(find "$O/prof_sac_$TAG" -name "*kernel_stats.csv" | head -1); cut -d, -f1-4,7 "$f" | head -12
+cd "$R"
+for b in 256 64; do  # per-block phase stamps of a diagnostics build (scripts/sac_phase_timing.py --build, here)
+  timeout -k 10 200 python scripts/sac_phase_timing.py --batch $b --out "$O/sac_phases_${TAG}_b$b.json" \
+    > "$O/sac_phases_${TAG}_b$b.log" 2>&1; hard $? sac_phases_$b
+done
+cd /tmp
 if [ "$SQ" = "sq" ]; then
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
     SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d "$O/pmc_sac_sq_$TAG" -o run -- \

@@ -1,0 +1,103 @@
+"""Where a SAC grad step's time goes, per kernel and block kind: a diagnostics build of libsacfused
+(-DSACF_PHASE_TIMING: wave 0 of every block stamps the device wall clock at entry, operands ready, products
+done and exit) runs graph-replayed steps, and the last step's stamps are summarised relative to each kernel's
+first block entry (median / max over the blocks of each kind, µs).
+
+  python scripts/sac_phase_timing.py --build          # here: compile ast_sac_amd/lib/diag/libsacfused_timing.so
+  python scripts/sac_phase_timing.py [--batch 256]    # on the GPU box
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIAG = os.path.join(ROOT, "ast_sac_amd", "lib", "diag", "libsacfused_timing.so")
+KSTAMP = 8192
+
+
+def build():
+    sys.path.insert(0, ROOT)
+    from __graft_entry__ import HIPCC, HIPFLAGS, SAC_SRC
+    from ast_sac_amd.build_hash import LIB_FLAGS
+    os.makedirs(os.path.dirname(DIAG), exist_ok=True)
+    subprocess.check_call([HIPCC] + HIPFLAGS + LIB_FLAGS["sacfused"] + ["-DSACF_PHASE_TIMING", '-DSACF_SRC_HASH="diag"']
+                          + SAC_SRC + ["-o", DIAG])
+    print("built", DIAG)
+
+
+def kinds(kernel, nblocks, bt, cb, n_mfma, n_valu):
+    """Block kind of each block id (mirrors tile_of and the kernels' dispatch)."""
+    out = []
+    for b in range(nblocks):
+        if kernel == 2:
+            out.append("mfma_tile" if b < n_mfma else ("valu" if b < n_mfma + n_valu else "scalar"))
+            continue
+        bx = b // cb
+        if kernel == 0:
+            out.append("actor_fwd" if bx < 2 * bt else "critic_data_fwd")
+        else:
+            out.append("critic_tangent" if bx < 2 * bt else "actor_factors" if bx < 3 * bt else
+                       "targets" if bx < 5 * bt else "critic_factors")
+    return out
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--build", action="store_true")
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--hidden", type=int, default=256)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--out", default=None)
+    a = p.parse_args()
+    if a.build:
+        return build()
+    os.environ["SACFUSED_LIB"] = DIAG
+    sys.path.insert(0, ROOT)
+    import torch
+    import bench
+    from ast_sac_amd import sacfused
+    dev = torch.device("cuda", 0)
+    r = bench.bench_sac(dev, 1, None, a.steps, a.batch, eager_steps=0, graph=True)
+    torch.cuda.synchronize()
+    L = sacfused.load_library()
+    buf = (C.c_ulonglong * (3 * KSTAMP * 4))()
+    assert L.sacf_debug_stamps(buf, len(buf)) == 0
+    import numpy as np
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(3, KSTAMP, 4).astype(np.float64)
+    bp = (a.batch + 31) // 32 * 32
+    bt, cb = bp // 32, a.hidden // 32
+    grids = [4 * bt * cb, 7 * bt * cb, 3 * cb * cb + 3 * ((a.hidden + 63) // 64) + 1]
+    names = ["fwd (P1)", "mid (P2)", "wgrad (P3)"]
+    res = {"step_us": r["ms_per_grad_step"] * 1e3, "batch": a.batch, "hidden": a.hidden, "kernels": {}}
+    for k in range(3):
+        s = st[k, :grids[k]]
+        t0 = s[:, 0].min()
+        rel = (s - t0) / 100.0  # 100 MHz ticks -> µs
+        ks = kinds(k, grids[k], bt, cb, 3 * cb * cb, 3 * ((a.hidden + 63) // 64))
+        per = {}
+        for kind in dict.fromkeys(ks):
+            m = rel[[i for i, x in enumerate(ks) if x == kind]]
+            per[kind] = {"blocks": int(m.shape[0]),
+                         "entry_med": float(np.median(m[:, 0])), "entry_max": float(m[:, 0].max()),
+                         "operands_ready_med": float(np.median(m[:, 1] - m[:, 0])),
+                         "operands_ready_max": float((m[:, 1] - m[:, 0]).max()),
+                         "products_med": float(np.median(m[:, 2] - m[:, 1])),
+                         "products_max": float((m[:, 2] - m[:, 1]).max()),
+                         "epilogue_med": float(np.median(m[:, 3] - m[:, 2])),
+                         "epilogue_max": float((m[:, 3] - m[:, 2]).max()),
+                         "exit_med": float(np.median(m[:, 3])), "exit_max": float(m[:, 3].max())}
+        res["kernels"][names[k]] = {"span_us": float(rel[:, 3].max()), "kinds": per}
+    gaps = [(st[k + 1, :grids[k + 1], 0].min() - st[k, :grids[k], 3].max()) / 100.0 for k in range(2)]
+    res["gaps_us"] = {"fwd_exit_to_mid_entry": gaps[0], "mid_exit_to_wgrad_entry": gaps[1]}
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()
