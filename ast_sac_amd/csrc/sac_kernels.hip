@@ -114,17 +114,26 @@ struct MArgs {
 
 // Diagnostics build only (-DSACF_PHASE_TIMING, scripts/sac_phase_timing.py): wave 0 of every block of the three
 // step kernels stamps the device wall clock (100 MHz) at entry (0), operands ready (1), products done (2) and exit
-// (3); the product build compiles the stamps out.
+// (3), and at up to four points inside the prologue (4..7; SAC_STAMP_ON: after the value `dep` has landed); the
+// product build compiles the stamps out.
 #ifdef SACF_PHASE_TIMING
-constexpr int kStampBlocks = 8192;
-__device__ unsigned long long g_sac_stamps[3][kStampBlocks][4];
+constexpr int kStampBlocks = 8192, kStamps = 8;
+__device__ unsigned long long g_sac_stamps[3][kStampBlocks][kStamps];
 #define SAC_STAMP(K, P)                                                                               \
   do {                                                                                                \
     if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) g_sac_stamps[K][blockIdx.x][P] = wall_clock64(); \
   } while (0)
+#define SAC_STAMP_ON(K, P, dep)                                                                          \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks && __float_as_uint((float)(dep)) != 0x7FBADBADu) \
+      g_sac_stamps[K][blockIdx.x][P] = wall_clock64();                                                   \
+  } while (0)
 #else
 #define SAC_STAMP(K, P) \
   do {                  \
+  } while (0)
+#define SAC_STAMP_ON(K, P, dep) \
+  do {                          \
   } while (0)
 #endif
 
@@ -264,6 +273,30 @@ __device__ __forceinline__ void splitk_finish(const f32x16& acc, float* lds, EPI
     v += lds[(2 * 16 + g) * 64 + lane];
     v += lds[(3 * 16 + g) * 64 + lane];
     epi(q, (g & 3) + 8 * (g >> 2) + 4 * (lane >> 5), lane & 31, v);
+  }
+}
+// the same for two accumulators (two split regions of lds) behind one barrier: epi(q, row, col, v0, v1)
+template <class EPI>
+__device__ __forceinline__ void splitk_finish2(const f32x16& acc0, const f32x16& acc1, float* lds0, float* lds1,
+                                               EPI&& epi) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    lds0[(w * 16 + g) * 64 + lane] = acc0[g];
+    lds1[(w * 16 + g) * 64 + lane] = acc1[g];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int g = 4 * w + q;
+    float v0 = lds0[(0 * 16 + g) * 64 + lane], v1 = lds1[(0 * 16 + g) * 64 + lane];
+    v0 += lds0[(1 * 16 + g) * 64 + lane];
+    v1 += lds1[(1 * 16 + g) * 64 + lane];
+    v0 += lds0[(2 * 16 + g) * 64 + lane];
+    v1 += lds1[(2 * 16 + g) * 64 + lane];
+    v0 += lds0[(3 * 16 + g) * 64 + lane];
+    v1 += lds1[(3 * 16 + g) * 64 + lane];
+    epi(q, (g & 3) + 8 * (g >> 2) + 4 * (lane >> 5), lane & 31, v0, v1);
   }
 }
 // the row of output register q (0..3) of this lane in splitk_finish's order
@@ -436,9 +469,11 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   const int item = nrow ? row - Bp : row;
   float e0, e1;
   const int64_t idx = batch_item(a, item, e0, e1);
+  SAC_STAMP_ON(0, 4, idx);
   const float* src = nrow ? a.nobs : a.obs;
   float x[kXLd];
   load_obs_row(src, idx, O, x);
+  SAC_STAMP_ON(0, 5, x[0]);
   float bv[CS];
   load_b<CS>(bv, a.T, H, kb, c0 + rl);  // actor W2ᵀ, chunk 0
   const float b2c = P[L.p_b2 + c0 + rl];
@@ -446,6 +481,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   float* lw1 = lds + FwdLds<H>::kW1Off;
   float* lx = lds + FwdLds<H>::kXOff;
   stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
+  SAC_STAMP(0, 6);
   if (w == 0 && h == 0) {
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = x[m];  // (zero past O: no per-m mask kept live)
@@ -595,8 +631,10 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   float* lw1 = lds + FwdLds<H>::kW1Off;
   float* lx = lds + FwdLds<H>::kXOff;
   stage_w1t<H>(lw1, C + L.c_w1, C + L.c_b1, O + 1);
+  SAC_STAMP(1, 5);
   float hd[6];
   row_head<CB>(a, (kTarget ? Bp : 0) + item, ev, hd);
+  SAC_STAMP_ON(1, 4, hd[HD_A]);
   if (w == 0 && h == 0) {
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
@@ -629,19 +667,21 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
     }
   }
   SAC_STAMP(1, 2);
-  bool gm[4];
-  splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
-    const int r = r0 + rr;
-    const float y = relu(v + b2c);
-    gm[q] = y > 0.0f;
-    const float pq = halfwave_sum(y * w3);
-    if (cc == 0) a.s.part[((int64_t)r * PS_N + (kTarget ? PS_T1 : PS_Q1A) + net) * CB + by] = pq;
-  });
-  if constexpr (!kTarget) {
-    splitk_finish(act, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v) {
-      const int r = r0 + rr;
-      const float pd = halfwave_sum(gm[q] ? w3 * v : 0.0f);  // this column block's part of ∂Q/∂ã
-      if (cc == 0) a.s.part[((int64_t)r * PS_N + PS_D1 + net) * CB + by] = pd;
+  if constexpr (kTarget) {
+    splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
+      const float pq = halfwave_sum(relu(v + b2c) * w3);
+      if (cc == 0) a.s.part[((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by] = pq;
+    });
+  } else {  // Q and its tangent reduced behind one barrier
+    splitk_finish2(acc, act, lds, lds + FwdLds<H>::kSplit, [&](int, int rr, int cc, float v, float t) {
+      const float y = relu(v + b2c);
+      const float pq = halfwave_sum(y * w3);
+      const float pd = halfwave_sum(y > 0.0f ? w3 * t : 0.0f);  // this column block's part of ∂Q/∂ã
+      if (cc == 0) {
+        float* pr = a.s.part + (int64_t)(r0 + rr) * PS_N * CB + by;
+        pr[(PS_Q1A + net) * CB] = pq;
+        pr[(PS_D1 + net) * CB] = pd;
+      }
     });
   }
 }
@@ -696,12 +736,15 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   }
   SAC_STAMP(1, 2);
   float* o1 = kActor ? a.s.um : a.s.uq[net];
-  splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
-    o1[(int64_t)(r0 + rr) * H + j0 + cc] = m1[q] > 0.0f ? v : 0.0f;
-  });
-  if constexpr (kActor) {
-    splitk_finish(acc2, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v) {
-      a.s.us[(int64_t)(r0 + rr) * H + j0 + cc] = m1[q] > 0.0f ? v : 0.0f;
+  if constexpr (kActor) {  // U_m and U_s behind one barrier
+    splitk_finish2(acc, acc2, lds, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v, float v2) {
+      const int64_t o = (int64_t)(r0 + rr) * H + j0 + cc;
+      o1[o] = m1[q] > 0.0f ? v : 0.0f;
+      a.s.us[o] = m1[q] > 0.0f ? v2 : 0.0f;
+    });
+  } else {
+    splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
+      o1[(int64_t)(r0 + rr) * H + j0 + cc] = m1[q] > 0.0f ? v : 0.0f;
     });
   }
 }
@@ -865,7 +908,7 @@ __device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// P3 (sac_wgrad_kernel): [3·CB² MFMA tiles of the H x H gradients | VALU blocks (3 nets x ⌈H/64⌉) | scalars]
+// P3 (sac_wgrad_kernel): [3·CB² MFMA tiles of the H x H gradients | VALU blocks (3 nets x H/16 units) | scalars]
 // ---------------------------------------------------------------------------------------------
 struct WArgs {
   MArgs m;
@@ -890,7 +933,7 @@ struct WLds {
       float split[4 * 16 * 64];
       float tt[2][kTile2][kTile2 + 1];
     } mm;
-    float vred[4][kValuAcc][64];
+    float vred[kThreads / 16][kValuAcc][16];  // VALU blocks: [row stream][accumulator][unit]
   } u;
   float s0[kRowChunk], s1[kRowChunk];
   float xs[kRowChunk][kXLd + 1];
@@ -962,6 +1005,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
       s0 = (2.0f / (float)B) * ((net == 0 ? cr.q1 : cr.q2) - cr.y);
     }
     if (rc + tid >= B) s0 = s1 = 0.0f;
+    SAC_STAMP_ON(2, 4, s0);
     // the chunk's operands as one straight-line batch of loads (a run-time guard per load would make a chain of
     // branches with a wait after every load): n2 = 32 for full chunks, 16 / 8 / 4 for Bp = 128 / 64 / 32
     float yv[kMaxN2], xv[kMaxN2];
@@ -987,6 +1031,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
         xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
       }
     }
+    SAC_STAMP_ON(2, 5, yv[kMaxN2 - 1] + xv[kMaxN2 - 1]);
     S.s0[tid] = s0;
     S.s1[tid] = s1;
     __syncthreads();
@@ -1035,20 +1080,23 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   }
 }
 
-// VALU block: hidden units j = jb .. jb + 63 of net (0 actor, 1 / 2 Q1 / Q2), one per lane; the four waves
-// split the rows and their partials are added in wave order. Per j: fc0 row (Σ dh1·x), fc0 bias (Σ dh1), fc1
-// bias (Σ dh2), head weight(s) (Σ dmean·h2, Σ dls·h2 / Σ dq·g2), with
+// VALU block: hidden units j = jb .. jb + 15 of net (0 actor, 1 / 2 Q1 / Q2). Lane l of wave w serves unit l % 16
+// on row stream 4w + l / 16: the 16 streams split the rows (16 per stream at B = 256, two batches of 8 in flight),
+// and their partials are added in stream order. Per j: fc0 row (Σ dh1·x), fc0 bias (Σ dh1), fc1 bias (Σ dh2), head
+// weight(s) (Σ dmean·h2, Σ dls·h2 / Σ dq·g2), with
 //   actor  dh1 = dmean U_m + dls U_s, dh2 = [h2 > 0] (wm dmean + ws dls);  critic  dg1 = dq U_q, dg2 = [g2 > 0] w3 dq
+constexpr int kValuUnits = 16, kValuStreams = kThreads / kValuUnits;
 template <int H>
 __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
-  constexpr int CB = H / kTile2, NB = (H + 63) / 64;
+  constexpr int CB = H / kTile2, NB = H / kValuUnits;
+  static_assert(H % kValuUnits == 0, "units per VALU block");
   const MArgs& m = a.m;
   const Layout& L = m.L;
   const int B = L.B, Bp = L.Bp;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int net = vb / NB, j = (vb % NB) * 64 + lane;
-  const bool actor = net == 0, jok = j < H;
-  const int jj = jok ? j : H - 1;
+  const int tid = threadIdx.x;
+  const int net = vb / NB, j0 = (vb % NB) * kValuUnits;
+  const int u = tid % kValuUnits, strm = tid / kValuUnits, j = j0 + u;
+  const bool actor = net == 0;
   const int cn = actor ? 0 : net - 1;
   const float* hw = m.s.snap + SN_HEAD;  // pre-update head weights: wm | ws | w3 Q1 | w3 Q2
   const int nin = actor ? L.O : L.O + 1;
@@ -1056,25 +1104,25 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
   const float* U2 = m.s.us;
   const float* A2 = actor ? m.s.h2 : m.s.g2[cn];
   const float* XR = actor ? m.s.x : m.s.qx;
-  const float c1 = actor ? hw[jj] : hw[(2 + cn) * H + jj];
-  const float c2 = actor ? hw[H + jj] : 0.0f;
+  const float c1 = actor ? hw[j] : hw[(2 + cn) * H + j];
+  const float c2 = actor ? hw[H + j] : 0.0f;
   const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
-  // this unit's outputs: fc0 row (nin), fc0 bias, fc1 bias, head weight(s); wave w finishes outputs w, w + 4, ...
-  // (at most 4 each), their optimizer state in flight during the row loop
+  // the block's outputs: per unit its fc0 row (nin), fc0 bias, fc1 bias, head weight(s); thread t finishes output
+  // t / 16 (and t / 16 + 16) of unit t % 16, their optimizer state in flight during the row pass
   const int n_el = nin + (actor ? 4 : 3);
   const int64_t base = actor ? 0 : L.q_base[cn];
   auto el_off = [&](int k) -> int64_t {
-    if (k < nin) return base + (actor ? L.p_w1 : L.c_w1) + (int64_t)jj * nin + k;
-    if (k == nin) return base + (actor ? L.p_b1 : L.c_b1) + jj;
-    if (k == nin + 1) return base + (actor ? L.p_b2 : L.c_b2) + jj;
-    if (k == nin + 2) return base + (actor ? L.p_wm : L.c_w3) + jj;
-    return L.p_ws + jj;
+    if (k < nin) return base + (actor ? L.p_w1 : L.c_w1) + (int64_t)j * nin + k;
+    if (k == nin) return base + (actor ? L.p_b1 : L.c_b1) + j;
+    if (k == nin + 1) return base + (actor ? L.p_b2 : L.c_b2) + j;
+    if (k == nin + 2) return base + (actor ? L.p_wm : L.c_w3) + j;
+    return L.p_ws + j;
   };
-  AdamElem xe[4];
+  AdamElem xe[2];
   if (a.fuse)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (w + 4 * q < n_el) xe[q] = adam_ld(a.ap, el_off(w + 4 * q), !actor, false);
+    for (int q = 0; q < 2; ++q)
+      if (strm + kValuStreams * q < n_el) xe[q] = adam_ld(a.ap, el_off(strm + kValuStreams * q), !actor, false);
   float w1a[kXLd], b1a = 0.0f, b2a = 0.0f, ha1 = 0.0f, ha2 = 0.0f;
 #pragma unroll
   for (int i = 0; i < kXLd; ++i) w1a[i] = 0.0f;
@@ -1099,49 +1147,57 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
     for (int i = 0; i < kXLd; ++i) S.xs[tid][i] = xr[i];
     __syncthreads();
     SAC_STAMP(2, 1);
-    const int rows_w = nrow / 4;  // a multiple of 8
-    for (int q0 = w * rows_w; q0 < (w + 1) * rows_w; q0 += 8) {
-      float u1[8], u2[8], x2[8];
+    // this stream's rows (nrow / 16: even, a multiple of 8 from 128 rows up) in batches of R with every load of a
+    // batch in flight together; every load and LDS read unconditional (U2 is a valid buffer for a critic too, the
+    // input rows are zero past nin) and the actor / critic choice a select of values — a guard per read compiles
+    // into a wait per read
+    const int rows_s = nrow / kValuStreams;
+    auto run = [&](auto r_tag) __attribute__((always_inline)) {
+      constexpr int R = decltype(r_tag)::value;
+      for (int q0 = strm * rows_s; q0 < (strm + 1) * rows_s; q0 += R) {
+        float u1[R], u2[R], x2[R];
 #pragma unroll
-      // (every load and LDS read unconditional — U2 is a valid buffer for a critic too, and the input rows are zero
-      // past nin — with the actor / critic choice a select of values: a guard per read compiled into a wait per read)
-      for (int u = 0; u < 8; ++u) {
-        const int64_t o = (int64_t)(rc + q0 + u) * H + jj;
-        u1[u] = U1[o];
-        u2[u] = U2[o];
-        x2[u] = A2[o];
+        for (int t = 0; t < R; ++t) {
+          const int64_t o = (int64_t)(rc + q0 + t) * H + j;
+          u1[t] = U1[o];
+          u2[t] = U2[o];
+          x2[t] = A2[o];
+        }
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          const float a0 = S.s0[q0 + t], a1 = S.s1[q0 + t];
+          const float d1 = actor ? a0 * u1[t] + a1 * u2[t] : a0 * u1[t];
+          const float d2 = x2[t] > 0.0f ? (actor ? c1 * a0 + c2 * a1 : c1 * a0) : 0.0f;
+#pragma unroll
+          for (int i = 0; i < kXLd; ++i) w1a[i] = fmaf(d1, S.xs[q0 + t][i], w1a[i]);
+          b1a += d1;
+          b2a += d2;
+          ha1 = fmaf(a0, x2[t], ha1);
+          ha2 = fmaf(a1, x2[t], ha2);
+        }
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float a0 = S.s0[q0 + u], a1 = S.s1[q0 + u];
-        const float d1 = actor ? a0 * u1[u] + a1 * u2[u] : a0 * u1[u];
-        const float d2 = x2[u] > 0.0f ? (actor ? c1 * a0 + c2 * a1 : c1 * a0) : 0.0f;
-#pragma unroll
-        for (int i = 0; i < kXLd; ++i) w1a[i] = fmaf(d1, S.xs[q0 + u][i], w1a[i]);
-        b1a += d1;
-        b2a += d2;
-        ha1 = fmaf(a0, x2[u], ha1);
-        ha2 = fmaf(a1, x2[u], ha2);
-      }
-    }
+    };
+    if (rows_s % 8 == 0) run(std::integral_constant<int, 8>{});
+    else run(std::integral_constant<int, 2>{});
     __syncthreads();
   }
   SAC_STAMP(2, 2);
-  auto& vr = S.u.vred;
+  auto& vr = S.u.vred;  // [stream][accumulator][unit]
 #pragma unroll
-  for (int i = 0; i < kXLd; ++i) vr[w][i][lane] = w1a[i];
-  vr[w][kXLd][lane] = b1a;
-  vr[w][kXLd + 1][lane] = b2a;
-  vr[w][kXLd + 2][lane] = ha1;
-  vr[w][kXLd + 3][lane] = ha2;
+  for (int i = 0; i < kXLd; ++i) vr[strm][i][u] = w1a[i];
+  vr[strm][kXLd][u] = b1a;
+  vr[strm][kXLd + 1][u] = b2a;
+  vr[strm][kXLd + 2][u] = ha1;
+  vr[strm][kXLd + 3][u] = ha2;
   __syncthreads();
-  if (!jok) return;
-  auto total = [&](int i) { return ((vr[0][i][lane] + vr[1][i][lane]) + vr[2][i][lane]) + vr[3][i][lane]; };
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = w + 4 * q;
+  for (int q = 0; q < 2; ++q) {
+    const int k = strm + kValuStreams * q;
     if (k >= n_el) break;
-    const float g = total(k < nin ? k : kXLd + (k - nin));
+    const int i = k < nin ? k : kXLd + (k - nin);
+    float g = vr[0][i][u];
+#pragma unroll
+    for (int st = 1; st < kValuStreams; ++st) g += vr[st][i][u];
     const int64_t e = el_off(k);
     a.grads[e] = g;
     if (a.fuse) {
@@ -1491,9 +1547,9 @@ int32_t sacf_abi_version(void) { return SACF_ABI_VERSION; }
 const char* sacf_build_info(void) { return "sacfused gfx950 HIP src " SACF_SRC_HASH; }
 
 #ifdef SACF_PHASE_TIMING
-// diagnostics build: the last step's stamps, [3 kernels][kStampBlocks][4] (not in include/sac_fused.h)
+// diagnostics build: the last step's stamps, [3 kernels][kStampBlocks][kStamps] (not in include/sac_fused.h)
 int sacf_debug_stamps(unsigned long long* out, int n) {
-  const size_t bytes = sizeof(unsigned long long) * 3 * kStampBlocks * 4;
+  const size_t bytes = sizeof(unsigned long long) * 3 * kStampBlocks * kStamps;
   if (!out || (size_t)n * sizeof(unsigned long long) < bytes) return kStampBlocks;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sac_stamps), bytes) == hipSuccess ? 0 : -1;
 }
@@ -1703,7 +1759,7 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   w.ap = apply_args(h);
   const int CB = h->L.H / kTile2;
   w.n_mfma = 3 * CB * CB;
-  w.n_valu = 3 * ((h->L.H + 63) / 64);
+  w.n_valu = 3 * (h->L.H / kValuUnits);
   const Layout& L = h->L;
   for (int mat = 0; mat < 3; ++mat) {
     w.dy_src[mat] = mat == 0 ? h->s.h2 : h->s.g2[mat - 1];

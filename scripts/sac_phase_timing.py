@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DIAG = os.path.join(ROOT, "ast_sac_amd", "lib", "diag", "libsacfused_timing.so")
-KSTAMP = 8192
+KSTAMP, NST = 8192, 8
 
 
 def build():
@@ -63,20 +63,20 @@ def main():
     r = bench.bench_sac(dev, 1, None, a.steps, a.batch, eager_steps=0, graph=True)
     torch.cuda.synchronize()
     L = sacfused.load_library()
-    buf = (C.c_ulonglong * (3 * KSTAMP * 4))()
+    buf = (C.c_ulonglong * (3 * KSTAMP * NST))()
     assert L.sacf_debug_stamps(buf, len(buf)) == 0
     import numpy as np
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(3, KSTAMP, 4).astype(np.float64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(3, KSTAMP, NST).astype(np.float64)
     bp = (a.batch + 31) // 32 * 32
     bt, cb = bp // 32, a.hidden // 32
-    grids = [4 * bt * cb, 7 * bt * cb, 3 * cb * cb + 3 * ((a.hidden + 63) // 64) + 1]
+    grids = [4 * bt * cb, 7 * bt * cb, 3 * cb * cb + 3 * (a.hidden // 16) + 1]
     names = ["fwd (P1)", "mid (P2)", "wgrad (P3)"]
     res = {"step_us": r["ms_per_grad_step"] * 1e3, "batch": a.batch, "hidden": a.hidden, "kernels": {}}
     for k in range(3):
         s = st[k, :grids[k]]
         t0 = s[:, 0].min()
         rel = (s - t0) / 100.0  # 100 MHz ticks -> µs
-        ks = kinds(k, grids[k], bt, cb, 3 * cb * cb, 3 * ((a.hidden + 63) // 64))
+        ks = kinds(k, grids[k], bt, cb, 3 * cb * cb, 3 * (a.hidden // 16))
         per = {}
         for kind in dict.fromkeys(ks):
             m = rel[[i for i, x in enumerate(ks) if x == kind]]
@@ -89,6 +89,11 @@ def main():
                          "epilogue_med": float(np.median(m[:, 3] - m[:, 2])),
                          "epilogue_max": float((m[:, 3] - m[:, 2]).max()),
                          "exit_med": float(np.median(m[:, 3])), "exit_max": float(m[:, 3].max())}
+            for q in range(4, NST):  # prologue points stamped by this kind (0 = not stamped)
+                got = st[k, :grids[k]][[i for i, x in enumerate(ks) if x == kind], q] > 0
+                if got.all():
+                    per[kind][f"p{q}_since_entry_med"] = float(np.median(m[:, q] - m[:, 0]))
+                    per[kind][f"p{q}_since_entry_max"] = float((m[:, q] - m[:, 0]).max())
         res["kernels"][names[k]] = {"span_us": float(rel[:, 3].max()), "kinds": per}
     gaps = [(st[k + 1, :grids[k + 1], 0].min() - st[k, :grids[k], 3].max()) / 100.0 for k in range(2)]
     res["gaps_us"] = {"fwd_exit_to_mid_entry": gaps[0], "mid_exit_to_wgrad_entry": gaps[1]}
