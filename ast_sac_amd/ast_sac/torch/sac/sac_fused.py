@@ -211,14 +211,18 @@ class FusedSACTrainer(TorchTrainer):
         elif part == "b":
             sf.apply()
 
-    def _hip_step(self, replay_buffer):
-        sf = self._sf
+    def _hip_step_prepare(self, replay_buffer):
         if replay_buffer is not None and self._replay_key != id(replay_buffer):
             st = replay_buffer._store
-            sf.set_replay(st["observations"], st["actions"], st["rewards"], st["terminals"],
-                          st["next_observations"], replay_buffer._size_t, replay_buffer._max, self._seed)
+            self._sf.set_replay(st["observations"], st["actions"], st["rewards"], st["terminals"],
+                                st["next_observations"], replay_buffer._size_t, replay_buffer._max, self._seed)
             self._replay_key = id(replay_buffer)
             self._graphs = None
+            self._mgraph = None
+
+    def _hip_step(self, replay_buffer):
+        sf = self._sf
+        self._hip_step_prepare(replay_buffer)
         if self.noise_fn is not None:
             eps = self.noise_fn((2 * self.batch_size, 1)).reshape(-1)
             if self._eps_static is None:
@@ -236,10 +240,7 @@ class FusedSACTrainer(TorchTrainer):
             torch.cuda.synchronize(self.device)
             graphs = []
             if self.split and self.capture_collective:  # grads | all-reduce | update in one graph
-                if not self._collective_warm:  # the communicator's first collective runs eagerly (set-up)
-                    torch.distributed.all_reduce(torch.zeros(1, device=self.device), group=self.pg)
-                    torch.cuda.synchronize(self.device)
-                    self._collective_warm = True
+                self._warm_collective()
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     sf.set_stream()
@@ -261,6 +262,42 @@ class FusedSACTrainer(TorchTrainer):
         if len(graphs) > 1:
             self._allreduce()
             graphs[1].replay()
+
+    def _warm_collective(self):
+        if not self._collective_warm:  # the communicator's first collective runs eagerly (set-up)
+            torch.distributed.all_reduce(torch.zeros(1, device=self.device), group=self.pg)
+            torch.cuda.synchronize(self.device)
+            self._collective_warm = True
+
+    # grad steps per captured multi-step graph (hip backend, replay sampling on the device): consecutive steps
+    # inside one graph are separated by a kernel boundary instead of a graph launch from the host
+    GRAPH_STEPS = 8
+
+    def _multi_ok(self, replay_buffer):
+        return (self.backend == "hip" and self.use_graph and replay_buffer is not None and self.noise_fn is None
+                and (not self.split or self.capture_collective))
+
+    def _multi_graph(self, replay_buffer):
+        """The GRAPH_STEPS-step graph for this buffer: each step's kernels read the device step counter (the
+        Philox counter of the batch draw, Adam's bias corrections), so the steps are the same as one graph each."""
+        self._hip_step_prepare(replay_buffer)
+        key = (id(replay_buffer), self.GRAPH_STEPS)
+        if getattr(self, "_mgraph", None) is None or self._mgraph[0] != key:
+            sf = self._sf
+            torch.cuda.synchronize(self.device)
+            if self.split:
+                self._warm_collective()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                sf.set_stream()
+                for _ in range(self.GRAPH_STEPS):
+                    self._hip_launch(replay_buffer, "a" if self.split else "ab")
+                    if self.split:
+                        torch.distributed.all_reduce(self.flat_grad, group=self.pg)
+                        self._hip_launch(replay_buffer, "b")
+            sf.set_stream()
+            self._mgraph = (key, g)
+        return self._mgraph[1]
 
     # ---------------------------------------------------------------- math
     def _actor(self, x):
@@ -436,8 +473,22 @@ class FusedSACTrainer(TorchTrainer):
         self._after_step()
 
     def train_from_buffer(self, replay_buffer, n_steps=1):
-        """n_steps updates, each on a fresh uniform batch drawn on-device from a DeviceReplayBuffer."""
-        for _ in range(n_steps):
+        """n_steps updates, each on a fresh uniform batch drawn on-device from a DeviceReplayBuffer (hip backend:
+        runs of GRAPH_STEPS steps replay one multi-step graph; the steps and their results are the same)."""
+        done = 0
+        G = self.GRAPH_STEPS
+        if self._multi_ok(replay_buffer) and n_steps >= G:
+            if self._need_to_update_eval_statistics:  # the epoch's statistics are its first step's (sac.py:102-154)
+                self._num_train_steps += 1
+                self._run_step(replay_buffer)
+                self._after_step()
+                done = 1
+            while n_steps - done >= G:
+                self._multi_graph(replay_buffer).replay()
+                self._num_train_steps += G
+                self._n_train_steps_total += G
+                done += G
+        for _ in range(n_steps - done):
             self._num_train_steps += 1
             self._run_step(replay_buffer)
             self._after_step()

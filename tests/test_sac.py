@@ -275,6 +275,30 @@ def test_hip_sac_graph_replay_equals_eager_launches():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H,B", [(256, 256), (64, 96)])
+def test_hip_sac_multi_step_graph_equals_single_step_graphs(H, B):
+    """train_from_buffer's runs of GRAPH_STEPS steps in one captured graph give bitwise the parameters, targets,
+    Adam state, step counter and statistics of one graph replay per step (21 steps: the first alone for the
+    epoch statistics, two 8-step replays, four single steps)."""
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    rb = DeviceReplayBuffer(5000, 8, 1, "cuda")
+    b, _ = _rand_batch(3000, "cuda", seed=5)
+    rb.add_batch(b["observations"], b["actions"], b["rewards"], b["next_observations"], b["terminals"])
+    res = []
+    for multi in (True, False):
+        tr = _trainer("hip", H, B, "cuda", use_graph=True, seed=9)
+        tr._seed = 4321
+        if not multi:
+            tr.GRAPH_STEPS = 1 << 30  # (never reached: one graph per step)
+        tr.train_from_buffer(rb, 21)
+        torch.cuda.synchronize()
+        assert (getattr(tr, "_mgraph", None) is not None) == multi
+        assert int(tr._step_t.item()) == 21 and tr._n_train_steps_total == 21
+        res.append(torch.cat([tr.flat_param, tr.flat_target, tr._adam_m, tr._adam_v, tr._stats_t]).cpu())
+    assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("H,B", [(256, 256), (64, 96), (512, 100)])
 def test_hip_sac_split_update_equals_fused(H, B):
     """The data-parallel call pattern on one rank (sacf_grads | all-reduce over a world-size-1 group |
