@@ -320,18 +320,25 @@ __device__ __forceinline__ void load_b(float (&bv)[CS], const float* base, int H
   for (int i = 0; i < CS; ++i) bv[i] = base[(int64_t)(k0 + i) * H + col];
 }
 
-// W1 [H][nin] (row-major in the parameters) into LDS as W1ᵀ [nin][H], and b1 [H] after it. Every thread
-// issues all its loads before its first LDS store.
+// W1 [H][nin] (row-major in the parameters) into LDS as W1ᵀ [nin][H], and b1 [H] after it, in two halves: load()
+// issues this thread's loads into registers, store() writes LDS (and so waits for them) — the caller places other
+// loads in between by what its critical chain needs first (vmcnt counts loads in issue order)
 template <int H>
-__device__ __forceinline__ void stage_w1t(float* dst, const float* w1, const float* b1, int nin) {
-  constexpr int kIt = (H * kXLd + kThreads - 1) / kThreads;
+struct W1Stage {
+  static constexpr int kIt = (H * kXLd + kThreads - 1) / kThreads, kB = (H + kThreads - 1) / kThreads;
+  float v[kIt], bb[kB];
+  __device__ __forceinline__ void load(const float* w1, const float* b1, int nin) {
+    const int n = H * nin, tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) v[i] = tid + i * kThreads < n ? w1[tid + i * kThreads] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < kB; ++i) bb[i] = tid + i * kThreads < H ? b1[tid + i * kThreads] : 0.0f;
+  }
+  __device__ __forceinline__ void store(float* dst, int nin) const;
+};
+template <int H>
+__device__ __forceinline__ void W1Stage<H>::store(float* dst, int nin) const {
   const int n = H * nin, tid = threadIdx.x;
-  float v[kIt];
-#pragma unroll
-  for (int i = 0; i < kIt; ++i) v[i] = tid + i * kThreads < n ? w1[tid + i * kThreads] : 0.0f;
-  float bb[(H + kThreads - 1) / kThreads];
-#pragma unroll
-  for (int i = 0; i < (H + kThreads - 1) / kThreads; ++i) bb[i] = tid + i * kThreads < H ? b1[tid + i * kThreads] : 0.0f;
   int q = tid / nin, r = tid - q * nin;
   const int dq = kThreads / nin, dr = kThreads - dq * nin;
 #pragma unroll
@@ -345,7 +352,7 @@ __device__ __forceinline__ void stage_w1t(float* dst, const float* w1, const flo
     }
   }
 #pragma unroll
-  for (int i = 0; i < (H + kThreads - 1) / kThreads; ++i)
+  for (int i = 0; i < kB; ++i)
     if (tid + i * kThreads < H) dst[nin * H + tid + i * kThreads] = bb[i];
 }
 
@@ -474,13 +481,17 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   float x[kXLd];
   load_obs_row(src, idx, O, x);
   SAC_STAMP_ON(0, 5, x[0]);
+  // then W1 (needed before the barrier), then the B operand and epilogue weights (needed after it): the LDS
+  // stores below wait for W1 only
+  W1Stage<H> w1s;
+  w1s.load(P + L.p_w1, P + L.p_b1, O);
   float bv[CS];
   load_b<CS>(bv, a.T, H, kb, c0 + rl);  // actor W2ᵀ, chunk 0
   const float b2c = P[L.p_b2 + c0 + rl];
   const float wm = P[L.p_wm + c0 + rl], ws = P[L.p_ws + c0 + rl];
   float* lw1 = lds + FwdLds<H>::kW1Off;
   float* lx = lds + FwdLds<H>::kXOff;
-  stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
+  w1s.store(lw1, O);
   SAC_STAMP(0, 6);
   if (w == 0 && h == 0) {
 #pragma unroll
@@ -544,13 +555,15 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   float xin[kXLd];
   load_obs_row(a.obs, idx, O, xin);
   const float act = a.act[idx];
+  W1Stage<H> w1s;
+  w1s.load(C + L.c_w1, C + L.c_b1, O + 1);
   float bv[CS];
   const float* WT = a.T + (int64_t)(1 + net) * H * H;
   load_b<CS>(bv, WT, H, kb, c0 + rl);
   const float b2c = C[L.c_b2 + c0 + rl], w3 = C[L.c_w3 + c0 + rl];
   float* lw1 = lds + FwdLds<H>::kW1Off;
   float* lx = lds + FwdLds<H>::kXOff;
-  stage_w1t<H>(lw1, C + L.c_w1, C + L.c_b1, O + 1);
+  w1s.store(lw1, O + 1);
   if (w == 0 && h == 0) {
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
@@ -599,13 +612,18 @@ __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
 // ---------------------------------------------------------------------------------------------
 // the actor head of a row from its column-block parts (summed in block order) and its TanhNormal sample
 template <int CB>
-__device__ __forceinline__ void row_head(const MArgs& a, int hrow, float ev, float hd[6]) {
-  float pm[CB], pl[CB];
-  load_run<CB>(a.s.hpart + (int64_t)hrow * 2 * CB, pm);
-  load_run<CB>(a.s.hpart + (int64_t)hrow * 2 * CB + CB, pl);
-  const float* P = a.params;
-  tanh_normal(fold(pm) + P[a.L.p_bm], fold(pl) + P[a.L.p_bs], ev, hd);
-}
+struct RowHeadIn {
+  float pm[CB], pl[CB], bm, bs;
+  __device__ __forceinline__ void load(const MArgs& a, int hrow) {
+    load_run<CB>(a.s.hpart + (int64_t)hrow * 2 * CB, pm);
+    load_run<CB>(a.s.hpart + (int64_t)hrow * 2 * CB + CB, pl);
+    bm = a.params[a.L.p_bm];
+    bs = a.params[a.L.p_bs];
+  }
+  __device__ __forceinline__ void head(float ev, float hd[6]) const {
+    tanh_normal(fold(pm) + bm, fold(pl) + bs, ev, hd);
+  }
+};
 
 // Q(obs, ã) of critic `net` and its tangent along the action: with t1 = [g1 > 0] ⊙ W1[:, a] (fc0's action
 // column), v = t1 W2ᵀ and ∂Q/∂ã = Σ_cols w3 ⊙ [g2 > 0] ⊙ v (forward mode: one more MFMA chain on the same W2ᵀ
@@ -621,20 +639,27 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   const int r0 = rt * kTile2, c0 = by * kTile2;
   const int kb = w * (H / 4) + h * KS::N2;
   const int item = r0 + rl;
+  // loads in the order their consumers need them (vmcnt counts in issue order): the row's head parts (the head's
+  // transcendentals are the prologue's longest chain), its inputs, W1 (before the barrier), then the B operand and
+  // epilogue weights (after it)
+  RowHeadIn<CB> rh;
+  rh.load(a, (kTarget ? Bp : 0) + item);
   float xin[kXLd];
   load_run<kXLd>((kTarget ? a.s.xn : a.s.x) + (int64_t)item * kXLd, xin);
   const float ev = a.s.rec[(int64_t)item * kRec + (kTarget ? R_EPSN : R_EPS)];
+  W1Stage<H> w1s;
+  w1s.load(C + L.c_w1, C + L.c_b1, O + 1);
   float bv[CS];
   const float* WT = a.T + (int64_t)((kTarget ? 3 : 1) + net) * H * H;
   load_b<CS>(bv, WT, H, kb, c0 + rl);
   const float b2c = C[L.c_b2 + c0 + rl], w3 = C[L.c_w3 + c0 + rl];
   float* lw1 = lds + FwdLds<H>::kW1Off;
   float* lx = lds + FwdLds<H>::kXOff;
-  stage_w1t<H>(lw1, C + L.c_w1, C + L.c_b1, O + 1);
-  SAC_STAMP(1, 5);
   float hd[6];
-  row_head<CB>(a, (kTarget ? Bp : 0) + item, ev, hd);
+  rh.head(ev, hd);
   SAC_STAMP_ON(1, 4, hd[HD_A]);
+  w1s.store(lw1, O + 1);
+  SAC_STAMP(1, 5);
   if (w == 0 && h == 0) {
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
@@ -791,24 +816,36 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
 // per-row scalars (P3): everything the losses and the weight gradients need of one batch row, from the parts
 // the forward passes left (each reader sums them in block order, so every reader gets the same bits)
 // ---------------------------------------------------------------------------------------------
+// one row's inputs to its scalars: four consecutive part sets (critic: Q1, Q2 on the data rows and the two
+// targets; actor: Q1, Q2 on ã and the two tangents) and the row's record. load() only issues the loads, so a caller
+// can issue its other loads behind them before the scalars wait for these
+template <int CB>
+struct RowIn {
+  float p[4 * CB], rc[kRec];
+  __device__ __forceinline__ void load(const MArgs& a, int r, bool actor) {
+    load_run<4 * CB>(a.s.part + ((int64_t)r * PS_N + (actor ? PS_Q1A : PS_Q1D)) * CB, p);
+    load_run<kRec>(a.s.rec + (int64_t)r * kRec, rc);
+  }
+  // Σ of set k's column-block parts in block order (a left fold: every reader gets the same bits)
+  __device__ __forceinline__ float sum(int k) const {
+    float s = p[k * CB];
+#pragma unroll
+    for (int i = 1; i < CB; ++i) s += p[k * CB + i];
+    return s;
+  }
+};
+
 struct CriticRow {
   float q1, q2, y;  // Q1 / Q2 predictions on (obs, a), the clamped target (sac.py:232-247)
 };
 template <int CB>
-__device__ __forceinline__ CriticRow critic_row(const MArgs& a, int r, float alpha) {
-  const float* pt = a.s.part + (int64_t)r * PS_N * CB;
-  float p0[CB], p1[CB], p2[CB], p3[CB];
-  load_run<CB>(pt + PS_Q1D * CB, p0);
-  load_run<CB>(pt + PS_Q2D * CB, p1);
-  load_run<CB>(pt + PS_T1 * CB, p2);
-  load_run<CB>(pt + PS_T2 * CB, p3);
+__device__ __forceinline__ CriticRow critic_row(const MArgs& a, const RowIn<CB>& in, float alpha) {
   const float* sn = a.s.snap;  // (the pre-update biases: P3 updates the live ones)
-  const float* rc = a.s.rec + (int64_t)r * kRec;
-  const float logpn = rc[R_LOGPN], rw = rc[R_REW], tm = rc[R_TERM];
+  const float logpn = in.rc[R_LOGPN], rw = in.rc[R_REW], tm = in.rc[R_TERM];
   CriticRow o;
-  o.q1 = fold(p0) + sn[SN_BQ1];
-  o.q2 = fold(p1) + sn[SN_BQ2];
-  const float t1 = fold(p2) + sn[SN_BT1], t2 = fold(p3) + sn[SN_BT2];
+  o.q1 = in.sum(0) + sn[SN_BQ1];
+  o.q2 = in.sum(1) + sn[SN_BQ2];
+  const float t1 = in.sum(2) + sn[SN_BT1], t2 = in.sum(3) + sn[SN_BT2];
   const float tq = fminf(t1, t2) - alpha * logpn;
   float y = a.hp.rscale * rw + ((1.0f - tm) * a.hp.gamma) * tq;
   o.y = fminf(fmaxf(y, -a.hp.clip), a.hp.clip);
@@ -823,26 +860,19 @@ struct ActorRow {
 // π-loss through min(Q1, Q2)(obs, ã) (sac.py:185-205): dA = ∂/∂ã from the tangent parts, then TanhNormal's
 // reparameterised backward to (mean, log_std)
 template <int CB>
-__device__ __forceinline__ ActorRow actor_row(const MArgs& a, int r, float alpha, float log_alpha) {
+__device__ __forceinline__ ActorRow actor_row(const MArgs& a, const RowIn<CB>& in, float alpha, float log_alpha) {
   const Layout& L = a.L;
-  const float* pt = a.s.part + (int64_t)r * PS_N * CB;
-  float p4[CB], p5[CB], p6[CB], p7[CB];
-  load_run<CB>(pt + PS_Q1A * CB, p4);
-  load_run<CB>(pt + PS_Q2A * CB, p5);
-  load_run<CB>(pt + PS_D1 * CB, p6);
-  load_run<CB>(pt + PS_D2 * CB, p7);
-  float rc[kRec];
-  load_run<kRec>(a.s.rec + (int64_t)r * kRec, rc);
+  const float* rc = in.rc;
   const float mean = rc[HD_MEAN], ls_raw = rc[HD_LSRAW], std = rc[HD_STD];
   const float z = rc[HD_Z], act = rc[HD_A], logp = rc[HD_LOGP];
   const float eps_i = rc[R_EPS];
   const float* sn = a.s.snap;
-  const float q1a = fold(p4) + sn[SN_BQ1];
-  const float q2a = fold(p5) + sn[SN_BQ2];
+  const float q1a = in.sum(0) + sn[SN_BQ1];
+  const float q2a = in.sum(1) + sn[SN_BQ2];
   const float invB = 1.0f / (float)L.B;
   // d min(Q1, Q2): all to the smaller, split evenly on a tie (torch.min's backward)
   const float w1 = (q1a < q2a) ? 1.0f : ((q1a == q2a) ? 0.5f : 0.0f);
-  float dA = (-w1 * invB) * fold(p6) + (-(1.0f - w1) * invB) * fold(p7);
+  float dA = (-w1 * invB) * in.sum(2) + (-(1.0f - w1) * invB) * in.sum(3);
   if (a.hp.areg != 0.0f) dA += (a.hp.areg * invB) * (2.0f * act);
   const float ainv = alpha * invB;
   const float d = z - mean, var = std * std;
@@ -985,27 +1015,15 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
   const int64_t out_off = a.w2_off[mat];
   AdamElem xe[4];  // the optimizer state of the four outputs this lane finishes, in flight during the GEMM
-  if (a.fuse)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      xe[q] = adam_ld(a.ap, out_off + (int64_t)(j0 + finish_row(q)) * H + k0 + rl, !actor, false);
   f32x16 acc = zero16();
   for (int rc = 0; rc < Bp; rc += kRowChunk) {
     const int nrow = min(kRowChunk, Bp - rc);
     const int rows_w = nrow / 4, n2 = rows_w / 2, rl0 = w * rows_w + h * n2;
-    // the row scalars of rows rc + tid (every thread computes one: no branch splits the loads)
+    // loads in the order they are consumed (vmcnt counts in issue order): the inputs of row rc + tid's scalars
+    // (every thread computes one), the chunk's operands, then (first chunk) the Adam state
     const int r = min(rc + tid, Bp - 1);
-    float s0, s1 = 0.0f;
-    if (actor) {
-      const ActorRow ar = actor_row<CB>(m, r, alpha, log_alpha);
-      s0 = ar.dmean;
-      s1 = ar.dls;
-    } else {
-      const CriticRow cr = critic_row<CB>(m, r, alpha);
-      s0 = (2.0f / (float)B) * ((net == 0 ? cr.q1 : cr.q2) - cr.y);
-    }
-    if (rc + tid >= B) s0 = s1 = 0.0f;
-    SAC_STAMP_ON(2, 4, s0);
+    RowIn<CB> rin;
+    rin.load(m, r, actor);
     // the chunk's operands as one straight-line batch of loads (a run-time guard per load would make a chain of
     // branches with a wait after every load): n2 = 32 for full chunks, 16 / 8 / 4 for Bp = 128 / 64 / 32
     float yv[kMaxN2], xv[kMaxN2];
@@ -1031,6 +1049,21 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
         xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
       }
     }
+    if (rc == 0 && a.fuse)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        xe[q] = adam_ld(a.ap, out_off + (int64_t)(j0 + finish_row(q)) * H + k0 + rl, !actor, false);
+    float s0, s1 = 0.0f;
+    if (actor) {
+      const ActorRow ar = actor_row<CB>(m, rin, alpha, log_alpha);
+      s0 = ar.dmean;
+      s1 = ar.dls;
+    } else {
+      const CriticRow cr = critic_row<CB>(m, rin, alpha);
+      s0 = (2.0f / (float)B) * ((net == 0 ? cr.q1 : cr.q2) - cr.y);
+    }
+    if (rc + tid >= B) s0 = s1 = 0.0f;
+    SAC_STAMP_ON(2, 4, s0);
     SAC_STAMP_ON(2, 5, yv[kMaxN2 - 1] + xv[kMaxN2 - 1]);
     S.s0[tid] = s0;
     S.s1[tid] = s1;
@@ -1129,18 +1162,20 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
   for (int rc = 0; rc < Bp; rc += kRowChunk) {
     const int nrow = min(kRowChunk, Bp - rc);
     const int r = min(rc + tid, Bp - 1);
+    RowIn<CB> rin;
+    rin.load(m, r, actor);
+    float xr[kXLd];
+    load_run<kXLd>(XR + (int64_t)r * kXLd, xr);
     float s0, s1 = 0.0f;
     if (actor) {
-      const ActorRow ar = actor_row<CB>(m, r, alpha, log_alpha);
+      const ActorRow ar = actor_row<CB>(m, rin, alpha, log_alpha);
       s0 = ar.dmean;
       s1 = ar.dls;
     } else {
-      const CriticRow cr = critic_row<CB>(m, r, alpha);
+      const CriticRow cr = critic_row<CB>(m, rin, alpha);
       s0 = (2.0f / (float)B) * ((cn == 0 ? cr.q1 : cr.q2) - cr.y);
     }
     if (rc + tid >= B) s0 = s1 = 0.0f;
-    float xr[kXLd];
-    load_run<kXLd>(XR + (int64_t)r * kXLd, xr);
     S.s0[tid] = s0;
     S.s1[tid] = s1;
 #pragma unroll
@@ -1229,8 +1264,11 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   for (int rc = 0; rc < Bp; rc += kRowChunk) {
     const int r = rc + tid;
     if (r >= B) continue;
-    const CriticRow cr = critic_row<CB>(m, r, alpha);
-    const ActorRow ar = actor_row<CB>(m, r, alpha, log_alpha);
+    RowIn<CB> rq, ra;
+    rq.load(m, r, false);
+    ra.load(m, r, true);
+    const CriticRow cr = critic_row<CB>(m, rq, alpha);
+    const ActorRow ar = actor_row<CB>(m, ra, alpha, log_alpha);
     const float d1 = cr.q1 - cr.y, d2 = cr.q2 - cr.y;
     v[0] += ar.pl;
     v[1] += d1 * d1;
@@ -1397,13 +1435,15 @@ __global__ __launch_bounds__(256) void sac_act_fwd_kernel(ActArgs a) {
   float x[kXLd];
 #pragma unroll
   for (int m = 0; m < kXLd; ++m) x[m] = m < O ? a.obs[rowc * a.obs_stride + m] : 0.0f;
+  W1Stage<H> w1s;
+  w1s.load(P + L.p_w1, P + L.p_b1, O);
   float bv[CS];
   load_b<CS>(bv, a.T, H, kb, c0 + rl);
   const float b2c = P[L.p_b2 + c0 + rl];
   const float wm = P[L.p_wm + c0 + rl], ws = P[L.p_ws + c0 + rl];
   float* lw1 = lds + FwdLds<H>::kW1Off;
   float* lx = lds + FwdLds<H>::kXOff;
-  stage_w1t<H>(lw1, P + L.p_w1, P + L.p_b1, O);
+  w1s.store(lw1, O);
   if (w == 0 && h == 0)
     for (int m = 0; m < O; ++m) lx[rl * (kXLd + 1) + m] = x[m];
   __syncthreads();
