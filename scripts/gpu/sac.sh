@@ -10,7 +10,7 @@ if [ "$NOTESTS" != "notests" ]; then
     -p no:cacheprovider --timeout 300 --timeout-method thread > "$O/pytest_sac_$TAG.txt" 2>&1
   rc=$?; tail -3 "$O/pytest_sac_$TAG.txt"; soft_pytest $rc pytest_sac
 fi
-for b in 256 128 32 1024; do
+for b in 256 128 64 32 1024; do
   timeout -k 10 200 python scripts/prof_sac.py --steps 3000 --graph 1 --batch $b > "$O/sac_time_${TAG}_b$b.txt" 2>&1
   hard $? sac_time_$b; echo "B=$b $(tail -1 "$O/sac_time_${TAG}_b$b.txt")"
 done
