@@ -590,7 +590,6 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   if (psi_w != psi_d) sincos(psi_w, &sp0, &cp0);
   const double H2 = sbmpc_h2(in, ichi, jp);
   int i_last = n_samp - 1;  // (set by the skip test below)
-  int i_first = 1;          // first sample that can be within range (ditto)
   int i_past = n_samp + 1;  // first sample past the closest approach, with a one-sample margin (ditto)
   // Exact skip of the horizon loop: H0 can only be non-zero at samples with dist < max_d_safe.
   // After sample 0 both predictions are straight lines (the own ship's sway is zeroed after the
@@ -618,11 +617,6 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     const double disc = b * b - ww * cq;
     const double j2 = (ww > 0 && disc >= 0) ? (-b + sqrt(disc)) * iww : (double)n_samp;
     i_last = (j2 < (double)(n_samp - 2)) ? (int)floor(j2) + 2 : n_samp - 1;
-    // First sample that can be within range: before the smaller root j1 the relative position stays beyond lim
-    // too (convexity again). The horizon loop starts there, one sample early, after advancing the positions by
-    // the same incremental sums. Sample i = j + 1.
-    const double j1 = (ww > 0 && disc >= 0) ? (-b - sqrt(disc)) * iww : 0.0;
-    i_first = (j1 > 1.0) ? (int)fmin(floor(j1), (double)(n_samp - 1)) : 1;
     // Past the continuous minimum k of |P1 + j·W| both t and the distance grow, so the ranking t·d⁴ grows
     // sample by sample: once a sample there ranks beyond the best so far by more than the runner-up band,
     // no later sample can win or tie (and a later sample's flags cannot change the result). Sample i = j + 1;
@@ -670,30 +664,9 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   auto sample = [&](double tt, double d0, double d1, double d2s, bool inr) __attribute__((always_inline)) {
     hz_sample(hb, hc, tt, d0, d1, d2s, inr);
   };
-  // the samples before every lane's i_first cannot be in range for any lane: their positions only (the loop body's
-  // sums, in its order). The wave's smallest i_first by a ballot search (wave-uniform: the loops stay uniform)
-  int i_w = 1;
-  {
-    int hi = n_samp;  // the minimum is in [i_w, hi)
-    while (hi - i_w > 1) {
-      const int mid = (i_w + hi) >> 1;
-      if (__any(i_first < mid)) hi = mid;
-      else i_w = mid;
-    }
-  }
-  int i = 1;
-  for (; i < i_w; ++i) {
-    ox = ox + dox;
-    oy = oy + doy;
-    if (i > 1) {
-      sx = sx + dsx;
-      sy = sy + dsy;
-    }
-    t += DT;
-  }
 #ifdef SHIPSIM_SB_ROLLED  // diagnostics build: one sample per iteration
   bool done = false;  // past the minimum and beyond the best (see i_past)
-  for (; i < n_samp; ++i) {
+  for (int i = 1; i < n_samp; ++i) {
     if (!__any((i <= i_last) & !done)) break;  // every lane of the wave is past its last useful sample
     ox = ox + dox;
     oy = oy + doy;
@@ -713,6 +686,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   // two samples per iteration (i, i + 1): their bodies are independent chains the one wave of the SIMD
   // can interleave; the positions are the same incremental sums as one per iteration, and the samples
   // enter the running best in order (ties keep the earlier sample)
+  int i = 1;
   bool done = false;  // past the minimum and beyond the best (see i_past)
   for (; i + 1 < n_samp; i += 2) {
     if (!__any((i <= i_last) & !done)) break;  // every lane of the wave is past its last useful sample
