@@ -386,6 +386,19 @@ __device__ __forceinline__ void store_slice(float* base, int r0, int by, const f
 __device__ __forceinline__ void load_obs_row(const float* src, int64_t idx, int O, float (&x)[kXLd]) {
   int Ov = O;
   asm volatile("" : "+v"(Ov));
+  if ((O & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {  // (uniform) 16-byte rows: kXLd / 4 float4s
+    const float4* p = reinterpret_cast<const float4*>(src + idx * O);
+#pragma unroll
+    for (int q = 0; q < kXLd / 4; ++q) {
+      const float4 v = p[min(q, (Ov >> 2) - 1)];
+      const bool in = 4 * q < Ov;
+      x[4 * q] = in ? v.x : 0.0f;
+      x[4 * q + 1] = in ? v.y : 0.0f;
+      x[4 * q + 2] = in ? v.z : 0.0f;
+      x[4 * q + 3] = in ? v.w : 0.0f;
+    }
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < kXLd; ++m) {
     const float v = src[idx * O + min(m, Ov - 1)];
@@ -969,8 +982,13 @@ struct WLds {
   float xs[kRowChunk][kXLd + 1];
   float red[4][32];
   float sum[32];
-  AdamStep sst;
 };
+
+// this step's Adam bias corrections (the mid kernel wrote them): read by every block at its start, into registers,
+// for its epilogue (no block barrier on the load)
+__device__ __forceinline__ AdamStep adam_step_of(const MArgs& m) {
+  return AdamStep{m.stats[5], m.stats[6], m.stats[7]};
+}
 
 __device__ __forceinline__ float alpha_of(const MArgs& a) {
   return a.hp.auto_ent ? expf(a.s.snap[SN_LOGA]) : 1.0f;
@@ -999,6 +1017,7 @@ template <int H>
 __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   constexpr int CB = H / kTile2;
   const MArgs& m = a.m;
+  const AdamStep sst = adam_step_of(m);
   const Layout& L = m.L;
   const int B = L.B, Bp = L.Bp;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5, rl = lane & 31;
@@ -1095,7 +1114,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     a.grads[e] = v;
     if (a.fuse) {
       xe[q].g = v;
-      adam_st(a.ap, S.sst, e, xe[q], mat > 0);
+      adam_st(a.ap, sst, e, xe[q], mat > 0);
       tt[0][cc][rr] = xe[q].p;
       tt[1][cc][rr] = xe[q].t;
     }
@@ -1124,6 +1143,7 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
   constexpr int CB = H / kTile2, NB = H / kValuUnits;
   static_assert(H % kValuUnits == 0, "units per VALU block");
   const MArgs& m = a.m;
+  const AdamStep sst = adam_step_of(m);
   const Layout& L = m.L;
   const int B = L.B, Bp = L.Bp;
   const int tid = threadIdx.x;
@@ -1237,7 +1257,7 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
     a.grads[e] = g;
     if (a.fuse) {
       xe[q].g = g;
-      adam_st(a.ap, S.sst, e, xe[q], !actor);
+      adam_st(a.ap, sst, e, xe[q], !actor);
     }
   }
 }
@@ -1248,6 +1268,7 @@ template <int H>
 __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   constexpr int CB = H / kTile2;
   const MArgs& m = a.m;
+  const AdamStep sst = adam_step_of(m);
   const Layout& L = m.L;
   const int B = L.B, Bp = L.Bp, tid = threadIdx.x;
   const float alpha = alpha_of(m), log_alpha = m.s.snap[SN_LOGA];
@@ -1302,7 +1323,7 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   a.grads[off] = g;
   if (a.fuse && (tid > 0 || m.hp.auto_ent)) {
     xs.g = g;
-    adam_st(a.ap, S.sst, off, xs, tid >= 3);
+    adam_st(a.ap, sst, off, xs, tid >= 3);
   }
 }
 
@@ -1321,8 +1342,6 @@ __global__ __launch_bounds__(256) void sac_wgrad_kernel(WArgs a_arg) {
   __shared__ WLds S;
   const WArgs& a = wargs();
   SAC_STAMP(2, 0);
-  if (threadIdx.x == 0) S.sst = AdamStep{a.m.stats[5], a.m.stats[6], a.m.stats[7]};
-  __syncthreads();
   const int bx = (int)blockIdx.x;
   if (bx < a.n_mfma) p3_mfma_tile<H>(a, bx, S);
   else if (bx < a.n_mfma + a.n_valu) p3_valu_block<H>(a, bx - a.n_mfma, S);
