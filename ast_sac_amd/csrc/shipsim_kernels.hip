@@ -551,7 +551,10 @@ __device__ __forceinline__ void hz_sample(HzBest& h, const HzConst c, double tt,
   h.s1 = fmin(h.s1, sc);
 }
 
-__device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp) {
+// part -1: the whole horizon on this lane. part 0 / 1: this lane and its partner (lane ^ 32: the same scenario of the
+// same request) split the horizon's sample loop — part 0 takes the samples before i_split, part 1 the rest — and merge
+// their running bests (every other step is computed by both; the result is the same bits as part -1)
+__device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp, int part = -1) {
 #ifdef SHIPSIM_PHASE_TIMING
   SbTimer sb_timer;
 #endif
@@ -590,6 +593,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   if (psi_w != psi_d) sincos(psi_w, &sp0, &cp0);
   const double H2 = sbmpc_h2(in, ichi, jp);
   int i_last = n_samp - 1;  // (set by the skip test below)
+  int i_first = 1;          // first sample that can be within range (ditto; only places the split)
   int i_past = n_samp + 1;  // first sample past the closest approach, with a one-sample margin (ditto)
   // Exact skip of the horizon loop: H0 can only be non-zero at samples with dist < max_d_safe.
   // After sample 0 both predictions are straight lines (the own ship's sway is zeroed after the
@@ -617,6 +621,8 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     const double disc = b * b - ww * cq;
     const double j2 = (ww > 0 && disc >= 0) ? (-b + sqrt(disc)) * iww : (double)n_samp;
     i_last = (j2 < (double)(n_samp - 2)) ? (int)floor(j2) + 2 : n_samp - 1;
+    const double j1 = (ww > 0 && disc >= 0) ? (-b - sqrt(disc)) * iww : 0.0;
+    i_first = (j1 > 1.0) ? (int)fmin(floor(j1), (double)(n_samp - 1)) : 1;
     // Past the continuous minimum k of |P1 + j·W| both t and the distance grow, so the ranking t·d⁴ grows
     // sample by sample: once a sample there ranks beyond the best so far by more than the runner-up band,
     // no later sample can win or tie (and a later sample's flags cannot change the result). Sample i = j + 1;
@@ -664,7 +670,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   auto sample = [&](double tt, double d0, double d1, double d2s, bool inr) __attribute__((always_inline)) {
     hz_sample(hb, hc, tt, d0, d1, d2s, inr);
   };
-#ifdef SHIPSIM_SB_ROLLED  // diagnostics build: one sample per iteration
+#ifdef SHIPSIM_SB_ROLLED  // diagnostics build: one sample per iteration (no split: the caller passes part -1)
   bool done = false;  // past the minimum and beyond the best (see i_past)
   for (int i = 1; i < n_samp; ++i) {
     if (!__any((i <= i_last) & !done)) break;  // every lane of the wave is past its last useful sample
@@ -685,11 +691,30 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
 #else
   // two samples per iteration (i, i + 1): their bodies are independent chains the one wave of the SIMD
   // can interleave; the positions are the same incremental sums as one per iteration, and the samples
-  // enter the running best in order (ties keep the earlier sample)
-  int i = 1;
+  // enter the running best in order (ties keep the earlier sample).
+  // Split (part 0 / 1): the window of samples that can be in range, [i_first, min(i_last, i_past + 2)], is cut at
+  // its middle; part 1 first advances its positions to the cut by the loop's own sums (a uniform loop, the other
+  // lanes predicated off), then both parts run the loop side by side on their own sample indices.
+  int i_stop = n_samp, i = 1;
+  if (part >= 0) {
+    const int w0 = max(i_first, 1), w1 = max(w0, min(i_last, i_past + 2));
+    const int i_split = min(w0 + (w1 - w0 + 1) / 2, n_samp);
+    if (part == 0) i_stop = i_split;
+    const int i_start = part == 1 ? i_split : 1;
+    for (int c = 1; __any(c < i_start); ++c) {
+      const bool adv = c < i_start, adv_s = adv & (c > 1);
+      ox = adv ? ox + dox : ox;
+      oy = adv ? oy + doy : oy;
+      sx = adv_s ? sx + dsx : sx;
+      sy = adv_s ? sy + dsy : sy;
+      t = adv ? t + DT : t;
+    }
+    i = i_start;
+  }
   bool done = false;  // past the minimum and beyond the best (see i_past)
-  for (; i + 1 < n_samp; i += 2) {
-    if (!__any((i <= i_last) & !done)) break;  // every lane of the wave is past its last useful sample
+  for (;; i += 2) {
+    // (per lane: a split part has its own sample index; unsplit every lane has the same one)
+    if (!__any((i + 1 < n_samp) & (i <= i_last) & !done & (i < i_stop))) break;  // every lane past its useful samples
     const double oxa = ox + dox, oya = oy + doy;
     const double sxa = (i > 1) ? sx + dsx : sx, sya = (i > 1) ? sy + dsy : sy;
     const double ta = t + DT;
@@ -700,24 +725,44 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     t = ta + DT;
     const double d0a = oxa - sxa, d1a = oya - sya, d0b = ox - sx, d1b = oy - sy;
     const double d2a = d0a * d0a + d1a * d1a, d2b = d0b * d0b + d1b * d1b;
-    const bool ia = d2a < lim2, ib = d2b < lim2;
+    const bool ia = (d2a < lim2) & (i + 1 < n_samp) & (i < i_stop);
+    const bool ib = (d2b < lim2) & (i + 1 < n_samp) & (i + 1 < i_stop);
     if (ia | ib) {
       sample(ta, d0a, d1a, d2a, ia);
       sample(t, d0b, d1b, d2b, ib);
     }
     done = done | ((i + 1 >= i_past) & (hb.s1 < INFINITY) & (t * d2b * d2b > hb.s1 * (1.0 + 2e-10)));
   }
-  if (i < n_samp && __any((i <= i_last) & !done)) {  // the last sample of an odd count
-    ox = ox + dox;
-    oy = oy + doy;
-    if (i > 1) {
-      sx = sx + dsx;
-      sy = sy + dsy;
+  {
+    const bool lo = (i < n_samp) & (i < i_stop);
+    if (__any(lo & (i <= i_last) & !done)) {  // the last sample of an odd count
+      ox = ox + dox;
+      oy = oy + doy;
+      if (i > 1) {
+        sx = sx + dsx;
+        sy = sy + dsy;
+      }
+      t += DT;
+      const double d0 = ox - sx, d1 = oy - sy;
+      const double d2s = d0 * d0 + d1 * d1;
+      if ((d2s < lim2) & lo) sample(t, d0, d1, d2s, true);
     }
-    t += DT;
-    const double d0 = ox - sx, d1 = oy - sy;
-    const double d2s = d0 * d0 + d1 * d1;
-    if (d2s < lim2) sample(t, d0, d1, d2s, true);
+  }
+  if (part >= 0) {  // the two parts' running bests in sample order: part 0's samples come first
+    const int pl = (threadIdx.x & 63) ^ 32;
+    HzBest o;
+    o.s1 = shfl_d(hb.s1, pl);
+    o.s2 = shfl_d(hb.s2, pl);
+    o.t1 = shfl_d(hb.t1, pl);
+    o.q1 = shfl_d(hb.q1, pl);
+    o.unc = __shfl((int)hb.unc, pl, 64) != 0;
+    const HzBest A = part == 0 ? hb : o, Bp = part == 0 ? o : hb;
+    const bool bwin = Bp.s1 < A.s1;  // (ties keep the earlier sample)
+    hb.s1 = fmin(A.s1, Bp.s1);
+    hb.s2 = fmin(fmin(A.s2, Bp.s2), fmax(A.s1, Bp.s1));  // the second smallest of both
+    hb.t1 = bwin ? Bp.t1 : A.t1;
+    hb.q1 = bwin ? Bp.q1 : A.q1;
+    hb.unc = A.unc | Bp.unc;
   }
 #endif
   const double s1 = hb.s1, s2 = hb.s2, t1 = hb.t1, q1 = hb.q1;
@@ -791,8 +836,13 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
     g.ob_so = shfl_d(in.ob_so, srcc); g.ob_co = shfl_d(in.ob_co, srcc);
     double cost = INFINITY;
     int idx = 64;
-    if (src >= 0 && scen < 28) {
-      cost = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3);
+#ifdef SHIPSIM_SB_ROLLED
+    const bool split = false;
+#else
+    const bool split = src1 < 0;  // (uniform) one request this pass: both halves take it, each half of every horizon
+#endif
+    if ((split || src >= 0) && scen < 28) {
+      cost = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3, split ? half : -1);
       idx = scen;
     }
     // argmin over the half-wave; ties -> lowest scenario index (first strict improvement in the
