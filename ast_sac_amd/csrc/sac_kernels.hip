@@ -87,6 +87,12 @@ struct Scr {
   float *uq[2];              // critic backward factors (data rows)
   float *rec;                // [Bp][kRec] per-row record (HD_* / R_*)
   float *hpart;              // [2Bp][2][CB] actor head parts (mean | log_std) of the obs and next_obs rows
+  // fc0 of a critic up to (not including) its action term — b1 + Σ_{m < O} W1[:, m] x_m, the fmaf chain in input
+  // order — on the obs rows (Q1, Q2: from P1's data tiles) and the next_obs rows (T1, T2: P1's target tiles), and
+  // fc0's action column W1[:, O] of Q1, Q2, T1, T2 [4][H]: P2's critic tiles on (obs, ã) / (next_obs, ã') add the
+  // action term themselves (the same chain, so the same bits as fc0 on the whole row)
+  float *pre[4];             // [Bp][H] each: Q1, Q2 (obs rows), T1, T2 (next_obs rows)
+  float *w1a;                // [4][H]
   float *part;               // [Bp][PS_N][CB]
   // the parameters P3 reads, as they were before this step's update (P3 updates them in place with fused Adam,
   // so its blocks must not read the live values): [log α, b3 Q1, b3 Q2, b3 T1, b3 T2, -, -, -] then
@@ -371,6 +377,23 @@ __device__ __forceinline__ void first_layer(const float* lw1t, const float* xin,
   for (int i = 0; i < CS; ++i) av[i] = relu(av[i]);
 }
 
+// the same chain, also returning its value before the last input's term (the critics' pre-activation without the
+// action: fmaf(W1[k][nin - 1], x[nin - 1], pre) is exactly the chain's last step)
+template <int H, int CS>
+__device__ __forceinline__ void first_layer_pre(const float* lw1t, const float* xin, int nin, int k0, float (&pre)[CS],
+                                                float (&av)[CS]) {
+#pragma unroll
+  for (int i = 0; i < CS; ++i) pre[i] = lw1t[nin * H + k0 + i];
+  for (int m = 0; m < nin - 1; ++m) {
+    const float xm = xin[m];
+#pragma unroll
+    for (int i = 0; i < CS; ++i) pre[i] = fmaf(lw1t[m * H + k0 + i], xm, pre[i]);
+  }
+  const float xl = xin[nin - 1];
+#pragma unroll
+  for (int i = 0; i < CS; ++i) av[i] = relu(fmaf(lw1t[(nin - 1) * H + k0 + i], xl, pre[i]));
+}
+
 // this lane's first-layer chunk (row lane & 31, columns k0 .. k0 + CS) straight to its row of the matrix by the
 // block that owns column block k0 / 32 (every block computes the same values): float4 stores
 template <int H, int CS>
@@ -592,11 +615,14 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   for (int c = 0; c < KS::NCH; ++c) {
     const int k0 = kb + c * CS;
     if (c) load_b<CS>(bv, WT, H, k0, c0 + rl);
-    float av[CS];
-    first_layer<H, CS>(lw1, lx + rl * (kXLd + 1), O + 1, k0, av);
+    float av[CS], pre[CS];
+    first_layer_pre<H, CS>(lw1, lx + rl * (kXLd + 1), O + 1, k0, pre, av);
     store_slice<H, CS>(a.s.g1[net], r0, by, av, k0);
+    store_slice<H, CS>(a.s.pre[net], r0, by, pre, k0);
     mfma_n<CS>(acc, av, bv);
   }
+  if (rt == 0 && by == 0)  // fc0's action column, contiguous, for P2
+    for (int k = threadIdx.x; k < H; k += kThreads) a.s.w1a[net * H + k] = lw1[O * H + k];
   SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
@@ -607,6 +633,37 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   });
 }
 
+// target critic `net`'s fc0 pre-activation (without the action term) on the next_obs rows of row tile rt, columns
+// by·32 .. by·32 + 31: thread t takes row t / 8 and four columns, the fmaf chain from the bias in input order as
+// first_layer; also fc0's action column of those columns (row tile 0)
+template <int H>
+__device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int rt, int by) {
+  const Layout& L = a.L;
+  const int O = L.O, nin = O + 1;
+  const float* C = a.targets + (int64_t)net * L.q_size;
+  const int tid = threadIdx.x, row = tid >> 3, k0 = by * kTile2 + (tid & 7) * 4;
+  const int item = rt * kTile2 + row;
+  float e0, e1;
+  const int64_t idx = batch_item(a, item, e0, e1);
+  float x[kXLd];
+  load_obs_row(a.nobs, idx, O, x);
+  float w[4][kXLd], pre[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pre[j] = C[L.c_b1 + k0 + j];
+#pragma unroll
+    for (int m = 0; m < kXLd; ++m) w[j][m] = m < nin ? C[L.c_w1 + (int64_t)(k0 + j) * nin + m] : 0.0f;
+  }
+#pragma unroll
+  for (int m = 0; m < kXLd; ++m)  // (unrolled, the run-time bound a select: no dynamic index into w)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pre[j] = m < O ? fmaf(w[j][m], x[m], pre[j]) : pre[j];
+  *reinterpret_cast<float4*>(a.s.pre[2 + net] + (int64_t)item * H + k0) = make_float4(pre[0], pre[1], pre[2], pre[3]);
+  if (rt == 0 && row == 0)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a.s.w1a[(2 + net) * H + k0 + j] = C[L.c_w1 + (int64_t)(k0 + j) * nin + O];
+}
+
 template <int H>
 __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
   __shared__ float lds[FwdLds<H>::kFloats];
@@ -615,7 +672,8 @@ __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
   tile_of<H>(bx, by);
   const int bt = a.L.Bp / kTile2;
   if (bx < 2 * bt) p1_actor_tile<H>(a, bx, by, lds);
-  else p1_data_tile<H>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
+  else if (bx < 4 * bt) p1_data_tile<H>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
+  else p1_target_pre_tile<H>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by);
   SAC_STAMP(0, 3);
 }
 
@@ -652,55 +710,54 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   const int r0 = rt * kTile2, c0 = by * kTile2;
   const int kb = w * (H / 4) + h * KS::N2;
   const int item = r0 + rl;
-  // loads in the order their consumers need them (vmcnt counts in issue order): the row's head parts (the head's
-  // transcendentals are the prologue's longest chain), its inputs, W1 (before the barrier), then the B operand and
-  // epilogue weights (after it)
+  // fc0 from P1's pre-activation of this row (without the action term) plus the action term on ã — the same fmaf
+  // chain as fc0 on (obs, ã), so no W1 staging and no block barrier before the products. Loads in the order their
+  // consumers need them (vmcnt counts in issue order): the row's head parts (the head's transcendentals are the
+  // prologue's longest chain), the pre-activation and action column of this lane's K slice, the B operand
   RowHeadIn<CB> rh;
   rh.load(a, (kTarget ? Bp : 0) + item);
-  float xin[kXLd];
-  load_run<kXLd>((kTarget ? a.s.xn : a.s.x) + (int64_t)item * kXLd, xin);
   const float ev = a.s.rec[(int64_t)item * kRec + (kTarget ? R_EPSN : R_EPS)];
-  W1Stage<H> w1s;
-  w1s.load(C + L.c_w1, C + L.c_b1, O + 1);
+  const float* PRE = a.s.pre[(kTarget ? 2 : 0) + net] + (int64_t)item * H;
+  const float* W1A = a.s.w1a + ((kTarget ? 2 : 0) + net) * H;
+  float pre[CS], wa[CS];
+  load_run<CS>(PRE + kb, pre);
+  load_run<CS>(W1A + kb, wa);
   float bv[CS];
   const float* WT = a.T + (int64_t)((kTarget ? 3 : 1) + net) * H * H;
   load_b<CS>(bv, WT, H, kb, c0 + rl);
   const float b2c = C[L.c_b2 + c0 + rl], w3 = C[L.c_w3 + c0 + rl];
-  float* lw1 = lds + FwdLds<H>::kW1Off;
-  float* lx = lds + FwdLds<H>::kXOff;
   float hd[6];
   rh.head(ev, hd);
   SAC_STAMP_ON(1, 4, hd[HD_A]);
-  w1s.store(lw1, O + 1);
-  SAC_STAMP(1, 5);
-  if (w == 0 && h == 0) {
+  if (w == 0 && h == 0 && net == 0 && by == 0) {
+    float* rc = a.s.rec + (int64_t)item * kRec;
+    if (kTarget) {
+      rc[R_LOGPN] = hd[HD_LOGP];
+    } else {
 #pragma unroll
-    for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
-    lx[rl * (kXLd + 1) + O] = hd[HD_A];
-    if (net == 0 && by == 0) {
-      float* rc = a.s.rec + (int64_t)item * kRec;
-      if (kTarget) {
-        rc[R_LOGPN] = hd[HD_LOGP];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) rc[q] = hd[q];
-      }
+      for (int q = 0; q < 6; ++q) rc[q] = hd[q];
     }
   }
-  __syncthreads();
+  (void)O;
   SAC_STAMP(1, 1);
+  const float ah = hd[HD_A];
   f32x16 acc = zero16(), act = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
     const int k0 = kb + c * CS;
-    if (c) load_b<CS>(bv, WT, H, k0, c0 + rl);
+    if (c) {
+      load_b<CS>(bv, WT, H, k0, c0 + rl);
+      load_run<CS>(PRE + k0, pre);
+      load_run<CS>(W1A + k0, wa);
+    }
     float av[CS];
-    first_layer<H, CS>(lw1, lx + rl * (kXLd + 1), O + 1, k0, av);
+#pragma unroll
+    for (int i = 0; i < CS; ++i) av[i] = relu(fmaf(wa[i], ah, pre[i]));
     mfma_n<CS>(acc, av, bv);
     if constexpr (!kTarget) {
-      float tv[CS];
+      float tv[CS];  // the tangent's input: [g1 > 0] ⊙ W1[:, a]
 #pragma unroll
-      for (int i = 0; i < CS; ++i) tv[i] = av[i] > 0.0f ? lw1[O * H + k0 + i] : 0.0f;
+      for (int i = 0; i < CS; ++i) tv[i] = av[i] > 0.0f ? wa[i] : 0.0f;
       mfma_n<CS>(act, tv, bv);
     }
   }
@@ -1522,7 +1579,7 @@ __global__ __launch_bounds__(256) void sac_act_head_kernel(ActArgs a) {
 template <int H>
 void launch_step(const MArgs& m, const WArgs& w, hipStream_t st) {
   const unsigned bt = (unsigned)(m.L.Bp / kTile2), cb = H / kTile2;
-  hipLaunchKernelGGL(sac_fwd_kernel<H>, dim3(4 * bt * cb), dim3(256), 0, st, m);
+  hipLaunchKernelGGL(sac_fwd_kernel<H>, dim3(6 * bt * cb), dim3(256), 0, st, m);
   hipLaunchKernelGGL(sac_mid_kernel<H>, dim3(7 * bt * cb), dim3(256), 0, st, m);
   hipLaunchKernelGGL(sac_wgrad_kernel<H>, dim3((unsigned)(w.n_mfma + w.n_valu + 1)), dim3(256), 0, st, w);
 }
@@ -1674,7 +1731,7 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   SDev g(device);
   const int64_t Bp = L.Bp, BH = Bp * H, CB = H / kTile2;
   // rows 3·16, activations 10·H, the row record, parts (2 + 8)·CB, the snapshot
-  const int64_t n_scr = Bp * 3 * kXLd + 10 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H;
+  const int64_t n_scr = Bp * 3 * kXLd + 14 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H + 4 * H;
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
     *out = h;
@@ -1697,6 +1754,11 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   }
   sc.rec = s; s += Bp * kRec;
   sc.hpart = s; s += 2 * Bp * 2 * CB;
+  for (int k = 0; k < 4; ++k) {
+    sc.pre[k] = s;
+    s += BH;
+  }
+  sc.w1a = s; s += 4 * H;
   sc.part = s; s += PS_N * Bp * CB;
   sc.snap = s; s += SN_HEAD + 4 * H;
   e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);

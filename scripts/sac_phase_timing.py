@@ -37,7 +37,7 @@ def kinds(kernel, nblocks, bt, cb, n_mfma, n_valu):
             continue
         bx = b // cb
         if kernel == 0:
-            out.append("actor_fwd" if bx < 2 * bt else "critic_data_fwd")
+            out.append("actor_fwd" if bx < 2 * bt else "critic_data_fwd" if bx < 4 * bt else "target_pre")
         else:
             out.append("critic_tangent" if bx < 2 * bt else "actor_factors" if bx < 3 * bt else
                        "targets" if bx < 5 * bt else "critic_factors")
@@ -69,7 +69,7 @@ def main():
     st = np.frombuffer(buf, dtype=np.uint64).reshape(3, KSTAMP, NST).astype(np.float64)
     bp = (a.batch + 31) // 32 * 32
     bt, cb = bp // 32, a.hidden // 32
-    grids = [4 * bt * cb, 7 * bt * cb, 3 * cb * cb + 3 * (a.hidden // 16) + 1]
+    grids = [6 * bt * cb, 7 * bt * cb, 3 * cb * cb + 3 * (a.hidden // 16) + 1]
     names = ["fwd (P1)", "mid (P2)", "wgrad (P3)"]
     res = {"step_us": r["ms_per_grad_step"] * 1e3, "batch": a.batch, "hidden": a.hidden, "kernels": {}}
     for k in range(3):
