@@ -634,34 +634,38 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
 }
 
 // target critic `net`'s fc0 pre-activation (without the action term) on the next_obs rows of row tile rt, columns
-// by·32 .. by·32 + 31: thread t takes row t / 8 and four columns, the fmaf chain from the bias in input order as
-// first_layer; also fc0's action column of those columns (row tile 0)
+// by·32 .. by·32 + 31: the block stages those 32 rows of W1 (and b1) in LDS with coalesced loads, then thread t takes
+// row t / 8 and four columns, the fmaf chain from the bias in input order as first_layer; row tile 0 also writes
+// fc0's action column of those columns
 template <int H>
-__device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int rt, int by) {
+__device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int rt, int by, float* lds) {
   const Layout& L = a.L;
   const int O = L.O, nin = O + 1;
   const float* C = a.targets + (int64_t)net * L.q_size;
-  const int tid = threadIdx.x, row = tid >> 3, k0 = by * kTile2 + (tid & 7) * 4;
+  const int tid = threadIdx.x, row = tid >> 3, cq = (tid & 7) * 4, c0 = by * kTile2;
   const int item = rt * kTile2 + row;
   float e0, e1;
   const int64_t idx = batch_item(a, item, e0, e1);
   float x[kXLd];
   load_obs_row(a.nobs, idx, O, x);
-  float w[4][kXLd], pre[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    pre[j] = C[L.c_b1 + k0 + j];
-#pragma unroll
-    for (int m = 0; m < kXLd; ++m) w[j][m] = m < nin ? C[L.c_w1 + (int64_t)(k0 + j) * nin + m] : 0.0f;
+  float* w1 = lds;                   // [32][kXLd + 1]: W1 rows c0 .. c0 + 31
+  float* b1 = lds + kTile2 * (kXLd + 1);
+  const float* src = C + L.c_w1 + (int64_t)c0 * nin;  // the 32 rows are contiguous: 32·nin floats
+  for (int e = tid; e < kTile2 * nin; e += kThreads) {
+    const int kk = e / nin;
+    w1[kk * (kXLd + 1) + (e - kk * nin)] = src[e];
   }
+  if (tid < kTile2) b1[tid] = C[L.c_b1 + c0 + tid];
+  __syncthreads();
+  float pre[4];
 #pragma unroll
-  for (int m = 0; m < kXLd; ++m)  // (unrolled, the run-time bound a select: no dynamic index into w)
+  for (int j = 0; j < 4; ++j) pre[j] = b1[cq + j];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pre[j] = m < O ? fmaf(w[j][m], x[m], pre[j]) : pre[j];
-  *reinterpret_cast<float4*>(a.s.pre[2 + net] + (int64_t)item * H + k0) = make_float4(pre[0], pre[1], pre[2], pre[3]);
-  if (rt == 0 && row == 0)
+  for (int m = 0; m < kXLd; ++m)  // (unrolled, the run-time bound a select)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a.s.w1a[(2 + net) * H + k0 + j] = C[L.c_w1 + (int64_t)(k0 + j) * nin + O];
+    for (int j = 0; j < 4; ++j) pre[j] = m < O ? fmaf(w1[(cq + j) * (kXLd + 1) + m], x[m], pre[j]) : pre[j];
+  *reinterpret_cast<float4*>(a.s.pre[2 + net] + (int64_t)item * H + c0 + cq) = make_float4(pre[0], pre[1], pre[2], pre[3]);
+  if (rt == 0 && tid < kTile2) a.s.w1a[(2 + net) * H + c0 + tid] = w1[tid * (kXLd + 1) + O];
 }
 
 template <int H>
@@ -673,7 +677,7 @@ __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
   const int bt = a.L.Bp / kTile2;
   if (bx < 2 * bt) p1_actor_tile<H>(a, bx, by, lds);
   else if (bx < 4 * bt) p1_data_tile<H>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
-  else p1_target_pre_tile<H>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by);
+  else p1_target_pre_tile<H>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by, lds);
   SAC_STAMP(0, 3);
 }
 

@@ -1734,7 +1734,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   // CHAIN: the tick loop hands over to the (rare) chaining code below whenever a decision of the
   // wave completes, so the loop body itself is the per-decision kernel's.
   for (;;) {
-  while (__any(opaque_if<OPQ>(going)) && !(CHAIN && __any(ready && running))) {
+  while (__any(opaque_if<OPQ>(going)) && !(CHAIN && __any(opaque_if<OPQ>(ready) && opaque_if<OPQ>(running)))) {
     // this tick's constants: re-read (scalar loads, LDS) rather than kept in registers across ticks
     const StepArgs& A = step_args();
     const Params& P = A.P;
@@ -1805,10 +1805,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       cb = env_lane_d<LPE, 0>(cb, env_lane0);
       const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
       sb_active = need0;
-      if (going) {
+      if (opaque_if<OPQ>(going)) {  // (tested here, not held as a lane mask across the optimiser's loop)
         if (need0) { p_last = pb; chi_last = cb; }
         else { p_last = 1; chi_last = 0; }
-        if (is_test && need0) { sf = pb; off = cb; }
+        if (opaque_if<OPQ>(is_test ? 1 : 0) && need0) { sf = pb; off = cb; }
       }
     } else if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
       bool need = false;
@@ -1838,10 +1838,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       cb = env_lane_d<LPE, 0>(cb, env_lane0);
       const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
       sb_active = need0;
-      if (going) {
+      if (opaque_if<OPQ>(going)) {  // (tested here, not held as a lane mask across the optimiser's loop)
         if (need0) { p_last = pb; chi_last = cb; }
         else { p_last = 1; chi_last = 0; }
-        if (is_test && need0) { sf = pb; off = cb; }
+        if (opaque_if<OPQ>(is_test ? 1 : 0) && need0) { sf = pb; off = cb; }
       }
     }
 
