@@ -51,7 +51,8 @@ class BatchedPathCollector:
     SLICED_TICKS = 128   # sliced passes: an env idles after its decision until the pass ends
     FUSED_TICKS = 1024   # fused passes: envs chain decisions inside the launch; longer passes amortise its tail
     def __init__(self, env, policy, max_path_length=9, max_ticks=None, deterministic=False,
-                 max_num_epoch_paths_saved=None, device_policy=None, use_graph=None, path_ring=None, fused=None):
+                 max_num_epoch_paths_saved=None, device_policy=None, use_graph=None, path_ring=None, fused=None,
+                 stream_tail=0):
         self._env = env                       # BatchedNormalizedBoxEnv
         self._policy = policy
         self.max_path_length = int(max_path_length)
@@ -104,6 +105,9 @@ class BatchedPathCollector:
             raise ValueError("fused collection needs a device policy the env library can run (see _fused_supported)")
         if self.max_ticks is None:  # ticks per pass: the measured best of each kind (DESIGN.md §9, C4 shard)
             self.max_ticks = self.FUSED_TICKS if self.fused else self.SLICED_TICKS
+        # fused passes: the env launch's work-conserving tail (ShipSim.set_stream_tail) — an env whose wave met
+        # max_ticks ticks on, up to stream_tail more, while the launch's slowest wave has not (0: off)
+        self.stream_tail = max(0, int(stream_tail))
         self._mode = None                                         # "fused" / "sliced": the last pass's kind
         self._ep_idx = torch.zeros(N, dtype=torch.int32, device=dev)   # fused: episodes started per env
         self._dec_idx = torch.zeros(N, dtype=torch.int32, device=dev)  # fused: decisions of the current episode
@@ -226,7 +230,7 @@ class BatchedPathCollector:
     def _log_cap(self):
         """Decision records per env per fused pass: a decision takes ~100 ticks (RoA + the turn), so a third
         of that leaves room; an env whose log fills just waits for the next pass (no record is lost)."""
-        return max(4, -(-self.max_ticks // 32))
+        return max(4, -(-(self.max_ticks + self.stream_tail) // 32))
 
     @torch.no_grad()
     def _fused_pass(self, replay_buffer, record):
@@ -243,6 +247,8 @@ class BatchedPathCollector:
         dp = self._device_policy
         log_len.zero_()
         sim = self._base_env().sim
+        if getattr(sim, "stream_tail", 0) != self.stream_tail:  # (host state of the handle, read at launch)
+            sim.set_stream_tail(self.stream_tail)
         sim.run_policy(dp.weights(), self.max_ticks, T, self._ep_idx, self._dec_idx, deterministic=dp.deterministic,
                        seed=dp.seed, counter=None if dp.deterministic else dp.counter, out=self._fused_out,
                        log=log, log_len=log_len)
@@ -357,7 +363,8 @@ class BatchedPathCollector:
         return self._awaiting, n
 
     def _graph_pass(self, replay_buffer, record, fused=False):
-        key = (id(replay_buffer) if replay_buffer is not None else None, bool(record), self.max_ticks, fused)
+        key = (id(replay_buffer) if replay_buffer is not None else None, bool(record), self.max_ticks, fused,
+               self.stream_tail if fused else 0)
         g = self._graphs.get(key)
         pass_fn = self._fused_pass if fused else self._pass
         if g is None:

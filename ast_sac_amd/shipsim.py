@@ -204,6 +204,7 @@ class ShipSim:
         max_ticks keeps ticking, 32 ticks at a time, while any wave of the launch has not, up to extra_ticks more
         (0: off). Per-env results are unchanged; only where launches end moves."""
         self._check(self.L.shipsim_set_stream_tail(self.h, int(extra_ticks)), "shipsim_set_stream_tail")
+        self.stream_tail = int(extra_ticks)
 
     def run_table(self, table, max_ticks, ep_idx, dec_idx, out=None, log=None, log_len=None):
         """Open-loop decision stream (shipsim_run_table): table (n_eps, n_dec, N) float32 scoping angles

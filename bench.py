@@ -265,11 +265,12 @@ def bench_sac(dev, world, pg, steps, global_batch, eager_steps=40, graph=True, d
     return res
 
 
-def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1):
+def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1, tail_ticks=0):
     """The C3 envs with the policy in the loop (secondary line): shipsim_run_policy, every decision's action
     sampled inside the launch from a TanhGaussianPolicy (runner networks 2x256, random init, stochastic) held
     by a FusedSACTrainer — the collector's fused pass without the replay bookkeeping. env-ticks/s over
-    `launches` launches of `slice_ticks` ticks (HIP events on the launch stream)."""
+    `launches` launches of `slice_ticks` ticks (HIP events on the launch stream), with the table line's
+    work-conserving launch tail of `tail_ticks` (shipsim_set_stream_tail; 0: off)."""
     import torch
     from ast_sac_amd.ast_sac.torch.networks.mlp import ConcatMlp
     from ast_sac_amd.ast_sac.torch.sac.policies.gaussian_policy import TanhGaussianPolicy
@@ -290,6 +291,8 @@ def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1):
     dp = tr.device_policy(deterministic=False, seed=20251017)
     sim = ShipSim(cfg, n_envs, device=dev)
     sim.reset()
+    if tail_ticks > 0:
+        sim.set_stream_tail(tail_ticks)
     n_dec = cfg.max_sampling_frequency
     ep = torch.zeros(n_envs, dtype=torch.int32, device=dev)
     dec = torch.zeros(n_envs, dtype=torch.int32, device=dev)
@@ -318,7 +321,8 @@ def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1):
     dt = time.perf_counter() - t0
     kms = sum(a.elapsed_time(b) for a, b in zip(e0, e1)) / launches
     res = {"env_ticks_per_s": float(ticks.item()) / dt, "decisions_per_s": float(decs.item()) / dt,
-           "kernel_ms": kms, "envs": n_envs, "slice_ticks": slice_ticks, "launches": launches,
+           "kernel_ms": kms, "envs": n_envs, "slice_ticks": slice_ticks, "tail_ticks": tail_ticks,
+           "launches": launches,
            "lanes_per_env": sim.lanes_per_env,
            "impl": "shipsim_run_policy (ast_step_kernel CHAIN 2: TanhGaussianPolicy sample per decision in-kernel, "
                    "NormalizedBoxEnv mapping, in-place episode resets)"}
@@ -586,7 +590,8 @@ def main():
     progress("c2 single ships")
     c2 = bench_c2(dev) if (rank == 0 and not args.no_c2) else None
     progress("policy stream")
-    pstream = (bench_policy_stream(dev, cfg, N, args.slice if args.mode == "table" else 4096)
+    pstream = (bench_policy_stream(dev, cfg, N, args.slice if args.mode == "table" else 4096,
+                                   tail_ticks=max(args.tail_ticks, 0) if args.mode == "table" else 0)
                if (rank == 0 and not args.no_policy_stream and args.obs_ships == 1) else None)
     progress("sac")
     sac = sac_ar = None

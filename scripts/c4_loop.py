@@ -75,6 +75,18 @@ def main():
             res[f"collect_{'fused' if fused else 'sliced'}{sl}"] = dict(
                 decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
                 env_ticks_per_s=(k1 - k0) / t)
+        if fused:  # the launch tail (shipsim_set_stream_tail): envs of waves that met the pass's ticks tick on
+            for sl, tail in ((1024, 512), (1024, 1024)):
+                coll.max_ticks, coll.stream_tail = sl, tail
+                coll.collect(4 * n_envs, rb)
+                s0, k0 = counters()
+                _, t = timed(lambda: coll.collect(32 * n_envs, rb))
+                s1, k1 = counters()
+                progress(f"collect fused {sl} tail {tail}")
+                res[f"collect_fused{sl}_tail{tail}"] = dict(
+                    decisions=s1 - s0, env_ticks=k1 - k0, seconds=t, decisions_per_s=(s1 - s0) / t,
+                    env_ticks_per_s=(k1 - k0) / t)
+            coll.stream_tail = 0
     coll.fused = fused0
     coll.max_ticks = ticks0
     # SAC alone

@@ -169,3 +169,48 @@ def test_policy_stream_stochastic_noise():
     assert n_ok > 8 * N
     # the actions are not deterministic ones
     assert np.abs(a_log - np.tanh(mean)).max() > 0.05
+
+
+def test_policy_stream_launch_tail_keeps_every_record():
+    """run_policy with the work-conserving launch tail (shipsim_set_stream_tail): launch boundaries move,
+    a deterministic policy's records do not — every env's records equal the fixed-length launches' record for
+    record (the common prefix), every launch's decisions are logged, and no env ticks past max_ticks + extra."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    tr, _ = _trainer(256)
+    dp = tr.device_policy(True)
+    cfg = abi.ast_config("sbmpc")
+    n_dec = int(cfg.max_sampling_frequency)
+    N, max_ticks, n_calls, X = 256, 96, 20, 160
+
+    def step(sim, c, ep, dec, log, ln):
+        return sim.run_policy(dp.weights(), max_ticks, n_dec, ep, dec, deterministic=True, log=log, log_len=ln)
+
+    ref, _, init = _run(cfg, N, n_calls, max_ticks, step, cap=256)
+    sim = ShipSim(cfg, N)
+    sim.reset()
+    sim.set_stream_tail(X)
+    ep = torch.zeros(N, dtype=torch.int32, device="cuda")
+    dec = torch.zeros(N, dtype=torch.int32, device="cuda")
+    log = torch.zeros((N, 256, abi.DECLOG_COLS), dtype=torch.float64, device="cuda")
+    log_len = torch.zeros(N, dtype=torch.int32, device="cuda")
+    over = 0
+    for _ in range(n_calls):
+        before = log_len.clone()
+        o = step(sim, 0, ep, dec, log, log_len)
+        assert int(o["ticks"].max()) <= max_ticks + X
+        assert torch.equal(o["decisions"], log_len - before)
+        over += int((o["ticks"] > max_ticks).sum())
+    ln = log_len.cpu().numpy()
+    assert ln.max() <= 256
+    L = log.cpu().numpy()
+    sim.close()
+    got = [L[i, :ln[i]] for i in range(N)]
+    _check_rollout(got, n_dec, init)
+    keep = _KEEP + [abi.DL_ACTION]
+    for i in range(N):
+        n = min(len(got[i]), len(ref[i]))
+        assert len(got[i]) >= len(ref[i]) and n > 0
+        np.testing.assert_array_equal(got[i][:n][:, keep], ref[i][:n][:, keep], err_msg=f"env {i}")
+    assert over > 0  # the tail ran
+    print(f"\n[policy launch tail] env-launches past max_ticks: {over} of {N * n_calls}")
