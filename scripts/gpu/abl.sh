@@ -7,7 +7,7 @@ v() { python -c "import json;d=json.loads(open('$1').read().strip().splitlines()
 B="--collav sbmpc --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream"
 timeout -k 10 200 python bench.py $B > "$O/abl_${TAG}_base.log" 2>&1; hard $? base
 echo "in-tree     $(v "$O/abl_${TAG}_base.log")"
-for l in NO_MAPDIST NO_GROUND ALL3; do
+for l in NO_MAPDIST NO_GROUND NO_WIND ALL3; do
   SHIPSIM_LIB=$R/ast_sac_amd/lib/abl/lib_$l.so timeout -k 10 200 python bench.py $B > "$O/abl_${TAG}_$l.log" 2>&1; hard $? $l
   echo "$l  $(v "$O/abl_${TAG}_$l.log")"
 done

@@ -224,3 +224,37 @@ def test_sliced_then_fused_collect_rows_match_the_policy():
         ref = torch.tanh(pol(obs0).normal_mean)
     err = (act - ref).abs().max().item()
     assert err < 5e-6, err
+
+
+def test_fused_collect_with_launch_tail_rows_match_the_policy():
+    """The fused collector with the env launch's work-conserving tail (stream_tail): its log capacity covers the
+    extra ticks, every replay row is a real observation with the deterministic policy's action on it, and the
+    passes ran past max_ticks (the tail is in use). Per-env record parity under the tail is pinned in
+    test_gpu_run_policy.py::test_policy_stream_launch_tail_keeps_every_record."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from ast_sac_amd.rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, default_args
+    from ast_sac_amd.ast_sac.env_wrapper.normalized_box_env import BatchedNormalizedBoxEnv
+    from ast_sac_amd.ast_sac.samplers.data_collector.batched_collector import BatchedPathCollector
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    tr, pol = _trainer(128)
+    N, ticks, X = 256, 128, 256
+    env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), N), 0.75)
+    dp = tr.device_policy(True)
+    coll = BatchedPathCollector(env, pol, max_path_length=9, max_ticks=ticks, deterministic=True, device_policy=dp,
+                                stream_tail=X)
+    assert coll.fused and coll._log_cap() == (ticks + X) // 32
+    rb = DeviceReplayBuffer(200000, 8, 1, "cuda")
+    t0 = coll.device_diagnostics()["num env ticks total"]
+    got = coll.collect(4 * N, rb)
+    torch.cuda.synchronize()
+    n = rb.num_steps_can_sample()
+    assert n == got >= 4 * N
+    obs0, act = rb._observations[:n], rb._actions[:n]
+    assert bool((obs0.abs().sum(1) > 0).all()), "replay row with an all-zero observation"
+    with torch.no_grad():
+        ref = torch.tanh(pol(obs0).normal_mean)
+    err = (act - ref).abs().max().item()
+    assert err < 5e-6, err
+    assert coll._base_env().sim.stream_tail == X
+    print(f"\n[collector tail] rows {n}, env ticks {coll.device_diagnostics()['num env ticks total'] - t0}")
