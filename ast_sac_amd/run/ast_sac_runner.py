@@ -71,9 +71,10 @@ def build_parser():
                         "(1024 with the policy inside the env launch, 128 for sliced passes; DESIGN §9)")
     p.add_argument("--fused_collect", type=_bool, default=True,
                    help="the policy inside the env launch (shipsim_run_policy) where the networks allow it")
-    p.add_argument("--stream_tail", type=int, default=0,
+    p.add_argument("--stream_tail", type=int, default=-1,
                    help="fused passes: the env launch's work-conserving tail (shipsim_set_stream_tail) — envs whose "
-                        "wave met the pass's ticks tick on, up to this many more, while the slowest wave has not")
+                        "wave met the pass's ticks tick on, up to this many more, while the slowest wave has not; "
+                        "0: off, -1: the collector's measured best (512; DESIGN §9)")
     p.add_argument("--match_update_ratio", type=_bool, default=True,
                    help="grad steps per train loop = collected decisions (all ranks) x num_trains / num_expl_steps "
                         "(the reference's ratio); false: num_trains_per_train_loop per loop")
@@ -192,11 +193,11 @@ def experiment_device(variant, args, device, process_group=None):
     fused = None if args.fused_collect else False
     expl_coll = BatchedPathCollector(expl_env, policy, max_path_length=ak["max_path_length"],
                                      max_ticks=ticks, device_policy=trainer.device_policy(False), fused=fused,
-                                     stream_tail=args.stream_tail)
+                                     stream_tail=None if args.stream_tail < 0 else args.stream_tail)
     eval_coll = BatchedPathCollector(eval_env, MakeDeterministic(policy), max_path_length=ak["max_path_length"],
                                      max_ticks=ticks, deterministic=True,
                                      device_policy=trainer.device_policy(True), fused=fused,
-                                     stream_tail=args.stream_tail)
+                                     stream_tail=None if args.stream_tail < 0 else args.stream_tail)
     return DeviceBatchRLAlgorithm(trainer=trainer, exploration_env=expl_env, evaluation_env=eval_env,
                                   exploration_data_collector=expl_coll, evaluation_data_collector=eval_coll,
                                   replay_buffer=rb, match_update_ratio=variant.get("match_update_ratio", True), **ak)

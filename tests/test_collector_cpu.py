@@ -371,7 +371,7 @@ def test_fused_pass_rows_and_paths_follow_the_decision_log():
     N, T = 12, 4
     env = _PolicyEnv(N)
     coll = BatchedPathCollector(env, _Policy(), max_path_length=T, max_ticks=64, deterministic=True,
-                                device_policy=_DevicePolicy(), use_graph=False)
+                                device_policy=_DevicePolicy(), use_graph=False, stream_tail=0)
     assert coll.fused and coll._log_cap() == 4
     rb = DeviceReplayBuffer(1000, 8, 1, "cpu")
     got = coll.collect(60, rb, record_paths=True)

@@ -133,7 +133,7 @@ def test_fused_collector_rows_and_paths_follow_the_decision_log():
     env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), N), scale)
     dp = tr.device_policy(True)
     coll = BatchedPathCollector(env, pol, max_path_length=T, max_ticks=ticks, deterministic=True, device_policy=dp,
-                                use_graph=False)
+                                use_graph=False, stream_tail=0)  # (fixed launch boundaries: compared pass by pass)
     assert coll.fused
     rb = DeviceReplayBuffer(200000, 8, 1, "cuda")
     coll._take_over()
