@@ -50,7 +50,10 @@ from ...core.eval_util import create_stats_ordered_dict
 class BatchedPathCollector:
     SLICED_TICKS = 128   # sliced passes: an env idles after its decision until the pass ends
     FUSED_TICKS = 1024   # fused passes: envs chain decisions inside the launch; longer passes amortise its tail
-    FUSED_TAIL = 512     # fused passes: the launch's work-conserving tail (+11.6 % env-ticks/s)
+    # fused passes: the launch's work-conserving tail. Off by default: where a launch ends then depends on timing,
+    # and a stochastic policy's noise is drawn per pass, so runs would not repeat bit for bit; collection is ~1 % of
+    # the C4 loop at the reference's update ratio. 512 gives +11.6 % env-ticks/s on collection alone.
+    FUSED_TAIL = 0
     def __init__(self, env, policy, max_path_length=9, max_ticks=None, deterministic=False,
                  max_num_epoch_paths_saved=None, device_policy=None, use_graph=None, path_ring=None, fused=None,
                  stream_tail=None):
@@ -107,8 +110,8 @@ class BatchedPathCollector:
         if self.max_ticks is None:  # ticks per pass: the measured best of each kind (DESIGN.md §9, C4 shard)
             self.max_ticks = self.FUSED_TICKS if self.fused else self.SLICED_TICKS
         # fused passes: the env launch's work-conserving tail (ShipSim.set_stream_tail) — an env whose wave met
-        # max_ticks ticks on, up to stream_tail more, while the launch's slowest wave has not (0: off; None: the
-        # measured best)
+        # max_ticks ticks on, up to stream_tail more, while the launch's slowest wave has not (0: off; None:
+        # FUSED_TAIL)
         self.stream_tail = self.FUSED_TAIL if stream_tail is None else max(0, int(stream_tail))
         self._mode = None                                         # "fused" / "sliced": the last pass's kind
         self._ep_idx = torch.zeros(N, dtype=torch.int32, device=dev)   # fused: episodes started per env

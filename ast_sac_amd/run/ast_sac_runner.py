@@ -74,7 +74,8 @@ def build_parser():
     p.add_argument("--stream_tail", type=int, default=-1,
                    help="fused passes: the env launch's work-conserving tail (shipsim_set_stream_tail) — envs whose "
                         "wave met the pass's ticks tick on, up to this many more, while the slowest wave has not; "
-                        "0: off, -1: the collector's measured best (512; DESIGN §9)")
+                        "-1/0: off (the default: runs repeat bit for bit); 512: +11.6 %% collection rate (DESIGN §9), with launch "
+                        "boundaries (and so a stochastic policy's noise draws) depending on timing")
     p.add_argument("--match_update_ratio", type=_bool, default=True,
                    help="grad steps per train loop = collected decisions (all ranks) x num_trains / num_expl_steps "
                         "(the reference's ratio); false: num_trains_per_train_loop per loop")

@@ -97,7 +97,8 @@ def test_graph_replayed_collector_equals_eager_collector(fused):
     for use_graph in (True, False):
         env = BatchedNormalizedBoxEnv(BatchedMultiShipRLEnv(default_args(collav_mode="sbmpc"), 512), 0.75)
         coll = BatchedPathCollector(env, pol, max_path_length=9, max_ticks=128, deterministic=True,
-                                    device_policy=tr.device_policy(True), use_graph=use_graph, fused=fused)
+                                    device_policy=tr.device_policy(True), use_graph=use_graph, fused=fused,
+                                    stream_tail=0)  # (fixed launch boundaries: compared pass by pass)
         assert coll.fused == fused
         rb = DeviceReplayBuffer(40000, 8, 1, "cuda")
         got = coll.collect(6500, rb, record_paths=True)  # ~15 passes of 128 ticks: episodes end
