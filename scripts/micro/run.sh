@@ -1,10 +1,10 @@
 # Microbenchmarks (diagnostics): build with hipcc here, then run one under rocprofv3 on the GPU box.
 # Build (CPU container):  bash scripts/micro/run.sh build
-# Run (GPU box):          bash scripts/micro/run.sh run colread2|colread|icache|launch
+# Run (GPU box):          bash scripts/micro/run.sh run colread2|colread|icache|launch|firstload
 set -u
 D=$(cd "$(dirname "$0")" && pwd)
 if [ "${1:-}" = "build" ]; then
-  for f in colread colread2 icache launch; do /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 "$D/$f.hip" -o "$D/$f" || exit 1; done
+  for f in colread colread2 icache launch firstload; do /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 "$D/$f.hip" -o "$D/$f" || exit 1; done
   exit 0
 fi
 B=${2:-colread2}; O=${GRAFT_REPO_ROOT:-$D/../..}/gpurun_out/micro_$B; export TMPDIR=/tmp
