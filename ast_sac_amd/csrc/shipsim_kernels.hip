@@ -1342,6 +1342,20 @@ __device__ __forceinline__ void ship_reduce(double& d2, int& gri) {
   }
 }
 
+// the OR of an int over the same sub-lanes (ship_reduce without the double)
+template <int LPE, int SLOTS = 2>
+__device__ __forceinline__ void ship_or(int& gri) {
+  SHIPSIM_LANE_CHECK(LPE, 3);
+  if constexpr (LPE == 16) {
+    if constexpr (SLOTS == 2) gri |= dpp_i<kDppQuadXor2>(gri);
+    if constexpr (SLOTS <= 4) gri |= dpp_i<kDppRowRor4>(gri);
+    gri |= dpp_i<kDppRowRor8>(gri);
+  } else {
+#pragma unroll
+    for (int m = SLOTS; m < LPE; m <<= 1) gri |= __shfl_xor(gri, m, 64);
+  }
+}
+
 // |beta| > 165° of get_distance_and_encounter_type (compute_distance.py:16-40): beta =
 // wrap(atan2(dy, dx) - heading) and cos(beta) = (dx cos h + dy sin h) / dist, so the overtaking
 // sector is c < cos(165°)·dist with c = dx·cos h + dy·sin h (sin/cos(h) carried from the test ship's
@@ -1920,9 +1934,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         }
       }
 #endif
+      d2 = d2s;  // the ship's min over its sub-lanes' edge shares (reduced once, above)
     }
     int gri = gr ? XF_GROUND : 0;
-    ship_reduce<LPE, SLOTS>(d2, gri);
+    ship_or<LPE, SLOTS>(gri);
     const double my_ground = sqrt(d2);
     PT_MARK(2);
     bool my_end = false, my_outside = false, my_roa = false, my_nf = false;
