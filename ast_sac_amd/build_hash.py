@@ -19,8 +19,13 @@ HIPFLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shar
 # per-library additions. shipsim: no machine-level loop-invariant code motion — hoisting the tick loop's
 # constants (fp64 literals, addresses) out of the 4096-tick loop held them in registers for the whole
 # launch: 256 VGPR + 161 AGPR and 55 SGPR spill lanes in the headline kernel, against 256 + 46 and none
-# without it, at the same speed
-LIB_FLAGS = {"shipsim": ["-mllvm", "-disable-machine-licm"], "sacfused": []}
+# without it, at the same speed. And the machine scheduler's max-ILP strategy instead
+# of the occupancy-first default: the step kernels run one wave per SIMD whatever the schedule, so interleaving
+# independent FP64 chains is what shortens the tick (+0.7 % on the headline, spill-free; profiles/round4/
+# r4z_sched_ab.txt). sacfused keeps the default: max-ILP there is 0.6 µs faster per grad step but spills SGPRs in
+# three kernels at H = 448 / 512.
+LIB_FLAGS = {"shipsim": ["-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+             "sacfused": []}
 
 
 def source_hash(lib):
