@@ -22,10 +22,19 @@ HIPFLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shar
 # without it, at the same speed. And the machine scheduler's max-ILP strategy instead
 # of the occupancy-first default: the step kernels run one wave per SIMD whatever the schedule, so interleaving
 # independent FP64 chains is what shortens the tick (+0.7 % on the headline, spill-free; profiles/round4/
-# r4z_sched_ab.txt). sacfused keeps the default: max-ILP there is 0.6 µs faster per grad step but spills SGPRs in
-# three kernels at H = 448 / 512.
+# r4z_sched_ab.txt).
 LIB_FLAGS = {"shipsim": ["-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
              "sacfused": []}
+# libraries built from several objects of the same source, each with flags of its own (then linked into one .so).
+# sacfused: max-ILP is 0.6 µs faster per grad step at H = 256 but spills SGPRs in three kernels at H = 448 / 512,
+# so the widths up to 384 (and the C ABI) are one object with it and the two widest another without
+# (sac_kernels.hip SACF_TU).
+OBJECTS = {"sacfused": [["-DSACF_TU=1", "-mllvm", "-amdgpu-sched-strategy=max-ilp"], ["-DSACF_TU=2"]]}
+
+
+def lib_flag_sets(lib):
+    """The flag sets the library is compiled with: one per object (one set for a single-object library)."""
+    return [LIB_FLAGS[lib] + extra for extra in OBJECTS.get(lib, [[]])]
 
 
 def source_hash(lib):
@@ -33,7 +42,8 @@ def source_hash(lib):
     for rel in SOURCES[lib]:
         with open(os.path.join(_ROOT, rel), "rb") as f:
             h.update(rel.encode() + b"\0" + f.read() + b"\0")
-    h.update(" ".join(HIPFLAGS + LIB_FLAGS[lib]).encode())
+    for flags in lib_flag_sets(lib):
+        h.update(" ".join(HIPFLAGS + flags).encode() + b"\0")
     return h.hexdigest()[:16]
 
 

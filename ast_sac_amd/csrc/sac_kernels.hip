@@ -40,6 +40,20 @@
 
 #include "sac_fused.h"
 
+// Translation-unit role (the library is built from two objects of this file, ast_sac_amd/build_hash.py):
+//   SACF_TU 1: every hidden width but the two widest, with the C ABI; the two widest go to the other object
+//   SACF_TU 2: the kernels of the two widest widths (448, 512) and their two launch forwarders only
+//   SACF_TU 0: everything in one object (diagnostics builds)
+// so the narrow widths can use the max-ILP machine scheduler while the wide ones keep the default (max-ILP spills
+// SGPRs there).
+#ifndef SACF_TU
+#define SACF_TU 0
+#endif
+#if SACF_TU == 1
+bool sacf_wide_launch_step(int H, const void* m, const void* w, hipStream_t st);
+bool sacf_wide_launch_act(int H, const void* a, hipStream_t st);
+#endif
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -1605,14 +1619,50 @@ bool with_hidden(int H, F&& f) {
   switch (H) {
 #define SACF_H(h) \
   case h: f(std::integral_constant<int, h>{}); return true;
+#if SACF_TU != 2
     SACF_H(32) SACF_H(64) SACF_H(96) SACF_H(128) SACF_H(160) SACF_H(192) SACF_H(224) SACF_H(256)
-    SACF_H(320) SACF_H(384) SACF_H(448) SACF_H(512)
+    SACF_H(320) SACF_H(384)
+#endif
+#if SACF_TU != 1
+    SACF_H(448) SACF_H(512)
+#endif
 #undef SACF_H
     default: return false;
   }
 #endif
 }
 
+}  // namespace
+
+#if SACF_TU == 2
+// the wide widths' launches, called by the SACF_TU 1 object (the argument structs are this file's, identical there)
+bool sacf_wide_launch_step(int H, const void* m, const void* w, hipStream_t st) {
+  return with_hidden(H, [&](auto hc) {
+    launch_step<decltype(hc)::value>(*static_cast<const MArgs*>(m), *static_cast<const WArgs*>(w), st);
+  });
+}
+bool sacf_wide_launch_act(int H, const void* a, hipStream_t st) {
+  return with_hidden(H, [&](auto hc) { launch_act<decltype(hc)::value>(*static_cast<const ActArgs*>(a), st); });
+}
+#else
+namespace {
+// a width this object does not hold: the other object's launches (SACF_TU 1), or none (SACF_TU 0)
+bool wide_step(int H, const MArgs& m, const WArgs& w, hipStream_t st) {
+#if SACF_TU == 1
+  return sacf_wide_launch_step(H, &m, &w, st);
+#else
+  (void)H; (void)m; (void)w; (void)st;
+  return false;
+#endif
+}
+bool wide_act(int H, const ActArgs& a, hipStream_t st) {
+#if SACF_TU == 1
+  return sacf_wide_launch_act(H, &a, st);
+#else
+  (void)H; (void)a; (void)st;
+  return false;
+#endif
+}
 }  // namespace
 
 // =============================================================================================
@@ -1893,7 +1943,8 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
     w.hw_off[mat] = mat == 0 ? 0 : (mat + 1) * L.H;
   }
   SDev g(h->device);
-  if (!with_hidden(h->L.H, [&](auto hc) { launch_step<decltype(hc)::value>(a, w, h->stream); }))
+  if (!with_hidden(h->L.H, [&](auto hc) { launch_step<decltype(hc)::value>(a, w, h->stream); }) &&
+      !wide_step(h->L.H, a, w, h->stream))
     return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
@@ -1939,7 +1990,8 @@ int sacf_policy_act(sacf_handle* h, const float* obs, int64_t n, int32_t obs_str
   a.hpart = h->act_part; a.n_pad = n_pad; a.mask = mask; a.deterministic = deterministic;
   a.seed = seed; a.counter = counter; a.act = act; a.eps_out = eps_out;
   SDev g(h->device);
-  if (!with_hidden(h->L.H, [&](auto hc) { launch_act<decltype(hc)::value>(a, h->stream); }))
+  if (!with_hidden(h->L.H, [&](auto hc) { launch_act<decltype(hc)::value>(a, h->stream); }) &&
+      !wide_act(h->L.H, a, h->stream))
     return sfail(h, SACF_EINVAL, "sacf_policy_act: hidden %d", h->L.H);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_policy_act: %s", hipGetErrorString(e));
@@ -1956,3 +2008,4 @@ int sacf_policy_weights(const sacf_handle* h, const float** params, const float*
 }
 
 }  // extern "C"
+#endif  // SACF_TU != 2

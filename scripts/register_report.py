@@ -10,13 +10,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from __graft_entry__ import HIPCC, HIPFLAGS, SAC_SRC, SRC  # noqa: E402
-from ast_sac_amd.build_hash import LIB_FLAGS  # noqa: E402
+from ast_sac_amd.build_hash import lib_flag_sets  # noqa: E402
 
 
 def report(name, src):
-    cmd = [HIPCC] + HIPFLAGS + LIB_FLAGS[name] + ["-Rpass-analysis=kernel-resource-usage"] + src + \
-        ["-o", f"/tmp/regreport_{name}.so"]
-    err = subprocess.run(cmd, capture_output=True, text=True, check=True).stderr
+    err = ""
+    for i, flags in enumerate(lib_flag_sets(name)):  # every object of the library with its own flags
+        cmd = [HIPCC] + HIPFLAGS + flags + ["-Rpass-analysis=kernel-resource-usage"] + src + \
+            ["-o", f"/tmp/regreport_{name}_{i}.so"]
+        err += subprocess.run(cmd, capture_output=True, text=True, check=True).stderr
     rows, cur = {}, None
     for line in err.splitlines():
         m = re.search(r"Function Name: (\S+)", line)

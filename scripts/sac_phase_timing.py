@@ -23,7 +23,7 @@ def build():
     from __graft_entry__ import HIPCC, HIPFLAGS, SAC_SRC
     from ast_sac_amd.build_hash import LIB_FLAGS
     os.makedirs(os.path.dirname(DIAG), exist_ok=True)
-    subprocess.check_call([HIPCC] + HIPFLAGS + LIB_FLAGS["sacfused"] + ["-DSACF_PHASE_TIMING", '-DSACF_SRC_HASH="diag"']
+    subprocess.check_call([HIPCC] + HIPFLAGS + LIB_FLAGS["sacfused"] + ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + ["-DSACF_PHASE_TIMING", '-DSACF_SRC_HASH="diag"']
                           + SAC_SRC + ["-o", DIAG])
     print("built", DIAG)
 
