@@ -22,8 +22,9 @@ HIPFLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shar
 # without it, at the same speed. And the machine scheduler's max-ILP strategy instead
 # of the occupancy-first default: the step kernels run one wave per SIMD whatever the schedule, so interleaving
 # independent FP64 chains is what shortens the tick (+0.7 % on the headline, spill-free; profiles/round4/
-# r4z_sched_ab.txt).
-LIB_FLAGS = {"shipsim": ["-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+# r4z_sched_ab.txt), with the scheduler's AMDGPU register-pressure trackers (+0.5 %, r4zz_sched3_ab.txt).
+LIB_FLAGS = {"shipsim": ["-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-sched-strategy=max-ilp",
+                         "-mllvm", "-amdgpu-use-amdgpu-trackers"],
              "sacfused": []}
 # libraries built from several objects of the same source, each with flags of its own (then linked into one .so).
 # sacfused: max-ILP is 0.6 µs faster per grad step at H = 256 but spills SGPRs in three kernels at H = 448 / 512,

@@ -4,7 +4,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p /tmp/rc && cd /tmp/rc
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -fPIC -shared -std=c++17 -I$R/include -I$R/ast_sac_amd/csrc \
-  -mllvm -disable-machine-licm -mllvm -amdgpu-sched-strategy=max-ilp --save-temps "${@:2}" $R/ast_sac_amd/csrc/shipsim_kernels.hip -o /tmp/rc/x.so 2>/dev/null
+  -mllvm -disable-machine-licm -mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-use-amdgpu-trackers --save-temps "${@:2}" $R/ast_sac_amd/csrc/shipsim_kernels.hip -o /tmp/rc/x.so 2>/dev/null
 python3 - "$1" <<'PY'
 import sys
 L = open('/tmp/rc/shipsim_kernels-hip-amdgcn-amd-amdhsa-gfx950.s').read().split('\n')

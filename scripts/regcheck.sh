@@ -15,6 +15,6 @@ if [ "$N" = sac ]; then
   python3 scripts/regsummary.py /tmp/regcheck_sac.txt
   exit 0
 fi
-/opt/rocm/bin/hipcc $FLAGS -mllvm -disable-machine-licm -mllvm -amdgpu-sched-strategy=max-ilp -DSHIPSIM_REGCHECK=$N -Rpass-analysis=kernel-resource-usage "$@" \
+/opt/rocm/bin/hipcc $FLAGS -mllvm -disable-machine-licm -mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-use-amdgpu-trackers -DSHIPSIM_REGCHECK=$N -Rpass-analysis=kernel-resource-usage "$@" \
   ast_sac_amd/csrc/shipsim_kernels.hip -o /tmp/regcheck.so 2> /tmp/regcheck.txt
 python3 scripts/regsummary.py /tmp/regcheck.txt | grep -E "ast_step|sbmpc_eval|legacy"
