@@ -90,7 +90,7 @@ class DeviceBatchRLAlgorithm(BaseRLAlgorithm):
             self.training_mode(False)
 
     def _sync_buffer(self):
-        """Replicated data parallel: every rank's new rows into every rank's ring (one all-gather per collect)."""
+        """Replicated data parallel: every rank's new rows into every rank's ring (two all-gathers per collect: counts, rows)."""
         sync = getattr(self.replay_buffer, "sync", None)
         if sync is not None:
             sync()

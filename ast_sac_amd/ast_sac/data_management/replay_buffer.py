@@ -192,6 +192,10 @@ class DeviceReplayBuffer(ReplayBuffer):
         self._top_t.copy_((self._top_t + cnt) % self._max)
         self._size_t.copy_(torch.clamp(self._size_t + cnt, max=self._max))
 
+    def add_capacity(self):
+        """Rows one add_batch can take."""
+        return self._max
+
     def random_batch(self, batch_size, out=None):
         """Uniform with replacement over the filled rows; returns device tensors (float32)."""
         size = self._size_t.clamp(min=1)
@@ -217,12 +221,13 @@ class DeviceReplayBuffer(ReplayBuffer):
 class ReplicatedReplayBuffer(DeviceReplayBuffer):
     """The union of every rank's transitions, held identically by every rank of `process_group` — the
     replicated-trainer data-parallel shape. `add_batch` (the collector's, graph-capturable)
-    stages this rank's rows; `sync()` all-gathers every rank's staged rows — one collective per train loop,
+    stages this rank's rows; `sync()` all-gathers every rank's staged rows — once per train loop (a count, then the rows),
     76 B per row, instead of one gradient all-reduce per grad step — and appends them in rank order, so
     every rank's ring holds the same rows in the same slots. Every rank then runs the same SAC step on the
     same global batch (the reference's uniform sample over all collected transitions, replay_buffer.py /
     simple_replay_buffer.py:72-76) with the same seed, and the replicas stay bitwise equal without any
-    per-step exchange."""
+    per-step exchange. A sync is two all-gathers: the ranks' staged-row counts (one int64 each), then the rows
+    (the largest count of rows from every rank)."""
 
     def __init__(self, max_replay_buffer_size, observation_dim, action_dim, device, process_group, stage_size,
                  generator=None):
@@ -236,6 +241,14 @@ class ReplicatedReplayBuffer(DeviceReplayBuffer):
         n = obs.shape[0]
         self._stage.add_batch(obs, action, reward, next_obs, terminal, mask)
         self._staged_t += n if mask is None else mask.reshape(-1).to(torch.int64).sum()
+
+    def add_capacity(self):
+        """Rows one add_batch can take: the staging ring's."""
+        return self._stage._max
+
+    def staging_room(self):
+        """Rows that can still be staged before the next sync (a host read of the device count)."""
+        return self._stage._max - int(self._staged_t.item())
 
     def sync(self):
         """Append every rank's staged rows (rank order) to the shared ring; returns the rows appended."""

@@ -47,6 +47,18 @@ from .... import shipsim_abi as abi
 from ...core.eval_util import create_stats_ordered_dict
 
 
+def _add_capacity(replay_buffer):
+    """Rows one add_batch of the buffer can take (a ReplicatedReplayBuffer stages into a smaller ring)."""
+    cap = getattr(replay_buffer, "add_capacity", None)
+    return cap() if cap is not None else replay_buffer._max
+
+
+def _staging_room(replay_buffer):
+    """Rows the buffer can still stage before its next sync (host read), or None for a plain ring."""
+    room = getattr(replay_buffer, "staging_room", None) if replay_buffer is not None else None
+    return room() if room is not None else None
+
+
 class BatchedPathCollector:
     SLICED_TICKS = 128   # sliced passes: an env idles after its decision until the pass ends
     FUSED_TICKS = 1024   # fused passes: envs chain decisions inside the launch; longer passes amortise its tail
@@ -232,10 +244,18 @@ class BatchedPathCollector:
             idx = torch.nonzero_static(self._awaiting, size=k).squeeze(1)
             self._act.index_copy_(0, idx, self._actions(self._obs.index_select(0, idx)).to(torch.float32))
 
-    def _log_cap(self):
+    @staticmethod
+    def log_cap_for(max_ticks, stream_tail):
         """Decision records per env per fused pass: a decision takes ~100 ticks (RoA + the turn), so a third
         of that leaves room; an env whose log fills just waits for the next pass (no record is lost)."""
-        return max(4, -(-(self.max_ticks + self.stream_tail) // 32))
+        return max(4, -(-(max_ticks + stream_tail) // 32))
+
+    def _log_cap(self):
+        return self.log_cap_for(self.max_ticks, self.stream_tail)
+
+    def _rows_per_pass(self):
+        """The most replay rows one pass can add (fused: every log record; sliced: one per env)."""
+        return self.N * self._log_cap() if self.fused and self._trace_idx is None else self.N
 
     @torch.no_grad()
     def _fused_pass(self, replay_buffer, record):
@@ -267,8 +287,8 @@ class BatchedPathCollector:
         dec = log[:, :, abi.DL_DECISION].to(torch.int64)
         end = valid & ((log[:, :, abi.DL_DONE] != 0) | nonfinite | (dec + 1 >= T))
         act = log[:, :, abi.DL_ACTION].to(torch.float32)
-        if replay_buffer is not None:  # env-major, in env chunks no larger than the buffer
-            step = max(1, replay_buffer._max // cap)
+        if replay_buffer is not None:  # env-major, in env chunks no larger than one add can take
+            step = max(1, _add_capacity(replay_buffer) // cap)
             for a in range(0, N, step):
                 b = min(N, a + step)
                 n = (b - a) * cap
@@ -406,6 +426,15 @@ class BatchedPathCollector:
             start = int(self._steps_total.item())
             got, passes, batch = 0, 0, 1
             while got < num_steps:
+                room = _staging_room(replay_buffer)
+                if room is not None:  # a staging ring (ReplicatedReplayBuffer) takes rows only until its next sync
+                    fit = room // self._rows_per_pass()
+                    if fit < 1:
+                        raise RuntimeError(
+                            f"BatchedPathCollector: the replay buffer's staging ring has room for {room} rows, less "
+                            f"than one pass can add ({self._rows_per_pass()}); sync() it after every collect or "
+                            f"enlarge its stage_size (ast_sac_runner.replicated_stage_rows)")
+                    batch = min(batch, fit)
                 for _ in range(batch):
                     if self.use_graph:
                         self._graph_pass(replay_buffer, record, fused)

@@ -96,6 +96,11 @@ class FusedSACTrainer(TorchTrainer):
         # split_update=True forces it on one rank too (the all-reduce then runs over a world-size-1 group: the
         # same code path as N ranks, an identity on the values)
         self.split = (self.world > 1) if split_update is None else bool(split_update)
+        if self.replicated and (self.split or capture_collective):
+            # (every replica runs the whole global batch: an all-reduce would sum R identical gradients, and
+            # Adam would apply them R times over)
+            raise ValueError("replicated=True runs no gradient collective: split_update / capture_collective "
+                             "belong to the all-reduce shape (replicated=False)")
         # the all-reduce inside the one captured HIP graph of the step (RCCL kernels are capturable) instead of
         # an eager call between two graph halves; default with an RCCL ("nccl") group
         nccl = process_group is not None and torch.distributed.get_backend(process_group) == "nccl"

@@ -8,7 +8,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_HERE)
 
 SOURCES = {
-    "shipsim": ["ast_sac_amd/csrc/shipsim_kernels.hip", "ast_sac_amd/csrc/shipsim_device.hpp", "include/shipsim.h"],
+    "shipsim": ["ast_sac_amd/csrc/shipsim_kernels.hip", "ast_sac_amd/csrc/shipsim_device.hpp",
+                "ast_sac_amd/csrc/shipsim_diag.hpp", "include/shipsim.h"],
     "sacfused": ["ast_sac_amd/csrc/sac_kernels.hip", "include/sac_fused.h"],
 }
 

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "shipsim.h"
+#include "shipsim_diag.hpp"
 
 namespace shipsim {
 
@@ -188,10 +189,10 @@ __device__ __forceinline__ void sincos2(double a, double b, bool odd, double& sa
 template <bool PAIRED>
 __device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, const Ship& s, double sw, double cw,
                                            bool odd, double tau[3]) {
-#ifdef SHIPSIM_ABL_NO_WIND
-  tau[0] = tau[1] = tau[2] = 0.0;
-  return;
-#endif
+  if constexpr (diag::kNoWind) {  // (ablation build only)
+    tau[0] = tau[1] = tau[2] = 0.0;
+    return;
+  }
   double uw = P.wind_speed * cw;
   double vw = P.wind_speed * sw;
   double u_rw = uw - s.u;
@@ -218,6 +219,10 @@ __device__ __forceinline__ void wind_force(const ShipConst& c, const Params& P, 
 // one sqrt instead of atan2 and three sincos; equal to wind_force up to rounding (V = 0 gives 0).
 __device__ __forceinline__ void wind_force_alg(const ShipConst& c, const Params& P, const Ship& s, double sy,
                                                double cy, double wsin, double wcos, double tau[3]) {
+  if constexpr (diag::kNoWind) {  // (ablation build only)
+    tau[0] = tau[1] = tau[2] = 0.0;
+    return;
+  }
   const double cw = wcos * cy + wsin * sy;
   const double sw = wsin * cy - wcos * sy;
   const double u_rw = P.wind_speed * cw - s.u;

@@ -21,50 +21,7 @@
 #include "shipsim.h"
 #include "shipsim_device.hpp"
 
-// ---------------------------------------------------------------------------------------------
-// Diagnostics build (-DSHIPSIM_LANECHECK; scripts/build_abl.sh lib_lanecheck.so): every cross-lane exchange
-// checks that all lanes it reads are active (the env's LPE lanes for the DPP / shuffle helpers, the whole
-// wave for the wave-cooperative SBMPC and policy passes), and the data-dependent indices of the decision
-// path are range-checked. A violation is counted (first site and exec mask kept) and read back with
-// shipsim_diag_lane_faults; the default build compiles all of it out.
-// ---------------------------------------------------------------------------------------------
-#ifdef SHIPSIM_LANECHECK
-// [0] violations, [1] first site, [2] / [3] its exec mask lo / hi, [8 + site] violations per site
-__device__ unsigned g_lane_diag[32];
-__device__ __noinline__ void lane_fault(int site) {
-  const uint64_t ex = __builtin_amdgcn_read_exec();
-  atomicAdd(&g_lane_diag[8 + (site & 15)], 1u);
-  if (atomicAdd(&g_lane_diag[0], 1u) == 0u) {
-    atomicExch(&g_lane_diag[1], (unsigned)site);
-    atomicExch(&g_lane_diag[2], (unsigned)ex);
-    atomicExch(&g_lane_diag[3], (unsigned)(ex >> 32));
-  }
-}
-template <int LPE>
-__device__ __forceinline__ void lane_check(int site) {  // all LPE lanes of this lane's group active
-  const int l0 = (int)(threadIdx.x & 63) & ~(LPE - 1);
-  const uint64_t need = LPE >= 64 ? ~0ull : (((1ull << LPE) - 1) << l0);
-  if ((__builtin_amdgcn_read_exec() & need) != need) lane_fault(site);
-}
-template <int LPE, int SLOTS>
-__device__ __forceinline__ void ship_check(int site) {  // the lanes of this lane's ship within its env
-  const int lane = (int)(threadIdx.x & 63), l0 = lane & ~(LPE - 1);
-  uint64_t pat = 0;
-  for (int k = lane % SLOTS; k < LPE; k += SLOTS) pat |= 1ull << k;
-  const uint64_t need = pat << l0;
-  if ((__builtin_amdgcn_read_exec() & need) != need) lane_fault(site);
-}
-#define SHIPSIM_LANE_CHECK(LPE_, site) lane_check<LPE_>(site)
-#define SHIPSIM_SHIP_CHECK(LPE_, SLOTS_, site) ship_check<LPE_, SLOTS_>(site)
-#define SHIPSIM_INDEX_CHECK(cond, site) \
-  do {                                  \
-    if (!(cond)) lane_fault(site);      \
-  } while (0)
-#else
-#define SHIPSIM_LANE_CHECK(LPE_, site) ((void)0)
-#define SHIPSIM_SHIP_CHECK(LPE_, SLOTS_, site) ((void)0)
-#define SHIPSIM_INDEX_CHECK(cond, site) ((void)0)
-#endif
+#include "shipsim_diag.hpp"  // diagnostics / ablation hooks (none in the product build)
 
 
 using namespace shipsim;
@@ -112,20 +69,6 @@ struct DevState {
   static constexpr int kEnvArrays = 19;
   static constexpr int kShipArrays = 22;
 };
-#ifdef SHIPSIM_PHASE_TIMING
-// timing build only (scripts/phase_timing.sh): per-phase wall-clock cycles summed over waves
-__device__ unsigned long long g_phase_cycles[8];
-#define PT_MARK(k)                                                     \
-  do {                                                                 \
-    const unsigned long long _t = wall_clock64();                      \
-    pt_acc[k] += _t - pt_last;                                         \
-    pt_last = _t;                                                      \
-  } while (0)
-#else
-#define PT_MARK(k) \
-  do {             \
-  } while (0)
-#endif
 // dec_flags bits (per env, persistent across calls)
 #define DF_AWAITING 1
 #define DF_HAVE_IW 2
@@ -362,18 +305,12 @@ constexpr double kSinPhiAh = 0.93041756798202460;  // sin(68.5°)
 // it where the correctly rounded square root itself decides: the reference's boolean, without the
 // ~20-instruction f64 sqrt on every tick (NaN compares false either way)
 __device__ __forceinline__ bool sqrt_lt(double a, double c) {
-#ifdef SHIPSIM_PLAIN_SQRT  // diagnostics build: the square root on every call
-  return sqrt(a) < c;
-#endif
   const double c2 = c * c;
   if (a < c2 * (1.0 - 1e-12)) return true;
   if (!(a <= c2 * (1.0 + 1e-12))) return false;
   return sqrt(a) < c;
 }
 __device__ __forceinline__ bool sqrt_le(double a, double c) {
-#ifdef SHIPSIM_PLAIN_SQRT  // diagnostics build: the square root on every call
-  return sqrt(a) <= c;
-#endif
   const double c2 = c * c;
   if (a < c2 * (1.0 - 1e-12)) return true;
   if (!(a <= c2 * (1.0 + 1e-12))) return false;
@@ -386,15 +323,11 @@ __device__ __forceinline__ bool sqrt_le(double a, double c) {
 // in (0.9, 1000]) — in 11 VALU instructions instead of the general pow's 214. An infinite x⁴ (dist -> 0)
 // is returned as is.
 __device__ __forceinline__ double pow4(double x) {
-#ifdef SHIPSIM_GENERAL_POW  // diagnostics build: the general device pow
-  return pow(x, 4.0);
-#else
   const double h = x * x, l = fma(x, x, -h);
   const double h2 = h * h;
   if (!(h2 < INFINITY)) return h2;
   const double e = fma(h, h, -h2);
   return h2 + (e + (2.0 * h * l + l * l));
-#endif
 }
 
 // Per-sample collision cost H0 = C·R of sbmpc.py:205-289 (KAPPA_ = 0) for one prediction sample with
@@ -467,28 +400,6 @@ __device__ __forceinline__ double sbmpc_scenario_cost_direct(const SbIn& in, int
   return H1 + H2;
 }
 
-#ifdef SHIPSIM_PHASE_TIMING
-// timing build: split of one scenario evaluation into g_phase_cycles[4..7]
-struct SbTimer {
-  unsigned long long t0, acc[4] = {0, 0, 0, 0};
-  __device__ SbTimer() : t0(wall_clock64()) {}
-  __device__ void mark(int k) {
-    const unsigned long long t = wall_clock64();
-    acc[k] += t - t0;
-    t0 = t;
-  }
-  __device__ ~SbTimer() {
-    mark(3);
-    if ((threadIdx.x & 31) == 0)
-      for (int k = 0; k < 4; ++k) atomicAdd(&g_phase_cycles[4 + k], acc[k]);
-  }
-};
-#define SB_MARK(k) sb_timer.mark(k)
-#else
-#define SB_MARK(k) \
-  do {             \
-  } while (0)
-#endif
 
 // SBMPCParams.P_ca_ = [0.4, 0.6, 0.8, 1.0] (sbmpc.py:36) by selects: a per-lane indexed constant array would be
 // a memory load on the scenario's critical path
@@ -555,9 +466,7 @@ __device__ __forceinline__ void hz_sample(HzBest& h, const HzConst c, double tt,
 // same request) split the horizon's sample loop — part 0 takes the samples before i_split, part 1 the rest — and merge
 // their running bests (every other step is computed by both; the result is the same bits as part -1)
 __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int ichi, int jp, int part = -1) {
-#ifdef SHIPSIM_PHASE_TIMING
-  SbTimer sb_timer;
-#endif
+  SB_TIMER;
   const double os_l = 25.0;  // ShipLinearModel default length (sbmpc_misc.py:86, Q7)
   const double d_safe = 1000.0, d_close = 2000.0;
   // np.cos(np.deg2rad(PHI_OT_)) — PHI_OT_ is already in radians (sbmpc.py:248): a constant, taken
@@ -575,12 +484,7 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   // sincos(in.ob_psi) — in the AST kernels they are the obstacle ship's own carried sin/cos(yaw) with
   // ob_psi = -yaw, and the device sin is odd and cos even (both reduce |x|), so nothing is recomputed
   // per scenario
-#ifdef SHIPSIM_OB_SINCOS_CALL  // diagnostics build: the per-scenario call
-  double so, co;
-  sincos(in.ob_psi, &so, &co);
-#else
   const double so = in.ob_so, co = in.ob_co;
-#endif
   const double r11 = -so, r12 = co, r21 = co, r22 = so;
   const double vo0 = -so * in.ob_u + co * in.ob_v;  // rot2d(obstacle.psi_, [u, v])
   const double vo1 = co * in.ob_u + so * in.ob_v;
@@ -662,33 +566,12 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
   double ox = in.ob_x, oy = in.ob_y;
   double sx = in.os_x + DT * (q11 * ud + q12 * in.os_v), sy = in.os_y + DT * (q21 * ud + q22 * in.os_v);
   double t = DT;
-#ifdef SHIPSIM_ABL_NO_SBLOOP
-  n_samp = 1;  // ablation build only: no horizon samples after sample 0
-#endif
+  if constexpr (diag::kNoSbLoop) n_samp = 1;  // (ablation build only: no horizon samples after sample 0)
   HzBest hb{INFINITY, INFINITY, 0.0, 0.0, false};
   const HzConst hc{so, co, ovr2, ot2, ah2, cl2, ovr};
   auto sample = [&](double tt, double d0, double d1, double d2s, bool inr) __attribute__((always_inline)) {
     hz_sample(hb, hc, tt, d0, d1, d2s, inr);
   };
-#ifdef SHIPSIM_SB_ROLLED  // diagnostics build: one sample per iteration (no split: the caller passes part -1)
-  bool done = false;  // past the minimum and beyond the best (see i_past)
-  for (int i = 1; i < n_samp; ++i) {
-    if (!__any((i <= i_last) & !done)) break;  // every lane of the wave is past its last useful sample
-    ox = ox + dox;
-    oy = oy + doy;
-    if (i > 1) {
-      sx = sx + dsx;
-      sy = sy + dsy;
-    }
-    t += DT;
-    const double d0 = ox - sx, d1 = oy - sy;
-    const double d2s = d0 * d0 + d1 * d1;
-    // (The in-range branch stays: most samples of an env's requests are out of range, and a branch-free
-    // body measured 193 M vs 237 M env-ticks/s in the sbmpc bench.)
-    if (d2s < lim2) sample(t, d0, d1, d2s, true);
-    done = done | ((i >= i_past) & (hb.s1 < INFINITY) & (t * d2s * d2s > hb.s1 * (1.0 + 2e-10)));
-  }
-#else
   // two samples per iteration (i, i + 1): their bodies are independent chains the one wave of the SIMD
   // can interleave; the positions are the same incremental sums as one per iteration, and the samples
   // enter the running best in order (ties keep the earlier sample).
@@ -764,7 +647,6 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     hb.q1 = bwin ? Bp.q1 : A.q1;
     hb.unc = A.unc | Bp.unc;
   }
-#endif
   const double s1 = hb.s1, s2 = hb.s2, t1 = hb.t1, q1 = hb.q1;
   if (hb.unc)
     return sbmpc_scenario_cost_direct(in, n_samp, DT, ud, sp, cp, sp0, cp0, so, co, vo0, vo1, no, max_d_safe, lim2,
@@ -836,11 +718,7 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
     g.ob_so = shfl_d(in.ob_so, srcc); g.ob_co = shfl_d(in.ob_co, srcc);
     double cost = INFINITY;
     int idx = 64;
-#ifdef SHIPSIM_SB_ROLLED
-    const bool split = false;
-#else
     const bool split = src1 < 0;  // (uniform) one request this pass: both halves take it, each half of every horizon
-#endif
     if ((split || src >= 0) && scen < 28) {
       cost = sbmpc_scenario_cost(g, n_samp, DT, scen >> 2, scen & 3, split ? half : -1);
       idx = scen;
@@ -1418,11 +1296,7 @@ __device__ __forceinline__ const StepArgs& step_args() {
 // K > 1 obstacle ships (shipsim_create) ship k sits on the lanes of index k mod SLOTS, and slots past
 // the env's last ship repeat that ship (ghost lanes: same state and arithmetic, never stored).
 template <bool DETAILED, int COLLAV, int LPE, bool REC, int CHAIN = 0, int SLOTS = 2>
-#ifdef SHIPSIM_OCC2  // diagnostics build: two waves per SIMD (<= 256 VGPR + AGPR per wave)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ast_step_kernel(const StepArgs A_arg) {
-#else
 __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
-#endif
   constexpr bool POLICY = CHAIN == 2;  // CHAIN: 0 shipsim_step, 1 shipsim_run_table, 2 shipsim_run_policy
   (void)A_arg;  // read through step_args() only (see StepArgs)
   const StepArgs& A0 = step_args();
@@ -1443,18 +1317,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
   __shared__ float lds_pol[POLICY ? kPolMaxRows * kPolMaxHidden : 1];  // shipsim_run_policy: h1 rows
-#ifdef SHIPSIM_POISON_LDS
-  // diagnostics build (scripts, not the product): every LDS word gets a pattern before staging, so a
-  // read of LDS the kernel did not write sees the pattern instead of another kernel's leftovers
-  {
-    auto fill = [](void* p, size_t bytes) {
-      for (size_t i = threadIdx.x; i < bytes / 4; i += blockDim.x) ((uint32_t*)p)[i] = SHIPSIM_POISON_LDS;
-    };
-    fill(lds_sc, sizeof(lds_sc)); fill(lds_edges, sizeof(lds_edges));
-    fill(lds_edges_raw, sizeof(lds_edges_raw)); fill(lds_boxes, sizeof(lds_boxes));
+  if constexpr (diag::kPoisonLds) {  // (stale-LDS diagnostics build only)
+    diag::poison_lds(lds_sc, sizeof(lds_sc)); diag::poison_lds(lds_edges, sizeof(lds_edges));
+    diag::poison_lds(lds_edges_raw, sizeof(lds_edges_raw)); diag::poison_lds(lds_boxes, sizeof(lds_boxes));
     __syncthreads();
   }
-#endif
   const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
   for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) {
     const Edge ed = K.edges()[i];
@@ -1533,11 +1400,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   int tail_arrived = 0;  // this wave counted itself on the tail counter (an int: no lane mask held)
   int n_nonfinite = 0;
 
-#ifdef SHIPSIM_DEBUG_ENV
-  if (env == SHIPSIM_DEBUG_ENV && valid)
-    printf("[dbg] env %d lie %d start: running %d dflags %d sc %d n_base %f phase %d\n", env, lie, (int)running, dflags,
-           sampling_count, n_base, phase);
-#endif
+  SHIPSIM_DEBUG_PRINT(valid ? env : -1, "[dbg] env %d lie %d start: running %d dflags %d sc %d n_base %f phase %d\n", env,
+                      lie, (int)running, dflags, sampling_count, n_base, phase);
   // ---- intermediate waypoint sampling (env.py:659-696) for an env that waits for a decision ----
   // CHAIN: episode / decision counters, decisions completed and records written in this call
   int ep_i = 0, dec_i = 0, n_decided = 0, log_n = 0;
@@ -1741,10 +1605,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
 
   // (an int: OPQ kernels hold it in a VGPR, not as a lane mask live across the whole tick loop)
   int going = opaque_if<OPQ>((running && !ready && (budget <= 0 || ticks < budget)) ? 1 : 0);
-#ifdef SHIPSIM_PHASE_TIMING
-  unsigned long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long pt_last = wall_clock64();
-#endif
+  PT_DECL;
   // CHAIN: the tick loop hands over to the (rare) chaining code below whenever a decision of the
   // wave completes, so the loop body itself is the per-decision kernel's.
   for (;;) {
@@ -1835,11 +1696,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         const double los_arg = los_update(c, s, s.n, s.e);
         double d0 = pe - s.e, d1 = pn - s.n;
         need = sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_
-#if defined(SHIPSIM_ABL_SB_NEVER)  // timing diagnostics: SBMPC code kept, never requested (run-time false)
-        need = need && P.max_sampling < 0;
-#elif defined(SHIPSIM_ABL_SB_NONE)  // timing diagnostics: SBMPC compiled out of the tick loop
-        need = false;
-#endif
+        need = diag::sb_request(need, P.max_sampling);  // (the product: need itself)
         if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
         in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
@@ -1893,9 +1750,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     double d2 = INFINITY;
     bool gr = false;
     if (going) {
-#ifndef SHIPSIM_ABL_NO_MAPDIST
-      d2 = map_dist2_grid(K, lds_edges, s.n, s.e, sub, NSUB);
-#endif
+      if constexpr (!diag::kNoMapDist) d2 = map_dist2_grid(K, lds_edges, s.n, s.e, sub, NSUB);
       const double margin = c.l_ship / 2;  // check_condition.py:50-78 hull hard points
       // Every hull corner is within margin·√2 of the centre. With no coastline edge that close (the
       // ship's min over its cell's candidate edges, which hold every edge within kGroundReach) and the
@@ -1908,8 +1763,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       const int cc = K.cell(s.n, s.e);
       const int fcen = cc >= 0 ? (int)K.grid_flag[cc] : GRID_MIXED;
       const bool far_shore = d2s > lim * lim && fcen != GRID_MIXED && lim < kGroundReach;
-#ifndef SHIPSIM_ABL_NO_GROUND
-      if (far_shore) {
+      if constexpr (diag::kNoGround) {
+      } else if (far_shore) {
         gr = fcen == GRID_IN;
       } else if constexpr (NSUB == 8) {
         // 8 sub-lanes for 4 corners: sub-lanes k and k + 4 split corner k's ring edges (every other
@@ -1933,7 +1788,6 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
           if (corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) gr = true;
         }
       }
-#endif
       d2 = d2s;  // the ship's min over its sub-lanes' edge shares (reduced once, above)
     }
     int gri = gr ? XF_GROUND : 0;
@@ -2158,20 +2012,14 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     if (!__any(opaque_if<OPQ>(going))) break;  // (quota met, or every env of the wave stalled)
   }
   }
-#ifdef SHIPSIM_PHASE_TIMING
-  if ((threadIdx.x & 63) == 0)
-    for (int k = 0; k < 4; ++k) atomicAdd(&g_phase_cycles[k], pt_acc[k]);
-#endif
+  PT_FLUSH();
 
   if (touched == 0) return;  // (!valid || !touched)
   const StepArgs& AE = step_args();  // not the values loaded before the loop (no live range across it)
   const ChainArgs& CH = AE.CH;
   const Traj& TE = AE.T;
-#ifdef SHIPSIM_DEBUG_ENV
-  if (env == SHIPSIM_DEBUG_ENV)
-    printf("[dbg] env %d lie %d end: ready %d ticks %d sc %d n_base %f phase %d have_iw %d\n", env, lie, (int)ready,
-           ticks, sampling_count, n_base, phase, (int)have_iw);
-#endif
+  SHIPSIM_DEBUG_PRINT(env, "[dbg] env %d lie %d end: ready %d ticks %d sc %d n_base %f phase %d have_iw %d\n", env, lie,
+                      (int)ready, ticks, sampling_count, n_base, phase, (int)have_iw);
   const DevState So = opaque(AE.S);  // addresses recomputed here, not carried through the loop
   // the lane's role re-derived here (opaque), not lane masks carried through the loop
   const int lie_e = opaque_v(lie), sub_e = lie_e / SLOTS, ship_e = lie_e % SLOTS;
@@ -2317,11 +2165,7 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(LegacyArgs a_arg) {
         const double los_arg = los_update(c, s, s.n, s.e);
         const double d0 = pe - s.e, d1 = pn - s.n;
         need = sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_
-#if defined(SHIPSIM_ABL_SB_NEVER)  // timing diagnostics: SBMPC code kept, never requested (run-time false)
-        need = need && P.max_sampling < 0;
-#elif defined(SHIPSIM_ABL_SB_NONE)  // timing diagnostics: SBMPC compiled out of the tick loop
-        need = false;
-#endif
+        need = diag::sb_request(need, P.max_sampling);  // (the product: need itself)
         if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
         in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
         in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
@@ -2643,9 +2487,9 @@ int32_t shipsim_abi_version(void) { return SHIPSIM_ABI_VERSION; }
 #ifdef SHIPSIM_PHASE_TIMING
 // timing builds only (not part of the ABI): read and clear the per-phase cycle sums
 int shipsim_debug_phase_cycles(unsigned long long* out8) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(diag::g_phase_cycles), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
   unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)) == hipSuccess ? 0 : -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(diag::g_phase_cycles), z, sizeof(z)) == hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -3478,9 +3322,9 @@ int shipsim_diag_lane_faults(uint32_t* out32) {
   for (int i = 0; i < 32; ++i) out32[i] = 0;
 #ifdef SHIPSIM_LANECHECK
   if (hipDeviceSynchronize() != hipSuccess) return SHIPSIM_EHIP;
-  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_lane_diag), 32 * sizeof(uint32_t)) != hipSuccess) return SHIPSIM_EHIP;
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(diag::g_lane_diag), 32 * sizeof(uint32_t)) != hipSuccess) return SHIPSIM_EHIP;
   const uint32_t zero[32] = {};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_lane_diag), zero, sizeof(zero)) != hipSuccess) return SHIPSIM_EHIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(diag::g_lane_diag), zero, sizeof(zero)) != hipSuccess) return SHIPSIM_EHIP;
   return SHIPSIM_OK;
 #else
   return SHIPSIM_EINVAL;  // not a diagnostics build

@@ -8,8 +8,8 @@ Same CLI and variant as the reference. Two execution shapes:
 * `--n_envs N` (default 4096): the MI355X shape — N device-resident envs per GPU stepped in
   slices, transitions written straight into a DeviceReplayBuffer, FusedSACTrainer (HIP-graph
   step) and DeviceBatchRLAlgorithm. Under torch.distributed.run every rank owns N envs. With
-  --dp_mode replicated (default) every rank keeps the union of all ranks' transitions (one RCCL
-  all-gather of the new rows per train loop) and runs the same global-batch SAC step, so no
+  --dp_mode replicated (default) every rank keeps the union of all ranks' transitions (RCCL
+  all-gathers of the row counts and the new rows once per train loop) and runs the same global-batch SAC step, so no
   collective runs per grad step; --dp_mode allreduce gives each rank a local buffer and averages
   the SAC gradients with one RCCL all-reduce per grad step.
 
@@ -81,7 +81,7 @@ def build_parser():
                         "(the reference's ratio); false: num_trains_per_train_loop per loop")
     p.add_argument("--dp_mode", type=str, default="replicated", choices=["replicated", "allreduce"],
                    help="multi-rank SAC: replicated = every rank trains on the union of all ranks' transitions (one "
-                        "all-gather per train loop, no per-step collective); allreduce = local buffers, one gradient "
+                        "row all-gather (after a count all-gather) per train loop, no per-step collective); allreduce = local buffers, one gradient "
                         "all-reduce per grad step")
     p.add_argument("--machinery", type=str, default="detailed", choices=["detailed", "simplified"])
     p.add_argument("--seed", type=int, default=None)
@@ -148,6 +148,17 @@ def experiment_reference(variant, args, device):
     return algo
 
 
+def replicated_stage_rows(args, ak):
+    """Rows the replicated buffer's staging ring must hold between two syncs (one per collect): the largest
+    collect's decisions plus the overshoot of its last batch of passes, which the collector bounds to the ring's
+    free rows (batched_collector.py collect) — at least two passes of the widest kind (fused: N x the log cap)."""
+    from ..ast_sac.samplers.data_collector.batched_collector import BatchedPathCollector as C
+    ticks = args.slice_ticks or C.FUSED_TICKS
+    tail = C.FUSED_TAIL if args.stream_tail < 0 else args.stream_tail
+    per_pass = args.n_envs * C.log_cap_for(ticks, tail)
+    return max(65536, max(ak["min_num_steps_before_training"], ak["num_expl_steps_per_train_loop"]) + 2 * per_pass)
+
+
 def experiment_device(variant, args, device, process_group=None):
     from ..rl_env.ship_in_transit.env import BatchedMultiShipRLEnv, config_from_args
     from ..ast_sac.env_wrapper.normalized_box_env import BatchedNormalizedBoxEnv
@@ -173,10 +184,11 @@ def experiment_device(variant, args, device, process_group=None):
     ak = variant["algorithm_kwargs"]
     # --batch_size is the GLOBAL batch (the reference's 256, run/ast-sac_runner.py:55)
     world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
-    replicated = world > 1 and variant.get("dp_mode", "replicated") == "replicated"
+    # (a process group of one rank takes the replicated path too: the N-rank code, an identity on the data)
+    replicated = process_group is not None and variant.get("dp_mode", "replicated") == "replicated"
     if replicated:  # every rank: the union of all ranks' rows, the whole global batch, the same seed
-        stage = max(65536, args.n_envs * 64)  # rows one collect can stage (fused passes: <= 32 per env per pass)
-        rb = ReplicatedReplayBuffer(variant["replay_buffer_size"], obs_dim, act_dim, device, process_group, stage)
+        rb = ReplicatedReplayBuffer(variant["replay_buffer_size"], obs_dim, act_dim, device, process_group,
+                                    replicated_stage_rows(args, ak))
         per_rank_batch = ak["batch_size"]
     else:  # each rank samples batch_size / world rows from its own shard; the averaged gradient equals the
         # single-GPU B-row gradient in expectation

@@ -251,6 +251,24 @@ def bench_sac(dev, world, pg, steps, global_batch, eager_steps=40, graph=True, d
                                 "backward and weight-gradient products of every layer of the reference's "
                                 "formulation, per rank) / whole-step wall time (every launch of the step); "
                                 "v_mfma_f32_32x32x2_f32 dense f32 peak"}}
+    if replicated:  # the per-train-loop cost the step timing leaves out: ReplicatedReplayBuffer.sync()
+        from ast_sac_amd.ast_sac.data_management.replay_buffer import ReplicatedReplayBuffer
+        per_rank = 32768  # one fused collector pass of 4096 envs stages ~8 decisions per env
+        rbr = ReplicatedReplayBuffer(300000, 8, 1, dev, pg, stage_size=65536)
+
+        def stage_and_sync(k):
+            for _ in range(k):
+                rbr.add_batch(torch.randn(per_rank, 8, device=dev), torch.rand(per_rank, 1, device=dev),
+                              torch.randn(per_rank, 1, device=dev), torch.randn(per_rank, 8, device=dev),
+                              torch.zeros(per_rank, 1, device=dev))
+                rbr.sync()
+        stage_and_sync(2)
+        t_sync = timed(stage_and_sync, 10) / 10
+        loop_steps = per_rank * world * 240 / 256  # grad steps one such loop runs at the reference's ratio
+        res["replicated_sync"] = {"rows_per_rank": per_rank, "ms_per_sync": t_sync * 1e3,
+                                  "us_per_grad_step": t_sync / loop_steps * 1e6,
+                                  "note": "staging + two all-gathers (counts, rows) + the ring append, once per train "
+                                          "loop; amortised over the loop's grad steps at the reference's 240:256 ratio"}
     if world == 1 and eager_steps:
         res["torch_ops_graph_grad_steps_per_s"] = steps / fused("torch")
     if world == 1 and eager_steps:
@@ -539,6 +557,35 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
+    # the same stream without the launch tail (the training collector's default, FUSED_TAIL = 0), beside the
+    # headline, which runs with it (--tail-ticks): the same number of launches, continuing the same envs
+    tail_off = None
+    if args.mode == "table" and args.tail_ticks > 0:
+        progress("headline stream without the launch tail")
+        sim.set_stream_tail(0)
+        off_ticks = torch.zeros((), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t_off = time.perf_counter()
+        for i in range(args.steps):
+            dlog_len.zero_()
+            sim.run_table(table, args.slice, ep32, dec32, out=tout, log=dlog, log_len=dlog_len)
+            off_ticks.add_(tout["ticks"].sum())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        off = torch.tensor([time.perf_counter() - t_off, float(off_ticks.item())], dtype=torch.float64, device=dev)
+        if world > 1:
+            mx, sm = off.clone(), off.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+            off = torch.stack([mx[0], sm[1]])
+        tail_off = {"value": float(off[1]) / float(off[0]), "ms_per_step": float(off[0]) / args.steps * 1e3,
+                    "tail_ticks": 0, "note": "the same C3 stream and launches with the work-conserving launch tail "
+                                             "off (the training collector's default); the headline runs with it"}
+        sim.set_stream_tail(args.tail_ticks)
+
     all_ms = np.array([a.elapsed_time(b) for a, b in zip(ev0, ev1)])
     kern_ms = all_ms[:args.steps]
     local_ticks = int(total_ticks.item())
@@ -632,6 +679,8 @@ def main():
                        "mode": args.mode, "tail_ticks": args.tail_ticks if args.mode == "table" else 0,
                        "parallelism": f"env-shard x{world}" + (f" on {n_devices} device(s), {args.dist_backend}"
                                                                   if n_devices != world else "")},
+            "launch_tail": ({"headline_with_tail_ticks": args.tail_ticks, "without_tail": tail_off}
+                            if tail_off else None),
             "decisions_per_s": all_dec / elapsed,
             "env_ticks_per_decision": all_ticks / max(all_dec, 1),
             "decision_log": {"cap": dlog_cap, "max_per_launch": int(dlog_max.item())} if args.mode == "table" else None,

@@ -26,13 +26,15 @@ N = 4096
 N_EPS = 3
 
 
-def _run(cfg, a_norm, SLICE, LAUNCHES):
+def _run(cfg, a_norm, SLICE, LAUNCHES, tail=0):
     sim = ShipSim(cfg, N)
     sim.reset()
+    if tail:
+        sim.set_stream_tail(tail)
     table = torch.from_numpy(abi.normalized_to_scoping(a_norm)).cuda()
     ep = torch.zeros(N, dtype=torch.int32, device="cuda")
     dec = torch.zeros(N, dtype=torch.int32, device="cuda")
-    cap = 144
+    cap = 144 if not tail else 288  # (the tail case: up to 2 x 5120 ticks, decisions of >= ~76 ticks)
     log = torch.zeros((N, cap, abi.DECLOG_COLS), dtype=torch.float64, device="cuda")
     log_len = torch.zeros(N, dtype=torch.int32, device="cuda")
     ticks = []
@@ -75,20 +77,29 @@ def _match(g_eps, o_rec, rtol=1e-5):
     return worst
 
 
-@pytest.mark.parametrize("collav,SLICE,LAUNCHES,mach", [("sbmpc", 128, 12, "detailed"), ("none", 128, 12, "detailed"),
-                                                       ("sbmpc", 4096, 1, "detailed"), ("simple", 1024, 2, "detailed"),
-                                                       ("sbmpc", 1024, 2, "simplified"),
-                                                       ("none", 1024, 2, "simplified")])
-def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach):
+# The last case is bench.py's headline launch exactly: sbmpc, detailed machinery, 4096 envs, 4096-tick launches with
+# the 1024-tick work-conserving launch tail (shipsim_set_stream_tail), over bench.py's own 8-episode PCG64 table
+# (seed 20251015, rank 0); two launches, so the second resumes every env where the tail left it.
+@pytest.mark.parametrize("collav,SLICE,LAUNCHES,mach,tail,n_eps",
+                         [("sbmpc", 128, 12, "detailed", 0, N_EPS), ("none", 128, 12, "detailed", 0, N_EPS),
+                          ("sbmpc", 4096, 1, "detailed", 0, N_EPS), ("simple", 1024, 2, "detailed", 0, N_EPS),
+                          ("sbmpc", 1024, 2, "simplified", 0, N_EPS), ("none", 1024, 2, "simplified", 0, N_EPS),
+                          ("sbmpc", 4096, 2, "detailed", 1024, 8)])
+def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach, tail, n_eps):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     cfg = abi.ast_config(collav, machinery=abi.MACH_DETAILED if mach == "detailed" else abi.MACH_SIMPLIFIED)
     n_dec = cfg.max_sampling_frequency
-    a_norm = np.random.Generator(np.random.PCG64(20251015)).uniform(-1, 1, (N_EPS, n_dec, N)).astype(np.float32)
-    log, log_len, ticks, ep, dec = _run(cfg, a_norm, SLICE, LAUNCHES)
+    a_norm = np.random.Generator(np.random.PCG64(20251015)).uniform(-1, 1, (n_eps, n_dec, N)).astype(np.float32)
+    log, log_len, ticks, ep, dec = _run(cfg, a_norm, SLICE, LAUNCHES, tail)
 
     # invariants, every env
-    assert ticks.max() <= SLICE and (ticks == SLICE).mean() > 0.99  # the stream keeps every env busy
+    if tail:  # the tail extends a launch by whole chunks, up to `tail` more ticks per env
+        assert ticks.max() <= SLICE + tail and (ticks >= SLICE).mean() > 0.99, (ticks.min(), ticks.max())
+        print(f"\n[launch tail {tail}] ticks per env per launch: min {ticks.min()} mean {ticks.mean():.1f} "
+              f"max {ticks.max()}")
+    else:
+        assert ticks.max() <= SLICE and (ticks == SLICE).mean() > 0.99  # the stream keeps every env busy
     assert (log_len >= 4).all() and log_len.max() <= log.shape[1]
     total_dec = 0
     for i in range(N):
@@ -108,7 +119,7 @@ def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach):
 
     # oracle, every 4th env
     idx = np.arange(0, N, 4)
-    tables = [[a_norm[k % N_EPS, :, i] for k in range(int(log[i, log_len[i] - 1, abi.DL_EPISODE]) + 1)] for i in idx]
+    tables = [[a_norm[k % n_eps, :, i] for k in range(int(log[i, log_len[i] - 1, abi.DL_EPISODE]) + 1)] for i in idx]
     g_all = [_episodes(log[i, :log_len[i]]) for i in idx]
     orc = H.run_oracle(cfg, tables)
     worst, bad, perturbed = 0.0, [], 0
@@ -128,7 +139,7 @@ def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach):
         else:
             worst = max(worst, w)
     frac = perturbed / len(idx)
-    print(f"\n[{collav} {mach} slice {SLICE}] {len(idx)} envs vs oracle, {sum(len(e) for e in g_all)} decisions; "
+    print(f"\n[{collav} {mach} slice {SLICE} tail {tail}] {len(idx)} envs vs oracle, {sum(len(e) for e in g_all)} decisions; "
           f"matched only by a perturbed oracle run: {perturbed} ({100 * frac:.2f} %); off the oracle: {len(bad)}; "
           f"worst rel err {worst:.2e}")
     assert not bad, f"envs off the oracle: {bad[:20]}"
