@@ -935,15 +935,17 @@ __device__ __forceinline__ double map_dist2_part(const EdgeX* __restrict__ E, in
   return best;
 }
 
-// same value as map_dist2_part over every edge when the true distance is <= kGroundReach (see above)
-__device__ __forceinline__ double map_dist2_grid(const ConstBuf& K, const EdgeX* __restrict__ E, double n, double e,
-                                                 int sub, int nsub) {
-  const int c = K.cell(n, e);
-  if (c < 0) return map_dist2_part(E, K.n_edges, n, e, sub, nsub);
-  // this sub-lane's share of the cell's candidate edges: the set bits of rank = sub (mod nsub), read
-  // from the host-split masks (rank mod 8; nsub divides 8) — the min is over the same edges either way
+// this sub-lane's share of grid cell c's candidate edges: the set bits of rank = sub (mod nsub), read from the
+// host-split masks (rank mod 8; nsub divides 8) — the min over the shares is over the same edges either way
+__device__ __forceinline__ uint64_t grid_share(const ConstBuf& K, int c, int sub, int nsub) {
   uint64_t m = 0;
   for (int q = sub; q < 8; q += nsub) m |= K.grid_part[(size_t)c * 8 + q];
+  return m;
+}
+
+// map_dist2_part over the edges of mask m (a grid cell's share): the same value as map_dist2_part over every edge
+// when the true distance is <= kGroundReach (see above)
+__device__ __forceinline__ double map_dist2_mask(const EdgeX* __restrict__ E, uint64_t m, double n, double e) {
   const double px = e, py = n;
   double best = INFINITY;
   while (m) {
@@ -1603,6 +1605,11 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     }
   }
 
+  // The grid cell of the ship's position at its last map query, this sub-lane's share of the cell's candidate
+  // edges and the cell's class: a ship moves a few metres per tick through 200 m cells, so the two dependent
+  // global loads of a query are only issued when the cell changes (-2: none yet)
+  int g_cell = -2, g_flag = GRID_MIXED;
+  uint64_t g_mask = 0;
   // (an int: OPQ kernels hold it in a VGPR, not as a lane mask live across the whole tick loop)
   int going = opaque_if<OPQ>((running && !ready && (budget <= 0 || ticks < budget)) ? 1 : 0);
   PT_DECL;
@@ -1750,7 +1757,14 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     double d2 = INFINITY;
     bool gr = false;
     if (going) {
-      if constexpr (!diag::kNoMapDist) d2 = map_dist2_grid(K, lds_edges, s.n, s.e, sub, NSUB);
+      const int cc = K.cell(s.n, s.e);
+      if (cc != g_cell) {  // (rare) a new cell: its edge share and class
+        g_cell = cc;
+        g_mask = cc >= 0 ? grid_share(K, cc, sub, NSUB) : 0;
+        g_flag = cc >= 0 ? (int)K.grid_flag[cc] : GRID_MIXED;
+      }
+      if constexpr (!diag::kNoMapDist)
+        d2 = cc >= 0 ? map_dist2_mask(lds_edges, g_mask, s.n, s.e) : map_dist2_part(lds_edges, K.n_edges, s.n, s.e, sub, NSUB);
       const double margin = c.l_ship / 2;  // check_condition.py:50-78 hull hard points
       // Every hull corner is within margin·√2 of the centre. With no coastline edge that close (the
       // ship's min over its cell's candidate edges, which hold every edge within kGroundReach) and the
@@ -1760,8 +1774,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       int dummy = 0;
       ship_reduce<LPE, SLOTS>(d2s, dummy);
       const double lim = margin * 1.4142135623730951 + 1e-3;
-      const int cc = K.cell(s.n, s.e);
-      const int fcen = cc >= 0 ? (int)K.grid_flag[cc] : GRID_MIXED;
+      const int fcen = g_flag;
       const bool far_shore = d2s > lim * lim && fcen != GRID_MIXED && lim < kGroundReach;
       if constexpr (diag::kNoGround) {
       } else if (far_shore) {
@@ -2305,7 +2318,7 @@ struct shipsim_handle {
 };
 
 // ---------------------------------------------------------------------------------------------
-// map grid (host): exact, conservative cell classification used by corner_inside / map_dist2_grid
+// map grid (host): exact, conservative cell classification used by corner_inside / map_dist2_mask
 // ---------------------------------------------------------------------------------------------
 static const double kGridCell = 200.0;     // m
 static const double kGridPad = 2000.0;     // m of grid beyond the polygon bounding box
