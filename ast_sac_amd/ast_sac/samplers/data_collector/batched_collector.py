@@ -17,7 +17,7 @@ Two ways to pick the actions:
   on the host only every few passes (it plans the passes from the count per pass), and the episodes that
   ended go to a device ring that is copied to the host once per collect (record_paths).
   With `fused` (the default when the env library can run this policy itself: one obstacle ship, the
-  TanhGaussianPolicy's obs dim 8 and hidden 64/128/192/256), the policy is evaluated INSIDE the env launch
+  TanhGaussianPolicy's obs dim 8 and hidden a multiple of 64 up to 512), the policy is evaluated INSIDE the env launch
   (shipsim_run_policy): an env that completes a decision gets its next action at once and keeps ticking,
   an ended episode is reset in place, so no env idles until the pass ends. The launch logs every decision
   (observation, action, reward, next observation, events); the pass turns the log into replay rows and
@@ -134,7 +134,7 @@ class BatchedPathCollector:
 
     def _fused_supported(self):
         """The env library can run this collector's policy inside the env launch (shipsim_run_policy): a
-        device policy exposing its weights, one obstacle ship, obs dim 8, hidden 64/128/192/256, and the
+        device policy exposing its weights, one obstacle ship, obs dim 8, hidden a multiple of 64 up to 512, and the
         wrapper's action bounds equal to the env's (so the in-kernel NormalizedBoxEnv mapping is the
         wrapper's)."""
         dp = self._device_policy
@@ -145,7 +145,7 @@ class BatchedPathCollector:
         if sim is None or sim.n_ships != 2 or not hasattr(sim, "run_policy"):
             return False
         _, _, o, h = dp.weights()
-        if o != 8 or h % 64 or not 64 <= h <= 256:
+        if o != 8 or h % 64 or not 64 <= h <= 512:
             return False
         cfg = sim.cfg
         lb, ub = (-1.0, 1.0) if cfg.normalize_action else (cfg.action_low, cfg.action_high)

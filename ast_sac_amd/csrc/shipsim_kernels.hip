@@ -1029,7 +1029,7 @@ __device__ __forceinline__ DevState opaque(const DevState& S) {
 // h1 staged in LDS); the heads are reduced across the wave. fp32 as the policy.
 // ---------------------------------------------------------------------------------------------
 constexpr int kPolMaxRows = 8;
-constexpr int kPolMaxHidden = 256;
+constexpr int kPolMaxHidden = 512;
 
 __device__ inline void philox_env(uint32_t c[4], uint32_t k0, uint32_t k1) {  // Philox4x32-10
   for (int i = 0; i < 10; ++i) {
@@ -1054,23 +1054,30 @@ __device__ __forceinline__ float wave_sum_f(float x) {  // butterfly: every lane
 
 // Must be called by every lane of the wave. want: this lane's env needs its next action (all lanes of an
 // env agree); ns: its observation; seq: the env's decisions completed in this call (noise stream index).
-// Returns the normalized action a in (-1, 1) for lanes whose env wanted one. Lane l owns the nj = H / 64
-// consecutive hidden units [l·nj, l·nj + nj): one row of the transposed fc1 weight is one coalesced load
-// per lane (a float4 at H = 256), and the h1 rows in LDS are read as broadcast float4s.
+// Returns the normalized action a in (-1, 1) for lanes whose env wanted one. The hidden units are taken in slices
+// of 256 (one slice up to H = 256, two above): in slice c lane l owns the nj = min(4, (H - 256c) / 64) consecutive
+// units [256c + l·nj, 256c + l·nj + nj), so one row of the transposed fc1 weight is one coalesced load per lane (a
+// float4 in a full slice) and the h1 rows in LDS are read as broadcast float4s; the fc1 accumulators of one slice
+// are live at a time (the register budget of H = 256 at every width), and each lane's head partials run on across
+// the slices in unit order.
 __device__ __forceinline__ float policy_actions(bool want, const float ns[8], int env, bool env_leader, int env_lane0,
                                                 int seq, const ChainArgs& CH, float* lds_h1) {
   SHIPSIM_LANE_CHECK(64, 5);
   uint64_t req = __ballot(want && env_leader);
   float act = 0.0f;
   const int lane = threadIdx.x & 63;
-  const int H = CH.pol_hidden, nj = H / 64, u0 = lane * nj;
+  const int H = CH.pol_hidden, n_slices = (H + 255) / 256;
   const float* W1 = CH.policy;  // [H][8] (obs_dim 8: checked by the host)
   asm volatile("" : "+s"(W1));  // (the weight addresses below derived per call, not held across the tick loop)
-  const float* b1 = W1 + (size_t)H * 8;
-  const float* b2 = b1 + H + (size_t)H * H;
-  const float* wm = b2 + H;
-  const float* ws = wm + H + 1;
-  constexpr int kJ = kPolMaxHidden / 64;
+  // the parameter blocks after W1 [H][8]: b1 [H], W2 [H][H], b2 [H], wm [H], bm, ws [H], bs — their addresses
+  // derived where each is read, from a copy of W1 the compiler cannot hoist (no pointer pair live across the pass)
+  auto blk = [&](int which) __attribute__((always_inline)) {
+    const float* w = W1;
+    asm volatile("" : "+s"(w));
+    const size_t b1 = (size_t)H * 8, b2 = b1 + H + (size_t)H * H;
+    return w + (which == 0 ? b1 : which == 1 ? b2 : which == 2 ? b2 + H : b2 + 2 * (size_t)H + 1);
+  };
+  constexpr int kJ = 4;  // units per lane per slice, at most
   while (req) {
     // the next (up to) kPolMaxRows requesting envs: the lowest set bits of req (no indexed arrays: row e's
     // source lane is recomputed from the mask, so nothing lands in scratch)
@@ -1086,63 +1093,86 @@ __device__ __forceinline__ float policy_actions(bool want, const float ns[8], in
         float x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = __shfl(ns[i], src, 64);
+#pragma nounroll
+        for (int c = 0; c < n_slices; ++c) {
+          const int nj = min(4, (H - 256 * c) >> 6), u0 = 256 * c + lane * nj;
 #pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          if (j < nj) {
-            const int u = u0 + j;
-            float h = b1[u];  // (the parameters are 4-byte aligned only: log α leads them)
+          for (int j = 0; j < kJ; ++j) {
+            if (j < nj) {
+              const int u = u0 + j;
+              float h = blk(0)[u];  // (the parameters are 4-byte aligned only: log α leads them)
 #pragma unroll
-            for (int i = 0; i < 8; ++i) h = fmaf(W1[(size_t)u * 8 + i], x[i], h);
-            lds_h1[e * kPolMaxHidden + u] = fmaxf(h, 0.0f);
+              for (int i = 0; i < 8; ++i) h = fmaf(W1[(size_t)u * 8 + i], x[i], h);
+              lds_h1[e * kPolMaxHidden + u] = fmaxf(h, 0.0f);
+            }
           }
         }
       }
     }
     __syncthreads();  // (one wave per block)
-    // fc1 + relu: acc[e][j] = b2[u] + sum_k W2[u][k] h1[e][k], k ascending; W2T row k is [H] contiguous
-    float acc[kPolMaxRows][kJ];
+    // per slice: fc1 + relu, acc[e][j] = b2[u] + sum_k W2[u][k] h1[e][k], k ascending (W2T row k is [H]
+    // contiguous), folded into this lane's head partials pm / ps (fmaf chains over its units in order)
+    float pm[kPolMaxRows], ps[kPolMaxRows];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      const float bj = j < nj ? b2[u0 + j] : 0.0f;
+    for (int e = 0; e < kPolMaxRows; ++e) pm[e] = ps[e] = 0.0f;
+#pragma nounroll
+    for (int c = 0; c < n_slices; ++c) {
+      const int nj = min(4, (H - 256 * c) >> 6), u0 = 256 * c + lane * nj;
+      float acc[kPolMaxRows][kJ];
+      const float* b2 = blk(1);
 #pragma unroll
-      for (int e = 0; e < kPolMaxRows; ++e) acc[e][j] = bj;
-    }
-    for (int k = 0; k < H; k += 4) {
-      float w[4][kJ];
-      if (nj == 4) {  // H = 256: one float4 per row
+      for (int j = 0; j < kJ; ++j) {
+        const float bj = j < nj ? b2[u0 + j] : 0.0f;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const float4 v = *reinterpret_cast<const float4*>(CH.w2t + (size_t)(k + kk) * H + u0);
-          w[kk][0] = v.x; w[kk][1] = v.y; w[kk][2] = v.z; w[kk][3] = v.w;
+        for (int e = 0; e < kPolMaxRows; ++e) acc[e][j] = bj;
+      }
+      for (int k = 0; k < H; k += 4) {
+        float w[4][kJ];
+        if (nj == 4) {  // a full slice: one float4 per row
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const float4 v = *reinterpret_cast<const float4*>(CH.w2t + (size_t)(k + kk) * H + u0);
+            w[kk][0] = v.x; w[kk][1] = v.y; w[kk][2] = v.z; w[kk][3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int j = 0; j < kJ; ++j) w[kk][j] = j < nj ? CH.w2t[(size_t)(k + kk) * H + u0 + j] : 0.0f;
         }
-      } else {
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
+        for (int e = 0; e < kPolMaxRows; ++e) {
+          if (e < E) {
+            const float4 h4 = *reinterpret_cast<const float4*>(lds_h1 + e * kPolMaxHidden + k);
 #pragma unroll
-          for (int j = 0; j < kJ; ++j) w[kk][j] = j < nj ? CH.w2t[(size_t)(k + kk) * H + u0 + j] : 0.0f;
+            for (int j = 0; j < kJ; ++j) {
+              acc[e][j] = fmaf(w[0][j], h4.x, acc[e][j]);
+              acc[e][j] = fmaf(w[1][j], h4.y, acc[e][j]);
+              acc[e][j] = fmaf(w[2][j], h4.z, acc[e][j]);
+              acc[e][j] = fmaf(w[3][j], h4.w, acc[e][j]);
+            }
+          }
+        }
+      }
+      float wmj[kJ], wsj[kJ];
+      const float *wm = blk(2), *ws = blk(3);
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        wmj[j] = j < nj ? wm[u0 + j] : 0.0f;
+        wsj[j] = j < nj ? ws[u0 + j] : 0.0f;
       }
 #pragma unroll
       for (int e = 0; e < kPolMaxRows; ++e) {
-        if (e < E) {
-          const float4 h4 = *reinterpret_cast<const float4*>(lds_h1 + e * kPolMaxHidden + k);
 #pragma unroll
-          for (int j = 0; j < kJ; ++j) {
-            acc[e][j] = fmaf(w[0][j], h4.x, acc[e][j]);
-            acc[e][j] = fmaf(w[1][j], h4.y, acc[e][j]);
-            acc[e][j] = fmaf(w[2][j], h4.z, acc[e][j]);
-            acc[e][j] = fmaf(w[3][j], h4.w, acc[e][j]);
-          }
+        for (int j = 0; j < kJ; ++j) {
+          const float y = fmaxf(acc[e][j], 0.0f);
+          pm[e] = fmaf(wmj[j], y, pm[e]);
+          ps[e] = fmaf(wsj[j], y, ps[e]);
         }
       }
     }
     // heads (mean, log_std) reduced across the wave, the sample, and the hand-over to the env's lanes
-    float wmj[kJ], wsj[kJ];
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      wmj[j] = j < nj ? wm[u0 + j] : 0.0f;
-      wsj[j] = j < nj ? ws[u0 + j] : 0.0f;
-    }
-    const float bm = wm[H], bs = ws[H];
+    const float bm = blk(2)[H], bs = blk(3)[H];
     const uint64_t ctr = CH.pol_counter ? (uint64_t)*CH.pol_counter : 0;
     uint64_t m = rows;
 #pragma unroll
@@ -1150,15 +1180,8 @@ __device__ __forceinline__ float policy_actions(bool want, const float ns[8], in
       if (e < E) {
         const int src = __ffsll((unsigned long long)m) - 1;
         m &= m - 1;
-        float pm = 0.0f, ps = 0.0f;
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          const float y = fmaxf(acc[e][j], 0.0f);
-          pm = fmaf(wmj[j], y, pm);
-          ps = fmaf(wsj[j], y, ps);
-        }
-        const float mean = wave_sum_f(pm) + bm;
-        const float log_std = fminf(fmaxf(wave_sum_f(ps) + bs, -20.0f), 2.0f);
+        const float mean = wave_sum_f(pm[e]) + bm;
+        const float log_std = fminf(fmaxf(wave_sum_f(ps[e]) + bs, -20.0f), 2.0f);
         float z = mean;
         if (!CH.pol_det) {
           const int e_env = __shfl(env, src, 64), e_seq = __shfl(seq, src, 64);
@@ -3189,7 +3212,7 @@ int shipsim_run_policy(shipsim_handle* h, const float* policy, const float* w2t,
   if (h->T.ship) return fail(h, SHIPSIM_EINVAL, "run_policy: trajectory recording is on (use shipsim_step)");
   if (obs_dim != 8) return fail(h, SHIPSIM_EINVAL, "run_policy: observation dim %d (the AST observation has 8)", obs_dim);
   if (hidden < 64 || hidden > kPolMaxHidden || hidden % 64)
-    return fail(h, SHIPSIM_EINVAL, "run_policy: hidden %d (64, 128, 192 or 256)", hidden);
+    return fail(h, SHIPSIM_EINVAL, "run_policy: hidden %d (a multiple of 64 up to 512)", hidden);
   if (ship_slots(h) > 2) return fail(h, SHIPSIM_EINVAL, "run_policy: one obstacle ship only");
   ChainArgs ch = {};
   ch.n_eps = 1; ch.n_dec = n_dec; ch.ep_idx = ep_idx; ch.dec_idx = dec_idx;

@@ -283,9 +283,9 @@ def bench_sac(dev, world, pg, steps, global_batch, eager_steps=40, graph=True, d
     return res
 
 
-def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1, tail_ticks=0):
+def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1, tail_ticks=0, hidden=256):
     """The C3 envs with the policy in the loop (secondary line): shipsim_run_policy, every decision's action
-    sampled inside the launch from a TanhGaussianPolicy (runner networks 2x256, random init, stochastic) held
+    sampled inside the launch from a TanhGaussianPolicy (runner networks 2 x `hidden`, random init, stochastic) held
     by a FusedSACTrainer — the collector's fused pass without the replay bookkeeping. env-ticks/s over
     `launches` launches of `slice_ticks` ticks (HIP events on the launch stream), with the table line's
     work-conserving launch tail of `tail_ticks` (shipsim_set_stream_tail; 0: off)."""
@@ -301,8 +301,8 @@ def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1, tai
             shape = (1,)
 
     torch.manual_seed(0)
-    q = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[256, 256]).to(dev) for _ in range(4)]
-    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[256, 256]).to(dev)
+    q = [ConcatMlp(input_size=9, output_size=1, hidden_sizes=[hidden, hidden]).to(dev) for _ in range(4)]
+    pol = TanhGaussianPolicy(obs_dim=8, action_dim=1, hidden_sizes=[hidden, hidden]).to(dev)
     tr = FusedSACTrainer(env=_Env, policy=pol, qf1=q[0], qf2=q[1], target_qf1=q[2], target_qf2=q[3],
                          discount=0.965, soft_target_tau=1e-3, policy_lr=8e-5, qf_lr=8e-5, reward_scale=0.75,
                          batch_size=256, backend="hip")
@@ -640,6 +640,10 @@ def main():
     pstream = (bench_policy_stream(dev, cfg, N, args.slice if args.mode == "table" else 4096,
                                    tail_ticks=max(args.tail_ticks, 0) if args.mode == "table" else 0)
                if (rank == 0 and not args.no_policy_stream and args.obs_ships == 1) else None)
+    if pstream is not None:  # the runner's --layer_size 512: the in-kernel fc1 in two 256-unit slices
+        p512 = bench_policy_stream(dev, cfg, N, args.slice if args.mode == "table" else 4096, launches=1,
+                                   tail_ticks=max(args.tail_ticks, 0) if args.mode == "table" else 0, hidden=512)
+        pstream["hidden_512"] = {k: p512[k] for k in ("env_ticks_per_s", "decisions_per_s", "kernel_ms", "launches")}
     progress("sac")
     sac = sac_ar = None
     if args.sac_steps > 0:

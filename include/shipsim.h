@@ -405,7 +405,7 @@ int shipsim_run_table(shipsim_handle* h, const float* table, int32_t n_eps, int3
  *   policy   the policy's parameters in torch order (fcs[0].weight [H][obs_dim], .bias, fcs[1].weight
  *            [H][H], .bias, last_fc.weight [1][H], .bias, last_fc_log_std.weight, .bias), device
  *   w2t      fcs[1].weight transposed ([H][H], w2t[k][u] = W2[u][k]), device (sacf_policy_weights)
- *   obs_dim  8; hidden 64, 128, 192 or 256
+ *   obs_dim  8; hidden a multiple of 64 up to 512
  *   seed, counter  the noise: eps of env i's s-th decision of a call is Philox4x32-10 keyed by seed on
  *            {i, *counter (64 bits), 0x5A100000 ^ s} then Box-Muller; *counter is read, not changed —
  *            advance it between calls (ignored when deterministic; counter may then be NULL)

@@ -80,7 +80,8 @@ def _check_rollout(recs, n_dec, init):
     return n
 
 
-@pytest.mark.parametrize("collav,H", [("sbmpc", 256), ("none", 64), ("simple", 128)])
+# 512: two full 256-unit slices of the in-kernel fc1; 320: a full slice and a one-unit-per-lane one
+@pytest.mark.parametrize("collav,H", [("sbmpc", 256), ("none", 64), ("simple", 128), ("sbmpc", 512), ("none", 320)])
 def test_policy_stream_deterministic(collav, H):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -114,10 +115,11 @@ def test_policy_stream_deterministic(collav, H):
         np.testing.assert_array_equal(rep[i][:k][:, _KEEP], recs[i][:, _KEEP], err_msg=f"{collav} env {i}")
 
 
-def test_policy_stream_stochastic_noise():
+@pytest.mark.parametrize("H", [256, 512])
+def test_policy_stream_stochastic_noise(H):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    tr, pol = _trainer(256)
+    tr, pol = _trainer(H)
     seed = 0x1234_5678_9ABC
     dp = tr.device_policy(False, seed=seed)
     cfg = abi.ast_config("sbmpc")
