@@ -206,11 +206,14 @@ class FusedSACTrainer(TorchTrainer):
         self._eps_static = None
         self._replay_key = None
 
-    def _hip_launch(self, replay_buffer, part):
+    def _hip_launch(self, replay_buffer, part, chain=0):
         sf = self._sf
         if part in ("a", "ab"):
-            batch = None if replay_buffer is not None else self._static
-            sf.grads(batch, self._eps_static if self.noise_fn is not None else None)
+            eps = self._eps_static if self.noise_fn is not None else None
+            if chain:
+                sf.grads_chain(chain, eps)
+            else:
+                sf.grads(None if replay_buffer is not None else self._static, eps)
         if part == "ab":
             sf.apply()
         elif part == "b":
@@ -284,10 +287,14 @@ class FusedSACTrainer(TorchTrainer):
 
     def _multi_graph(self, replay_buffer):
         """The GRAPH_STEPS-step graph for this buffer: each step's kernels read the device step counter (the
-        Philox counter of the batch draw, Adam's bias corrections), so the steps are the same as one graph each."""
+        Philox counter of the batch draw, Adam's bias corrections), so the steps are the same as one graph each.
+        The steps form a chain (sacf_grads_chain): each but the last stages the next step's batch in its
+        weight-gradient pass, and each but the first starts from that staged batch (nothing writes the replay
+        ring inside the graph, so it is the batch its own gather would draw)."""
         self._hip_step_prepare(replay_buffer)
         key = (id(replay_buffer), self.GRAPH_STEPS)
         if getattr(self, "_mgraph", None) is None or self._mgraph[0] != key:
+            from .... import sacfused as sfb
             sf = self._sf
             torch.cuda.synchronize(self.device)
             if self.split:
@@ -295,8 +302,10 @@ class FusedSACTrainer(TorchTrainer):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 sf.set_stream()
-                for _ in range(self.GRAPH_STEPS):
-                    self._hip_launch(replay_buffer, "a" if self.split else "ab")
+                for k in range(self.GRAPH_STEPS):
+                    chain = ((sfb.CHAIN_FROM_STAGED if k > 0 else 0) |
+                             (sfb.CHAIN_STAGE_NEXT if k < self.GRAPH_STEPS - 1 else 0))
+                    self._hip_launch(replay_buffer, "a" if self.split else "ab", chain)
                     if self.split:
                         torch.distributed.all_reduce(self.flat_grad, group=self.pg)
                         self._hip_launch(replay_buffer, "b")

@@ -112,7 +112,11 @@ struct Scr {
   // so its blocks must not read the live values): [log α, b3 Q1, b3 Q2, b3 T1, b3 T2, -, -, -] then
   // wm [H], ws [H], w3 Q1 [H], w3 Q2 [H]
   float *snap;
+  // the next step's batch, staged by P3 of a chained step (sacf_grads_chain): obs / next_obs rows [Bp][kXLd] and
+  // [Bp][kAux] (act, rew, term, the two reparameterisation normals)
+  float *sx, *sxn, *saux;
 };
+enum { AUX_ACT, AUX_REW, AUX_TERM, AUX_E0, AUX_E1, kAux = 8 };
 enum { SN_LOGA, SN_BQ1, SN_BQ2, SN_BT1, SN_BT2, SN_HEAD = 8 };
 
 struct MArgs {
@@ -127,6 +131,7 @@ struct MArgs {
   const float* eps;
   int64_t* step;
   float* stats;
+  int chain;  // SACF_CHAIN_* of this step
   Scr s;
   Layout L;
   Hyper hp;
@@ -495,6 +500,29 @@ __device__ __forceinline__ int64_t batch_item(const MArgs& a, int item, float& e
   return idx;
 }
 
+// the obs row (next_obs with nx) of batch item `item` into x: gathered from the replay (batch_item's draw; e0 / e1
+// its normals, idx its replay row), or (chain FROM_STAGED) the row the previous step's P3 staged — the same values
+__device__ __forceinline__ int64_t batch_row(const MArgs& a, int item, bool nx, float (&x)[kXLd], float& e0, float& e1) {
+  if (a.chain & SACF_CHAIN_FROM_STAGED) {
+    load_run<kXLd>((nx ? a.s.sxn : a.s.sx) + (int64_t)item * kXLd, x);
+    e0 = e1 = 0.0f;  // (read from the staged aux where needed)
+    return -1;
+  }
+  const int64_t idx = batch_item(a, item, e0, e1);
+  load_obs_row(nx ? a.nobs : a.obs, idx, a.L.O, x);
+  return idx;
+}
+// (act, rew, term, e0, e1) of batch item `item` whose row batch_row returned idx / e0 / e1
+__device__ __forceinline__ void batch_aux(const MArgs& a, int item, int64_t idx, float e0, float e1, float (&v)[5]) {
+  if (a.chain & SACF_CHAIN_FROM_STAGED) {
+    const float* q = a.s.saux + (int64_t)item * kAux;
+    const float4 u = *reinterpret_cast<const float4*>(q);
+    v[AUX_ACT] = u.x; v[AUX_REW] = u.y; v[AUX_TERM] = u.z; v[AUX_E0] = u.w; v[AUX_E1] = q[AUX_E1];
+    return;
+  }
+  v[AUX_ACT] = a.act[idx]; v[AUX_REW] = a.rew[idx]; v[AUX_TERM] = a.term[idx]; v[AUX_E0] = e0; v[AUX_E1] = e1;
+}
+
 // linear block id -> (row tile bx, column tile by): column tile = id mod CB, so with CB a multiple of 8 every
 // block of one column tile runs on one XCD (blocks are dealt round-robin over the 8 XCDs) and that XCD's L2
 // holds the column's weight slice (any placement gives the same results)
@@ -525,11 +553,9 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   const bool nrow = row >= Bp;
   const int item = nrow ? row - Bp : row;
   float e0, e1;
-  const int64_t idx = batch_item(a, item, e0, e1);
-  SAC_STAMP_ON(0, 4, idx);
-  const float* src = nrow ? a.nobs : a.obs;
   float x[kXLd];
-  load_obs_row(src, idx, O, x);
+  const int64_t idx = batch_row(a, item, nrow, x, e0, e1);
+  SAC_STAMP_ON(0, 4, idx);
   SAC_STAMP_ON(0, 5, x[0]);
   // then W1 (needed before the barrier), then the B operand and epilogue weights (needed after it): the LDS
   // stores below wait for W1 only
@@ -552,12 +578,14 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) xd[m] = x[m];
     if (!nrow) {
+      float v[5];
+      batch_aux(a, item, idx, e0, e1, v);
       float* rc = a.s.rec + (int64_t)item * kRec;
-      rc[R_ACT] = a.act[idx];
-      rc[R_REW] = a.rew[idx];
-      rc[R_TERM] = a.term[idx];
-      rc[R_EPS] = e0;
-      rc[R_EPSN] = e1;
+      rc[R_ACT] = v[AUX_ACT];
+      rc[R_REW] = v[AUX_REW];
+      rc[R_TERM] = v[AUX_TERM];
+      rc[R_EPS] = v[AUX_E0];
+      rc[R_EPSN] = v[AUX_E1];
     }
   }
   (void)B;
@@ -601,10 +629,9 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   const int kb = w * (H / 4) + h * KS::N2;
   const int item = r0 + rl;
   float e0, e1;
-  const int64_t idx = batch_item(a, item, e0, e1);
   float xin[kXLd];
-  load_obs_row(a.obs, idx, O, xin);
-  const float act = a.act[idx];
+  const int64_t idx = batch_row(a, item, false, xin, e0, e1);
+  const float act = (a.chain & SACF_CHAIN_FROM_STAGED) ? a.s.saux[(int64_t)item * kAux + AUX_ACT] : a.act[idx];
   W1Stage<H> w1s;
   w1s.load(C + L.c_w1, C + L.c_b1, O + 1);
   float bv[CS];
@@ -659,9 +686,8 @@ __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int 
   const int tid = threadIdx.x, row = tid >> 3, cq = (tid & 7) * 4, c0 = by * kTile2;
   const int item = rt * kTile2 + row;
   float e0, e1;
-  const int64_t idx = batch_item(a, item, e0, e1);
   float x[kXLd];
-  load_obs_row(a.nobs, idx, O, x);
+  (void)batch_row(a, item, true, x, e0, e1);
   float* w1 = lds;                   // [32][kXLd + 1]: W1 rows c0 .. c0 + 31
   float* b1 = lds + kTile2 * (kXLd + 1);
   const float* src = C + L.c_w1 + (int64_t)c0 * nin;  // the 32 rows are contiguous: 32·nin floats
@@ -1033,6 +1059,7 @@ struct WArgs {
   float* grads;
   int fuse;   // single process: each block also applies Adam / soft update / W2ᵀ to the elements it finished
   int n_mfma, n_valu;
+  int n_stage;  // chain STAGE_NEXT: blocks staging the next step's batch (after the scalar block), else 0
   ApplyArgs ap;
   // per H x H matrix (0 actor, 1 / 2 Q1 / Q2): the MFMA tiles' operands and output offset, indexed (one scalar
   // load) rather than selected between fields (a live mask and both candidates across the GEMM loop)
@@ -1402,6 +1429,30 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   }
 }
 
+// chain STAGE_NEXT: the next step's batch (P2 has advanced the step counter, so batch_item draws what the next
+// P1 would): item sb·256 + thread — its replay row, both observation rows, act / rew / term and its two normals
+__device__ __forceinline__ void p3_stage_block(const WArgs& a, int sb) {
+  const MArgs& m = a.m;
+  const int item = sb * kThreads + (int)threadIdx.x;
+  if (item >= m.L.Bp) return;
+  float e0, e1;
+  const int64_t idx = batch_item(m, item, e0, e1);
+  float x[kXLd], xn[kXLd];
+  load_obs_row(m.obs, idx, m.L.O, x);
+  load_obs_row(m.nobs, idx, m.L.O, xn);
+  const float act = m.act[idx], rew = m.rew[idx], term = m.term[idx];
+  float4* dx = reinterpret_cast<float4*>(m.s.sx + (int64_t)item * kXLd);
+  float4* dn = reinterpret_cast<float4*>(m.s.sxn + (int64_t)item * kXLd);
+#pragma unroll
+  for (int q = 0; q < kXLd / 4; ++q) {
+    dx[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    dn[q] = make_float4(xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
+  }
+  float* q = m.s.saux + (int64_t)item * kAux;
+  *reinterpret_cast<float4*>(q) = make_float4(act, rew, term, e0);
+  q[AUX_E1] = e1;
+}
+
 // the kernel's WArgs read through the kernarg segment pointer, laundered: a field is a scalar load where a block
 // uses it instead of ~150 argument dwords held in SGPRs (which spilled) across the whole kernel
 typedef const __attribute__((address_space(4))) WArgs* WArgsPtr;
@@ -1420,7 +1471,8 @@ __global__ __launch_bounds__(256) void sac_wgrad_kernel(WArgs a_arg) {
   const int bx = (int)blockIdx.x;
   if (bx < a.n_mfma) p3_mfma_tile<H>(a, bx, S);
   else if (bx < a.n_mfma + a.n_valu) p3_valu_block<H>(a, bx - a.n_mfma, S);
-  else p3_scalar_block<H>(a, S);
+  else if (bx == a.n_mfma + a.n_valu) p3_scalar_block<H>(a, S);
+  else p3_stage_block(a, bx - a.n_mfma - a.n_valu - 1);
   SAC_STAMP(2, 3);
 }
 
@@ -1599,7 +1651,7 @@ void launch_step(const MArgs& m, const WArgs& w, hipStream_t st) {
   const unsigned bt = (unsigned)(m.L.Bp / kTile2), cb = H / kTile2;
   hipLaunchKernelGGL(sac_fwd_kernel<H>, dim3(6 * bt * cb), dim3(256), 0, st, m);
   hipLaunchKernelGGL(sac_mid_kernel<H>, dim3(7 * bt * cb), dim3(256), 0, st, m);
-  hipLaunchKernelGGL(sac_wgrad_kernel<H>, dim3((unsigned)(w.n_mfma + w.n_valu + 1)), dim3(256), 0, st, w);
+  hipLaunchKernelGGL(sac_wgrad_kernel<H>, dim3((unsigned)(w.n_mfma + w.n_valu + 1 + w.n_stage)), dim3(256), 0, st, w);
 }
 
 template <int H>
@@ -1680,6 +1732,7 @@ struct sacf_handle {
   const int64_t* r_size;
   int64_t r_cap;
   uint64_t seed;
+  bool staged;  // the last sacf_grads* call staged the next batch (SACF_CHAIN_STAGE_NEXT)
   float* T;
   float* scratch;
   Scr s;
@@ -1785,7 +1838,8 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   SDev g(device);
   const int64_t Bp = L.Bp, BH = Bp * H, CB = H / kTile2;
   // rows 3·16, activations 10·H, the row record, parts (2 + 8)·CB, the snapshot
-  const int64_t n_scr = Bp * 3 * kXLd + 14 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H + 4 * H;
+  const int64_t n_scr = Bp * 3 * kXLd + 14 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H + 4 * H +
+                        Bp * (2 * kXLd + kAux);
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
     *out = h;
@@ -1815,6 +1869,9 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   sc.w1a = s; s += 4 * H;
   sc.part = s; s += PS_N * Bp * CB;
   sc.snap = s; s += SN_HEAD + 4 * H;
+  sc.sx = s; s += Bp * kXLd;
+  sc.sxn = s; s += Bp * kXLd;
+  sc.saux = s; s += Bp * kAux;
   e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);
   if (e != hipSuccess) {
     *out = h;
@@ -1882,6 +1939,7 @@ int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const fl
   h->r_size = size_dev;
   h->r_cap = capacity;
   h->seed = seed;
+  h->staged = false;
   return SACF_OK;
 }
 
@@ -1900,8 +1958,8 @@ static ApplyArgs apply_args(const sacf_handle* h) {
   return a;
 }
 
-int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
-               const float* next_obs, const float* eps) {
+static int grads_impl(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
+                      const float* next_obs, const float* eps, int chain) {
   if (!h || !h->params) return sfail(h, SACF_ESTATE, "sacf_grads: buffers not bound");
   MArgs a;
   memset(&a, 0, sizeof(a));
@@ -1921,6 +1979,7 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   }
   a.seed = h->seed;
   a.eps = eps;
+  a.chain = chain;
   a.step = h->step;
   a.stats = h->stats;
   a.s = h->s;
@@ -1935,6 +1994,7 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   const int CB = h->L.H / kTile2;
   w.n_mfma = 3 * CB * CB;
   w.n_valu = 3 * (h->L.H / kValuUnits);
+  w.n_stage = (chain & SACF_CHAIN_STAGE_NEXT) ? (int)((h->L.Bp + kThreads - 1) / kThreads) : 0;
   const Layout& L = h->L;
   for (int mat = 0; mat < 3; ++mat) {
     w.dy_src[mat] = mat == 0 ? h->s.h2 : h->s.g2[mat - 1];
@@ -1946,8 +2006,23 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
   if (!with_hidden(h->L.H, [&](auto hc) { launch_step<decltype(hc)::value>(a, w, h->stream); }) &&
       !wide_step(h->L.H, a, w, h->stream))
     return sfail(h, SACF_EINVAL, "sacf_grads: hidden %d", h->L.H);
+  h->staged = (chain & SACF_CHAIN_STAGE_NEXT) != 0;
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_grads: %s", hipGetErrorString(e));
+}
+
+int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
+               const float* next_obs, const float* eps) {
+  return grads_impl(h, obs, act, rew, term, next_obs, eps, 0);
+}
+
+int sacf_grads_chain(sacf_handle* h, const float* eps, int32_t flags) {
+  if (!h) return SACF_EINVAL;
+  if (flags & ~(SACF_CHAIN_STAGE_NEXT | SACF_CHAIN_FROM_STAGED)) return sfail(h, SACF_EINVAL, "sacf_grads_chain: flags");
+  if (!h->r_obs) return sfail(h, SACF_ESTATE, "sacf_grads_chain: no replay bound");
+  if ((flags & SACF_CHAIN_FROM_STAGED) && !h->staged)
+    return sfail(h, SACF_ESTATE, "sacf_grads_chain: FROM_STAGED without a staging step before it");
+  return grads_impl(h, nullptr, nullptr, nullptr, nullptr, nullptr, eps, flags);
 }
 
 int sacf_apply(sacf_handle* h) {

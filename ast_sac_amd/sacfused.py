@@ -9,10 +9,11 @@ import torch  # noqa: F401  (HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACFUSED_LIB") or os.path.join(_HERE, "lib", "libsacfused.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
+CHAIN_STAGE_NEXT, CHAIN_FROM_STAGED = 1, 2  # sacf_grads_chain flags
 EXPORTED_SYMBOLS = ("sacf_abi_version", "sacf_build_info", "sacf_create", "sacf_destroy", "sacf_last_error", "sacf_set_stream",
                     "sacf_param_count", "sacf_target_count", "sacf_stats_count", "sacf_bind", "sacf_sync_params",
-                    "sacf_set_replay", "sacf_grads", "sacf_apply", "sacf_policy_reserve", "sacf_policy_act",
+                    "sacf_set_replay", "sacf_grads", "sacf_grads_chain", "sacf_apply", "sacf_policy_reserve", "sacf_policy_act",
                     "sacf_policy_weights", "sacf_hidden_supported")
 _lib = None
 
@@ -51,6 +52,7 @@ def load_library(path=LIB_PATH):
     L.sacf_sync_params.argtypes = [P]
     L.sacf_set_replay.argtypes = [P, P, P, P, P, P, P, C.c_int64, C.c_uint64]
     L.sacf_grads.argtypes = [P] * 7
+    L.sacf_grads_chain.argtypes = [P, P, C.c_int32]
     L.sacf_apply.argtypes = [P]
     L.sacf_policy_reserve.argtypes = [P, C.c_int64]
     L.sacf_hidden_supported.argtypes = [C.c_int32]
@@ -128,6 +130,11 @@ class SacFused:
         b = [None] * 5 if batch is None else [batch[k] for k in ("observations", "actions", "rewards", "terminals",
                                                                     "next_observations")]
         self._check(self.L.sacf_grads(self.h, *[_p(t) for t in b], _p(eps)), "sacf_grads")
+
+    def grads_chain(self, flags, eps=None):
+        """A replay-sampled step of a chain (sacf_grads_chain): CHAIN_STAGE_NEXT stages the next step's batch,
+        CHAIN_FROM_STAGED starts from the batch the previous call staged (no replay change in between)."""
+        self._check(self.L.sacf_grads_chain(self.h, _p(eps), int(flags)), "sacf_grads_chain")
 
     def apply(self):
         self._check(self.L.sacf_apply(self.h), "sacf_apply")

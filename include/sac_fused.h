@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SACF_ABI_VERSION 2 /* 2: three-pass step, any batch, hidden up to 512, no step_kernel */
+#define SACF_ABI_VERSION 3 /* 3: sacf_grads_chain (steps in a chain stage the next batch); 2: three-pass step */
 #define SACF_OK 0
 #define SACF_EINVAL -1
 #define SACF_EHIP -2
@@ -102,6 +102,18 @@ int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const fl
  * Philox stream, else eps = [B normals for obs rows | B normals for next_obs rows]. */
 int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* rew, const float* term,
                const float* next_obs, const float* eps);
+/* A step of a chain of replay-sampled steps (the trainer's multi-step graph; no replay change between the steps):
+ * sacf_grads(h, NULL x 5, eps) with `flags`:
+ *   SACF_CHAIN_STAGE_NEXT   the weight-gradient pass also gathers the NEXT step's batch (its Philox row draw, the
+ *                           replay rows, the reparameterisation normals) into library buffers;
+ *   SACF_CHAIN_FROM_STAGED  the forward pass starts from the batch the previous call staged instead of gathering
+ *                           it (the same rows and normals: results are bitwise those of sacf_grads). Only right
+ *                           after a call with SACF_CHAIN_STAGE_NEXT on this handle (SACF_ESTATE otherwise), and
+ *                           the caller guarantees the replay ring and its size did not change in between.
+ * A replay ring must be bound (sacf_set_replay). */
+#define SACF_CHAIN_STAGE_NEXT 1
+#define SACF_CHAIN_FROM_STAGED 2
+int sacf_grads_chain(sacf_handle* h, const float* eps, int32_t flags);
 /* Adam + soft target update from `grads` (divided by world_size); a no-op when sacf_grads applied it. */
 int sacf_apply(sacf_handle* h);
 
