@@ -368,11 +368,20 @@ __device__ __forceinline__ void load_segment(Ship& s, const double* __restrict__
   segment_changed(s);
 }
 
-// PidController.pid_ctrl controllers.py:106-118
+// 1 / x when x is a power of two (then y · (1 / x) is y / x exactly: both are the correctly rounded y / x), else 0
+__host__ __device__ __forceinline__ double pow2_inverse(double x) {
+  int e;
+  const double m = frexp(x, &e);
+  return (m == 0.5 && e > -1000 && e < 1000) ? ldexp(1.0, 1 - e) : 0.0;
+}
+
+// PidController.pid_ctrl controllers.py:106-118; MUL: dt is a power of two and inv_dt = pow2_inverse(dt), the
+// derivative term's division a multiplication (the same bits)
+template <bool MUL = false>
 __device__ __forceinline__ double pid(double& ei, double& prev, double kp, double kd, double ki, double dt,
-                                      double setpoint, double meas) {
+                                      double setpoint, double meas, double inv_dt = 0.0) {
   double error = setpoint - meas;
-  double d_error = (error - prev) / dt;
+  double d_error = MUL ? (error - prev) * inv_dt : (error - prev) / dt;
   double error_i = ei + error * dt;
   prev = error;
   ei = error_i;
@@ -388,15 +397,16 @@ __device__ __forceinline__ double pi_ctrl(double& ei, double kp, double ki, doub
 
 // speed control: EngineThrottleFromSpeedSetPoint.throttle controllers.py:185-189 (Q2: shaft
 // measurement = forward speed) | ThrustFromSpeedSetPoint.thrust run_colav controllers.py:183-185
+template <bool MUL = false>
 __device__ __forceinline__ double speed_ctrl(const ShipConst& c, Ship& s, double setpoint, double u, double dt,
-                                             bool detailed) {
+                                             bool detailed, double inv_dt = 0.0) {
   if (detailed) {
     double desired_shaft = pi_ctrl(s.spd_a, c.kp_ship_speed, c.ki_ship_speed, dt, setpoint, u);
     desired_shaft = sat(desired_shaft, 0, c.shaft_speed_max);
     double thr = pi_ctrl(s.spd_b, c.kp_shaft_speed, c.ki_shaft_speed, dt, desired_shaft, u);
     return sat(thr, 0, 1.1);
   }
-  double t = pid(s.spd_a, s.spd_b, c.spd_kp, c.spd_kd, c.spd_ki, dt, setpoint, u);
+  double t = pid<MUL>(s.spd_a, s.spd_b, c.spd_kp, c.spd_kd, c.spd_ki, dt, setpoint, u, inv_dt);
   return sat(t, -c.max_thrust, c.max_thrust);
 }
 
@@ -429,9 +439,10 @@ __device__ __forceinline__ void fuel_consumption(const ShipConst& c, double load
 }
 
 // HeadingByReferenceController.rudder_angle_from_heading_setpoint :246-255
+template <bool MUL = false>
 __device__ __forceinline__ double heading_ctrl(const ShipConst& c, Ship& s, double heading_ref, double heading,
-                                               double dt) {
-  double rudder = -pid(s.hdg_ei, s.hdg_prev, c.hdg_kp, c.hdg_kd, c.hdg_ki, dt, heading_ref, heading);
+                                               double dt, double inv_dt = 0.0) {
+  double rudder = -pid<MUL>(s.hdg_ei, s.hdg_prev, c.hdg_kp, c.hdg_kd, c.hdg_ki, dt, heading_ref, heading, inv_dt);
   return sat(rudder, -c.max_rudder, c.max_rudder);
 }
 

@@ -7,6 +7,7 @@
 //   -DSHIPSIM_DEBUG_ENV=e    printf of env e's entry / exit state
 //   -DSHIPSIM_ABL_*          ablations (scripts/build_ablations.sh; timing only, results intentionally differ):
 //                            NO_WIND, NO_MAPDIST, NO_GROUND, NO_SBLOOP, SB_NEVER, SB_NONE
+//   -DSHIPSIM_C2_ONE_WAVE    C2 simplified ticks on the one-wave single_tick_kernel (same results; timing A/B)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,6 +35,12 @@ constexpr bool kNoGround = false;
 constexpr bool kNoSbLoop = true;    // SBMPC horizon: sample 0 only
 #else
 constexpr bool kNoSbLoop = false;
+#endif
+
+#ifdef SHIPSIM_C2_ONE_WAVE
+constexpr bool kC2OneWave = true;
+#else
+constexpr bool kC2OneWave = false;
 #endif
 
 // the test ship's SBMPC request as the tick loop makes it: SB_NEVER keeps the optimiser's code in the tick loop

@@ -1,5 +1,5 @@
 // shipsim_kernels.hip — HIP kernels (gfx950) + C ABI (include/shipsim.h) of the batched
-// ship-in-transit simulator. One translation unit -> ast_sac_amd/lib/libshipsim.so.
+// ship-in-transit simulator -> ast_sac_amd/lib/libshipsim.so, linked from two objects of this file (SHIPSIM_TU below).
 //
 // Kernels
 //   init_kernel    : state as constructed (ShipModelAST/SimpleShipModel.__init__, controllers,
@@ -8,6 +8,7 @@
 //   ast_step_kernel: MultiShipRLEnv.step (env.py:624-773) — event-driven: each env ticks
 //                    (_step :563-622) until its decision point (RoA + 1 tick) or done
 //   single_tick_kernel: C2 single-ship loop body (run_colav/run_simplified_model.py:248-249 shape)
+//   single_tick_pipe_kernel: the same for the simplified machinery, three waves per 64 ships
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -25,6 +26,19 @@
 
 
 using namespace shipsim;
+
+// Translation-unit role (ast_sac_amd/build_hash.py OBJECTS):
+//   SHIPSIM_TU 1: every kernel but single_tick_pipe_kernel, and the C ABI — built without machine-level LICM (the
+//                 tick loops' constants are rematerialised rather than held in registers: DESIGN.md §7a)
+//   SHIPSIM_TU 2: single_tick_pipe_kernel and its launch only — with LICM: its three short loops have registers to
+//                 spare, and the fp64 constants of atan / sincos are hoisted out of the tick loop
+//   SHIPSIM_TU 0: everything in one object (diagnostics and register-report builds)
+#ifndef SHIPSIM_TU
+#define SHIPSIM_TU 0
+#endif
+// (defined with single_tick_pipe_kernel, in the SHIPSIM_TU 2 object of the product build)
+void shipsim_c2_pipe_launch(int blocks, hipStream_t st, const Params& P, const struct DevState& S,
+                            const struct ConstBuf& K, int k);
 
 // ---------------------------------------------------------------------------------------------
 // device state (SoA). Ship arrays are indexed q = env * n_ships + ship (lane order).
@@ -167,6 +181,7 @@ __device__ __forceinline__ const ShipConst* stage_consts(const ConstBuf& K, Ship
   return lds;
 }
 
+#if SHIPSIM_TU != 2
 // control half of one ship tick: autopilot -> speed control -> (simple collav) -> store
 // (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339); returns (ctrl, rudder)
 template <bool DETAILED, bool REC>
@@ -2126,6 +2141,134 @@ __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevStat
   store_ship(S, q, s);
 }
 
+#endif  // SHIPSIM_TU != 2
+
+#if SHIPSIM_TU != 1
+// C2 with the simplified machinery (the C2 configuration, SimpleShipModel + ThrustFromSpeedSetPoint): the same ticks
+// as single_tick_kernel<false>, bit for bit, on THREE waves per 64 ships, software-pipelined so that one workgroup
+// barrier per tick separates them. A tick t only needs, besides its own (u, v, r):
+//   sin/cos ψ_t    — ψ_t = ψ_{t-1} + r_{t-1} dt is known one tick early;
+//   the rudder_t   — waypoint switch, LOS guidance (sqrt, divide, atan) and heading PID on (n, e, ψ)_t, which follow
+//                    from tick t - 1's state by the explicit Euler step before tick t - 1's kinetics matter.
+// So in interval t
+//   wave 0 (guidance): (n, e, ψ)_{t+1} from (u, v, r)_t and sin/cos ψ_t, then the rudder of tick t + 1;
+//   wave 1 (heading):  ψ_{t+1} and sin/cos ψ_{t+1};
+//   wave 2 (dynamics): tick t's thrust (speed PID), wind force and kinetics -> (u, v, r)_{t+1};
+// each reading what the others wrote in interval t - 1 (LDS, double-buffered by tick parity). Every value is formed
+// by the same expression as in the one-wave tick (control_and_store, differentials, integrate): the same bits.
+template <bool POW2_DT>  // dt a power of two: the PIDs' derivative division as the exact multiplication (pid)
+__global__ __launch_bounds__(192) void single_tick_pipe_kernel(const Params P, DevState S, ConstBuf K, int k) {
+  __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
+  __shared__ double x_uvr[2][3][64];  // (u, v, r) of a tick, by tick parity
+  __shared__ double x_sc[2][2][64];   // sin / cos ψ of a tick
+  __shared__ double x_rud[2][64];     // rudder of a tick
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
+  const int lane = threadIdx.x & 63, role = threadIdx.x >> 6;  // (wave-uniform)
+  const int q0 = blockIdx.x * 64 + lane, q = min(q0, P.n_envs - 1);  // (every lane takes part in the barriers)
+  const bool live = q0 < P.n_envs;
+  const ShipConst& c = SC[0];
+  const double dt = P.dt, inv_dt = pow2_inverse(dt);  // (the PIDs' derivative terms: see pid)
+  Ship s;
+  load_ship(S, q, s);
+  // the kinematic rates of integrate's Euler step (differentials_body's expressions)
+  auto advance_pose = [&](double u, double v, double r, double sy, double cy) __attribute__((always_inline)) {
+    const double dn = cy * u + (-sy) * v + 0 * r;
+    const double de = sy * u + cy * v + 0 * r;
+    const double dyaw = 0 * u + 0 * v + 1 * r;
+    s.n = s.n + dn * dt;
+    s.e = s.e + de * dt;
+    s.yaw = s.yaw + dyaw * dt;
+  };
+  if (role == 0) {
+    // guidance: the rudder of tick j from (n, e, ψ)_j — control_and_store's route half (DETAILED false, no collav)
+    const double* rn = S.route_n() + (size_t)q * kMaxRoute;
+    const double* re = S.route_e() + (size_t)q * kMaxRoute;
+    auto guide = [&]() __attribute__((always_inline)) {
+      const double N = s.n, E = s.e, H = s.yaw;
+      if (next_wpt_advance(c, s, N, E)) {
+        s.next_wpt += 1;
+        load_segment(s, rn, re);
+      }
+      const double href = los_guidance(c, s, N, E);
+      const double rudder = heading_ctrl<POW2_DT>(c, s, href + 0.0, H, dt, inv_dt);
+      s.log_rudder = rudder;
+      s.log_ect = s.e_ct;
+      s.log_n = N;
+      s.log_e = E;
+      return rudder;
+    };
+    x_rud[0][lane] = guide();
+    __syncthreads();
+    for (int t = 0; t < k; ++t) {
+      const int b = t & 1;
+      advance_pose(x_uvr[b][0][lane], x_uvr[b][1][lane], x_uvr[b][2][lane], x_sc[b][0][lane], x_sc[b][1][lane]);
+      if (t + 1 < k) x_rud[b ^ 1][lane] = guide();
+      __syncthreads();
+    }
+    if (live) {
+      S.f(SF_N)[q] = s.n; S.f(SF_E)[q] = s.e; S.f(SF_YAW)[q] = s.yaw;
+      S.f(SF_ECT)[q] = s.e_ct; S.f(SF_ECT_INT)[q] = s.e_ct_int;
+      S.f(SF_HDG_EI)[q] = s.hdg_ei; S.f(SF_HDG_PREV)[q] = s.hdg_prev;
+      S.f(SF_RUDDER)[q] = s.log_rudder; S.f(SF_LOG_ECT)[q] = s.log_ect;
+      S.f(SF_LOG_N)[q] = s.log_n; S.f(SF_LOG_E)[q] = s.log_e;
+      S.next_wpt()[q] = s.next_wpt;
+    }
+  } else if (role == 1) {
+    // heading: sin/cos ψ of the next tick (differentials' sincos(s.yaw))
+    double sy, cy;
+    sincos(s.yaw, &sy, &cy);
+    x_sc[0][0][lane] = sy; x_sc[0][1][lane] = cy;
+    __syncthreads();
+    for (int t = 0; t < k; ++t) {
+      const int b = t & 1;
+      const double r = x_uvr[b][2][lane];
+      s.yaw = s.yaw + (0 * x_uvr[b][0][lane] + 0 * x_uvr[b][1][lane] + 1 * r) * dt;
+      if (t + 1 < k) {
+        sincos(s.yaw, &sy, &cy);
+        x_sc[b ^ 1][0][lane] = sy; x_sc[b ^ 1][1][lane] = cy;
+      }
+      __syncthreads();
+    }
+  } else {
+    // dynamics: tick t's thrust, wind force and kinetics (control_and_store's speed half, differentials, integrate)
+    double wsin, wcos;
+    sincos(P.wind_dir, &wsin, &wcos);
+    x_uvr[0][0][lane] = s.u; x_uvr[0][1][lane] = s.v; x_uvr[0][2][lane] = s.r;
+    __syncthreads();
+    for (int t = 0; t < k; ++t) {
+      const int b = t & 1;
+      const double sy = x_sc[b][0][lane], cy = x_sc[b][1][lane], rudder = x_rud[b][lane];
+      const double thrust = speed_ctrl<POW2_DT>(c, s, c.desired_speed * 1.0, s.u, dt, false, inv_dt);
+      s.log_thrust = thrust;
+      double tau[3];
+      wind_force_alg(c, P, s, sy, cy, wsin, wcos, tau);
+      const Deriv d = differentials_body(c, P, s, thrust, rudder, false, sy, cy, tau);
+      s.u = s.u + d.du * dt;
+      s.v = s.v + d.dv * dt;
+      s.r = s.r + d.dr * dt;
+      s.time = s.time + dt;
+      x_uvr[b ^ 1][0][lane] = s.u; x_uvr[b ^ 1][1][lane] = s.v; x_uvr[b ^ 1][2][lane] = s.r;
+      __syncthreads();
+    }
+    if (live) {
+      S.f(SF_U)[q] = s.u; S.f(SF_V)[q] = s.v; S.f(SF_R)[q] = s.r; S.f(SF_TIME)[q] = s.time;
+      S.f(SF_SPD_A)[q] = s.spd_a; S.f(SF_SPD_B)[q] = s.spd_b; S.f(SF_THRUST)[q] = s.log_thrust;
+    }
+  }
+}
+
+#endif  // SHIPSIM_TU != 1
+
+#if SHIPSIM_TU != 1
+void shipsim_c2_pipe_launch(int blocks, hipStream_t st, const Params& P, const DevState& S, const ConstBuf& K, int k) {
+  if (pow2_inverse(P.dt) != 0.0)
+    hipLaunchKernelGGL(single_tick_pipe_kernel<true>, dim3(blocks), dim3(192), 0, st, P, S, K, k);
+  else
+    hipLaunchKernelGGL(single_tick_pipe_kernel<false>, dim3(blocks), dim3(192), 0, st, P, S, K, k);
+}
+#endif
+
+#if SHIPSIM_TU != 2
 // Legacy per-tick MultiShipEnv.step (rl_env/ship_in_transit/env.py:1104-1173), k steps per launch.
 // Two lanes per env (lane & 1 = ship); the termination flags of get_termination_status
 // (termination_flags.py:5-70) are evaluated in fp64 on the next_states, as the reference does on
@@ -3101,8 +3244,10 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
   const int threads = 64, blocks = (h->P.n_envs + threads - 1) / threads;
   if (h->P.machinery == SHIPSIM_MACH_DETAILED)
     hipLaunchKernelGGL(single_tick_kernel<true>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
-  else
+  else if (diag::kC2OneWave)  // (comparison builds: the one-wave form)
     hipLaunchKernelGGL(single_tick_kernel<false>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);
+  else
+    shipsim_c2_pipe_launch(blocks, h->stream, h->P, h->S, h->K, k);
   HIPCHK(h, hipGetLastError());
   return SHIPSIM_OK;
 }
@@ -3368,3 +3513,4 @@ int shipsim_diag_lane_faults(uint32_t* out32) {
 }
 
 }  // extern "C"
+#endif  // SHIPSIM_TU != 2

@@ -348,20 +348,21 @@ def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1, tai
     return res
 
 
-def bench_c2(dev, n_ships=4096):
+def bench_c2(dev, n_ships=4096, per_launch=None):
     """configs[1] (C2): 4096 single ships, SimpleShipModel + ThrustFromSpeedSetPoint +
     HeadingByRouteController, PCG64-perturbed initial states, the whole 10,000 s
-    horizon with shipsim_tick (single_tick_kernel, one lane per ship); secondary line, ship-ticks/s."""
+    horizon in one shipsim_tick launch (single_tick_pipe_kernel: three waves per 64 ships); secondary line,
+    ship-ticks/s."""
     import numpy as np
     import torch
     from ast_sac_amd import shipsim_abi as abi
     from ast_sac_amd.shipsim import ShipSim
-    res = {"ships": n_ships, "unit": "ship-ticks/s", "kernel": "single_tick_kernel"}
+    res = {"ships": n_ships, "unit": "ship-ticks/s", "kernel": "single_tick_pipe_kernel"}
     init = abi.c2_initial_states(n_ships)
     for dt in (30, 4):
         cfg = abi.c2_config(dt)
         n_ticks = int(np.ceil(cfg.simulation_time / dt))
-        per = 64 if dt == 30 else 250
+        per = (per_launch or {})[dt] if per_launch else n_ticks  # ticks per shipsim_tick launch (default: all)
         best = None
         for rep in range(2):  # first pass warms up
             sim = ShipSim(cfg, n_ships, device=dev)

@@ -9,6 +9,6 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
 SRC=${SRC:-$R/ast_sac_amd/csrc}
 mkdir -p "$R/ast_sac_amd/lib/abl"
-F="$(cd "$R" && python3 -c 'from ast_sac_amd.build_hash import HIPFLAGS, LIB_FLAGS; print(" ".join(HIPFLAGS + LIB_FLAGS["shipsim"]))')"
+F="$(cd "$R" && python3 -c 'from ast_sac_amd.build_hash import HIPFLAGS, LIB_FLAGS; print(" ".join(HIPFLAGS + LIB_FLAGS["shipsim"] + ["-mllvm", "-disable-machine-licm"]))')"
 /opt/rocm/bin/hipcc $F -I"$R/include" -I"$SRC" -I"$R/ast_sac_amd/csrc" -DSHIPSIM_REGCHECK=1 -DSHIPSIM_SRC_HASH="\"variant-$NAME\"" "$@" \
   "$SRC/shipsim_kernels.hip" -o "$R/ast_sac_amd/lib/abl/$NAME.so"

@@ -44,6 +44,29 @@ def test_c2_single_ship_vs_golden_trace(golden, torch_cuda, dt):
     assert_close(fin, g[f"dt{dt}_final"], what="c2 final")
 
 
+@pytest.mark.parametrize("dt", [30, 4])
+def test_c2_launch_boundaries_do_not_move_the_state(torch_cuda, dt):
+    """The C2 kernel (three pipelined waves per 64 ships, shipsim_tick) carries every ship's state exactly across
+    launches: 97 ticks as one launch and as launches of 1, 2, 3, 5, 8, 13, 21 and 44 ticks give the same bits in
+    every state field, for ship counts that do and do not fill the last 64-ship block."""
+    from ast_sac_amd.shipsim import ShipSim
+    torch = torch_cuda
+    fields = (abi.F_TIME, abi.F_NORTH, abi.F_EAST, abi.F_YAW, abi.F_U, abi.F_V, abi.F_R, abi.F_E_CT, abi.F_E_CT_INT,
+              abi.F_HDG_EI, abi.F_HDG_PREV, abi.F_SPD_A, abi.F_SPD_B, abi.F_RUDDER, abi.F_THRUST, abi.F_LOG_ECT,
+              abi.F_NEXT_WPT)
+    for n in (4096, 1000):
+        init = abi.c2_initial_states(n)
+        out = []
+        for chunks in ([97], [1, 2, 3, 5, 8, 13, 21, 44]):
+            sim = ShipSim(abi.c2_config(dt), n)
+            _set_c2_initial(sim, init, torch)
+            for k in chunks:
+                sim.tick(k)
+            out.append(np.stack([sim.get(f).cpu().numpy().astype(np.float64) for f in fields], 1))
+            sim.close()
+        np.testing.assert_array_equal(out[0], out[1], err_msg=f"dt {dt}, {n} ships")
+
+
 @pytest.mark.parametrize("dt,ticks", [(30, 334), (4, 2500)])
 def test_c2_4096_ships_vs_oracle(torch_cuda, dt, ticks):
     """C2 config at full size: 4096 perturbed ships over the 10000 s horizon in one launch.
