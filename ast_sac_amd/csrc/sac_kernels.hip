@@ -330,12 +330,21 @@ __device__ __forceinline__ int finish_row(int q) {
   return (g & 3) + 8 * (g >> 2) + 4 * ((threadIdx.x & 63) >> 5);
 }
 
-// Σ of x over the 32 lanes of this half wave (the 32 columns of one output row), butterfly order: every
-// lane gets the same bits
+// Σ of x over the 32 lanes of this half wave (the 32 columns of one output row), every lane ending with the same
+// bits: a pairwise tree in registers — lane ^ 1, lane ^ 2 (quad permutes), the two quads of each 8 (half-row
+// mirror), the two halves of each 16 (row mirror), then the two rows of the half wave (v_permlane16_swap) — each
+// step adds a pair of equal values in either order, so the partners' sums are equal (no LDS round trip per step)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float halfwave_sum(float x) {
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
+  x += dpp_f<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+  x += dpp_f<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+  x += dpp_f<0x141>(x);  // row_half_mirror
+  x += dpp_f<0x140>(x);  // row_mirror
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // (rows 2k, 2k + 1: the same order in both)
 }
 
 // B operand chunk: bv[i] = base[(k0 + i)·H + col] (W2ᵀ for a forward product, W2 for a backward factor)
