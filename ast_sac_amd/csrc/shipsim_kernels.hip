@@ -1673,9 +1673,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     (void)ghost;
     // partner ship's pre-tick state (the test ship's SBMPC reads the obstacle ship before it moves)
     SHIPSIM_LANE_CHECK(LPE, 7);
-    const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
-    const double pu = pair_swap(s.u), pv = pair_swap(s.v);
-    const double psy = pair_swap(sy), pcy = pair_swap(cy);  // sin/cos(pyaw), carried by the partner
+    const double pn = pair_swap(s.n), pe = pair_swap(s.e);
     double sf = 1.0, off = 0.0;
     bool sb_active = false;
     if (COLLAV == SHIPSIM_COLLAV_SBMPC && SLOTS > 2) {  // do_list of every obstacle ship (env.py:366-370)
@@ -1732,27 +1730,37 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       }
     } else if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
       bool need = false;
-      SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      in.u_d = SC[0].desired_speed;  // the same in every lane (sbmpc_cooperative<true>)
-      in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
+      double los_arg = 0.0;
       if (going && is_test) {
         // env.py:362-363: next_wpt result discarded; los_guidance integrates e_ct_int (Q3). The
         // course (atan) only feeds the optimisation, so it is evaluated for requesting envs only.
-        const double los_arg = los_update(c, s, s.n, s.e);
+        los_arg = los_update(c, s, s.n, s.e);
         double d0 = pe - s.e, d1 = pn - s.n;
         need = sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_
         need = diag::sb_request(need, P.max_sampling);  // (the product: need itself)
-        if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
-        in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
-        in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
-        in.ob_so = -psy; in.ob_co = pcy;  // sin(-yaw) = -sin(yaw), cos(-yaw) = cos(yaw)
-        in.p_last = p_last; in.chi_last = chi_last;
       }
       double pb = 1.0, cb = 0.0;
-      sbmpc_cooperative<true>(need && sub == 0, in, P.sbmpc_nsamp, P.sbmpc_dt, pb, cb);
-      pb = env_lane_d<LPE, 0>(pb, env_lane0);
-      cb = env_lane_d<LPE, 0>(cb, env_lane0);
-      const int need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
+      int need0 = 0;
+      // the optimiser's inputs, pass and hand-out only in a wave where some env requests it this tick (a
+      // wave-uniform branch: every lane takes part in the exchanges inside)
+      if (__any(need)) {
+        const double pyaw = pair_swap(s.yaw), pu = pair_swap(s.u), pv = pair_swap(s.v);
+        const double psy = pair_swap(sy), pcy = pair_swap(cy);  // sin/cos(pyaw), carried by the partner
+        SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        in.u_d = SC[0].desired_speed;  // the same in every lane (sbmpc_cooperative<true>)
+        in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
+        if (going && is_test) {
+          if (need) in.chi_d = -(s.seg_alpha + atan(los_arg));
+          in.os_x = s.e; in.os_y = s.n; in.os_v = s.v;
+          in.ob_x = pe; in.ob_y = pn; in.ob_psi = -pyaw; in.ob_u = pu; in.ob_v = pv;
+          in.ob_so = -psy; in.ob_co = pcy;  // sin(-yaw) = -sin(yaw), cos(-yaw) = cos(yaw)
+          in.p_last = p_last; in.chi_last = chi_last;
+        }
+        sbmpc_cooperative<true>(need && sub == 0, in, P.sbmpc_nsamp, P.sbmpc_dt, pb, cb);
+        pb = env_lane_d<LPE, 0>(pb, env_lane0);
+        cb = env_lane_d<LPE, 0>(cb, env_lane0);
+        need0 = env_lane_i<LPE, 0>((int)need, env_lane0);
+      }
       sb_active = need0;
       if (opaque_if<OPQ>(going)) {  // (tested here, not held as a lane mask across the optimiser's loop)
         if (need0) { p_last = pb; chi_last = cb; }
