@@ -1235,6 +1235,17 @@ __device__ __forceinline__ int env_lane_i(int x, int env_lane0) {
   else return __shfl(x, env_lane0 + K, 64);
 }
 
+// The env lane that evaluates each reward term's exp (LPE >= 8), and the term of env lane j < 5. Two-ship envs
+// (lanes alternate test / obstacle ship, each computing from its own perspective): the obstacle ship's lanes 1 and 3
+// take the terms of its own ground distance and cross-track error.
+template <int SLOTS>
+__host__ __device__ constexpr int reward_lane(int k) {
+  return SLOTS != 2 ? k : k == 0 ? 0 : k == 1 ? 2 : k == 2 ? 4 : k == 3 ? 1 : 3;
+}
+template <int SLOTS>
+__host__ __device__ constexpr int reward_term(int j) {
+  return SLOTS != 2 ? j : j == 0 ? 0 : j == 1 ? 3 : j == 2 ? 1 : j == 3 ? 4 : 2;
+}
 // min of a double / OR of an int over the sub-lanes of one ship (same lane parity) of a 16-lane env:
 // quad_perm [2,3,0,1], row_ror 4, row_ror 8 (parity-preserving) — DPP only, no LDS permute
 template <int LPE, int SLOTS = 2>
@@ -1357,6 +1368,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
   __shared__ float lds_pol[POLICY ? kPolMaxRows * kPolMaxHidden : 1];  // shipsim_run_policy: h1 rows
+  __shared__ double2 lds_rterm[8];  // the reward exp each lane of an env evaluates: (target, scale) of its term
   if constexpr (diag::kPoisonLds) {  // (stale-LDS diagnostics build only)
     diag::poison_lds(lds_sc, sizeof(lds_sc)); diag::poison_lds(lds_edges, sizeof(lds_edges));
     diag::poison_lds(lds_edges_raw, sizeof(lds_edges_raw)); diag::poison_lds(lds_boxes, sizeof(lds_boxes));
@@ -1374,6 +1386,12 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     lds_edges_raw[i] = ed;
   }
   for (int i = threadIdx.x; i < P.n_polys; i += blockDim.x) lds_boxes[i] = K.boxes()[i];
+  if (threadIdx.x < 8) {  // reward_designs.py:33-55 targets / scales, term reward_term(j) for env lane j
+    const int j = threadIdx.x, t = j < 5 ? reward_term<SLOTS>(j) : 0;
+    const double tg[5] = {0.0, 0.0, 3000.0, 0.0, 500.0};
+    const double of[5] = {200000000.0, 175000.0, 1250000.0, 50000.0, 12500.0};
+    lds_rterm[j] = make_double2(j < 5 ? tg[t] : 0.0, j < 5 ? of[t] : 1.0);
+  }
   __syncthreads();
 
   // one wave per block: envs [blockIdx.x * epw, + epw) on lanes [0, epw * LPE); lanes past them idle
@@ -1871,26 +1889,19 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     double Tn, Te, Th, Tsh, Tch, Tect, Tground, Ttime, On, Oe, Oyaw, Oect, Oground, Ospeed, Odtravel, Odtime, Cn, Ce;
     int Tf, Of;
     bool any_nf;
-    if constexpr (SLOTS == 2) {  // the partner lane (lane ^ 1) holds the other ship
+    if constexpr (SLOTS == 2) {
+      // each lane's own perspective: T = its own ship, O = the partner lane's (lane ^ 1). That is the env's view
+      // on the test ship's lanes; the env's outcome is the test ship's first lane's (its event bits, taken by every
+      // lane of the env below), so the obstacle ship's lanes need no role selects
       SHIPSIM_LANE_CHECK(LPE, 8);
-      const int o_flags = pair_swap_i(my_flags);
-      const double o_n = pair_swap(s.n), o_e = pair_swap(s.e), o_yaw = pair_swap(s.yaw);
-      const double o_ect = pair_swap(s.log_ect), o_ground = pair_swap(my_ground);
-      const double o_speed = pair_swap(my_speed_out), o_dtravel = pair_swap(dtravel), o_dtime = pair_swap(dtime);
-      const double o_time = pair_swap(s.time);
-      const double o_sy = pair_swap(sy), o_cy = pair_swap(cy);
-      Tn = is_test ? s.n : o_n; Te = is_test ? s.e : o_e; Th = is_test ? s.yaw : o_yaw;
-      Tsh = is_test ? sy : o_sy; Tch = is_test ? cy : o_cy;
-      On = is_test ? o_n : s.n; Oe = is_test ? o_e : s.e; Oyaw = is_test ? o_yaw : s.yaw;
-      Tect = is_test ? s.log_ect : o_ect; Oect = is_test ? o_ect : s.log_ect;
-      Tground = is_test ? my_ground : o_ground; Oground = is_test ? o_ground : my_ground;
-      Tf = is_test ? my_flags : o_flags; Of = is_test ? o_flags : my_flags;
-      Ospeed = is_test ? o_speed : my_speed_out;
-      Ttime = is_test ? s.time : o_time;
-      Odtravel = is_test ? o_dtravel : dtravel;
-      Odtime = is_test ? o_dtime : dtime;
+      Tn = s.n; Te = s.e; Th = s.yaw; Tsh = sy; Tch = cy; Tect = s.log_ect; Tground = my_ground; Ttime = s.time;
+      Tf = my_flags;
+      Of = pair_swap_i(my_flags);
+      On = pair_swap(s.n); Oe = pair_swap(s.e); Oyaw = pair_swap(s.yaw);
+      Oect = pair_swap(s.log_ect); Oground = pair_swap(my_ground);
+      Ospeed = pair_swap(my_speed_out); Odtravel = pair_swap(dtravel); Odtime = pair_swap(dtime);
       Cn = On; Ce = Oe;
-      any_nf = (my_flags | o_flags) & XF_NONFINITE;
+      any_nf = (my_flags | Of) & XF_NONFINITE;
     } else {  // slot k's first lane of the env row holds ship k
       Tn = env_lane_d<LPE, 0>(s.n, env_lane0); Te = env_lane_d<LPE, 0>(s.e, env_lane0);
       Th = env_lane_d<LPE, 0>(s.yaw, env_lane0); Tsh = env_lane_d<LPE, 0>(sy, env_lane0);
@@ -1939,15 +1950,18 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       double ex[5];
       if (LPE >= 8) {
         const int j = opaque_v(lie) & 7;  // (recomputed in the loop: no lane masks kept across it)
-        const double xj = (j == 0) ? xv[0] : (j == 1) ? xv[1] : (j == 2) ? xv[2] : (j == 3) ? xv[3] : xv[4];
-        const double tj = (j == 2) ? tg[2] : (j == 4) ? tg[4] : 0.0;
-        const double oj = (j == 0) ? of[0] : (j == 1) ? of[1] : (j == 2) ? of[2] : (j == 3) ? of[3] : of[4];
-        const double ej = exp(-((xj - tj) * (xj - tj)) / oj);
-        ex[0] = env_lane_d<LPE, 0>(ej, env_lane0);
-        ex[1] = env_lane_d<LPE, 1>(ej, env_lane0);
-        ex[2] = env_lane_d<LPE, 2>(ej, env_lane0);
-        ex[3] = env_lane_d<LPE, 3>(ej, env_lane0);
-        ex[4] = env_lane_d<LPE, 4>(ej, env_lane0);
+        double xj;
+        if constexpr (SLOTS == 2)  // lanes 1 / 3 (obstacle ship): its own ground / |e_ct| (terms 3 / 4)
+          xj = (j == 0) ? dist : (j < 3) ? Tground : fabs(Tect);
+        else
+          xj = (j == 0) ? xv[0] : (j == 1) ? xv[1] : (j == 2) ? xv[2] : (j == 3) ? xv[3] : xv[4];
+        const double2 to = lds_rterm[j];
+        const double ej = exp(-((xj - to.x) * (xj - to.x)) / to.y);
+        ex[0] = env_lane_d<LPE, reward_lane<SLOTS>(0)>(ej, env_lane0);
+        ex[1] = env_lane_d<LPE, reward_lane<SLOTS>(1)>(ej, env_lane0);
+        ex[2] = env_lane_d<LPE, reward_lane<SLOTS>(2)>(ej, env_lane0);
+        ex[3] = env_lane_d<LPE, reward_lane<SLOTS>(3)>(ej, env_lane0);
+        ex[4] = env_lane_d<LPE, reward_lane<SLOTS>(4)>(ej, env_lane0);
       } else {
 #pragma unroll
         for (int k = 0; k < 5; ++k) ex[k] = exp(-((xv[k] - tg[k]) * (xv[k] - tg[k])) / of[k]);
@@ -1972,14 +1986,21 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       }
       const bool t6 = Tf & XF_END, t7 = Tf & XF_OUTSIDE, t8 = Of & XF_END, t9 = Of & XF_OUTSIDE;
       const bool t10 = Ttime > P.sim_time;
+      constexpr uint32_t kRoaBit = 1u << 31;  // (private: the obstacle ship reached its waypoint radius)
       uint32_t bits = (is_collision ? SHIPSIM_EV_COLLISION : 0) | (is_tg ? SHIPSIM_EV_TEST_GROUNDING : 0) |
                       (is_tnav ? SHIPSIM_EV_TEST_NAV_FAILURE : 0) | (is_og ? SHIPSIM_EV_OBS_GROUNDING : 0) |
                       (is_onav ? SHIPSIM_EV_OBS_NAV_FAILURE : 0) | (t6 ? SHIPSIM_EV_TEST_REACHES_END : 0) |
                       (t7 ? SHIPSIM_EV_TEST_OUTSIDE_MAP : 0) | (t8 ? SHIPSIM_EV_OBS_REACHES_END : 0) |
-                      (t9 ? SHIPSIM_EV_OBS_OUTSIDE_MAP : 0) | (t10 ? SHIPSIM_EV_TIME_LIMIT : 0);
+                      (t9 ? SHIPSIM_EV_OBS_OUTSIDE_MAP : 0) | (t10 ? SHIPSIM_EV_TIME_LIMIT : 0) |
+                      ((Of & XF_ROA) ? kRoaBit : 0u);
+      if constexpr (SLOTS == 2) bits = (uint32_t)env_lane_i<LPE, 0>((int)bits, env_lane0);  // the test ship's view
+      const bool roa_o = bits & kRoaBit;
+      bits &= ~kRoaBit;
       const bool terminal = bits & 0x1F;
-      const bool test_stop = is_collision || is_tg || is_tnav || t6 || t7 || t10;
-      const bool obs_stop = is_collision || is_og || is_onav || t8 || t9 || t10;
+      const bool test_stop = bits & (SHIPSIM_EV_COLLISION | SHIPSIM_EV_TEST_GROUNDING | SHIPSIM_EV_TEST_NAV_FAILURE |
+                                     SHIPSIM_EV_TEST_REACHES_END | SHIPSIM_EV_TEST_OUTSIDE_MAP | SHIPSIM_EV_TIME_LIMIT);
+      const bool obs_stop = bits & (SHIPSIM_EV_COLLISION | SHIPSIM_EV_OBS_GROUNDING | SHIPSIM_EV_OBS_NAV_FAILURE |
+                                    SHIPSIM_EV_OBS_REACHES_END | SHIPSIM_EV_OBS_OUTSIDE_MAP | SHIPSIM_EV_TIME_LIMIT);
       if (terminal) bits |= SHIPSIM_EV_TERMINAL;
       if (test_stop) bits |= SHIPSIM_EV_TEST_STOP;
       if (obs_stop) bits |= SHIPSIM_EV_OBS_STOP;
@@ -2013,7 +2034,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
       dec_ticks += 1;
       bool finish = nonfinite;
       if (phase == 0) {
-        const bool roa = Of & XF_ROA;
+        const bool roa = roa_o;
         if (combined_done) finish = true;
         else if (roa) {
           if (opaque_if<OPQ>(have_iw) != 0) phase = 1;
@@ -2118,13 +2139,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     if (AE.ticks_out) AE.ticks_out[env] = ticks;
     if (AE.ready_out) AE.ready_out[env] = ready ? 1 : 0;
   }
-  if (ready && AE.obs_out && sub_e == 0 && ship_e < 2) {  // test ship writes obs[0..3], obstacle ship obs[4..7]
+  if (ready && AE.obs_out && lie_e == 0) {  // the test ship's first lane holds the env's observation
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {  // (values in registers first: a select of two ns elements would become
-      float a = ns[i], b = ns[4 + i];  // an indexed ns, i.e. the whole array in scratch)
-      asm volatile("" : "+v"(a), "+v"(b));
-      AE.obs_out[env * 8 + ship_e * 4 + i] = ship_e ? b : a;
-    }
+    for (int i = 0; i < 8; ++i) AE.obs_out[env * 8 + i] = ns[i];
   }
 }
 
