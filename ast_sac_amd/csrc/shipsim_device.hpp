@@ -325,18 +325,26 @@ __device__ __forceinline__ void integrate(Ship& s, const Deriv& d, double dt, do
 // ---------------------------------------------------------------------------------------------
 // LOS_guidance.py:100-117 (k = next_wpt; waypoints k-1, k are register-cached): the state update
 // (e_ct, windup-limited e_ct_int) and the argument of the course correction atan
-__device__ __forceinline__ double los_update(const ShipConst& c, Ship& s, double x, double y) {
+// split in its two halves: the cross-track term q = e_ct / delta at (x, y) (e_ct: the windup-clamped cross-track
+// error the caller stores as s.e_ct), and the integrator update with the course correction's argument
+__device__ __forceinline__ double los_q(const ShipConst& c, const Ship& s, double x, double y, double& e_ct_out) {
   // alpha_k = atan2(dy, dx) and its sin/cos depend on the segment only: cached by segment_changed()
   const double sa = s.seg_sin, ca = s.seg_cos;
   double e_ct = -(x - s.wp_prev_n) * sa + (y - s.wp_prev_e) * ca;
+  if (e_ct * e_ct >= c.los_r2) e_ct = 0.99 * c.los_r;
+  e_ct_out = e_ct;
+  const double delta = py_max(1e-6, sqrt(c.los_r2 - e_ct * e_ct));
+  return e_ct / delta;
+}
+__device__ __forceinline__ double los_windup(const ShipConst& c, Ship& s, double q) {
+  if (fabs(s.e_ct_int + q) <= c.los_limit) s.e_ct_int += q;
+  return -q - s.e_ct_int * c.los_ki;  // (-e_ct / delta is -(e_ct / delta) exactly)
+}
+__device__ __forceinline__ double los_update(const ShipConst& c, Ship& s, double x, double y) {
+  double e_ct;
+  const double q = los_q(c, s, x, y, e_ct);
   s.e_ct = e_ct;
-  if (e_ct * e_ct >= c.los_r2) {
-    e_ct = 0.99 * c.los_r;
-    s.e_ct = e_ct;
-  }
-  double delta = py_max(1e-6, sqrt(c.los_r2 - e_ct * e_ct));
-  if (fabs(s.e_ct_int + e_ct / delta) <= c.los_limit) s.e_ct_int += e_ct / delta;
-  return -e_ct / delta - s.e_ct_int * c.los_ki;
+  return los_windup(c, s, q);
 }
 __device__ __forceinline__ double los_guidance(const ShipConst& c, Ship& s, double x, double y) {
   const double arg = los_update(c, s, x, y);

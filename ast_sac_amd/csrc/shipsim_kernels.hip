@@ -184,19 +184,33 @@ __device__ __forceinline__ const ShipConst* stage_consts(const ConstBuf& K, Ship
 #if SHIPSIM_TU != 2
 // control half of one ship tick: autopilot -> speed control -> (simple collav) -> store
 // (env.py test_step :389-433 / obs_step :481-512 / init_step :309-339); returns (ctrl, rudder)
-template <bool DETAILED, bool REC>
+// PRE: (pre_q, pre_e) = los_q at (s.n, s.e) on the current segment, evaluated earlier in the tick; used unless the
+// waypoint index advances here
+template <bool DETAILED, bool REC, bool PRE = false>
 __device__ __forceinline__ void control_and_store(const ShipConst& c, const Params& P, Ship& s,
                                                   const double* __restrict__ rn, const double* __restrict__ re,
                                                   double offset, double speed_factor, double mach_dt,
                                                   int simple_collav_flag /*0 none, 1 rl(-15deg), 2 noniw(+15)*/,
                                                   bool imminent, double* row, double* fuel, double& ctrl_out,
-                                                  double& rudder_out) {
+                                                  double& rudder_out, double pre_q = 0.0, double pre_e = 0.0) {
   const double N = s.n, E = s.e, H = s.yaw, U = s.u;
-  if (next_wpt_advance(c, s, N, E)) {
-    s.next_wpt += 1;
-    load_segment(s, rn, re);
+  double href;
+  if constexpr (PRE) {
+    double q = pre_q, e_ct = pre_e;
+    if (next_wpt_advance(c, s, N, E)) {
+      s.next_wpt += 1;
+      load_segment(s, rn, re);
+      q = los_q(c, s, N, E, e_ct);
+    }
+    s.e_ct = e_ct;
+    href = s.seg_alpha + atan(los_windup(c, s, q));
+  } else {
+    if (next_wpt_advance(c, s, N, E)) {
+      s.next_wpt += 1;
+      load_segment(s, rn, re);
+    }
+    href = los_guidance(c, s, N, E);
   }
-  double href = los_guidance(c, s, N, E);
   double rudder = heading_ctrl(c, s, href + offset, H, P.dt);
   double ctrl = speed_ctrl(c, s, c.desired_speed * speed_factor, U, P.dt, DETAILED);
   if (simple_collav_flag && imminent) {
@@ -250,16 +264,16 @@ __device__ __forceinline__ void control_and_integrate(const ShipConst& c, const 
 // the same tick in the AST kernels (step, decision stream, reset / init_step): algebraic wind force
 // and sin/cos(yaw) carried in (sy, cy) — valid for s.yaw on entry, refreshed after the integration
 // step, so one sincos per ship-tick serves both the kinematics and the reward's encounter angle.
-template <bool DETAILED, bool REC = false>
+template <bool DETAILED, bool REC = false, bool PRE = false>
 __device__ __forceinline__ void control_and_integrate_sc(const ShipConst& c, const Params& P, Ship& s,
                                                          const double* __restrict__ rn,
                                                          const double* __restrict__ re, double offset,
                                                          double speed_factor, double mach_dt, int simple_collav_flag,
                                                          bool imminent, double* row, double* fuel, double& sy,
-                                                         double& cy) {
+                                                         double& cy, double pre_q = 0.0, double pre_e = 0.0) {
   double ctrl, rudder;
-  control_and_store<DETAILED, REC>(c, P, s, rn, re, offset, speed_factor, mach_dt, simple_collav_flag, imminent, row,
-                                   fuel, ctrl, rudder);
+  control_and_store<DETAILED, REC, PRE>(c, P, s, rn, re, offset, speed_factor, mach_dt, simple_collav_flag, imminent,
+                                        row, fuel, ctrl, rudder, pre_q, pre_e);
   Deriv d = differentials_sc(c, P, s, ctrl, rudder, DETAILED, sy, cy);
   integrate(s, d, P.dt, mach_dt, DETAILED);
   sincos(s.yaw, &sy, &cy);
@@ -1693,6 +1707,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     SHIPSIM_LANE_CHECK(LPE, 7);
     const double pn = pair_swap(s.n), pe = pair_swap(s.e);
     double sf = 1.0, off = 0.0;
+    constexpr bool LOS_PRE = COLLAV == SHIPSIM_COLLAV_SBMPC && SLOTS == 2;  // the LOS term evaluated once per tick
+    double los_pre_q = 0.0, los_pre_e = 0.0;
     bool sb_active = false;
     if (COLLAV == SHIPSIM_COLLAV_SBMPC && SLOTS > 2) {  // do_list of every obstacle ship (env.py:366-370)
       constexpr int NOB = SLOTS - 1;
@@ -1749,10 +1765,16 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     } else if (COLLAV == SHIPSIM_COLLAV_SBMPC) {
       bool need = false;
       double los_arg = 0.0;
+      if (going) {
+        // the LOS cross-track term at this position, for every ship: its control below reuses it (its position
+        // and segment are the same there unless the waypoint index advances)
+        los_pre_q = los_q(c, s, s.n, s.e, los_pre_e);
+      }
       if (going && is_test) {
         // env.py:362-363: next_wpt result discarded; los_guidance integrates e_ct_int (Q3). The
         // course (atan) only feeds the optimisation, so it is evaluated for requesting envs only.
-        los_arg = los_update(c, s, s.n, s.e);
+        s.e_ct = los_pre_e;
+        los_arg = los_windup(c, s, los_pre_q);
         double d0 = pe - s.e, d1 = pn - s.n;
         need = sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_
         need = diag::sb_request(need, P.max_sampling);  // (the product: need itself)
@@ -1805,9 +1827,10 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
           imminent = (dn * dn + de * de) < 9000000.0f;
         }
         SHIPSIM_SHIP_CHECK(LPE, SLOTS, 6);  // (its DPP exchanges pair sub-lanes of one ship)
-        control_and_integrate_sc<DETAILED, REC>(c, P, s, rn, re, -off, sf, mach_dt, (SIMPLE && is_test) ? 1 : 0,
-                                                imminent, (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel,
-                                                sy, cy);
+        control_and_integrate_sc<DETAILED, REC, LOS_PRE>(c, P, s, rn, re, -off, sf, mach_dt,
+                                                         (SIMPLE && is_test) ? 1 : 0, imminent,
+                                                         (REC && sub == 0) ? T.ship_row(qc, rec_t) : nullptr, fuel, sy,
+                                                         cy, los_pre_q, los_pre_e);
         my_speed_out = U;
         if (is_obs1) {  // travel tracker (env.py:527-534, Q6)
           double tn = s.log_n - prev_log_n, te = s.log_e - prev_log_e;
