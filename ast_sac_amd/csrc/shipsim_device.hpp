@@ -54,7 +54,27 @@ struct ShipConst {
   // SimulationConfiguration
   double init_n, init_e, init_yaw, init_u, init_v, init_r;
   int32_t n_route, pad_;
+  // filled on the device by stage_consts (the host leaves them 0): div_rcp of r_me, r_hsg, jp and of the step dt
+  double rcp_r_me, rcp_r_hsg, rcp_jp, rcp_dt;
 };
+
+// fp64 division with the divisor's reciprocal formed once. The compiler's n / d is
+//   y = div_rcp(d) (v_rcp_f64 + two Newton steps on d), q0 = n·y, rem = fma(−d, q0, n), q = fma(rem, y, q0),
+//   then v_div_fixup(q, d, n), with v_div_scale pre-scaling both operands only near the ends of the exponent range;
+// div_by runs the same operations with y computed once for a divisor that is reused (a constant of the ship, or
+// one denominator of two quotients). The same bits as n / d whenever v_div_scale leaves the operands unscaled:
+// finite d with 2^-1021 < |d| < 2^1021 (so 1/d is normal), |n| > 2^-969 or n = 0, and |n / d| normal — every
+// divisor and quotient of the ship model (scripts/div_check.hip checks the identity on the device).
+__device__ __forceinline__ double div_rcp(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return fma(r, fma(-d, r, 1.0), r);
+}
+__device__ __forceinline__ double div_by(double n, double d, double y) {
+  const double q0 = n * y;
+  const double rem = fma(-d, q0, n);
+  return __builtin_amdgcn_div_fixup(fma(rem, y, q0), d, n);
+}
 
 struct Params {
   int32_t kind, machinery, collav, n_ships;
@@ -249,11 +269,13 @@ __device__ __forceinline__ Deriv differentials_body(const ShipConst& c, const Pa
   d.domega = 0.0;
   if (detailed) {
     // main_engine_torque / hsg_torque :416-432
-    double t_me = py_min(ctrl * c.avail_me / (s.omega + 0.1), c.cap_me);
-    double t_hsg = py_min(ctrl * c.avail_el / (s.omega + 0.1), c.cap_el);
-    double eq_me = (t_me - c.d_me * s.omega) / c.r_me;
-    double eq_hsg = (t_hsg - c.d_hsg * s.omega) / c.r_hsg;
-    d.domega = (eq_me + eq_hsg - c.kp_prop * (s.omega * s.omega)) / c.jp;
+    // (the divisions by the ship's constants, and the two by one denominator, with the reciprocals formed once)
+    const double den = s.omega + 0.1, y_den = div_rcp(den);
+    double t_me = py_min(div_by(ctrl * c.avail_me, den, y_den), c.cap_me);
+    double t_hsg = py_min(div_by(ctrl * c.avail_el, den, y_den), c.cap_el);
+    double eq_me = div_by(t_me - c.d_me * s.omega, c.r_me, c.rcp_r_me);
+    double eq_hsg = div_by(t_hsg - c.d_hsg * s.omega, c.r_hsg, c.rcp_r_hsg);
+    d.domega = div_by(eq_me + eq_hsg - c.kp_prop * (s.omega * s.omega), c.jp, c.rcp_jp);
     thrust = c.thrust_coeff * s.omega * fabs(s.omega);
   }
   // inv(rotation()) @ vel_c
@@ -384,12 +406,12 @@ __host__ __device__ __forceinline__ double pow2_inverse(double x) {
 }
 
 // PidController.pid_ctrl controllers.py:106-118; MUL: dt is a power of two and inv_dt = pow2_inverse(dt), the
-// derivative term's division a multiplication (the same bits)
+// derivative term's division a multiplication (the same bits); else inv_dt = div_rcp(dt) (ShipConst::rcp_dt)
 template <bool MUL = false>
 __device__ __forceinline__ double pid(double& ei, double& prev, double kp, double kd, double ki, double dt,
-                                      double setpoint, double meas, double inv_dt = 0.0) {
+                                      double setpoint, double meas, double inv_dt) {
   double error = setpoint - meas;
-  double d_error = MUL ? (error - prev) * inv_dt : (error - prev) / dt;
+  double d_error = MUL ? (error - prev) * inv_dt : div_by(error - prev, dt, inv_dt);
   double error_i = ei + error * dt;
   prev = error;
   ei = error_i;
@@ -407,7 +429,7 @@ __device__ __forceinline__ double pi_ctrl(double& ei, double kp, double ki, doub
 // measurement = forward speed) | ThrustFromSpeedSetPoint.thrust run_colav controllers.py:183-185
 template <bool MUL = false>
 __device__ __forceinline__ double speed_ctrl(const ShipConst& c, Ship& s, double setpoint, double u, double dt,
-                                             bool detailed, double inv_dt = 0.0) {
+                                             bool detailed, double inv_dt) {
   if (detailed) {
     double desired_shaft = pi_ctrl(s.spd_a, c.kp_ship_speed, c.ki_ship_speed, dt, setpoint, u);
     desired_shaft = sat(desired_shaft, 0, c.shaft_speed_max);
@@ -449,7 +471,7 @@ __device__ __forceinline__ void fuel_consumption(const ShipConst& c, double load
 // HeadingByReferenceController.rudder_angle_from_heading_setpoint :246-255
 template <bool MUL = false>
 __device__ __forceinline__ double heading_ctrl(const ShipConst& c, Ship& s, double heading_ref, double heading,
-                                               double dt, double inv_dt = 0.0) {
+                                               double dt, double inv_dt) {
   double rudder = -pid<MUL>(s.hdg_ei, s.hdg_prev, c.hdg_kp, c.hdg_kd, c.hdg_ki, dt, heading_ref, heading, inv_dt);
   return sat(rudder, -c.max_rudder, c.max_rudder);
 }

@@ -172,11 +172,17 @@ __device__ __forceinline__ void store_ship(const DevState& S, int q, const Ship&
 }
 
 // per-block LDS copy of the ships' ShipConst (lanes of one ship read one address)
-__device__ __forceinline__ const ShipConst* stage_consts(const ConstBuf& K, ShipConst* lds, int n_ships) {
+// (and the reciprocals div_by uses, formed here on the device: the bits of the division sequence's own)
+__device__ __forceinline__ const ShipConst* stage_consts(const ConstBuf& K, ShipConst* lds, int n_ships, double dt) {
   const int nwords = (int)(sizeof(ShipConst) * n_ships / sizeof(double));
   const double* src = reinterpret_cast<const double*>(K.ships());
   double* dst = reinterpret_cast<double*>(lds);
   for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  if ((int)threadIdx.x < n_ships) {
+    ShipConst& c = lds[threadIdx.x];
+    c.rcp_r_me = div_rcp(c.r_me); c.rcp_r_hsg = div_rcp(c.r_hsg); c.rcp_jp = div_rcp(c.jp); c.rcp_dt = div_rcp(dt);
+  }
   __syncthreads();
   return lds;
 }
@@ -211,8 +217,8 @@ __device__ __forceinline__ void control_and_store(const ShipConst& c, const Para
     }
     href = los_guidance(c, s, N, E);
   }
-  double rudder = heading_ctrl(c, s, href + offset, H, P.dt);
-  double ctrl = speed_ctrl(c, s, c.desired_speed * speed_factor, U, P.dt, DETAILED);
+  double rudder = heading_ctrl(c, s, href + offset, H, P.dt, c.rcp_dt);
+  double ctrl = speed_ctrl(c, s, c.desired_speed * speed_factor, U, P.dt, DETAILED, c.rcp_dt);
   if (simple_collav_flag && imminent) {
     ctrl *= 0.5;
     ctrl = py_min(py_max(ctrl, 0.0), 1.1);
@@ -891,7 +897,7 @@ template <bool DETAILED, bool REC>
 __global__ __launch_bounds__(256) void reset_kernel(const Params P, DevState S, ConstBuf K, Traj T,
                                                    const uint8_t* mask, float* obs_out) {
   __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
-  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships, P.dt);
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   const int nq = P.n_envs * P.n_ships;
   if (q >= nq) return;
@@ -1252,6 +1258,9 @@ __device__ __forceinline__ int env_lane_i(int x, int env_lane0) {
 // The env lane that evaluates each reward term's exp (LPE >= 8), and the term of env lane j < 5. Two-ship envs
 // (lanes alternate test / obstacle ship, each computing from its own perspective): the obstacle ship's lanes 1 and 3
 // take the terms of its own ground distance and cross-track error.
+struct RewardTerm {
+  double t, o, y, pad;  // target, scale, div_rcp(scale)
+};
 template <int SLOTS>
 __host__ __device__ constexpr int reward_lane(int k) {
   return SLOTS != 2 ? k : k == 0 ? 0 : k == 1 ? 2 : k == 2 ? 4 : k == 3 ? 1 : 3;
@@ -1382,13 +1391,13 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
   __shared__ float lds_pol[POLICY ? kPolMaxRows * kPolMaxHidden : 1];  // shipsim_run_policy: h1 rows
-  __shared__ double2 lds_rterm[8];  // the reward exp each lane of an env evaluates: (target, scale) of its term
+  __shared__ RewardTerm lds_rterm[8];  // the reward exp each lane of an env evaluates: its term's constants
   if constexpr (diag::kPoisonLds) {  // (stale-LDS diagnostics build only)
     diag::poison_lds(lds_sc, sizeof(lds_sc)); diag::poison_lds(lds_edges, sizeof(lds_edges));
     diag::poison_lds(lds_edges_raw, sizeof(lds_edges_raw)); diag::poison_lds(lds_boxes, sizeof(lds_boxes));
     __syncthreads();
   }
-  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships, P.dt);
   for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) {
     const Edge ed = K.edges()[i];
     EdgeX x;
@@ -1404,7 +1413,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     const int j = threadIdx.x, t = j < 5 ? reward_term<SLOTS>(j) : 0;
     const double tg[5] = {0.0, 0.0, 3000.0, 0.0, 500.0};
     const double of[5] = {200000000.0, 175000.0, 1250000.0, 50000.0, 12500.0};
-    lds_rterm[j] = make_double2(j < 5 ? tg[t] : 0.0, j < 5 ? of[t] : 1.0);
+    const double o = j < 5 ? of[t] : 1.0;
+    lds_rterm[j] = RewardTerm{j < 5 ? tg[t] : 0.0, o, div_rcp(o), 0.0};
   }
   __syncthreads();
 
@@ -1978,8 +1988,8 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
           xj = (j == 0) ? dist : (j < 3) ? Tground : fabs(Tect);
         else
           xj = (j == 0) ? xv[0] : (j == 1) ? xv[1] : (j == 2) ? xv[2] : (j == 3) ? xv[3] : xv[4];
-        const double2 to = lds_rterm[j];
-        const double ej = exp(-((xj - to.x) * (xj - to.x)) / to.y);
+        const RewardTerm to = lds_rterm[j];
+        const double ej = exp(div_by(-((xj - to.t) * (xj - to.t)), to.o, to.y));
         ex[0] = env_lane_d<LPE, reward_lane<SLOTS>(0)>(ej, env_lane0);
         ex[1] = env_lane_d<LPE, reward_lane<SLOTS>(1)>(ej, env_lane0);
         ex[2] = env_lane_d<LPE, reward_lane<SLOTS>(2)>(ej, env_lane0);
@@ -2172,7 +2182,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
 template <bool DETAILED>
 __global__ __launch_bounds__(64) void single_tick_kernel(const Params P, DevState S, ConstBuf K, int k) {
   __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
-  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships, P.dt);
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P.n_envs) return;
   const ShipConst& c = SC[0];
@@ -2210,7 +2220,7 @@ __global__ __launch_bounds__(192) void single_tick_pipe_kernel(const Params P, D
   __shared__ double x_uvr[2][3][64];  // (u, v, r) of a tick, by tick parity
   __shared__ double x_sc[2][2][64];   // sin / cos ψ of a tick
   __shared__ double x_rud[2][64];     // rudder of a tick
-  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships);
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships, P.dt);
   const int lane = threadIdx.x & 63, role = threadIdx.x >> 6;  // (wave-uniform)
   const int q0 = blockIdx.x * 64 + lane, q = min(q0, P.n_envs - 1);  // (every lane takes part in the barriers)
   const bool live = q0 < P.n_envs;
@@ -2238,7 +2248,7 @@ __global__ __launch_bounds__(192) void single_tick_pipe_kernel(const Params P, D
         load_segment(s, rn, re);
       }
       const double href = los_guidance(c, s, N, E);
-      const double rudder = heading_ctrl<POW2_DT>(c, s, href + 0.0, H, dt, inv_dt);
+      const double rudder = heading_ctrl<POW2_DT>(c, s, href + 0.0, H, dt, POW2_DT ? inv_dt : c.rcp_dt);
       s.log_rudder = rudder;
       s.log_ect = s.e_ct;
       s.log_n = N;
@@ -2286,7 +2296,7 @@ __global__ __launch_bounds__(192) void single_tick_pipe_kernel(const Params P, D
     for (int t = 0; t < k; ++t) {
       const int b = t & 1;
       const double sy = x_sc[b][0][lane], cy = x_sc[b][1][lane], rudder = x_rud[b][lane];
-      const double thrust = speed_ctrl<POW2_DT>(c, s, c.desired_speed * 1.0, s.u, dt, false, inv_dt);
+      const double thrust = speed_ctrl<POW2_DT>(c, s, c.desired_speed * 1.0, s.u, dt, false, POW2_DT ? inv_dt : c.rcp_dt);
       s.log_thrust = thrust;
       double tau[3];
       wind_force_alg(c, P, s, sy, cy, wsin, wcos, tau);
@@ -2346,7 +2356,7 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(LegacyArgs a_arg) {
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
   const LegacyArgs& A0 = legacy_args();
-  const ShipConst* SC = stage_consts(A0.K, lds_sc, A0.P.n_ships);
+  const ShipConst* SC = stage_consts(A0.K, lds_sc, A0.P.n_ships, A0.P.dt);
   for (int i = threadIdx.x; i < A0.K.n_edges; i += blockDim.x) lds_edges_raw[i] = A0.K.edges()[i];
   for (int i = threadIdx.x; i < A0.P.n_polys; i += blockDim.x) lds_boxes[i] = A0.K.boxes()[i];
   __syncthreads();
