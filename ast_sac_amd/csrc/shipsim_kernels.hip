@@ -2517,6 +2517,17 @@ __global__ __launch_bounds__(64) void sbmpc_eval_kernel(int n, double tf, double
   }
 }
 
+// shipsim_div_check: div_by with div_rcp (the kernels' division by a reused divisor) beside the plain division
+__global__ __launch_bounds__(256) void div_check_kernel(int n, const double* __restrict__ num,
+                                                        const double* __restrict__ den, double* __restrict__ fast,
+                                                        double* __restrict__ ref) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double a = num[i], d = den[i];
+  fast[i] = div_by(a, d, div_rcp(d));
+  ref[i] = a / d;
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -3532,6 +3543,14 @@ int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double
   if (n < 0 || (n > 0 && (!in || !out)) || !(dt > 0) || tf / dt > 4096) return SHIPSIM_EINVAL;
   if (n == 0) return SHIPSIM_OK;
   hipLaunchKernelGGL(sbmpc_eval_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, tf, dt, in, out);
+  return hipGetLastError() == hipSuccess ? SHIPSIM_OK : SHIPSIM_EHIP;
+}
+
+int shipsim_div_check(int32_t n, const double* num, const double* den, double* fast, double* ref, void* stream) {
+  if (n < 0 || (n > 0 && (!num || !den || !fast || !ref))) return SHIPSIM_EINVAL;
+  if (n == 0) return SHIPSIM_OK;
+  hipLaunchKernelGGL(div_check_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, num, den, fast,
+                     ref);
   return hipGetLastError() == hipSuccess ? SHIPSIM_OK : SHIPSIM_EHIP;
 }
 

@@ -56,6 +56,7 @@ def load_library(path=LIB_PATH):
     L.shipsim_nonfinite_count.restype = C.c_int32
     L.shipsim_set_trajectory.argtypes = [P, P, P, C.c_int32, P]
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
+    L.shipsim_div_check.argtypes = [C.c_int32, P, P, P, P, P]
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
     L.shipsim_set_stream_tail.argtypes = [P, C.c_int32]
@@ -82,7 +83,7 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
                     "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
                     "shipsim_nonfinite_count", "shipsim_lanes_per_env", "shipsim_set_stream",
-                    "shipsim_run_policy", "shipsim_diag_lane_faults", "shipsim_set_stream_tail")
+                    "shipsim_run_policy", "shipsim_diag_lane_faults", "shipsim_set_stream_tail", "shipsim_div_check")
 
 
 def diag_lane_faults():
@@ -320,6 +321,22 @@ class ShipSim:
     def nonfinite_count(self):
         """Decisions flagged SHIPSIM_EV_NONFINITE since create (as of the last synchronize)."""
         return int(self.L.shipsim_nonfinite_count(self.h))
+
+
+def div_check(num, den, device="cuda"):
+    """The kernels' fp64 division by a reused divisor (reciprocal formed once) beside the plain division, on the
+    device: (fast, ref) float64 tensors of num / den (shipsim_div_check)."""
+    L = load_library()
+    a = torch.as_tensor(num, dtype=torch.float64, device=device).contiguous().reshape(-1)
+    d = torch.as_tensor(den, dtype=torch.float64, device=device).contiguous().reshape(-1)
+    if a.shape != d.shape:
+        raise ShipSimError("num and den must have the same size")
+    fast, ref = torch.empty_like(a), torch.empty_like(a)
+    stream = torch.cuda.current_stream(a.device)
+    rc = L.shipsim_div_check(int(a.numel()), _ptr(a), _ptr(d), _ptr(fast), _ptr(ref), C.c_void_p(stream.cuda_stream))
+    if rc:
+        raise ShipSimError(f"shipsim_div_check failed ({rc})")
+    return fast, ref
 
 
 def sbmpc_eval(requests, tf=1000.0, dt=20.0, device="cuda"):

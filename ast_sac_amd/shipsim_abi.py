@@ -13,7 +13,7 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAP_GRID, MAP_ALL_EDGES = 0, 1  # shipsim_config.map_query (results identical)
 ENONFINITE = -5  # shipsim_synchronize status (include/shipsim.h)
 MAX_ROUTE = 16

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 8
+#define SHIPSIM_ABI_VERSION 9
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -366,6 +366,13 @@ int shipsim_set_trajectory(shipsim_handle* h, double* ship_rows, double* env_row
  * SBMPC(tf, dt) horizon; stream is a hipStream_t (NULL = default); device pointers. */
 #define SHIPSIM_SBMPC_IN 17
 int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double* out, void* stream);
+
+/* Diagnostics: the kernels' division by a reused divisor (the divisor's refined reciprocal formed once, the rest of
+ * the compiler's fp64 division sequence per quotient) next to the plain IEEE division, for n operand
+ * pairs: fast[i] = num[i] / den[i] as the kernels form it, ref[i] = num[i] / den[i]. Device pointers (n doubles
+ * each); stream a hipStream_t (NULL = default). The two agree bit for bit for operands away from the ends of the
+ * exponent range (tests/test_gpu_div_identity.py). */
+int shipsim_div_check(int32_t n, const double* num, const double* den, double* fast, double* ref, void* stream);
 
 /* ---- open-loop decision stream (the C3 workload of SURVEY.md §8(d)) -------------------------
  * Every env draws the scoping angle (radians, already denormalised) of decision d of its episode e from
