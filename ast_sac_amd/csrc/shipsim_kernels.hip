@@ -2493,6 +2493,143 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(LegacyArgs a_arg) {
   }
 }
 
+// C1: MultiShipNonIWEnv._step (run_colav/env.py:613-676) inside the run_simplified_model.py:245-249 loop, k ticks per
+// launch (shipsim_tick). Two lanes per env (lane & 1 = ship); both ships follow fixed routes. Per tick, in the
+// reference's order: the test ship's step (test_step :326-455: the SBMPC block when collav is sbmpc, control with the
+// simple collision avoidance's +15° when imminent, one ship tick), then the obstacle ship's (obs_step :457-586: the
+// same SBMPC block — its own LOS course and desired speed, the test ship's state after its tick as the own ship, the
+// obstacle ship itself as the obstacle — then control and tick), each frozen ship storing its last row and advancing
+// its clock twice instead; then get_env_info (:53-225, the flags of reward_function.py without the rewards) on the
+// post-tick states and the stop flags (:658-664). The env's SBMPC memory (P_ca_last, Chi_ca_last) is one object that
+// both ships' blocks update in turn. Event bits of the last tick to events_out.
+template <int COLLAV>
+__global__ __launch_bounds__(64) void noniw_tick_kernel(const Params P, DevState S, ConstBuf K, int k,
+                                                        uint32_t* events_out) {
+  __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
+  __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
+  __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
+  const ShipConst* SC = stage_consts(K, lds_sc, P.n_ships, P.dt);
+  for (int i = threadIdx.x; i < K.n_edges; i += blockDim.x) lds_edges_raw[i] = K.edges()[i];
+  for (int i = threadIdx.x; i < P.n_polys; i += blockDim.x) lds_boxes[i] = K.boxes()[i];
+  __syncthreads();
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int env = gl >> 1, ship = gl & 1;
+  const bool is_test = ship == 0;
+  const bool valid = env < P.n_envs;  // (invalid lanes run along: every lane takes part in the exchanges)
+  const int envc = valid ? env : 0, qc = envc * 2 + ship;
+  const ShipConst& c = SC[ship];
+  const double* rn = S.route_n() + (size_t)qc * kMaxRoute;
+  const double* re = S.route_e() + (size_t)qc * kMaxRoute;
+  Ship s;
+  load_ship(S, qc, s);
+  double sy, cy;
+  sincos(s.yaw, &sy, &cy);
+  double p_last = S.p_last()[envc], chi_last = S.chi_last()[envc];
+  float st[4];  // self.states (float32): test (n, e), obstacle (n, e) as the previous tick left them
+  for (int i = 0; i < 4; ++i) st[i] = S.states4()[envc * 4 + i];
+  const int n_samp = (int)(P.sbmpc_tf / P.sbmpc_dt);
+  constexpr int kFlag = COLLAV == SHIPSIM_COLLAV_SIMPLE ? 2 : 0;  // the +15° avoidance (control_and_store)
+  uint32_t bits = 0;
+  for (int it = 0; it < k; ++it) {
+    const float dn = st[0] - st[2], de = st[1] - st[3];
+    const bool imminent = (dn * dn + de * de) < 9000000.0f;  // is_collision_imminent on self.states
+    // one ship's step: its SBMPC block (need: the own ship within D_INIT of the obstacle) and control + tick
+    auto ship_step = [&](int who, double os_n, double os_e, double os_v, double ob_n, double ob_e, double ob_yaw,
+                         double ob_u, double ob_v) __attribute__((always_inline)) {
+      const bool mine = ship == who;
+      double sf = 1.0, off = 0.0;
+      if constexpr (COLLAV == SHIPSIM_COLLAV_SBMPC) {
+        const bool act = valid && mine && !s.stop;
+        bool need = false;
+        double los_arg = 0.0;
+        if (act) {  // next_wpt's result discarded; los_guidance integrates e_ct_int (Q3)
+          los_arg = los_update(c, s, s.n, s.e);
+          const double d0 = ob_e - os_e, d1 = ob_n - os_n;
+          need = sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_
+        }
+        double pb = 1.0, cb = 0.0;
+        if (__any(need)) {
+          SbIn in = SbIn{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+          in.u_d = SC[who].desired_speed;  // (every request of this pass is ship `who`'s: the same in each lane)
+          in.obs_l = SC[1].obs_l_cfg; in.obs_w = SC[1].obs_w_cfg;
+          if (need) {
+            in.chi_d = -(s.seg_alpha + atan(los_arg));
+            in.os_x = os_e; in.os_y = os_n; in.os_v = os_v;
+            in.ob_x = ob_e; in.ob_y = ob_n; in.ob_psi = -ob_yaw; in.ob_u = ob_u; in.ob_v = ob_v;
+            sb_set_heading_trig(in);
+            in.p_last = p_last; in.chi_last = chi_last;
+          }
+          sbmpc_cooperative<true>(need, in, n_samp, P.sbmpc_dt, pb, cb);
+        }
+        if (act) {
+          if (need) { p_last = pb; chi_last = cb; sf = pb; off = cb; }
+          else { p_last = 1; chi_last = 0; }
+        }
+      }
+      if (valid && mine) {
+        if (s.stop) {  // store_last_simulation_data + two next_time
+          s.time = s.time + P.dt;
+          s.time = s.time + P.dt;
+        } else {
+          control_and_integrate_sc<false, false>(c, P, s, rn, re, -off, sf, 0.0, kFlag, imminent, nullptr, nullptr, sy,
+                                                 cy);
+        }
+      }
+    };
+    {  // the test ship: the obstacle ship before it moves
+      const double pn = pair_swap(s.n), pe = pair_swap(s.e), pyaw = pair_swap(s.yaw);
+      const double pu = pair_swap(s.u), pv = pair_swap(s.v);
+      ship_step(0, s.n, s.e, s.v, pn, pe, pyaw, pu, pv);
+    }
+    {  // the obstacle ship: the test ship after its tick, the env's SBMPC memory as the test ship's block left it
+      const double tn = pair_swap(s.n), te = pair_swap(s.e), tv = pair_swap(s.v);
+      const double pl = pair_swap(p_last), cl = pair_swap(chi_last);
+      if (!is_test) { p_last = pl; chi_last = cl; }
+      ship_step(1, tn, te, tv, s.n, s.e, s.yaw, s.u, s.v);
+      const double pl2 = pair_swap(p_last), cl2 = pair_swap(chi_last);
+      if (is_test) { p_last = pl2; chi_last = cl2; }
+    }
+    // get_env_info on the post-tick states (check_condition.py), both ships' own flags exchanged
+    const double margin = c.l_ship / 2;
+    const bool my_end = sqrt_le((s.n - s.end_n) * (s.n - s.end_n) + (s.e - s.end_e) * (s.e - s.end_e), 200.0);
+    const bool my_out = (s.n < P.min_north + margin || s.n > P.max_north - margin) ||
+                        (s.e < P.min_east + margin || s.e > P.max_east - margin);
+    bool my_gr = false;
+    for (int q = 0; q < 4; ++q) {
+      const double cn = (q < 2) ? s.n - margin : s.n + margin;
+      const double ce = (q & 1) ? s.e + margin : s.e - margin;
+      if (corner_inside(K, lds_edges_raw, lds_boxes, P.n_polys, cn, ce)) my_gr = true;
+    }
+    const bool my_nav = fabs(s.log_ect) > (is_test ? 3000.0 : 500.0);  // is_tnav / is_onav (no travel tracker)
+    const int my_flags = (my_end ? 1 : 0) | (my_out ? 2 : 0) | (my_gr ? 4 : 0) | (my_nav ? 8 : 0);
+    const int o_flags = pair_swap_i(my_flags);
+    const double on = pair_swap(s.n), oe = pair_swap(s.e);
+    const int Tf = is_test ? my_flags : o_flags, Of = is_test ? o_flags : my_flags;
+    const double cd = (s.n - on) * (s.n - on) + (s.e - oe) * (s.e - oe);
+    const bool t10 = pair_swap(s.time) > P.sim_time;  // (the test ship's clock: read on its partner lane too)
+    const bool t10_t = s.time > P.sim_time;
+    const bool f[10] = {cd < 2500.0, (Tf & 4) != 0, (Tf & 8) != 0, (Of & 4) != 0, (Of & 8) != 0,
+                        (Tf & 1) != 0, (Tf & 2) != 0, (Of & 1) != 0, (Of & 2) != 0, is_test ? t10_t : t10};
+    bits = 0;
+    for (int i = 0; i < 10; ++i)
+      if (f[i]) bits |= 1u << i;
+    if (bits & 0x1Fu) bits |= SHIPSIM_EV_TERMINAL;
+    if (bits & 0x267u) bits |= SHIPSIM_EV_TEST_STOP;  // collision, test grounding / nav, test end / outside, time
+    if (bits & 0x399u) bits |= SHIPSIM_EV_OBS_STOP;   // collision, obs grounding / nav, obs end / outside, time
+    const bool terminal = bits & SHIPSIM_EV_TERMINAL;
+    if (valid && !terminal && (bits & (is_test ? SHIPSIM_EV_TEST_STOP : SHIPSIM_EV_OBS_STOP))) s.stop = 1;
+    const double Tn = is_test ? s.n : on, Te = is_test ? s.e : oe, On = is_test ? on : s.n, Oe = is_test ? oe : s.e;
+    st[0] = (float)Tn; st[1] = (float)Te; st[2] = (float)On; st[3] = (float)Oe;
+  }
+  if (!valid) return;
+  store_ship(S, qc, s);
+  if (is_test) {
+    S.p_last()[env] = p_last; S.chi_last()[env] = chi_last;
+    for (int i = 0; i < 4; ++i) S.states4()[env * 4 + i] = st[i];
+    if (events_out && k > 0) events_out[env] = bits;
+  }
+}
+
 // SBMPC.get_optimal_ctrl_offset (sbmpc.py:113-185) for a batch of independent single-obstacle
 // requests (shipsim_sbmpc_eval): one request per lane, optimisations served wave-cooperatively.
 __global__ __launch_bounds__(64) void sbmpc_eval_kernel(int n, double tf, double dt, const double* __restrict__ in,
@@ -2979,7 +3116,6 @@ static void make_ship_const(const shipsim_config* cfg, const shipsim_ship_config
 static int validate(const shipsim_config* cfg, char* err, size_t n) {
   if (cfg->abi_version != SHIPSIM_ABI_VERSION) return snprintf(err, n, "abi_version %d != %d", cfg->abi_version, SHIPSIM_ABI_VERSION), 1;
   if (cfg->kind < 0 || cfg->kind > 2) return snprintf(err, n, "bad kind %d", cfg->kind), 1;
-  if (cfg->kind == SHIPSIM_KIND_NONIW) return snprintf(err, n, "KIND_NONIW (C1) runs on the CPU oracle only"), 1;
   if (cfg->machinery < 0 || cfg->machinery > 1) return snprintf(err, n, "bad machinery %d", cfg->machinery), 1;
   if (cfg->collav < 0 || cfg->collav > 2) return snprintf(err, n, "bad collav %d", cfg->collav), 1;
   int ns = cfg->kind == SHIPSIM_KIND_SINGLE ? 1 : 2;
@@ -2997,7 +3133,7 @@ static int validate(const shipsim_config* cfg, char* err, size_t n) {
   for (int i = 0; i < ns; ++i) {
     int nr = cfg->ship[i].n_route;
     if (nr < 2 || nr > SHIPSIM_MAX_ROUTE) return snprintf(err, n, "ship %d route length %d out of range", i, nr), 1;
-    if (i == 1 && nr + cfg->max_sampling_frequency > SHIPSIM_MAX_ROUTE)
+    if (cfg->kind == SHIPSIM_KIND_AST && i == 1 && nr + cfg->max_sampling_frequency > SHIPSIM_MAX_ROUTE)
       return snprintf(err, n, "obstacle route %d + samplings %d exceeds %d", nr, cfg->max_sampling_frequency, SHIPSIM_MAX_ROUTE), 1;
   }
   if (cfg->n_polys < 0 || cfg->n_polys > SHIPSIM_MAX_POLYS) return snprintf(err, n, "n_polys %d out of range", cfg->n_polys), 1;
@@ -3241,7 +3377,7 @@ int32_t shipsim_lanes_per_env(const shipsim_handle* h) { return h ? h->lpe : -1;
 
 int shipsim_reset(shipsim_handle* h, const uint8_t* env_mask, float* obs_out) {
   if (!h || !h->dev_block) return SHIPSIM_EINVAL;
-  if (h->P.kind != SHIPSIM_KIND_AST && h->P.kind != SHIPSIM_KIND_SINGLE)
+  if (h->P.kind < SHIPSIM_KIND_SINGLE || h->P.kind > SHIPSIM_KIND_AST)
     return fail(h, SHIPSIM_EINVAL, "reset: kind %d not supported on device", h->P.kind);
   DeviceGuard g(h->device);
   int S = h->P.n_envs * h->P.n_ships, threads = 256, blocks = (S + threads - 1) / threads;
@@ -3305,11 +3441,23 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
 
 int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
   if (!h || !h->dev_block || k < 0) return SHIPSIM_EINVAL;
-  if (h->P.kind != SHIPSIM_KIND_SINGLE)
-    return fail(h, SHIPSIM_EINVAL, "tick: device raw ticks implemented for SHIPSIM_KIND_SINGLE");
-  (void)events_out;
+  if (h->P.kind != SHIPSIM_KIND_SINGLE && h->P.kind != SHIPSIM_KIND_NONIW)
+    return fail(h, SHIPSIM_EINVAL, "tick: device raw ticks for SHIPSIM_KIND_SINGLE and SHIPSIM_KIND_NONIW");
   if (k == 0) return SHIPSIM_OK;
   DeviceGuard g(h->device);
+  if (h->P.kind == SHIPSIM_KIND_NONIW) {  // two lanes per env
+    if (h->P.machinery != SHIPSIM_MACH_SIMPLIFIED)
+      return fail(h, SHIPSIM_EINVAL, "tick: KIND_NONIW runs the simplified machinery (run_colav SimpleShipModel)");
+    const int blocks = (2 * h->P.n_envs + 63) / 64;
+#define NT(CA) \
+  hipLaunchKernelGGL(noniw_tick_kernel<CA>, dim3(blocks), dim3(64), 0, h->stream, h->P, h->S, h->K, k, events_out)
+    if (h->P.collav == SHIPSIM_COLLAV_SBMPC) NT(SHIPSIM_COLLAV_SBMPC);
+    else if (h->P.collav == SHIPSIM_COLLAV_SIMPLE) NT(SHIPSIM_COLLAV_SIMPLE);
+    else NT(SHIPSIM_COLLAV_NONE);
+#undef NT
+    HIPCHK(h, hipGetLastError());
+    return SHIPSIM_OK;
+  }
   const int threads = 64, blocks = (h->P.n_envs + threads - 1) / threads;
   if (h->P.machinery == SHIPSIM_MACH_DETAILED)
     hipLaunchKernelGGL(single_tick_kernel<true>, dim3(blocks), dim3(threads), 0, h->stream, h->P, h->S, h->K, k);

@@ -196,9 +196,11 @@ class ShipSim:
         self._keep = (a, act)
         return out
 
-    def tick(self, k=1):
+    def tick(self, k=1, events=None):
+        """k raw ticks of the loop body (shipsim_tick: SINGLE, and NONIW's MultiShipNonIWEnv._step). events: an
+        optional (N,) int32 / uint32 device tensor for the env_info bits of the last tick (NONIW)."""
         self._follow_stream()
-        self._check(self.L.shipsim_tick(self.h, int(k), None), "shipsim_tick")
+        self._check(self.L.shipsim_tick(self.h, int(k), _ptr(events)), "shipsim_tick")
 
     def set_stream_tail(self, extra_ticks):
         """Work-conserving launch tail of run_table / run_policy (shipsim_set_stream_tail): a wave whose envs met

@@ -299,9 +299,11 @@ int shipsim_step(shipsim_handle* h, const float* action, const uint8_t* active, 
                  float* obs_out, double* reward_out, uint8_t* done_out, uint32_t* events_out,
                  int32_t* ticks_out, uint8_t* ready_out);
 
-/* Raw ticks for the SINGLE and NONIW kinds (and debugging AST): advance every env by k ticks of
- * the reference loop body (run_simplified_model.py:248-249 / env._step). events_out (N uint32,
- * may be NULL) receives the OR of the per-tick env_info bits of the last tick. */
+/* Raw ticks for the SINGLE and NONIW kinds: advance every env by k ticks of the reference loop body
+ * (run_simplified_model.py:248-249; for NONIW MultiShipNonIWEnv._step, run_colav/env.py:613-676: both ships'
+ * steps with their SBMPC blocks in the reference's order, get_env_info's flags and the stop flags; simplified
+ * machinery only). events_out (N uint32, may be NULL) receives the env_info bits (SHIPSIM_EV_*) of the last tick
+ * (NONIW). The C1 loop runs while the test ship's F_TIME < simulation_time. */
 int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out);
 
 /* Read / write one state field for all envs (device pointer dst/src). Ship fields are laid out

@@ -1,0 +1,65 @@
+"""C1 on the device: MultiShipNonIWEnv._step (run_colav/env.py:613-676) in the run_simplified_model.py:245-249 loop,
+two ships on fixed routes, collav none / simple / sbmpc (shipsim_tick on a KIND_NONIW handle). Pinned to the
+reference's own run of the scenario (tests/golden/c1_noniw.npz, made by tests/golden/gen_golden.py from
+/root/reference): the env_info bits and both stop flags of every tick exactly, each ship's state after every tick
+against the reference's next simulation_results row while the ship runs, and the final states, within the
+north-star tolerance (tests/parity.py)."""
+import numpy as np
+import pytest
+import torch
+
+from ast_sac_amd import shipsim_abi as abi
+from ast_sac_amd.shipsim import ShipSim
+from parity import assert_close
+
+pytestmark = pytest.mark.gpu
+
+N_ENVS = 3  # identical envs: every lane pair must give the same bits
+
+
+@pytest.mark.parametrize("collav", ["none", "simple", "sbmpc"])
+def test_c1_noniw_vs_reference(golden, collav):
+    g = golden("c1_noniw")
+    ref_bits = g[f"{collav}_event_bits"]
+    ref_stops = g[f"{collav}_stops"][:, :2]
+    logs = (g[f"{collav}_test_log"], g[f"{collav}_obs_log"])
+    cfg = abi.c1_config(collav)
+    sim = ShipSim(cfg, N_ENVS)
+    sim.reset()  # init_step (run_colav/env.py:279-323)
+    ev = torch.zeros(N_ENVS, dtype=torch.int32, device=sim.device)
+    sim_time = float(cfg.simulation_time) if hasattr(cfg, "simulation_time") else None
+    # simulation_results row k holds the state at the start of the k-th stored tick (row 0: init_step), so the state
+    # after loop tick t is row t + 2 — while the ship runs (a frozen ship's rows repeat its last one)
+    cols = [0, 1, 2, 3, 5, 6, 7]  # time, north, east, yaw [deg], u, v, yaw rate [deg/s] (log_cols)
+    fields = (abi.F_TIME, abi.F_NORTH, abi.F_EAST, abi.F_YAW, abi.F_U, abi.F_V, abi.F_R)
+    for t in range(len(ref_bits)):
+        time_before = sim.get(abi.F_TIME).cpu().numpy().reshape(N_ENVS, 2)[:, 0]
+        assert sim_time is None or np.all(time_before < sim_time), f"tick {t}: the loop would have ended"
+        sim.tick(1, ev)
+        bits = ev.cpu().numpy().astype(np.uint32) & abi.EVENT_MASK
+        assert np.all(bits == ref_bits[t]), f"tick {t}: bits {bits} vs reference {ref_bits[t]}"
+        stops = sim.get(abi.F_STOP).cpu().numpy().reshape(N_ENVS, 2)
+        assert np.all(stops == ref_stops[t]), f"tick {t}: stops {stops} vs reference {ref_stops[t]}"
+        state = np.stack([sim.get(f).cpu().numpy().reshape(N_ENVS, 2) for f in fields], axis=-1)  # (N, 2, 7)
+        assert np.all(state == state[:1]), f"tick {t}: envs differ"
+        for ship in (0, 1):
+            if not ref_stops[t][ship] and t + 2 < len(logs[ship]):
+                got = state[0, ship].copy()
+                got[3] = np.rad2deg(got[3])
+                got[6] = np.rad2deg(got[6])
+                assert_close(got, logs[ship][t + 2, cols], what=f"c1 {collav} tick {t} ship {ship}")
+    if sim_time is not None:
+        assert np.all(sim.get(abi.F_TIME).cpu().numpy().reshape(N_ENVS, 2)[:, 0] >= sim_time)
+    names = (abi.F_TIME, abi.F_NORTH, abi.F_EAST, abi.F_YAW, abi.F_U, abi.F_V, abi.F_R)
+    fin = np.stack([sim.get(f).cpu().numpy().reshape(N_ENVS, 2)[0] for f in names], axis=-1)  # (2, 7)
+    assert_close(fin, g[f"{collav}_final"], what=f"c1 {collav} final")
+    sim.close()
+
+
+def test_c1_noniw_rejects_detailed_machinery():
+    cfg = abi.c1_config("none")
+    cfg.machinery = abi.MACH_DETAILED
+    sim = ShipSim(cfg, 2)
+    with pytest.raises(Exception):
+        sim.tick(1)
+    sim.close()
