@@ -56,11 +56,11 @@ def load_library(path=LIB_PATH):
     L.shipsim_nonfinite_count.restype = C.c_int32
     L.shipsim_set_trajectory.argtypes = [P, P, P, C.c_int32, P]
     L.shipsim_sbmpc_eval.argtypes = [C.c_int32, C.c_double, C.c_double, P, P, P]
-    L.shipsim_div_check.argtypes = [C.c_int32, P, P, P, P, P]
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
     L.shipsim_set_stream_tail.argtypes = [P, C.c_int32]
     try:
+        L.shipsim_div_check.argtypes = [C.c_int32, P, P, P, P, P]
         L.shipsim_diag_lane_faults.argtypes = [P]
         L.shipsim_run_policy.argtypes = [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, P, C.c_int32,
                                          C.c_int32, P, P, P, P, P, C.c_int32, P]
