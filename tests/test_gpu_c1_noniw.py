@@ -63,3 +63,27 @@ def test_c1_noniw_rejects_detailed_machinery():
     with pytest.raises(Exception):
         sim.tick(1)
     sim.close()
+
+
+@pytest.mark.parametrize("collav", [None, "sbmpc"])
+def test_c1_facade_loop_matches_reference(golden, collav):
+    """the facade's run_simplified_model loop (BatchedMultiShipNonIWEnv.run) and the one-env object API"""
+    from ast_sac_amd.run_colav.env import BatchedMultiShipNonIWEnv, MultiShipNonIWEnv
+    name = "none" if collav is None else collav
+    g = golden("c1_noniw")
+    env = BatchedMultiShipNonIWEnv(collav=collav, n_envs=2)
+    events, stops = env.run()
+    ev = events.cpu().numpy().astype(np.uint32) & abi.EVENT_MASK
+    assert ev.shape[0] == len(g[f"{name}_event_bits"])
+    for j in range(2):
+        np.testing.assert_array_equal(ev[:, j], g[f"{name}_event_bits"])
+        np.testing.assert_array_equal(stops[:, j].cpu().numpy(), g[f"{name}_stops"][:, :2])
+    one = MultiShipNonIWEnv(collav=collav)
+    one.init_step()
+    k = 0
+    while one.time < one.sim_time:
+        s, done, info = one._step()
+        assert s.dtype == np.float32 and s.shape == (6,)
+        assert info["events"] == abi.events_to_string(int(g[f"{name}_event_bits"][k]))
+        k += 1
+    assert k == len(g[f"{name}_event_bits"])
