@@ -2230,9 +2230,10 @@ __global__ __launch_bounds__(192) void single_tick_pipe_kernel(const Params P, D
   load_ship(S, q, s);
   // the kinematic rates of integrate's Euler step (differentials_body's expressions)
   auto advance_pose = [&](double u, double v, double r, double sy, double cy) __attribute__((always_inline)) {
-    const double dn = cy * u + (-sy) * v + 0 * r;
-    const double de = sy * u + cy * v + 0 * r;
-    const double dyaw = 0 * u + 0 * v + 1 * r;
+    // (the rotation's structural zero terms dropped: a ±0 addend leaves every non-zero rate's bits as they are)
+    const double dn = cy * u + (-sy) * v;
+    const double de = sy * u + cy * v;
+    const double dyaw = r;
     s.n = s.n + dn * dt;
     s.e = s.e + de * dt;
     s.yaw = s.yaw + dyaw * dt;
@@ -2280,7 +2281,7 @@ __global__ __launch_bounds__(192) void single_tick_pipe_kernel(const Params P, D
     for (int t = 0; t < k; ++t) {
       const int b = t & 1;
       const double r = x_uvr[b][2][lane];
-      s.yaw = s.yaw + (0 * x_uvr[b][0][lane] + 0 * x_uvr[b][1][lane] + 1 * r) * dt;
+      s.yaw = s.yaw + r * dt;  // (advance_pose's ψ rate)
       if (t + 1 < k) {
         sincos(s.yaw, &sy, &cy);
         x_sc[b ^ 1][0][lane] = sy; x_sc[b ^ 1][1][lane] = cy;
