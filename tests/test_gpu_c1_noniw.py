@@ -87,3 +87,43 @@ def test_c1_facade_loop_matches_reference(golden, collav):
         assert info["events"] == abi.events_to_string(int(g[f"{name}_event_bits"][k]))
         k += 1
     assert k == len(g[f"{name}_event_bits"])
+
+
+def _c1_device_run(cfg):
+    sim = ShipSim(cfg, 1)
+    sim.reset()
+    ev = torch.zeros(1, dtype=torch.int32, device=sim.device)
+    bits, stops = [], []
+    while float(sim.get(abi.F_TIME).cpu()[0]) < float(cfg.simulation_time):
+        sim.tick(1, ev)
+        bits.append(int(ev.cpu()[0]) & abi.EVENT_MASK)
+        stops.append(sim.get(abi.F_STOP).cpu().numpy().reshape(2).copy())
+        assert len(bits) < 5000
+    names = (abi.F_TIME, abi.F_NORTH, abi.F_EAST, abi.F_YAW, abi.F_U, abi.F_V, abi.F_R)
+    fin = np.stack([sim.get(f).cpu().numpy().reshape(2) for f in names], axis=-1)
+    sim.close()
+    return np.array(bits, np.uint32), np.array(stops, np.int32).reshape(-1, 2), fin
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_c1_noniw_vs_oracle_perturbed(case):
+    """C1 scenarios off the record (both ships' start moved / turned, every collav mode) against the CPU oracle
+    (oracle/shipsim_oracle.c, itself pinned to the reference's run above): event bits and stop flags of every tick
+    exactly, the final states within the north-star tolerance"""
+    import oracle_ffi as O
+    rng = np.random.default_rng(100 + case)
+    cfg = abi.c1_config(("none", "simple", "sbmpc")[case % 3])
+    t, o = cfg.ship[0], cfg.ship[1]
+    t.initial_north_position_m += float(rng.uniform(-300, 300))
+    t.initial_east_position_m += float(rng.uniform(-300, 300))
+    t.initial_yaw_angle_rad += float(rng.uniform(-0.2, 0.2))
+    o.initial_north_position_m += float(rng.uniform(-500, 500))
+    o.initial_east_position_m += float(rng.uniform(-500, 500))
+    bits, stops, fin = _c1_device_run(cfg)
+    env = O.OracleEnv(cfg, log_cap=0)
+    ref_bits, ref_stops = env.run_c1()
+    assert len(bits) == len(ref_bits)
+    np.testing.assert_array_equal(bits, ref_bits.astype(np.uint32) & abi.EVENT_MASK)
+    np.testing.assert_array_equal(stops, ref_stops)
+    ref_fin = np.array([env.ship_state(s)[[7, 0, 1, 2, 3, 4, 5]] for s in (0, 1)])
+    assert_close(fin, ref_fin, what=f"c1 perturbed case {case} final")
