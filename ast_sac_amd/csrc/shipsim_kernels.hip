@@ -714,7 +714,14 @@ __device__ __forceinline__ void scenario_argmin(double& cost, int& idx, int lane
   take(dpp_d<kDppQuadXor2>(cost), dpp_i<kDppQuadXor2>(idx));
   take(dpp_d<kDppRowRor4>(cost), dpp_i<kDppRowRor4>(idx));
   take(dpp_d<kDppRowRor8>(cost), dpp_i<kDppRowRor8>(idx));
-  take(shfl_d(cost, lane ^ 16), __shfl(idx, lane ^ 16, 64));
+  // the other row of the half-wave (lane ^ 16) by v_permlane16_swap: after the swap of a value with itself the even
+  // rows hold their partner row's value in the second result, the odd rows in the first
+  const bool odd_row = (lane >> 4) & 1;
+  const auto sl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(cost), (unsigned)__double2loint(cost), false, false);
+  const auto sh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(cost), (unsigned)__double2hiint(cost), false, false);
+  const auto si = __builtin_amdgcn_permlane16_swap((unsigned)idx, (unsigned)idx, false, false);
+  const double oc = __hiloint2double((int)(odd_row ? sh[0] : sh[1]), (int)(odd_row ? sl[0] : sl[1]));
+  take(oc, (int)(odd_row ? si[0] : si[1]));
 }
 
 // Must be called by every lane of the wave (wave-uniform control flow). `need` marks lanes that
