@@ -667,13 +667,23 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
     }
   }
   if (part >= 0) {  // the two parts' running bests in sample order: part 0's samples come first
-    const int pl = (threadIdx.x & 63) ^ 32;
+    // the partner lane (lane ^ 32) by v_permlane32_swap: after the swap of a value with itself the lower half holds
+    // the upper half's value in the second result, the upper half the lower half's in the first
+    const bool upper = part == 1;
+    auto other_u = [&](unsigned x) __attribute__((always_inline)) {
+      const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+      return upper ? r[0] : r[1];
+    };
+    auto other_d = [&](double x) __attribute__((always_inline)) {
+      const unsigned lo = other_u((unsigned)__double2loint(x)), hi = other_u((unsigned)__double2hiint(x));
+      return __hiloint2double((int)hi, (int)lo);
+    };
     HzBest o;
-    o.s1 = shfl_d(hb.s1, pl);
-    o.s2 = shfl_d(hb.s2, pl);
-    o.t1 = shfl_d(hb.t1, pl);
-    o.q1 = shfl_d(hb.q1, pl);
-    o.unc = __shfl((int)hb.unc, pl, 64) != 0;
+    o.s1 = other_d(hb.s1);
+    o.s2 = other_d(hb.s2);
+    o.t1 = other_d(hb.t1);
+    o.q1 = other_d(hb.q1);
+    o.unc = other_u((unsigned)hb.unc) != 0u;
     const HzBest A = part == 0 ? hb : o, Bp = part == 0 ? o : hb;
     const bool bwin = Bp.s1 < A.s1;  // (ties keep the earlier sample)
     hb.s1 = fmin(A.s1, Bp.s1);
