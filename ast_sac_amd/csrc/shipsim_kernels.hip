@@ -716,6 +716,9 @@ __device__ double sbmpc_scenario_cost(const SbIn& in, int n_samp, double DT, int
 // gives the same result: inside each 16-lane row by DPP (quad xor 1, quad xor 2, row_ror 4, row_ror 8: every lane
 // then holds its row's minimum), then one LDS permute across the half-wave's two rows. Every lane of the wave
 // must be active (the cooperative passes are called wave-uniformly).
+// SHFL: the cross-row step by an LDS permute instead (the multi-obstacle and C1 kernels: the swap's lane-mask select
+// costs them SGPRs they do not have; the same result)
+template <bool SHFL = false>
 __device__ __forceinline__ void scenario_argmin(double& cost, int& idx, int lane) {
   auto take = [&](double oc, int oi) __attribute__((always_inline)) {
     if (oc < cost || (oc == cost && oi < idx)) { cost = oc; idx = oi; }
@@ -726,6 +729,10 @@ __device__ __forceinline__ void scenario_argmin(double& cost, int& idx, int lane
   take(dpp_d<kDppRowRor8>(cost), dpp_i<kDppRowRor8>(idx));
   // the other row of the half-wave (lane ^ 16) by v_permlane16_swap: after the swap of a value with itself the even
   // rows hold their partner row's value in the second result, the odd rows in the first
+  if constexpr (SHFL) {
+    take(shfl_d(cost, lane ^ 16), __shfl(idx, lane ^ 16, 64));
+    return;
+  }
   const bool odd_row = (lane >> 4) & 1;
   const auto sl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(cost), (unsigned)__double2loint(cost), false, false);
   const auto sh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(cost), (unsigned)__double2hiint(cost), false, false);
@@ -738,7 +745,7 @@ __device__ __forceinline__ void scenario_argmin(double& cost, int& idx, int lane
 // request an optimisation with inputs `in`; they receive (P_best, Chi_best). SHIP_UNIFORM: u_d, obs_l and
 // obs_w are the same for every request and set in every lane's `in` (the AST kernels: the ships'
 // configured desired speed and obstacle size), so they are not gathered from the requesting lane.
-template <bool SHIP_UNIFORM = false>
+template <bool SHIP_UNIFORM = false, bool SHFL_ARGMIN = false>
 __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double DT, double& p_best,
                                   double& chi_best) {
   SHIPSIM_LANE_CHECK(64, 4);
@@ -777,7 +784,7 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
     }
     // argmin over the half-wave; ties -> lowest scenario index (first strict improvement in the
     // reference's i-major / j-minor loop)
-    scenario_argmin(cost, idx, lane);
+    scenario_argmin<SHFL_ARGMIN>(cost, idx, lane);
     const int best0 = __builtin_amdgcn_readlane(idx, 0);
     const int best1 = __builtin_amdgcn_readlane(idx, 32);
     if (lane == src0) {
@@ -854,7 +861,7 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
       cost = worst;
       idx = scen;
     }
-    scenario_argmin(cost, idx, lane);
+    scenario_argmin<true>(cost, idx, lane);
     const int best0 = __builtin_amdgcn_readlane(idx, 0);
     const int best1 = __builtin_amdgcn_readlane(idx, 32);
     if (lane == src0) {
@@ -2577,7 +2584,7 @@ __global__ __launch_bounds__(64) void noniw_tick_kernel(const Params P, DevState
             sb_set_heading_trig(in);
             in.p_last = p_last; in.chi_last = chi_last;
           }
-          sbmpc_cooperative<true>(need, in, n_samp, P.sbmpc_dt, pb, cb);
+          sbmpc_cooperative<true, true>(need, in, n_samp, P.sbmpc_dt, pb, cb);
         }
         if (act) {
           if (need) { p_last = pb; chi_last = cb; sf = pb; off = cb; }
