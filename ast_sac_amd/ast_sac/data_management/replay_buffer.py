@@ -16,7 +16,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from ...spaces import get_dim
+from ..env_wrapper.env_utils import get_dim
 
 
 class ReplayBuffer(metaclass=abc.ABCMeta):

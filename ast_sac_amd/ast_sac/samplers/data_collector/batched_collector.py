@@ -423,6 +423,16 @@ class BatchedPathCollector:
                 got += int(n.item())                      # transitions (non-finite decisions left out)
                 self._n_awaiting = int(self._n_ready.item())  # envs that wait for an action
         else:
+            room0 = _staging_room(replay_buffer)
+            if room0 is not None and room0 < num_steps + 2 * self._rows_per_pass():
+                # checked once, before any pass: every rank of a replicated group has the same room (each sync
+                # empties the stage), the same num_steps and the same pass size, so all of them fail here together
+                # instead of one rank failing mid-collect while the others wait in the next sync's all-gather
+                raise RuntimeError(
+                    f"BatchedPathCollector: the replay buffer's staging ring has room for {room0} rows; a collect of "
+                    f"{num_steps} decisions needs {num_steps + 2 * self._rows_per_pass()} (plus two passes of "
+                    f"{self._rows_per_pass()} rows): sync() it after every collect or enlarge its stage_size "
+                    f"(ast_sac_runner.replicated_stage_rows)")
             start = int(self._steps_total.item())
             got, passes, batch = 0, 0, 1
             while got < num_steps:

@@ -210,6 +210,37 @@ __device__ inline void block_sum(float (&v)[N], float (*red)[32], float* out) {
   __syncthreads();
 }
 
+// Publication stores. Every value one launch of the step writes for a later launch (activations, parts, the row
+// record, the step counter, the updated parameters, optimizer state and transposed copies) is stored write-through
+// (`sc1`): the line leaves the XCD's L2 as it is written instead of waiting, dirty, for the end-of-kernel release,
+// which otherwise writes back every dirty byte before the next launch may start (MI355X_MICROARCH.md "boundary":
+// + B ÷ 6 TB/s for B dirty bytes; "publish-large": write-through wins for tens of KB per workgroup). The readers
+// are other launches, so no store here is read back through the writer's L2. SACF_WT selects which stores publish
+// write-through (a bit mask, for A/Bs): 1 the row inputs, parts, records and first-layer slices P1 / P2 hand on;
+// 4 the split-K epilogues' activation and factor matrices (one word per lane and output); 2 what P3 (and the apply
+// kernel) writes: gradients, Adam state, parameters, targets and the transposed copies. 0: plain stores.
+#ifndef SACF_WT
+#define SACF_WT 7
+#endif
+enum { WT_ACT = 1, WT_OPT = 2, WT_EPI = 4 };
+template <int KIND, class T>
+__device__ __forceinline__ void pub(T* p, T v) {
+  if constexpr ((SACF_WT & KIND) != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // … sc1
+  else *p = v;
+}
+template <int KIND>
+__device__ __forceinline__ void pub4(float* p, float x, float y, float z, float w) {
+  if constexpr ((SACF_WT & KIND) != 0) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const f32x4 v = {x, y, z, w};
+    // (the compiler's hazard recognizer does not see an asm store: a store of more than 8 bytes needs a wait state
+    // before a VALU instruction may overwrite its data registers, hence the s_nop)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(x, y, z, w);
+  }
+}
+
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.0f); }
 __device__ __forceinline__ float softplus(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
@@ -427,9 +458,9 @@ __device__ __forceinline__ void first_layer_pre(const float* lw1t, const float* 
 template <int H, int CS>
 __device__ __forceinline__ void store_slice(float* base, int r0, int by, const float (&av)[CS], int k0) {
   if (k0 / kTile2 != by) return;
-  float4* d = reinterpret_cast<float4*>(base + (int64_t)(r0 + (threadIdx.x & 31)) * H + k0);
+  float* d = base + (int64_t)(r0 + (threadIdx.x & 31)) * H + k0;
 #pragma unroll
-  for (int q = 0; q < CS / 4; ++q) d[q] = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+  for (int q = 0; q < CS / 4; ++q) pub4<WT_ACT>(d + 4 * q, av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
 }
 
 // a batch row's O inputs, zero past O, branch-free: a clamped index and a compare against O held in a VGPR, so
@@ -585,16 +616,18 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   if (by == 0 && w == 0 && h == 0) {  // the gathered batch for the later passes
     float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
 #pragma unroll
-    for (int m = 0; m < kXLd; ++m) xd[m] = x[m];
+    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     if (!nrow) {
       float v[5];
       batch_aux(a, item, idx, e0, e1, v);
       float* rc = a.s.rec + (int64_t)item * kRec;
-      rc[R_ACT] = v[AUX_ACT];
-      rc[R_REW] = v[AUX_REW];
-      rc[R_TERM] = v[AUX_TERM];
-      rc[R_EPS] = v[AUX_E0];
-      rc[R_EPSN] = v[AUX_E1];
+      // (R_EPS .. R_ACT are record words 6 .. 10: two words and one 16-byte store of words 8 .. 11, whose last word,
+      // R_LOGPN, P2 writes later in the step)
+      static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11,
+                    "record layout");
+      pub<WT_ACT>(rc + R_EPS, v[AUX_E0]);
+      pub<WT_ACT>(rc + R_EPSN, v[AUX_E1]);
+      pub4<WT_ACT>(rc + R_REW, v[AUX_REW], v[AUX_TERM], v[AUX_ACT], 0.0f);
     }
   }
   (void)B;
@@ -614,11 +647,11 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
-    if (r < Bp) a.s.h2[(int64_t)r * H + col] = y;
+    if (r < Bp) pub<WT_EPI>(a.s.h2 + (int64_t)r * H + col, y);
     const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
     if (cc == 0) {
-      a.s.hpart[(int64_t)r * 2 * CB + by] = pm;
-      a.s.hpart[(int64_t)r * 2 * CB + CB + by] = ps;
+      pub<WT_ACT>(a.s.hpart + (int64_t)r * 2 * CB + by, pm);
+      pub<WT_ACT>(a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
     }
   });
 }
@@ -654,9 +687,14 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
     lx[rl * (kXLd + 1) + O] = act;
-    if (net == 0 && by == 0)
+    if (net == 0 && by == 0) {
+      float q[kXLd];
 #pragma unroll
-      for (int m = 0; m < kXLd; ++m) a.s.qx[(int64_t)item * kXLd + m] = m == O ? act : xin[m];
+      for (int m = 0; m < kXLd; ++m) q[m] = m == O ? act : xin[m];
+      float* qd = a.s.qx + (int64_t)item * kXLd;
+#pragma unroll
+      for (int k = 0; k < kXLd / 4; ++k) pub4<WT_ACT>(qd + 4 * k, q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+    }
   }
   __syncthreads();
   SAC_STAMP(0, 1);
@@ -672,14 +710,14 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
     mfma_n<CS>(acc, av, bv);
   }
   if (rt == 0 && by == 0)  // fc0's action column, contiguous, for P2
-    for (int k = threadIdx.x; k < H; k += kThreads) a.s.w1a[net * H + k] = lw1[O * H + k];
+    for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(a.s.w1a + net * H + k, lw1[O * H + k]);
   SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
-    a.s.g2[net][(int64_t)r * H + col] = y;
+    pub<WT_EPI>(a.s.g2[net] + (int64_t)r * H + col, y);
     const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
-    if (cc == 0) a.s.part[((int64_t)r * PS_N + PS_Q1D + net) * CB + by] = pq;
+    if (cc == 0) pub<WT_ACT>(a.s.part + ((int64_t)r * PS_N + PS_Q1D + net) * CB + by, pq);
   });
 }
 
@@ -713,8 +751,8 @@ __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int 
   for (int m = 0; m < kXLd; ++m)  // (unrolled, the run-time bound a select)
 #pragma unroll
     for (int j = 0; j < 4; ++j) pre[j] = m < O ? fmaf(w1[(cq + j) * (kXLd + 1) + m], x[m], pre[j]) : pre[j];
-  *reinterpret_cast<float4*>(a.s.pre[2 + net] + (int64_t)item * H + c0 + cq) = make_float4(pre[0], pre[1], pre[2], pre[3]);
-  if (rt == 0 && tid < kTile2) a.s.w1a[(2 + net) * H + c0 + tid] = w1[tid * (kXLd + 1) + O];
+  pub4<WT_ACT>(a.s.pre[2 + net] + (int64_t)item * H + c0 + cq, pre[0], pre[1], pre[2], pre[3]);
+  if (rt == 0 && tid < kTile2) pub<WT_ACT>(a.s.w1a + (2 + net) * H + c0 + tid, w1[tid * (kXLd + 1) + O]);
 }
 
 template <int H>
@@ -785,10 +823,10 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   if (w == 0 && h == 0 && net == 0 && by == 0) {
     float* rc = a.s.rec + (int64_t)item * kRec;
     if (kTarget) {
-      rc[R_LOGPN] = hd[HD_LOGP];
+      pub<WT_ACT>(rc + R_LOGPN, hd[HD_LOGP]);
     } else {
 #pragma unroll
-      for (int q = 0; q < 6; ++q) rc[q] = hd[q];
+      for (int q = 0; q < 6; ++q) pub<WT_ACT>(rc + q, hd[q]);
     }
   }
   (void)O;
@@ -818,7 +856,7 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   if constexpr (kTarget) {
     splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
       const float pq = halfwave_sum(relu(v + b2c) * w3);
-      if (cc == 0) a.s.part[((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by] = pq;
+      if (cc == 0) pub<WT_ACT>(a.s.part + ((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by, pq);
     });
   } else {  // Q and its tangent reduced behind one barrier
     splitk_finish2(acc, act, lds, lds + FwdLds<H>::kSplit, [&](int, int rr, int cc, float v, float t) {
@@ -827,8 +865,8 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
       const float pd = halfwave_sum(y > 0.0f ? w3 * t : 0.0f);  // this column block's part of ∂Q/∂ã
       if (cc == 0) {
         float* pr = a.s.part + (int64_t)(r0 + rr) * PS_N * CB + by;
-        pr[(PS_Q1A + net) * CB] = pq;
-        pr[(PS_D1 + net) * CB] = pd;
+        pub<WT_ACT>(pr + (PS_Q1A + net) * CB, pq);
+        pub<WT_ACT>(pr + (PS_D1 + net) * CB, pd);
       }
     });
   }
@@ -887,12 +925,12 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   if constexpr (kActor) {  // U_m and U_s behind one barrier
     splitk_finish2(acc, acc2, lds, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v, float v2) {
       const int64_t o = (int64_t)(r0 + rr) * H + j0 + cc;
-      o1[o] = m1[q] > 0.0f ? v : 0.0f;
-      a.s.us[o] = m1[q] > 0.0f ? v2 : 0.0f;
+      pub<WT_EPI>(o1 + o, m1[q] > 0.0f ? v : 0.0f);
+      pub<WT_EPI>(a.s.us + o, m1[q] > 0.0f ? v2 : 0.0f);
     });
   } else {
     splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
-      o1[(int64_t)(r0 + rr) * H + j0 + cc] = m1[q] > 0.0f ? v : 0.0f;
+      pub<WT_EPI>(o1 + (int64_t)(r0 + rr) * H + j0 + cc, m1[q] > 0.0f ? v : 0.0f);
     });
   }
 }
@@ -904,11 +942,11 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
       const int64_t t = *a.step + 1;
-      *a.step = t;
+      pub<WT_ACT>(a.step, t);
       const AdamStep st = adam_step(a.hp, t);
-      a.stats[5] = st.step_pi;
-      a.stats[6] = st.step_q;
-      a.stats[7] = st.bc2_sqrt;
+      pub<WT_ACT>(a.stats + 5, st.step_pi);
+      pub<WT_ACT>(a.stats + 6, st.step_q);
+      pub<WT_ACT>(a.stats + 7, st.bc2_sqrt);
     }
     // the parameters P3 reads (it updates them in place), before this step's update
     const Layout& L = a.L;
@@ -916,13 +954,13 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
     float* sn = a.s.snap;
     if (threadIdx.x < 5) {
       const int i = threadIdx.x;
-      sn[i] = i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3];
+      pub<WT_ACT>(sn + i, i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3]);
     }
     for (int j = threadIdx.x; j < L.H; j += kThreads) {
-      sn[SN_HEAD + j] = P[L.p_wm + j];
-      sn[SN_HEAD + L.H + j] = P[L.p_ws + j];
-      sn[SN_HEAD + 2 * L.H + j] = P[L.q_base[0] + L.c_w3 + j];
-      sn[SN_HEAD + 3 * L.H + j] = P[L.q_base[1] + L.c_w3 + j];
+      pub<WT_ACT>(sn + SN_HEAD + j, P[L.p_wm + j]);
+      pub<WT_ACT>(sn + SN_HEAD + L.H + j, P[L.p_ws + j]);
+      pub<WT_ACT>(sn + SN_HEAD + 2 * L.H + j, P[L.q_base[0] + L.c_w3 + j]);
+      pub<WT_ACT>(sn + SN_HEAD + 3 * L.H + j, P[L.q_base[1] + L.c_w3 + j]);
     }
   }
   int bx, by;
@@ -1050,13 +1088,13 @@ __device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, 
   const float v = x.v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);   // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
   const float denom = sqrtf(v) / st.bc2_sqrt + a.hp.eps;
   const float p = x.p + (-(q ? st.step_q : st.step_pi)) * (m / denom);
-  a.m[e] = m;
-  a.v[e] = v;
-  a.params[e] = p;
+  pub<WT_OPT>(a.m + e, m);
+  pub<WT_OPT>(a.v + e, v);
+  pub<WT_OPT>(a.params + e, p);
   x.p = p;
   if (q) {
     x.t = x.t * (1.0f - a.hp.tau) + p * a.hp.tau;
-    a.targets[e - a.L.q_base[0]] = x.t;
+    pub<WT_OPT>(a.targets + (e - a.L.q_base[0]), x.t);
   }
 }
 
@@ -1222,7 +1260,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   const int64_t out_off = a.w2_off[mat];
   splitk_finish(acc, S.u.mm.split, [&](int q, int rr, int cc, float v) {
     const int64_t e = out_off + (int64_t)(j0 + rr) * H + k0 + cc;
-    a.grads[e] = v;
+    pub<WT_OPT>(a.grads + e, v);
     if (a.fuse) {
       xe[q].g = v;
       adam_st(a.ap, sst, e, xe[q], mat > 0);
@@ -1236,8 +1274,8 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     const int tc = tid % kTile2, tr = tid / kTile2;
     for (int cc = tr; cc < kTile2; cc += kThreads / kTile2) {
       const int64_t o = (int64_t)(k0 + cc) * H + j0 + tc;
-      a.ap.T[(size_t)mat * HH + o] = tt[0][cc][tc];
-      if (mat > 0) a.ap.T[(size_t)(2 + mat) * HH + o] = tt[1][cc][tc];
+      pub<WT_OPT>(a.ap.T + (size_t)mat * HH + o, tt[0][cc][tc]);
+      if (mat > 0) pub<WT_OPT>(a.ap.T + (size_t)(2 + mat) * HH + o, tt[1][cc][tc]);
     }
   }
   }
@@ -1365,7 +1403,7 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
 #pragma unroll
     for (int st = 1; st < kValuStreams; ++st) g += vr[st][i][u];
     const int64_t e = el_off(k);
-    a.grads[e] = g;
+    pub<WT_OPT>(a.grads + e, g);
     if (a.fuse) {
       xe[q].g = g;
       adam_st(a.ap, sst, e, xe[q], !actor);
@@ -1431,7 +1469,7 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   }
   if (tid >= 5) return;
   const float g = tid == 0 ? (m.hp.auto_ent ? sum[4] * invB : 0.0f) : sum[4 + tid];
-  a.grads[off] = g;
+  pub<WT_OPT>(a.grads + off, g);
   if (a.fuse && (tid > 0 || m.hp.auto_ent)) {
     xs.g = g;
     adam_st(a.ap, sst, off, xs, tid >= 3);
@@ -1450,16 +1488,16 @@ __device__ __forceinline__ void p3_stage_block(const WArgs& a, int sb) {
   load_obs_row(m.obs, idx, m.L.O, x);
   load_obs_row(m.nobs, idx, m.L.O, xn);
   const float act = m.act[idx], rew = m.rew[idx], term = m.term[idx];
-  float4* dx = reinterpret_cast<float4*>(m.s.sx + (int64_t)item * kXLd);
-  float4* dn = reinterpret_cast<float4*>(m.s.sxn + (int64_t)item * kXLd);
+  float* dx = m.s.sx + (int64_t)item * kXLd;
+  float* dn = m.s.sxn + (int64_t)item * kXLd;
 #pragma unroll
   for (int q = 0; q < kXLd / 4; ++q) {
-    dx[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-    dn[q] = make_float4(xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
+    pub4<WT_ACT>(dx + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    pub4<WT_ACT>(dn + 4 * q, xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
   }
   float* q = m.s.saux + (int64_t)item * kAux;
-  *reinterpret_cast<float4*>(q) = make_float4(act, rew, term, e0);
-  q[AUX_E1] = e1;
+  pub4<WT_ACT>(q, act, rew, term, e0);
+  pub<WT_ACT>(q + AUX_E1, e1);
 }
 
 // the kernel's WArgs read through the kernarg segment pointer, laundered: a field is a scalar load where a block
@@ -1514,10 +1552,10 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
     for (int cc = tr; cc < kTile2; cc += kThreads / kTile2) {
       const int64_t o = (int64_t)(c0 + cc) * H + r0 + tc;  // T[col][row]
       if (mat == 0) {
-        a.T[o] = tile[0][cc][tc];
+        pub<WT_OPT>(a.T + o, tile[0][cc][tc]);
       } else {
-        a.T[(size_t)mat * HH + o] = tile[0][cc][tc];
-        a.T[(size_t)(2 + mat) * HH + o] = tile[1][cc][tc];
+        pub<WT_OPT>(a.T + (size_t)mat * HH + o, tile[0][cc][tc]);
+        pub<WT_OPT>(a.T + (size_t)(2 + mat) * HH + o, tile[1][cc][tc]);
       }
     }
     return;
@@ -2028,6 +2066,9 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
 int sacf_grads_chain(sacf_handle* h, const float* eps, int32_t flags) {
   if (!h) return SACF_EINVAL;
   if (flags & ~(SACF_CHAIN_STAGE_NEXT | SACF_CHAIN_FROM_STAGED)) return sfail(h, SACF_EINVAL, "sacf_grads_chain: flags");
+  // a staged batch carries the normals of the call that staged it, so a chained step cannot take the caller's eps
+  if (flags && eps)
+    return sfail(h, SACF_EINVAL, "sacf_grads_chain: STAGE_NEXT / FROM_STAGED need eps == NULL (in-kernel normals)");
   if (!h->r_obs) return sfail(h, SACF_ESTATE, "sacf_grads_chain: no replay bound");
   if ((flags & SACF_CHAIN_FROM_STAGED) && !h->staged)
     return sfail(h, SACF_ESTATE, "sacf_grads_chain: FROM_STAGED without a staging step before it");

@@ -799,10 +799,14 @@ __device__ void sbmpc_cooperative(bool need, const SbIn& in, int n_samp, double 
 }
 
 // SBMPC over a do_list of NOB obstacles (sbmpc.py:150-183; env.py:366-370 passes every obstacle ship):
-// per scenario the worst obstacle's cost (cost_i = -1, then every strictly larger cost_k), the scenario
-// with the least worst cost wins (lowest index on ties). Same wave-cooperative layout as
-// sbmpc_cooperative; slots of an env that duplicate its last ship repeat an obstacle, which changes
-// neither the max nor the D_INIT test, and are not evaluated.
+// per scenario the worst obstacle's cost (cost_i = -1, then every strictly larger cost_k: the max of the costs),
+// the scenario with the least worst cost wins (lowest index on ties). Slots of an env that duplicate its last
+// ship repeat an obstacle, which changes neither the max nor the D_INIT test, and are not evaluated.
+// Lanes: scenario = lane & 31 (28 used). With two or more requests pending a pass serves two, one per half-wave,
+// each lane taking its scenario's obstacles in turn; with one request both halves serve it and split its
+// obstacles — half h takes obstacles h, h + 2, … — and the two halves' worst costs are merged (lane ^ 32) before
+// the argmin, so a lone request costs ⌈K / 2⌉ scenario evaluations per lane instead of K (the max over the same
+// set of costs: the same value in either order).
 template <int NOB>
 struct SbMulti {
   double u_d, chi_d, os_x, os_y, os_v, p_last, chi_last;
@@ -827,8 +831,9 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
       src1 = __ffsll((unsigned long long)req) - 1;
       req &= req - 1;
     }
+    const bool split = src1 < 0;  // (uniform) one request this pass: the halves split its obstacles
     int src = half ? src1 : src0;
-    int srcc = src < 0 ? src0 : src;
+    const int srcc = src < 0 ? src0 : src;
     SbIn g;
     g.u_d = shfl_d(in.u_d, srcc); g.chi_d = shfl_d(in.chi_d, srcc);
     g.os_x = shfl_d(in.os_x, srcc); g.os_y = shfl_d(in.os_y, srcc); g.os_v = shfl_d(in.os_v, srcc);
@@ -837,27 +842,44 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
     int idx = 64;
     double worst = -1.0;
     bool any_far = false;
-    const bool act = src >= 0 && scen < 28;
+    const bool act = (split || src >= 0) && scen < 28;
+    // obstacles in pairs (2j, 2j + 1): split, half h takes obstacle 2j + h; otherwise each lane both, in order
 #pragma unroll
-    for (int k = 0; k < NOB; ++k) {
-      if (k >= n_obs_p) break;  // (wave-uniform) slots past the env's K obstacles duplicate the last one
-      g.ob_x = shfl_d(in.ob_x[k], srcc); g.ob_y = shfl_d(in.ob_y[k], srcc); g.ob_psi = shfl_d(in.ob_psi[k], srcc);
-      g.ob_u = shfl_d(in.ob_u[k], srcc); g.ob_v = shfl_d(in.ob_v[k], srcc);
-      g.obs_l = shfl_d(in.obs_l[k], srcc); g.obs_w = shfl_d(in.obs_w[k], srcc);
-      // an obstacle out of reach costs exactly sbmpc_h2 in every scenario (added once below)
-      const bool far = act && sbmpc_far(g, n_samp_p, DT);
-      any_far = any_far || far;
-      if (act && !far) {
-        sb_set_heading_trig(g);
-        const double ck = sbmpc_scenario_cost(g, opaque_s(n_samp_p), DT, scen >> 2, scen & 3);
-        if (ck > worst) worst = ck;
+    for (int j = 0; j < (NOB + 1) / 2; ++j) {
+      const int ka = 2 * j, kb = 2 * j + 1 < NOB ? 2 * j + 1 : 2 * j;
+      if (ka >= n_obs_p) break;  // (wave-uniform) slots past the env's K obstacles duplicate the last one
+      const bool b_ok = 2 * j + 1 < NOB && 2 * j + 1 < n_obs_p;
+      for (int t = 0; t < (split ? 1 : 2); ++t) {  // (uniform trip count)
+        const bool use_b = split ? half == 1 : t == 1;
+        // this lane's obstacle, field by field (both candidates gathered, one kept: short live ranges)
+        auto pick = [&](const double (&f)[NOB]) __attribute__((always_inline)) {
+          const double a = shfl_d(f[ka], srcc);
+          const double b = shfl_d(f[kb], srcc);
+          return use_b ? b : a;
+        };
+        SbIn q = g;
+        q.ob_x = pick(in.ob_x); q.ob_y = pick(in.ob_y); q.ob_psi = pick(in.ob_psi);
+        q.ob_u = pick(in.ob_u); q.ob_v = pick(in.ob_v); q.obs_l = pick(in.obs_l); q.obs_w = pick(in.obs_w);
+        const bool ok = act && (use_b ? b_ok : true);
+        // an obstacle out of reach costs exactly sbmpc_h2 in every scenario (added once below)
+        const bool far = ok && sbmpc_far(q, n_samp_p, DT);
+        any_far = any_far || far;
+        if (ok && !far) {
+          sb_set_heading_trig(q);
+          const double ck = sbmpc_scenario_cost(q, opaque_s(n_samp_p), DT, scen >> 2, scen & 3);
+          if (ck > worst) worst = ck;
+        }
       }
     }
+    if (act && any_far) {
+      const double h2 = sbmpc_h2(g, scen >> 2, scen & 3);
+      if (h2 > worst) worst = h2;
+    }
+    if (split) {  // (uniform) the other half's worst over its obstacles (lane ^ 32)
+      const double ow = shfl_d(worst, lane ^ 32);
+      if (ow > worst) worst = ow;
+    }
     if (act) {
-      if (any_far) {
-        const double h2 = sbmpc_h2(g, scen >> 2, scen & 3);
-        if (h2 > worst) worst = h2;
-      }
       cost = worst;
       idx = scen;
     }
@@ -1745,7 +1767,7 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
     double los_pre_q = 0.0, los_pre_e = 0.0;
     bool sb_active = false;
     if (COLLAV == SHIPSIM_COLLAV_SBMPC && SLOTS > 2) {  // do_list of every obstacle ship (env.py:366-370)
-      constexpr int NOB = SLOTS - 1;
+      constexpr int NOB = SLOTS - 1 < SHIPSIM_MAX_OBS ? SLOTS - 1 : SHIPSIM_MAX_OBS;  // (slots past K duplicate a ship)
       SbMulti<NOB> in;
       double obn[NOB], obe[NOB];
 #pragma unroll
@@ -2527,9 +2549,28 @@ __global__ __launch_bounds__(64) void legacy_step_kernel(LegacyArgs a_arg) {
 // its clock twice instead; then get_env_info (:53-225, the flags of reward_function.py without the rewards) on the
 // post-tick states and the stop flags (:658-664). The env's SBMPC memory (P_ca_last, Chi_ca_last) is one object that
 // both ships' blocks update in turn. Event bits of the last tick to events_out.
+// (its arguments as one struct read through the laundered kernarg pointer, as ast_step_kernel's StepArgs: a field is
+// a scalar load where it is used, not ~100 dwords held in SGPRs across the tick loop, which spilled)
+struct NoniwArgs {
+  Params P;
+  DevState S;
+  ConstBuf K;
+  int k;
+  uint32_t* events_out;
+};
+typedef const __attribute__((address_space(4))) NoniwArgs* NoniwArgsPtr;
+__device__ __forceinline__ const NoniwArgs& noniw_args() {
+  NoniwArgsPtr q = (NoniwArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return *(const NoniwArgs*)q;
+}
 template <int COLLAV>
-__global__ __launch_bounds__(64) void noniw_tick_kernel(const Params P, DevState S, ConstBuf K, int k,
-                                                        uint32_t* events_out) {
+__global__ __launch_bounds__(64) void noniw_tick_kernel(NoniwArgs A_arg) {
+  (void)A_arg;  // read through noniw_args()
+#define P (noniw_args().P)
+#define S (noniw_args().S)
+#define K (noniw_args().K)
+  const int k = noniw_args().k;
   __shared__ ShipConst lds_sc[SHIPSIM_MAX_SHIPS];
   __shared__ Edge lds_edges_raw[SHIPSIM_MAX_VERTS];
   __shared__ PolyBox lds_boxes[SHIPSIM_MAX_POLYS];
@@ -2651,8 +2692,12 @@ __global__ __launch_bounds__(64) void noniw_tick_kernel(const Params P, DevState
   if (is_test) {
     S.p_last()[env] = p_last; S.chi_last()[env] = chi_last;
     for (int i = 0; i < 4; ++i) S.states4()[env * 4 + i] = st[i];
+    uint32_t* events_out = noniw_args().events_out;
     if (events_out && k > 0) events_out[env] = bits;
   }
+#undef P
+#undef S
+#undef K
 }
 
 // SBMPC.get_optimal_ctrl_offset (sbmpc.py:113-185) for a batch of independent single-obstacle
@@ -2672,6 +2717,36 @@ __global__ __launch_bounds__(64) void sbmpc_eval_kernel(int n, double tf, double
   const bool active = valid && sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_ (sbmpc.py:154-159)
   double pb = 1.0, cb = 0.0;
   sbmpc_cooperative(active, q, (int)(tf / dt), dt, pb, cb);
+  if (valid) {
+    out[(size_t)i * 3 + 0] = active ? pb : 1.0;
+    out[(size_t)i * 3 + 1] = active ? cb : 0.0;
+    out[(size_t)i * 3 + 2] = active ? 1.0 : 0.0;
+  }
+}
+
+// SBMPC.get_optimal_ctrl_offset over a do_list of n_obs obstacles (sbmpc.py:113-185) for n independent requests
+// (shipsim_sbmpc_eval_multi): one request per lane, the optimisations served wave-cooperatively by the optimiser the
+// multi-obstacle env kernels run (sbmpc_cooperative_multi)
+__global__ __launch_bounds__(64) void sbmpc_multi_eval_kernel(int n, int n_obs, int n_samp, double dt,
+                                                              const double* __restrict__ in, double* __restrict__ out) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const bool valid = i < n;
+  const double* r = in + (size_t)(valid ? i : 0) * SHIPSIM_SBMPC_MULTI_IN;
+  SbMulti<SHIPSIM_MAX_OBS> q;
+  q.p_last = r[0]; q.chi_last = r[1]; q.u_d = r[2]; q.chi_d = r[3];
+  q.os_x = r[4]; q.os_y = r[5]; q.os_v = r[8];  // os_state (x, y, psi, u, v, r): linear_pred uses x, y, v
+  bool active = false;
+#pragma unroll
+  for (int k = 0; k < SHIPSIM_MAX_OBS; ++k) {
+    const double* o = r + 10 + 7 * k;
+    q.ob_x[k] = o[0]; q.ob_y[k] = o[1]; q.ob_psi[k] = o[2]; q.ob_u[k] = o[3]; q.ob_v[k] = o[4];
+    q.obs_l[k] = o[5]; q.obs_w[k] = o[6];
+    const double d0 = o[0] - q.os_x, d1 = o[1] - q.os_y;
+    if (k < n_obs) active = active || sqrt_lt(d0 * d0 + d1 * d1, 2000.0);  // D_INIT_ (sbmpc.py:153-159)
+  }
+  active = valid && active;
+  double pb = 1.0, cb = 0.0;
+  sbmpc_cooperative_multi<SHIPSIM_MAX_OBS>(active, q, n_obs, n_samp, dt, pb, cb);  // (n_samp: int(tf / dt))
   if (valid) {
     out[(size_t)i * 3 + 0] = active ? pb : 1.0;
     out[(size_t)i * 3 + 1] = active ? cb : 0.0;
@@ -3475,7 +3550,7 @@ int shipsim_tick(shipsim_handle* h, int32_t k, uint32_t* events_out) {
       return fail(h, SHIPSIM_EINVAL, "tick: KIND_NONIW runs the simplified machinery (run_colav SimpleShipModel)");
     const int blocks = (2 * h->P.n_envs + 63) / 64;
 #define NT(CA) \
-  hipLaunchKernelGGL(noniw_tick_kernel<CA>, dim3(blocks), dim3(64), 0, h->stream, h->P, h->S, h->K, k, events_out)
+  hipLaunchKernelGGL(noniw_tick_kernel<CA>, dim3(blocks), dim3(64), 0, h->stream, NoniwArgs{h->P, h->S, h->K, k, events_out})
     if (h->P.collav == SHIPSIM_COLLAV_SBMPC) NT(SHIPSIM_COLLAV_SBMPC);
     else if (h->P.collav == SHIPSIM_COLLAV_SIMPLE) NT(SHIPSIM_COLLAV_SIMPLE);
     else NT(SHIPSIM_COLLAV_NONE);
@@ -3716,6 +3791,16 @@ int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double
   if (n < 0 || (n > 0 && (!in || !out)) || !(dt > 0) || tf / dt > 4096) return SHIPSIM_EINVAL;
   if (n == 0) return SHIPSIM_OK;
   hipLaunchKernelGGL(sbmpc_eval_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, tf, dt, in, out);
+  return hipGetLastError() == hipSuccess ? SHIPSIM_OK : SHIPSIM_EHIP;
+}
+
+int shipsim_sbmpc_eval_multi(int32_t n, int32_t n_obs, double tf, double dt, const double* in, double* out,
+                             void* stream) {
+  if (n < 0 || n_obs < 1 || n_obs > SHIPSIM_MAX_OBS || (n > 0 && (!in || !out)) || !(dt > 0) || tf / dt > 4096)
+    return SHIPSIM_EINVAL;
+  if (n == 0) return SHIPSIM_OK;
+  hipLaunchKernelGGL(sbmpc_multi_eval_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, n_obs,
+                     (int)(tf / dt), dt, in, out);
   return hipGetLastError() == hipSuccess ? SHIPSIM_OK : SHIPSIM_EHIP;
 }
 

@@ -59,14 +59,18 @@ def load_library(path=LIB_PATH):
     L.shipsim_legacy_step.argtypes = [P, C.c_int32, P, P, P]
     L.shipsim_run_table.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, C.c_int32, P]
     L.shipsim_set_stream_tail.argtypes = [P, C.c_int32]
-    try:
-        L.shipsim_div_check.argtypes = [C.c_int32, P, P, P, P, P]
-        L.shipsim_diag_lane_faults.argtypes = [P]
-        L.shipsim_run_policy.argtypes = [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, P, C.c_int32,
-                                         C.c_int32, P, P, P, P, P, C.c_int32, P]
-    except AttributeError:  # an explicitly chosen older build (SHIPSIM_LIB, A/B timing only)
-        if "SHIPSIM_LIB" not in os.environ:
-            raise
+    # entry points added in later ABI versions: each bound on its own, so an explicitly chosen older build (SHIPSIM_LIB,
+    # A/B timing only) that lacks one still gets the argument types of every other
+    for name, argtypes in (("shipsim_div_check", [C.c_int32, P, P, P, P, P]),
+                           ("shipsim_diag_lane_faults", [P]),
+                           ("shipsim_run_policy", [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, P, C.c_int32,
+                                                   C.c_int32, P, P, P, P, P, C.c_int32, P]),
+                           ("shipsim_sbmpc_eval_multi", [C.c_int32, C.c_int32, C.c_double, C.c_double, P, P, P])):
+        try:
+            getattr(L, name).argtypes = argtypes
+        except AttributeError:
+            if "SHIPSIM_LIB" not in os.environ:
+                raise
     if L.shipsim_abi_version() != abi.ABI_VERSION:
         raise ShipSimError(f"ABI mismatch: library {L.shipsim_abi_version()} vs binding {abi.ABI_VERSION}")
     from .build_hash import check_library
@@ -83,7 +87,8 @@ EXPORTED_SYMBOLS = ("shipsim_abi_version", "shipsim_build_info", "shipsim_defaul
                     "shipsim_tick", "shipsim_get_state", "shipsim_set_state", "shipsim_synchronize",
                     "shipsim_set_trajectory", "shipsim_sbmpc_eval", "shipsim_legacy_step", "shipsim_run_table",
                     "shipsim_nonfinite_count", "shipsim_lanes_per_env", "shipsim_set_stream",
-                    "shipsim_run_policy", "shipsim_diag_lane_faults", "shipsim_set_stream_tail", "shipsim_div_check")
+                    "shipsim_run_policy", "shipsim_diag_lane_faults", "shipsim_set_stream_tail", "shipsim_div_check",
+                    "shipsim_sbmpc_eval_multi")
 
 
 def diag_lane_faults():
@@ -354,4 +359,22 @@ def sbmpc_eval(requests, tf=1000.0, dt=20.0, device="cuda"):
     rc = L.shipsim_sbmpc_eval(int(x.shape[0]), float(tf), float(dt), _ptr(x), _ptr(out), C.c_void_p(stream.cuda_stream))
     if rc:
         raise ShipSimError(f"shipsim_sbmpc_eval failed ({rc})")
+    return out
+
+
+def sbmpc_eval_multi(requests, n_obs, tf=1000.0, dt=20.0, device="cuda"):
+    """SBMPC.get_optimal_ctrl_offset over a do_list of n_obs obstacles on the device, for a batch of
+    (n, SBMPC_MULTI_IN) requests [P_ca_last, Chi_ca_last, u_d, chi_d, os_state(6), then per obstacle slot
+    (SHIPSIM_MAX_OBS of them) x, y, psi, u, v, length, width] -> (n, 3) tensor [speed factor, course offset, active]
+    (shipsim_sbmpc_eval_multi)."""
+    L = load_library()
+    x = torch.as_tensor(requests, dtype=torch.float64, device=device).contiguous()
+    if x.dim() != 2 or x.shape[1] != abi.SBMPC_MULTI_IN:
+        raise ShipSimError(f"requests must be (n, {abi.SBMPC_MULTI_IN})")
+    out = torch.empty((x.shape[0], 3), dtype=torch.float64, device=x.device)
+    stream = torch.cuda.current_stream(x.device)
+    rc = L.shipsim_sbmpc_eval_multi(int(x.shape[0]), int(n_obs), float(tf), float(dt), _ptr(x), _ptr(out),
+                                    C.c_void_p(stream.cuda_stream))
+    if rc:
+        raise ShipSimError(f"shipsim_sbmpc_eval_multi failed ({rc}): n_obs must be 1..{abi.MAX_OBS}")
     return out

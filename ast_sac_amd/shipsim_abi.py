@@ -13,7 +13,7 @@ import math
 
 import numpy as np
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAP_GRID, MAP_ALL_EDGES = 0, 1  # shipsim_config.map_query (results identical)
 ENONFINITE = -5  # shipsim_synchronize status (include/shipsim.h)
 MAX_ROUTE = 16
@@ -96,6 +96,7 @@ TRAJ_ENV_COLS = 8
  TE_FLAGS) = range(8)
 TE_FLAG_COLLISION, TE_FLAG_IMMINENT = 1, 2
 SBMPC_IN = 17
+SBMPC_MULTI_IN = 10 + 7 * MAX_OBS  # shipsim_sbmpc_eval_multi rows (include/shipsim.h)
 
 
 def events_to_string(bits):

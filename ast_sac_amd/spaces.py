@@ -45,14 +45,3 @@ Box = _GymBox if _GymBox is not None else _Box
 class Discrete:
     def __init__(self, n):
         self.n = n
-
-
-def get_dim(space):
-    """ast_sac/env_wrapper/env_utils.py:get_dim"""
-    if hasattr(space, "low") and hasattr(space, "shape"):
-        return int(np.prod(space.shape))
-    if hasattr(space, "n"):
-        return space.n
-    if hasattr(space, "spaces"):
-        return sum(get_dim(s) for s in space.spaces)
-    raise TypeError(f"Unknown space: {space}")

@@ -81,6 +81,10 @@ def parse():
                    help="SAC batch summed over all ranks (runner: 256); each rank samples global / N rows "
                         "(SURVEY.md §8(e))")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, one GPU per rank) | gloo (rehearsal)")
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 leg (runner experiment at the reference ratio)")
+    p.add_argument("--c4-envs", type=int, default=8192, help="C4 leg: envs per rank (C4: 65,536 over 8 GPUs)")
+    p.add_argument("--c4-loops", type=int, default=3, help="C4 leg: timed train loops")
+    p.add_argument("--no-c5", action="store_true", help="skip the C5 legs (K = 2 and 4 obstacle ships, sbmpc)")
     return p.parse_args()
 
 
@@ -346,6 +350,140 @@ def bench_policy_stream(dev, cfg, n_envs, slice_ticks, launches=3, warmup=1, tai
                    "NormalizedBoxEnv mapping, in-place episode resets)"}
     sim.close()
     return res
+
+
+def bench_c4(dev, world, rank, pg, n_envs=8192, slice_ticks=128, loops=3, warmup_loops=1, dp_mode="replicated"):
+    """configs[3] (C4) as the runner runs it, at whatever N the job has: the runner's device experiment
+    (ast_sac_amd/run/ast_sac_runner.py experiment_device: `n_envs` two-ship AST envs per rank, sbmpc, PTI, dt 4,
+    policy sampled inside the env launch, device replay, FusedSACTrainer 2 x 256, global batch 256), then `loops`
+    train loops at the reference's update ratio (run/ast-sac_runner.py:66-72, batch_rl_algorithm.py:81-106: 240 grad
+    steps per 256 collected decisions, counted over ALL ranks): per loop every rank collects one fused pass of
+    `slice_ticks` ticks, the replicated buffers all-gather the new rows (ReplicatedReplayBuffer.sync, RCCL over xGMI
+    with nccl), and every rank runs round(decisions_all_ranks x 240 / 256) identical global-batch grad steps
+    (DESIGN.md §6). Reports the job's grad steps/s (one chain, whatever N), env-ticks/s and decisions/s summed over
+    the ranks, and the sync's share; the timed region is bracketed by barriers, times are the max over ranks."""
+    import torch
+    import torch.distributed as dist
+    from ast_sac_amd.run.ast_sac_runner import experiment_device, make_variant, parse_cli_args
+    argv = ["--n_envs", str(n_envs), "--do_logging", "False", "--seed", "0", "--slice_ticks", str(slice_ticks),
+            "--dp_mode", dp_mode]
+    args = parse_cli_args(argv)
+    algo = experiment_device(make_variant(args), args, dev, pg)
+    coll, rb, tr = algo.expl_data_collector, algo.replay_buffer, algo.trainer
+    ak = make_variant(args)["algorithm_kwargs"]
+
+    def counters():
+        return coll.get_diagnostics()["num steps total"], coll.device_diagnostics()["num env ticks total"]
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    # epoch 0's initial exploration fills the buffers (every rank's rows into every replica)
+    coll.collect(ak["min_num_steps_before_training"], rb)
+    algo._sync_buffer()
+    tr.train_from_buffer(rb, 20)
+
+    def loop(k):
+        t_sync = 0.0
+        for _ in range(k):
+            got = coll.collect(1, rb)  # one pass
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            algo._sync_buffer()
+            torch.cuda.synchronize()
+            t_sync += time.perf_counter() - t0
+            n = algo._n_grad_steps(got)  # all ranks' decisions x 240 / 256 (an all-reduce of the count)
+            if n:
+                tr.train_from_buffer(rb, n)
+            algo.num_train_steps_total += n
+        return t_sync
+
+    loop(warmup_loops)
+    g0 = algo.num_train_steps_total
+    s0, k0 = counters()
+    barrier()
+    t0 = time.perf_counter()
+    t_sync = loop(loops)
+    barrier()
+    el = time.perf_counter() - t0
+    s1, k1 = counters()
+    grad = algo.num_train_steps_total - g0
+    v = torch.tensor([el, t_sync, float(s1 - s0), float(k1 - k0)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx, sm = v.clone(), v.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        v = torch.stack([mx[0], mx[1], sm[2], sm[3]])
+    el, t_sync, dec, ticks = (float(x) for x in v)
+    res = {"grad_steps_per_s": grad / el, "env_ticks_per_s": ticks / el, "decisions_per_s": dec / el,
+           "grad_steps": grad, "decisions": dec, "env_ticks": ticks, "seconds": el, "loops": loops,
+           "sync_ms_per_loop": t_sync / loops * 1e3, "sync_frac": t_sync / el,
+           "grad_steps_per_decision": grad / max(dec, 1.0), "ranks": world, "envs_per_rank": n_envs,
+           "global_envs": n_envs * world, "slice_ticks": slice_ticks, "dp_mode": dp_mode if world > 1 else None,
+           "global_batch": ak["batch_size"],
+           "note": "the runner's device experiment at the reference's update ratio (240 grad steps per 256 decisions "
+                   "over all ranks); per loop one fused collector pass per rank, the replicated buffers' row "
+                   "all-gather, then the identical global-batch grad steps on every rank; grad steps are one serial "
+                   "chain for the whole job, so they do not add up over ranks"}
+    del algo, coll, rb, tr
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_c5(dev, world, n_envs, n_obs, collav="sbmpc", slice_ticks=4096, tail_ticks=1024, launches=3, warmup=1,
+             rank=0):
+    """configs[4] (C5) multi-obstacle envs: the headline's decision stream (shipsim_run_table, PTI machinery, dt 4,
+    bench.py's PCG64 table) with K = `n_obs` obstacle ships per env (the test ship's SBMPC over all of them,
+    sbmpc.py:149-178). env-ticks/s summed over the ranks / max-over-ranks time of `launches` timed launches."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ast_sac_amd import shipsim_abi as abi
+    from ast_sac_amd.shipsim import ShipSim
+    cfg = abi.ast_config(collav, machinery=abi.MACH_DETAILED, n_obs_ships=n_obs)
+    sim = ShipSim(cfg, n_envs, device=dev, n_obs_ships=n_obs)
+    n_dec = cfg.max_sampling_frequency
+    gen = np.random.Generator(np.random.PCG64(20251015 + rank))
+    table = torch.from_numpy(abi.normalized_to_scoping(gen.uniform(-1, 1, (8, n_dec, n_envs)).astype(np.float32))).to(dev)
+    ep = torch.zeros(n_envs, dtype=torch.int32, device=dev)
+    dec = torch.zeros(n_envs, dtype=torch.int32, device=dev)
+    out = dict(ticks=torch.empty(n_envs, dtype=torch.int32, device=dev),
+               decisions=torch.empty(n_envs, dtype=torch.int32, device=dev))
+    cap = max(8, (slice_ticks + tail_ticks) // 32 + 16)
+    log = torch.zeros((n_envs, cap, abi.DECLOG_COLS), dtype=torch.float64, device=dev)
+    log_len = torch.zeros(n_envs, dtype=torch.int32, device=dev)
+    sim.reset()
+    if tail_ticks > 0:
+        sim.set_stream_tail(tail_ticks)
+    ticks = torch.zeros((), dtype=torch.int64, device=dev)
+    for i in range(warmup + launches):
+        if i == warmup:
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            ticks.zero_()
+            t0 = time.perf_counter()
+        log_len.zero_()
+        sim.run_table(table, slice_ticks, ep, dec, out=out, log=log, log_len=log_len)
+        ticks.add_(out["ticks"].sum())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    v = torch.tensor([time.perf_counter() - t0, float(ticks.item())], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx, sm = v.clone(), v.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        v = torch.stack([mx[0], sm[1]])
+    lpe = sim.lanes_per_env
+    sim.close()
+    return {"env_ticks_per_s": float(v[1]) / float(v[0]), "ms_per_launch": float(v[0]) / launches * 1e3,
+            "obs_ships": n_obs, "collav": collav, "envs_per_gpu": n_envs, "slice_ticks": slice_ticks,
+            "tail_ticks": tail_ticks, "launches": launches, "lanes_per_env": lpe,
+            "parity": "K = 1 is the reference env; K > 1 generalises it (include/shipsim.h shipsim_create); its "
+                      "SBMPC over K obstacles is pinned to the reference (tests/golden/sbmpc_multi.npz)"}
 
 
 def bench_c2(dev, n_ships=4096, per_launch=None):
@@ -655,6 +793,15 @@ def main():
         if world > 1:  # the alternative data-parallel shape, for DESIGN.md §6's comparison
             sac_ar = bench_sac(dev, world, pgw, args.sac_steps, args.sac_global_batch, eager_steps=0,
                                dp_mode="allreduce")
+    c4 = None
+    if not args.no_c4:
+        progress("c4 loop")
+        c4 = bench_c4(dev, world, rank, dist.group.WORLD if world > 1 else None, n_envs=args.c4_envs,
+                      loops=args.c4_loops)
+    c5 = None
+    if not args.no_c5 and args.obs_ships == 1:
+        progress("c5 multi-obstacle")
+        c5 = {f"k{k}": bench_c5(dev, world, N, k, rank=rank, tail_ticks=max(args.tail_ticks, 0)) for k in (2, 4)}
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure
@@ -700,6 +847,8 @@ def main():
             "sac_allreduce": sac_ar,
             "c2_single_ship": c2,
             "policy_stream": pstream,
+            "c4": c4,
+            "c5": c5,
         }
         print(json.dumps(line))
     if world > 1:

@@ -110,7 +110,9 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
  *                           it (the same rows and normals: results are bitwise those of sacf_grads). Only right
  *                           after a call with SACF_CHAIN_STAGE_NEXT on this handle (SACF_ESTATE otherwise), and
  *                           the caller guarantees the replay ring and its size did not change in between.
- * A replay ring must be bound (sacf_set_replay). */
+ * A replay ring must be bound (sacf_set_replay). With either flag eps must be NULL (the normals then come from the
+ * in-kernel Philox stream, and a staged batch carries the ones of the call that staged it): SACF_EINVAL otherwise.
+ * flags == 0 is sacf_grads(h, NULL x 5, eps). */
 #define SACF_CHAIN_STAGE_NEXT 1
 #define SACF_CHAIN_FROM_STAGED 2
 int sacf_grads_chain(sacf_handle* h, const float* eps, int32_t flags);

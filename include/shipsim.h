@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHIPSIM_ABI_VERSION 9
+#define SHIPSIM_ABI_VERSION 10
 
 #define SHIPSIM_MAX_ROUTE 16   /* waypoints per ship route (obs ship: 2 + max_sampling_frequency) */
 #define SHIPSIM_MAX_POLYS 16   /* land polygons in the map */
@@ -368,6 +368,18 @@ int shipsim_set_trajectory(shipsim_handle* h, double* ship_rows, double* env_row
  * SBMPC(tf, dt) horizon; stream is a hipStream_t (NULL = default); device pointers. */
 #define SHIPSIM_SBMPC_IN 17
 int shipsim_sbmpc_eval(int32_t n, double tf, double dt, const double* in, double* out, void* stream);
+
+/* SBMPC.get_optimal_ctrl_offset (sbmpc.py:113-185) over a do_list of n_obs dynamic obstacles (1 <= n_obs <=
+ * SHIPSIM_MAX_OBS; active when any of them is within D_INIT, per scenario the worst obstacle's cost, the least worst
+ * scenario: :149-178) for n independent requests, stateless like shipsim_sbmpc_eval (ABI 10). in: n x
+ * SHIPSIM_SBMPC_MULTI_IN doubles [P_ca_last, Chi_ca_last, u_d, chi_d, os_state(6: x, y, psi, u, v, r), then per
+ * obstacle slot k < SHIPSIM_MAX_OBS: x, y, psi, u, v, length, width (the do_list tuple's state and size; slots
+ * k >= n_obs are ignored)]; out: n x 3 doubles [speed factor, course offset, active]. The optimiser is the one the
+ * multi-obstacle env kernels (n_obs_ships > 1) run. Replaces, per request, one call of the reference method with a
+ * do_list of n_obs entries. */
+#define SHIPSIM_SBMPC_MULTI_IN (10 + 7 * SHIPSIM_MAX_OBS)
+int shipsim_sbmpc_eval_multi(int32_t n, int32_t n_obs, double tf, double dt, const double* in, double* out,
+                             void* stream);
 
 /* Diagnostics: the kernels' division by a reused divisor (the divisor's refined reciprocal formed once, the rest of
  * the compiler's fp64 division sequence per quotient) next to the plain IEEE division, for n operand

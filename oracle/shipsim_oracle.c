@@ -1393,6 +1393,24 @@ void oracle_sbmpc(double tf, double dt, double* p_last, double* chi_last, double
   out[0] = p; out[1] = c; out[2] = sb.active;
 }
 
+/* get_optimal_ctrl_offset (sbmpc.py:113-185) over a do_list of n_obst obstacles, ob[k] = [x, y, psi, u, v, l, w]
+ * (the do_list tuple's state and its length / width), the controller's last offsets in/out */
+void oracle_sbmpc_multi(double tf, double dt, double* p_last, double* chi_last, double u_d, double chi_d,
+                        const double os[6], int n_obst, const double (*ob)[7], double out[3]) {
+  o_sbmpc sb = {*p_last, *chi_last, 0};
+  double st[SHIPSIM_MAX_OBS][5], l[SHIPSIM_MAX_OBS], w[SHIPSIM_MAX_OBS];
+  if (n_obst > SHIPSIM_MAX_OBS) n_obst = SHIPSIM_MAX_OBS;
+  for (int k = 0; k < n_obst; ++k) {
+    for (int j = 0; j < 5; ++j) st[k][j] = ob[k][j];
+    l[k] = ob[k][5];
+    w[k] = ob[k][6];
+  }
+  double p, c;
+  sbmpc_offset_multi(&sb, tf, dt, u_d, chi_d, os, n_obst, (const double (*)[5])st, l, w, &p, &c);
+  *p_last = sb.P_last; *chi_last = sb.Chi_last;
+  out[0] = p; out[1] = c; out[2] = sb.active;
+}
+
 void oracle_map_query(const shipsim_config* cfg, int n, const double* ne, int32_t* inside, double* dist) {
   o_map mp;
   map_init(&mp, cfg);

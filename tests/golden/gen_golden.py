@@ -802,6 +802,59 @@ def gen_sbmpc_geometry():
     print("sbmpc/geometry: survey KA", out["sbmpc_survey_ka"])
 
 
+def gen_sbmpc_multi():
+    """F5b: get_optimal_ctrl_offset over a do_list of K = 2, 3, 4 dynamic obstacles (sbmpc.py:113-185: active when
+    any obstacle is within D_INIT, per scenario the worst obstacle's cost, the least worst scenario). One persistent
+    controller per K, so P_ca_last_ / Chi_ca_last_ carry from call to call (Q7). Per call (96 per K): the obstacles at mixed
+    ranges (all beyond D_INIT every 8th call: inactive; some beyond reach of every scenario, some close), a repeated
+    obstacle every 5th call, and per-obstacle sizes (the do_list's length / width) varied every 3rd call.
+    Rows: in [u_d, chi_d, os_state(6), then per obstacle slot x, y, psi, u, v, l, w (4 slots, unused zero)], out
+    [speed factor, course offset, active, P_ca_last_, Chi_ca_last_]."""
+    from rl_env.ship_in_transit.sub_systems.sbmpc import SBMPC
+    rng = np.random.Generator(np.random.PCG64(11))
+    out = {}
+    for K in (2, 3, 4):
+        sb = SBMPC(tf=1000, dt=20)
+        ins, outs = [], []
+        for call in range(96):
+            os_state = np.array([rng.uniform(0, 20000), rng.uniform(0, 10000), rng.uniform(-np.pi, np.pi),
+                                 rng.uniform(0, 6), rng.uniform(-0.5, 0.5), rng.uniform(-0.01, 0.01)])
+            u_d = rng.uniform(3, 5)
+            chi_d = rng.uniform(-4, 4)
+            obs, row = [], [u_d, chi_d] + list(os_state)
+            for k in range(K):
+                ang = rng.uniform(-np.pi, np.pi)
+                if call % 8 == 0:
+                    rad = rng.uniform(2100, 6000)
+                elif k == 0:
+                    rad = rng.uniform(50, 1900)
+                else:
+                    rad = rng.uniform(50, 6000)
+                ob = np.array([os_state[0] + rad * np.cos(ang), os_state[1] + rad * np.sin(ang),
+                               rng.uniform(-np.pi, np.pi), rng.uniform(0, 6), rng.uniform(-0.5, 0.5)])
+                if call % 8 and rng.uniform() < 0.6:
+                    # on a collision course: ahead of the own ship's nominal course (linear_pred moves along
+                    # (-sin psi, cos psi)), heading back towards it
+                    rad = rng.uniform(300, 1900)
+                    ax = chi_d + rng.uniform(-0.6, 0.6)
+                    ob = np.array([os_state[0] - rad * np.sin(ax), os_state[1] + rad * np.cos(ax),
+                                   chi_d + np.pi + rng.uniform(-0.5, 0.5), rng.uniform(2, 6), rng.uniform(-0.3, 0.3)])
+                l, w = (80.0, 16.0) if call % 3 else (float(rng.uniform(40, 140)), float(rng.uniform(8, 30)))
+                if call % 5 == 1 and k == K - 1:  # a repeated obstacle (the env's duplicate slots)
+                    ob, l, w = obs[0][1].copy(), obs[0][3], obs[0][4]
+                obs.append((k, ob, None, l, w))
+                row += list(ob) + [l, w]
+            row += [0.0] * (7 * (4 - K))
+            p, c = sb.get_optimal_ctrl_offset(u_d=u_d, chi_d=chi_d, os_state=os_state, do_list=obs)
+            ins.append(row)
+            outs.append([p, c, float(sb.is_stephen_useful()), sb._params.P_ca_last_, sb._params.Chi_ca_last_])
+        out[f"k{K}_in"] = np.array(ins)
+        out[f"k{K}_out"] = np.array(outs)
+        print(f"sbmpc multi K={K}: active {int(out[f'k{K}_out'][:, 2].sum())} / 96, "
+              f"non-default {int(((out[f'k{K}_out'][:, 0] != 1) | (out[f'k{K}_out'][:, 1] != 0)).sum())}")
+    np.savez_compressed(os.path.join(OUT, "sbmpc_multi.npz"), **out)
+
+
 # ----------------------------------------------------------------------------------------------
 # F7 SAC grad steps (sac.py:102-154) with fixed weights, batch and reparameterisation noise
 # ----------------------------------------------------------------------------------------------
@@ -1066,6 +1119,8 @@ if __name__ == "__main__":
         gen_ast_single()
     if "sbmpc" in what:
         gen_sbmpc_geometry()
+    if "sbmpc_multi" in what:
+        gen_sbmpc_multi()
     if "sac" in what:
         gen_sac()
     if "rl" in what:

@@ -71,6 +71,8 @@ def _bind(L):
         L.oracle_env_get_route.argtypes = [P, dp, dp]
         L.oracle_sbmpc.argtypes = [C.c_double, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double,
                                    C.c_double, dp, dp, C.c_double, C.c_double, dp]
+        L.oracle_sbmpc_multi.argtypes = [C.c_double, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                         C.c_double, C.c_double, dp, C.c_int, dp, dp]
         L.oracle_map_query.argtypes = [cfgp, C.c_int, dp, ip, dp]
         L.oracle_encounter.argtypes = [C.c_int, dp, dp]
         L.oracle_reward_terms.argtypes = [C.c_int, dp, dp]
@@ -192,6 +194,18 @@ def sbmpc(p_last, chi_last, u_d, chi_d, os_state, ob, obs_l=80, obs_w=16, tf=100
     out = np.zeros(3)
     lib().oracle_sbmpc(tf, dt, C.byref(p), C.byref(c), u_d, chi_d, np.ascontiguousarray(os_state, np.float64),
                        np.ascontiguousarray(ob, np.float64), obs_l, obs_w, out)
+    return out, p.value, c.value
+
+
+def sbmpc_multi(p_last, chi_last, u_d, chi_d, os_state, obs, tf=1000, dt=20):
+    """get_optimal_ctrl_offset over a do_list: obs (K, 7) rows [x, y, psi, u, v, length, width]. Returns
+    ([speed factor, course offset, active], P_ca_last_, Chi_ca_last_)."""
+    p = C.c_double(p_last)
+    c = C.c_double(chi_last)
+    out = np.zeros(3)
+    obs = np.ascontiguousarray(obs, np.float64).reshape(-1, 7)
+    lib().oracle_sbmpc_multi(tf, dt, C.byref(p), C.byref(c), u_d, chi_d, np.ascontiguousarray(os_state, np.float64),
+                             obs.shape[0], obs, out)
     return out, p.value, c.value
 
 

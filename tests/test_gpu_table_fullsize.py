@@ -6,10 +6,15 @@ it, in 128-tick launches and in one 4096-tick launch, the bench default), checke
   - every 4th env: decision by decision against the CPU oracle replaying the same episodes
     (reward, termination bits, done, obs, and the decision's tick count exactly), with the oracle's
     few-ulp initial-condition variants (gpu_harness.run_oracle_variants) as the acceptance
-    envelope; at most 10 % of the checked envs may need a perturbed variant (the fraction is
-    printed).
+    envelope; at most 1 % of the checked envs may need a perturbed variant (every case so far: none).
+Each case's statistics (fraction matched only by a perturbed oracle run, worst relative error) are printed and
+appended as one JSON line to $SHIPSIM_PARITY_LOG (default gpurun_out/parity_fullsize.jsonl; committed copies under
+profiles/).
 Needs an MI355X."""
 import copy
+import json
+import os
+import time
 
 import numpy as np
 import pytest
@@ -142,6 +147,20 @@ def test_bench_workload_full_size(collav, SLICE, LAUNCHES, mach, tail, n_eps):
     print(f"\n[{collav} {mach} slice {SLICE} tail {tail}] {len(idx)} envs vs oracle, {sum(len(e) for e in g_all)} decisions; "
           f"matched only by a perturbed oracle run: {perturbed} ({100 * frac:.2f} %); off the oracle: {len(bad)}; "
           f"worst rel err {worst:.2e}")
+    _record(dict(collav=collav, machinery=mach, slice=SLICE, launches=LAUNCHES, tail=tail, episodes_in_table=n_eps,
+                 envs_checked=len(idx), decisions_checked=int(sum(len(d) for e in g_all for d in e)),
+                 perturbed=perturbed, perturbed_frac=frac, off_oracle=len(bad), worst_rel_err=worst,
+                 ticks_per_env_launch=[int(ticks.min()), float(ticks.mean()), int(ticks.max())]))
     assert not bad, f"envs off the oracle: {bad[:20]}"
-    assert frac <= 0.10, f"{perturbed} of {len(idx)} envs matched only by a perturbed oracle run"
+    assert frac <= 0.01, f"{perturbed} of {len(idx)} envs matched only by a perturbed oracle run"
     assert worst <= 1e-5
+
+
+def _record(row):
+    path = os.environ.get("SHIPSIM_PARITY_LOG") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity_fullsize.jsonl")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    row = dict(row, time=time.strftime("%Y-%m-%dT%H:%M:%S"),
+               library=__import__("ast_sac_amd.shipsim", fromlist=["x"]).load_library().shipsim_build_info().decode())
+    with open(path, "a") as f:
+        f.write(json.dumps(row) + "\n")

@@ -206,6 +206,20 @@ def test_sbmpc_known_answers(golden):
     np.testing.assert_array_equal(res[:2], g["sbmpc_survey_ka"])
 
 
+@pytest.mark.parametrize("K", [2, 3, 4])
+def test_sbmpc_multi_obstacle_known_answers(golden, K):
+    """get_optimal_ctrl_offset over a do_list of K obstacles (sbmpc.py:149-178), one persistent controller per K:
+    the reference's own answers (tests/golden/gen_golden.py gen_sbmpc_multi), exactly, call after call."""
+    g = golden("sbmpc_multi")
+    p_last, chi_last = 1.0, 0.0
+    for row, out in zip(g[f"k{K}_in"], g[f"k{K}_out"]):
+        obs = row[8:8 + 7 * K].reshape(K, 7)
+        res, p_last, chi_last = O.sbmpc_multi(p_last, chi_last, row[0], row[1], row[2:8], obs)
+        np.testing.assert_array_equal(res[:2], out[:2])
+        assert res[2] == out[2]
+        assert (p_last, chi_last) == (out[3], out[4])
+
+
 def test_polygon_map_queries(golden):
     g = golden("sbmpc_geometry_reward")
     inside, dist = O.map_query(abi.ast_config(), g["poly_pts_ne"])

@@ -299,6 +299,28 @@ def test_hip_sac_multi_step_graph_equals_single_step_graphs(H, B):
 
 
 @pytest.mark.gpu
+def test_hip_sac_chain_refuses_caller_normals():
+    """sacf_grads_chain with STAGE_NEXT or FROM_STAGED takes its normals from the in-kernel stream (a staged batch
+    carries the ones of the call that staged it): a caller's eps is refused (SACF_EINVAL), not silently ignored;
+    flags 0 with eps is sacf_grads."""
+    from ast_sac_amd import sacfused
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    rb = DeviceReplayBuffer(2000, 8, 1, "cuda")
+    b, _ = _rand_batch(1000, "cuda", seed=6)
+    rb.add_batch(b["observations"], b["actions"], b["rewards"], b["next_observations"], b["terminals"])
+    tr = _trainer("hip", 64, 32, "cuda", use_graph=False, seed=3)
+    tr.train_from_buffer(rb, 1)  # binds the replay ring
+    sf = tr._sf
+    eps = torch.zeros(2 * 32, device="cuda")
+    for flags in (sacfused.CHAIN_STAGE_NEXT, sacfused.CHAIN_FROM_STAGED,
+                  sacfused.CHAIN_STAGE_NEXT | sacfused.CHAIN_FROM_STAGED):
+        with pytest.raises(RuntimeError, match="eps"):
+            sf.grads_chain(flags, eps)
+    sf.grads_chain(0, eps)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("H,B", [(256, 256), (64, 96), (512, 100)])
 def test_hip_sac_split_update_equals_fused(H, B):
     """The data-parallel call pattern on one rank (sacf_grads | all-reduce over a world-size-1 group |
