@@ -108,6 +108,10 @@ struct Scr {
   float *pre[4];             // [Bp][H] each: Q1, Q2 (obs rows), T1, T2 (next_obs rows)
   float *w1a;                // [4][H]
   float *part;               // [Bp][PS_N][CB]
+  // [h2 > 0] and [g2 > 0] of Q1 / Q2 as bit masks, [Bp][CB] words (bit c of word (r, b): column 32b + c of row r):
+  // the backward factors (P2) and the MFMA weight-gradient tiles (P3) use the layer-2 activations only through this
+  // mask, so they read 1 bit per element instead of the float
+  uint32_t *h2m, *g2m[2];
   // the parameters P3 reads, as they were before this step's update (P3 updates them in place with fused Adam,
   // so its blocks must not read the live values): [log α, b3 Q1, b3 Q2, b3 T1, b3 T2, -, -, -] then
   // wm [H], ws [H], w3 Q1 [H], w3 Q2 [H]
@@ -132,6 +136,7 @@ struct MArgs {
   int64_t* step;
   float* stats;
   int chain;  // SACF_CHAIN_* of this step
+  int wt;     // write-through mask of this launch (WT_*, wt_mask_for)
   Scr s;
   Layout L;
   Hyper hp;
@@ -218,19 +223,23 @@ __device__ inline void block_sum(float (&v)[N], float (*red)[32], float* out) {
 // are other launches, so no store here is read back through the writer's L2. SACF_WT selects which stores publish
 // write-through (a bit mask, for A/Bs): 1 the row inputs, parts, records and first-layer slices P1 / P2 hand on;
 // 4 the split-K epilogues' activation and factor matrices (one word per lane and output); 2 what P3 (and the apply
-// kernel) writes: gradients, Adam state, parameters, targets and the transposed copies. 0: plain stores.
+// kernel) writes: gradients, Adam state, parameters, targets and the transposed copies. 0: plain stores. The launch
+// chooses within that mask at run time (MArgs / ApplyArgs::wt, wt_mask_for below): the split-K epilogues' matrices
+// are written through from 128 batch rows up — at B = 256 write-through takes 28.7 µs per step against 29.8 µs, at
+// B = 64 the same stores cost more than the smaller dirty set's write-back (25.6 against 25.0 µs; without the
+// row / part bits 24.6 µs): profiles/round6/r6b_*
 #ifndef SACF_WT
 #define SACF_WT 7
 #endif
 enum { WT_ACT = 1, WT_OPT = 2, WT_EPI = 4 };
 template <int KIND, class T>
-__device__ __forceinline__ void pub(T* p, T v) {
-  if constexpr ((SACF_WT & KIND) != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // … sc1
-  else *p = v;
+__device__ __forceinline__ void pub(int wt, T* p, T v) {
+  if ((SACF_WT & KIND) != 0 && (wt & KIND) != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;  // (wt: the launch's mask, uniform)
 }
 template <int KIND>
-__device__ __forceinline__ void pub4(float* p, float x, float y, float z, float w) {
-  if constexpr ((SACF_WT & KIND) != 0) {
+__device__ __forceinline__ void pub4(int wt, float* p, float x, float y, float z, float w) {
+  if ((SACF_WT & KIND) != 0 && (wt & KIND) != 0) {
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     const f32x4 v = {x, y, z, w};
     // (the compiler's hazard recognizer does not see an asm store: a store of more than 8 bytes needs a wait state
@@ -456,11 +465,11 @@ __device__ __forceinline__ void first_layer_pre(const float* lw1t, const float* 
 // this lane's first-layer chunk (row lane & 31, columns k0 .. k0 + CS) straight to its row of the matrix by the
 // block that owns column block k0 / 32 (every block computes the same values): float4 stores
 template <int H, int CS>
-__device__ __forceinline__ void store_slice(float* base, int r0, int by, const float (&av)[CS], int k0) {
+__device__ __forceinline__ void store_slice(int wt, float* base, int r0, int by, const float (&av)[CS], int k0) {
   if (k0 / kTile2 != by) return;
   float* d = base + (int64_t)(r0 + (threadIdx.x & 31)) * H + k0;
 #pragma unroll
-  for (int q = 0; q < CS / 4; ++q) pub4<WT_ACT>(d + 4 * q, av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+  for (int q = 0; q < CS / 4; ++q) pub4<WT_ACT>(wt, d + 4 * q, av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
 }
 
 // a batch row's O inputs, zero past O, branch-free: a clamped index and a compare against O held in a VGPR, so
@@ -616,7 +625,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   if (by == 0 && w == 0 && h == 0) {  // the gathered batch for the later passes
     float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
 #pragma unroll
-    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(a.wt, xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     if (!nrow) {
       float v[5];
       batch_aux(a, item, idx, e0, e1, v);
@@ -625,9 +634,9 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
       // R_LOGPN, P2 writes later in the step)
       static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11,
                     "record layout");
-      pub<WT_ACT>(rc + R_EPS, v[AUX_E0]);
-      pub<WT_ACT>(rc + R_EPSN, v[AUX_E1]);
-      pub4<WT_ACT>(rc + R_REW, v[AUX_REW], v[AUX_TERM], v[AUX_ACT], 0.0f);
+      pub<WT_ACT>(a.wt, rc + R_EPS, v[AUX_E0]);
+      pub<WT_ACT>(a.wt, rc + R_EPSN, v[AUX_E1]);
+      pub4<WT_ACT>(a.wt, rc + R_REW, v[AUX_REW], v[AUX_TERM], v[AUX_ACT], 0.0f);
     }
   }
   (void)B;
@@ -640,18 +649,20 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
     if (c) load_b<CS>(bv, a.T, H, k0, c0 + rl);
     float av[CS];
     first_layer<H, CS>(lw1, lx + rl * (kXLd + 1), O, k0, av);
-    if (!nrow) store_slice<H, CS>(a.s.h1, r0, by, av, k0);
+    if (!nrow) store_slice<H, CS>(a.wt, a.s.h1, r0, by, av, k0);
     mfma_n<CS>(acc, av, bv);
   }
   SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
-    if (r < Bp) pub<WT_EPI>(a.s.h2 + (int64_t)r * H + col, y);
+    if (r < Bp) pub<WT_EPI>(a.wt, a.s.h2 + (int64_t)r * H + col, y);
+    const uint64_t pos = __ballot(y > 0.0f);  // (rows of the two half waves: the low / high 32 bits)
+    if (r < Bp && cc == 0) pub<WT_ACT>(a.wt, a.s.h2m + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
     const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
     if (cc == 0) {
-      pub<WT_ACT>(a.s.hpart + (int64_t)r * 2 * CB + by, pm);
-      pub<WT_ACT>(a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
+      pub<WT_ACT>(a.wt, a.s.hpart + (int64_t)r * 2 * CB + by, pm);
+      pub<WT_ACT>(a.wt, a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
     }
   });
 }
@@ -693,7 +704,7 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
       for (int m = 0; m < kXLd; ++m) q[m] = m == O ? act : xin[m];
       float* qd = a.s.qx + (int64_t)item * kXLd;
 #pragma unroll
-      for (int k = 0; k < kXLd / 4; ++k) pub4<WT_ACT>(qd + 4 * k, q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+      for (int k = 0; k < kXLd / 4; ++k) pub4<WT_ACT>(a.wt, qd + 4 * k, q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
     }
   }
   __syncthreads();
@@ -705,19 +716,21 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
     if (c) load_b<CS>(bv, WT, H, k0, c0 + rl);
     float av[CS], pre[CS];
     first_layer_pre<H, CS>(lw1, lx + rl * (kXLd + 1), O + 1, k0, pre, av);
-    store_slice<H, CS>(a.s.g1[net], r0, by, av, k0);
-    store_slice<H, CS>(a.s.pre[net], r0, by, pre, k0);
+    store_slice<H, CS>(a.wt, a.s.g1[net], r0, by, av, k0);
+    store_slice<H, CS>(a.wt, a.s.pre[net], r0, by, pre, k0);
     mfma_n<CS>(acc, av, bv);
   }
   if (rt == 0 && by == 0)  // fc0's action column, contiguous, for P2
-    for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(a.s.w1a + net * H + k, lw1[O * H + k]);
+    for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(a.wt, a.s.w1a + net * H + k, lw1[O * H + k]);
   SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
-    pub<WT_EPI>(a.s.g2[net] + (int64_t)r * H + col, y);
+    pub<WT_EPI>(a.wt, a.s.g2[net] + (int64_t)r * H + col, y);
+    const uint64_t pos = __ballot(y > 0.0f);
+    if (cc == 0) pub<WT_ACT>(a.wt, a.s.g2m[net] + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
     const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
-    if (cc == 0) pub<WT_ACT>(a.s.part + ((int64_t)r * PS_N + PS_Q1D + net) * CB + by, pq);
+    if (cc == 0) pub<WT_ACT>(a.wt, a.s.part + ((int64_t)r * PS_N + PS_Q1D + net) * CB + by, pq);
   });
 }
 
@@ -751,8 +764,8 @@ __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int 
   for (int m = 0; m < kXLd; ++m)  // (unrolled, the run-time bound a select)
 #pragma unroll
     for (int j = 0; j < 4; ++j) pre[j] = m < O ? fmaf(w1[(cq + j) * (kXLd + 1) + m], x[m], pre[j]) : pre[j];
-  pub4<WT_ACT>(a.s.pre[2 + net] + (int64_t)item * H + c0 + cq, pre[0], pre[1], pre[2], pre[3]);
-  if (rt == 0 && tid < kTile2) pub<WT_ACT>(a.s.w1a + (2 + net) * H + c0 + tid, w1[tid * (kXLd + 1) + O]);
+  pub4<WT_ACT>(a.wt, a.s.pre[2 + net] + (int64_t)item * H + c0 + cq, pre[0], pre[1], pre[2], pre[3]);
+  if (rt == 0 && tid < kTile2) pub<WT_ACT>(a.wt, a.s.w1a + (2 + net) * H + c0 + tid, w1[tid * (kXLd + 1) + O]);
 }
 
 template <int H>
@@ -823,10 +836,10 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   if (w == 0 && h == 0 && net == 0 && by == 0) {
     float* rc = a.s.rec + (int64_t)item * kRec;
     if (kTarget) {
-      pub<WT_ACT>(rc + R_LOGPN, hd[HD_LOGP]);
+      pub<WT_ACT>(a.wt, rc + R_LOGPN, hd[HD_LOGP]);
     } else {
 #pragma unroll
-      for (int q = 0; q < 6; ++q) pub<WT_ACT>(rc + q, hd[q]);
+      for (int q = 0; q < 6; ++q) pub<WT_ACT>(a.wt, rc + q, hd[q]);
     }
   }
   (void)O;
@@ -856,7 +869,7 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   if constexpr (kTarget) {
     splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
       const float pq = halfwave_sum(relu(v + b2c) * w3);
-      if (cc == 0) pub<WT_ACT>(a.s.part + ((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by, pq);
+      if (cc == 0) pub<WT_ACT>(a.wt, a.s.part + ((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by, pq);
     });
   } else {  // Q and its tangent reduced behind one barrier
     splitk_finish2(acc, act, lds, lds + FwdLds<H>::kSplit, [&](int, int rr, int cc, float v, float t) {
@@ -865,11 +878,22 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
       const float pd = halfwave_sum(y > 0.0f ? w3 * t : 0.0f);  // this column block's part of ∂Q/∂ã
       if (cc == 0) {
         float* pr = a.s.part + (int64_t)(r0 + rr) * PS_N * CB + by;
-        pub<WT_ACT>(pr + (PS_Q1A + net) * CB, pq);
-        pub<WT_ACT>(pr + (PS_D1 + net) * CB, pd);
+        pub<WT_ACT>(a.wt, pr + (PS_Q1A + net) * CB, pq);
+        pub<WT_ACT>(a.wt, pr + (PS_D1 + net) * CB, pd);
       }
     });
   }
+}
+
+// mask words a lane's K slice (kb = w·H/4 + h·H/8, H/8 columns) spans, the most over the lanes
+__host__ __device__ constexpr int mask_words(int H) {
+  int most = 1;
+  for (int w = 0; w < 4; ++w)
+    for (int h = 0; h < 2; ++h) {
+      const int kb = w * (H / 4) + h * (H / 8), n = ((kb & 31) + H / 8 - 1) / 32 + 1;
+      most = n > most ? n : most;
+    }
+  return most;
 }
 
 // backward factors (the backward pass of layer 2 for a unit head gradient): out[r][j] = [x1[r][j] > 0] ·
@@ -887,13 +911,20 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   const int r0 = rt * kTile2, j0 = by * kTile2;
   const int kb = w * (H / 4) + h * N2;
   const float* X1 = kActor ? a.s.h1 : a.s.g1[net];
-  const float* X2 = kActor ? a.s.h2 : a.s.g2[net];
+  const uint32_t* X2M = kActor ? a.s.h2m : a.s.g2m[net];
   const float* W2 = kActor ? P + L.p_w2 : C + L.c_w2;
   const float* HW1 = kActor ? P + L.p_wm : C + L.c_w3;
   const float* HW2 = P + L.p_ws;
-  // this lane's layer-2 row segment (its K slice) and the head weights of those columns
-  float x2[N2];
-  load_run<N2>(X2 + (int64_t)(r0 + rl) * H + kb, x2);
+  // [x2 > 0] of this lane's K slice (row r0 + rl, columns kb .. kb + N2 - 1): the mask words covering it, and the
+  // head weights of those columns
+  constexpr int CB = KS::CB, NW = mask_words(H);
+  uint32_t mw[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) mw[q] = X2M[(int64_t)(r0 + rl) * CB + min(kb / 32 + q, CB - 1)];
+  auto pos2 = [&](int i) __attribute__((always_inline)) {  // bit kb + i (compile-time i)
+    const int b = (kb & 31) + i;
+    return ((mw[b >> 5] >> (b & 31)) & 1u) != 0u;
+  };
   float bv[CS];
   load_b<CS>(bv, W2, H, kb, j0 + rl);
   float m1[4];  // [x1 > 0] of the four outputs this lane finishes
@@ -912,11 +943,11 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
     if (c) load_b<CS>(bv, W2, H, kb + c * CS, j0 + rl);
     float av[CS];
 #pragma unroll
-    for (int i = 0; i < CS; ++i) av[i] = x2[c * CS + i] > 0.0f ? hw1[c * CS + i] : 0.0f;
+    for (int i = 0; i < CS; ++i) av[i] = pos2(c * CS + i) ? hw1[c * CS + i] : 0.0f;
     mfma_n<CS>(acc, av, bv);
     if constexpr (kActor) {
 #pragma unroll
-      for (int i = 0; i < CS; ++i) av[i] = x2[c * CS + i] > 0.0f ? hw2[c * CS + i] : 0.0f;
+      for (int i = 0; i < CS; ++i) av[i] = pos2(c * CS + i) ? hw2[c * CS + i] : 0.0f;
       mfma_n<CS>(acc2, av, bv);
     }
   }
@@ -925,12 +956,12 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   if constexpr (kActor) {  // U_m and U_s behind one barrier
     splitk_finish2(acc, acc2, lds, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v, float v2) {
       const int64_t o = (int64_t)(r0 + rr) * H + j0 + cc;
-      pub<WT_EPI>(o1 + o, m1[q] > 0.0f ? v : 0.0f);
-      pub<WT_EPI>(a.s.us + o, m1[q] > 0.0f ? v2 : 0.0f);
+      pub<WT_EPI>(a.wt, o1 + o, m1[q] > 0.0f ? v : 0.0f);
+      pub<WT_EPI>(a.wt, a.s.us + o, m1[q] > 0.0f ? v2 : 0.0f);
     });
   } else {
     splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
-      pub<WT_EPI>(o1 + (int64_t)(r0 + rr) * H + j0 + cc, m1[q] > 0.0f ? v : 0.0f);
+      pub<WT_EPI>(a.wt, o1 + (int64_t)(r0 + rr) * H + j0 + cc, m1[q] > 0.0f ? v : 0.0f);
     });
   }
 }
@@ -942,11 +973,11 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
       const int64_t t = *a.step + 1;
-      pub<WT_ACT>(a.step, t);
+      pub<WT_ACT>(a.wt, a.step, t);
       const AdamStep st = adam_step(a.hp, t);
-      pub<WT_ACT>(a.stats + 5, st.step_pi);
-      pub<WT_ACT>(a.stats + 6, st.step_q);
-      pub<WT_ACT>(a.stats + 7, st.bc2_sqrt);
+      pub<WT_ACT>(a.wt, a.stats + 5, st.step_pi);
+      pub<WT_ACT>(a.wt, a.stats + 6, st.step_q);
+      pub<WT_ACT>(a.wt, a.stats + 7, st.bc2_sqrt);
     }
     // the parameters P3 reads (it updates them in place), before this step's update
     const Layout& L = a.L;
@@ -954,13 +985,13 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
     float* sn = a.s.snap;
     if (threadIdx.x < 5) {
       const int i = threadIdx.x;
-      pub<WT_ACT>(sn + i, i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3]);
+      pub<WT_ACT>(a.wt, sn + i, i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3]);
     }
     for (int j = threadIdx.x; j < L.H; j += kThreads) {
-      pub<WT_ACT>(sn + SN_HEAD + j, P[L.p_wm + j]);
-      pub<WT_ACT>(sn + SN_HEAD + L.H + j, P[L.p_ws + j]);
-      pub<WT_ACT>(sn + SN_HEAD + 2 * L.H + j, P[L.q_base[0] + L.c_w3 + j]);
-      pub<WT_ACT>(sn + SN_HEAD + 3 * L.H + j, P[L.q_base[1] + L.c_w3 + j]);
+      pub<WT_ACT>(a.wt, sn + SN_HEAD + j, P[L.p_wm + j]);
+      pub<WT_ACT>(a.wt, sn + SN_HEAD + L.H + j, P[L.p_ws + j]);
+      pub<WT_ACT>(a.wt, sn + SN_HEAD + 2 * L.H + j, P[L.q_base[0] + L.c_w3 + j]);
+      pub<WT_ACT>(a.wt, sn + SN_HEAD + 3 * L.H + j, P[L.q_base[1] + L.c_w3 + j]);
     }
   }
   int bx, by;
@@ -1066,6 +1097,7 @@ struct ApplyArgs {
   Layout L;
   Hyper hp;
   int n_tile_blocks;  // blocks [0, n_tile_blocks) take 32x32 tiles of the three H x H W2 matrices
+  int wt;             // write-through mask (WT_*)
 };
 
 // one element: loads (ld) and update/stores (st) split so several elements' loads are in flight first. q: the
@@ -1088,13 +1120,13 @@ __device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, 
   const float v = x.v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);   // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
   const float denom = sqrtf(v) / st.bc2_sqrt + a.hp.eps;
   const float p = x.p + (-(q ? st.step_q : st.step_pi)) * (m / denom);
-  pub<WT_OPT>(a.m + e, m);
-  pub<WT_OPT>(a.v + e, v);
-  pub<WT_OPT>(a.params + e, p);
+  pub<WT_OPT>(a.wt, a.m + e, m);
+  pub<WT_OPT>(a.wt, a.v + e, v);
+  pub<WT_OPT>(a.wt, a.params + e, p);
   x.p = p;
   if (q) {
     x.t = x.t * (1.0f - a.hp.tau) + p * a.hp.tau;
-    pub<WT_OPT>(a.targets + (e - a.L.q_base[0]), x.t);
+    pub<WT_OPT>(a.wt, a.targets + (e - a.L.q_base[0]), x.t);
   }
 }
 
@@ -1110,7 +1142,7 @@ struct WArgs {
   ApplyArgs ap;
   // per H x H matrix (0 actor, 1 / 2 Q1 / Q2): the MFMA tiles' operands and output offset, indexed (one scalar
   // load) rather than selected between fields (a live mask and both candidates across the GEMM loop)
-  const float* dy_src[3];  // h2 | g2 Q1 | g2 Q2
+  const uint32_t* dy_mask[3];  // [h2 > 0] | [g2 > 0] Q1 | Q2 (Scr::h2m / g2m)
   const float* x_src[3];   // h1 | g1 Q1 | g1 Q2
   int64_t w2_off[3];       // the W2 block in params (and grads, Adam state)
   int hw_off[3];           // the first head-weight row in snap's SN_HEAD block: wm | w3 Q1 | w3 Q2
@@ -1175,7 +1207,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   const bool actor = mat == 0;
   const int net = actor ? 0 : mat - 1;
   const float* hw = m.s.snap + SN_HEAD;  // pre-update head weights: wm | ws | w3 Q1 | w3 Q2
-  const gptr Y = as_global(a.dy_src[mat]);
+  const uint32_t __attribute__((address_space(1)))* Y = (const uint32_t __attribute__((address_space(1)))*)a.dy_mask[mat];
   const gptr X = as_global(a.x_src[mat]);
   const int jc = j0 + rl;
   const float c1 = hw[a.hw_off[mat] + jc];
@@ -1194,13 +1226,15 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     rin.load(m, r, actor);
     // the chunk's operands as one straight-line batch of loads (a run-time guard per load would make a chain of
     // branches with a wait after every load): n2 = 32 for full chunks, 16 / 8 / 4 for Bp = 128 / 64 / 32
-    float yv[kMaxN2], xv[kMaxN2];
-    const int rb = rc + rl0;
+    // (Y: the [dY-side activation > 0] mask word of column block j0 / 32 per row; this lane's column is bit rl)
+    uint32_t yv[kMaxN2];
+    float xv[kMaxN2];
+    const int rb = rc + rl0, jw = j0 >> 5;
     auto load_chunk = [&](auto n_tag) __attribute__((always_inline)) {
       constexpr int N = decltype(n_tag)::value;
 #pragma unroll
       for (int i = 0; i < N; ++i) {
-        yv[i] = Y[(int64_t)(rb + i) * H + jc];
+        yv[i] = Y[(int64_t)(rb + i) * CB + jw];
         xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
       }
     };
@@ -1211,9 +1245,10 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     else {
 #pragma unroll
       for (int i = 0; i < kMaxN2; ++i) {
-        yv[i] = xv[i] = 0.0f;
+        yv[i] = 0u;
+        xv[i] = 0.0f;
         if (i >= n2) continue;  // (continue, not break: the constant trip count keeps the loop unrolled)
-        yv[i] = Y[(int64_t)(rb + i) * H + jc];
+        yv[i] = Y[(int64_t)(rb + i) * CB + jw];
         xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
       }
     }
@@ -1232,7 +1267,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     }
     if (rc + tid >= B) s0 = s1 = 0.0f;
     SAC_STAMP_ON(2, 4, s0);
-    SAC_STAMP_ON(2, 5, yv[kMaxN2 - 1] + xv[kMaxN2 - 1]);
+    SAC_STAMP_ON(2, 5, (float)yv[kMaxN2 - 1] + xv[kMaxN2 - 1]);
     S.s0[tid] = s0;
     S.s1[tid] = s1;
     __syncthreads();
@@ -1244,7 +1279,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     for (int i = 0; i < kMaxN2; ++i) {
       const float s0v = S.s0[rl0 + i], s1v = S.s1[rl0 + i];
       const float d = actor ? c1 * s0v + c2 * s1v : c1 * s0v;
-      av[i] = yv[i] > 0.0f ? d : 0.0f;
+      av[i] = ((yv[i] >> rl) & 1u) ? d : 0.0f;
     }
     if (n2 == kMaxN2) mfma_n<kMaxN2>(acc, av, xv);  // (full chunks: one straight chain)
     else mfma_chain(acc, av, xv, n2);
@@ -1260,7 +1295,7 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   const int64_t out_off = a.w2_off[mat];
   splitk_finish(acc, S.u.mm.split, [&](int q, int rr, int cc, float v) {
     const int64_t e = out_off + (int64_t)(j0 + rr) * H + k0 + cc;
-    pub<WT_OPT>(a.grads + e, v);
+    pub<WT_OPT>(a.ap.wt, a.grads + e, v);
     if (a.fuse) {
       xe[q].g = v;
       adam_st(a.ap, sst, e, xe[q], mat > 0);
@@ -1274,8 +1309,8 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     const int tc = tid % kTile2, tr = tid / kTile2;
     for (int cc = tr; cc < kTile2; cc += kThreads / kTile2) {
       const int64_t o = (int64_t)(k0 + cc) * H + j0 + tc;
-      pub<WT_OPT>(a.ap.T + (size_t)mat * HH + o, tt[0][cc][tc]);
-      if (mat > 0) pub<WT_OPT>(a.ap.T + (size_t)(2 + mat) * HH + o, tt[1][cc][tc]);
+      pub<WT_OPT>(a.ap.wt, a.ap.T + (size_t)mat * HH + o, tt[0][cc][tc]);
+      if (mat > 0) pub<WT_OPT>(a.ap.wt, a.ap.T + (size_t)(2 + mat) * HH + o, tt[1][cc][tc]);
     }
   }
   }
@@ -1403,7 +1438,7 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
 #pragma unroll
     for (int st = 1; st < kValuStreams; ++st) g += vr[st][i][u];
     const int64_t e = el_off(k);
-    pub<WT_OPT>(a.grads + e, g);
+    pub<WT_OPT>(a.ap.wt, a.grads + e, g);
     if (a.fuse) {
       xe[q].g = g;
       adam_st(a.ap, sst, e, xe[q], !actor);
@@ -1469,7 +1504,7 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   }
   if (tid >= 5) return;
   const float g = tid == 0 ? (m.hp.auto_ent ? sum[4] * invB : 0.0f) : sum[4 + tid];
-  pub<WT_OPT>(a.grads + off, g);
+  pub<WT_OPT>(a.ap.wt, a.grads + off, g);
   if (a.fuse && (tid > 0 || m.hp.auto_ent)) {
     xs.g = g;
     adam_st(a.ap, sst, off, xs, tid >= 3);
@@ -1492,12 +1527,12 @@ __device__ __forceinline__ void p3_stage_block(const WArgs& a, int sb) {
   float* dn = m.s.sxn + (int64_t)item * kXLd;
 #pragma unroll
   for (int q = 0; q < kXLd / 4; ++q) {
-    pub4<WT_ACT>(dx + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-    pub4<WT_ACT>(dn + 4 * q, xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
+    pub4<WT_ACT>(m.wt, dx + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    pub4<WT_ACT>(m.wt, dn + 4 * q, xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
   }
   float* q = m.s.saux + (int64_t)item * kAux;
-  pub4<WT_ACT>(q, act, rew, term, e0);
-  pub<WT_ACT>(q + AUX_E1, e1);
+  pub4<WT_ACT>(m.wt, q, act, rew, term, e0);
+  pub<WT_ACT>(m.wt, q + AUX_E1, e1);
 }
 
 // the kernel's WArgs read through the kernarg segment pointer, laundered: a field is a scalar load where a block
@@ -1552,10 +1587,10 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
     for (int cc = tr; cc < kTile2; cc += kThreads / kTile2) {
       const int64_t o = (int64_t)(c0 + cc) * H + r0 + tc;  // T[col][row]
       if (mat == 0) {
-        pub<WT_OPT>(a.T + o, tile[0][cc][tc]);
+        pub<WT_OPT>(a.wt, a.T + o, tile[0][cc][tc]);
       } else {
-        pub<WT_OPT>(a.T + (size_t)mat * HH + o, tile[0][cc][tc]);
-        pub<WT_OPT>(a.T + (size_t)(2 + mat) * HH + o, tile[1][cc][tc]);
+        pub<WT_OPT>(a.wt, a.T + (size_t)mat * HH + o, tile[0][cc][tc]);
+        pub<WT_OPT>(a.wt, a.T + (size_t)(2 + mat) * HH + o, tile[1][cc][tc]);
       }
     }
     return;
@@ -1886,7 +1921,7 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   const int64_t Bp = L.Bp, BH = Bp * H, CB = H / kTile2;
   // rows 3·16, activations 10·H, the row record, parts (2 + 8)·CB, the snapshot
   const int64_t n_scr = Bp * 3 * kXLd + 14 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H + 4 * H +
-                        Bp * (2 * kXLd + kAux);
+                        Bp * (2 * kXLd + kAux) + 3 * Bp * CB;
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
     *out = h;
@@ -1919,6 +1954,11 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   sc.sx = s; s += Bp * kXLd;
   sc.sxn = s; s += Bp * kXLd;
   sc.saux = s; s += Bp * kAux;
+  sc.h2m = reinterpret_cast<uint32_t*>(s); s += Bp * CB;
+  for (int k = 0; k < 2; ++k) {
+    sc.g2m[k] = reinterpret_cast<uint32_t*>(s);
+    s += Bp * CB;
+  }
   e = hipMalloc(&h->T, sizeof(float) * 5 * (size_t)H * H);
   if (e != hipSuccess) {
     *out = h;
@@ -1990,8 +2030,13 @@ int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const fl
   return SACF_OK;
 }
 
+// the write-through mask of a step's launches (see pub): everything from 128 padded rows up, below that not the row
+// inputs / parts / records (WT_ACT), whose write-through costs more there than the write-back it saves
+static int wt_mask_for(const Layout& L) { return L.Bp >= 128 ? (WT_ACT | WT_OPT | WT_EPI) : (WT_OPT | WT_EPI); }
+
 static ApplyArgs apply_args(const sacf_handle* h) {
   ApplyArgs a;
+  a.wt = wt_mask_for(h->L);
   a.params = h->params;
   a.targets = h->targets;
   a.grads = h->grads;
@@ -2027,6 +2072,7 @@ static int grads_impl(sacf_handle* h, const float* obs, const float* act, const 
   a.seed = h->seed;
   a.eps = eps;
   a.chain = chain;
+  a.wt = wt_mask_for(h->L);
   a.step = h->step;
   a.stats = h->stats;
   a.s = h->s;
@@ -2044,7 +2090,7 @@ static int grads_impl(sacf_handle* h, const float* obs, const float* act, const 
   w.n_stage = (chain & SACF_CHAIN_STAGE_NEXT) ? (int)((h->L.Bp + kThreads - 1) / kThreads) : 0;
   const Layout& L = h->L;
   for (int mat = 0; mat < 3; ++mat) {
-    w.dy_src[mat] = mat == 0 ? h->s.h2 : h->s.g2[mat - 1];
+    w.dy_mask[mat] = mat == 0 ? h->s.h2m : h->s.g2m[mat - 1];
     w.x_src[mat] = mat == 0 ? h->s.h1 : h->s.g1[mat - 1];
     w.w2_off[mat] = mat == 0 ? L.p_w2 : L.q_base[mat - 1] + L.c_w2;
     w.hw_off[mat] = mat == 0 ? 0 : (mat + 1) * L.H;

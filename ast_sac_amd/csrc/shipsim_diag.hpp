@@ -8,6 +8,8 @@
 //   -DSHIPSIM_ABL_*          ablations (scripts/build_ablations.sh; timing only, results intentionally differ):
 //                            NO_WIND, NO_MAPDIST, NO_GROUND, NO_SBLOOP, SB_NEVER, SB_NONE
 //   -DSHIPSIM_C2_ONE_WAVE    C2 simplified ticks on the one-wave single_tick_kernel (same results; timing A/B)
+//   -DSHIPSIM_SB_STATS       multi-obstacle SBMPC counters (requests, passes, lone passes, obstacle evaluations),
+//                            read back through shipsim_diag_lane_faults (words 16..31: eight u64)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -56,6 +58,28 @@ __device__ __forceinline__ bool sb_request(bool need, int max_sampling) {
   return need;
 #endif
 }
+
+// ---- multi-obstacle SBMPC counters (SHIPSIM_SB_STATS) -----------------------------------------------------------
+// [0] wave-ticks whose optimiser ran a pass, [1] passes, [2] lone-request passes, [3] requests served, [4] obstacle
+// evaluations (scenario lanes with a horizon), [5] far-skipped obstacle evaluations (scenario lanes), [6] env-ticks
+// with a request, [7] env-ticks (the test ship's sub-lane 0 ticking)
+#ifdef SHIPSIM_SB_STATS
+__device__ unsigned long long g_sb_stats[8];
+// v summed over the wave's active lanes, one atomic per wave
+__device__ __forceinline__ void sb_stat_lanes(int k, unsigned v) {
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  const unsigned long long t = __popcll(__ballot(v != 0));
+  if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)ex) - 1 && t) atomicAdd(&g_sb_stats[k], t);
+}
+// v once per wave (a wave-uniform value)
+__device__ __forceinline__ void sb_stat_wave(int k, unsigned v) {
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)ex) - 1 && v) atomicAdd(&g_sb_stats[k], (unsigned long long)v);
+}
+#else
+__device__ __forceinline__ void sb_stat_lanes(int, unsigned) {}
+__device__ __forceinline__ void sb_stat_wave(int, unsigned) {}
+#endif
 
 // ---- lane / index checks ---------------------------------------------------------------------------------------
 // Every cross-lane exchange checks that the lanes it reads are active (the env's LPE lanes for the DPP / shuffle

@@ -821,6 +821,7 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
   const int half = lane >> 5;
   const int scen = lane & 31;
   uint64_t req = __ballot(need);
+  diag::sb_stat_wave(0, req ? 1u : 0u);
   while (req) {
     // the counts re-derived per pass: tests on them are not hoisted out of this loop and held across it
     const int n_obs_p = opaque_s(n_obs), n_samp_p = opaque_s(n_samp);
@@ -832,6 +833,9 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
       req &= req - 1;
     }
     const bool split = src1 < 0;  // (uniform) one request this pass: the halves split its obstacles
+    diag::sb_stat_wave(1, 1u);
+    diag::sb_stat_wave(2, split ? 1u : 0u);
+    diag::sb_stat_wave(3, split ? 1u : 2u);
     int src = half ? src1 : src0;
     const int srcc = src < 0 ? src0 : src;
     SbIn g;
@@ -864,6 +868,8 @@ __device__ __forceinline__ void sbmpc_cooperative_multi(bool need, const SbMulti
         // an obstacle out of reach costs exactly sbmpc_h2 in every scenario (added once below)
         const bool far = ok && sbmpc_far(q, n_samp_p, DT);
         any_far = any_far || far;
+        diag::sb_stat_lanes(4, (ok && !far) ? 1u : 0u);
+        diag::sb_stat_lanes(5, far ? 1u : 0u);
         if (ok && !far) {
           sb_set_heading_trig(q);
           const double ck = sbmpc_scenario_cost(q, opaque_s(n_samp_p), DT, scen >> 2, scen & 3);
@@ -1808,6 +1814,9 @@ __global__ __launch_bounds__(64) void ast_step_kernel(const StepArgs A_arg) {
         in.p_last = p_last; in.chi_last = chi_last;
       }
       double pb = 1.0, cb = 0.0;
+      need = diag::sb_request(need, P.max_sampling);  // (the product: need itself)
+      diag::sb_stat_lanes(6, (need && sub == 0) ? 1u : 0u);
+      diag::sb_stat_lanes(7, (going && is_test && sub == 0) ? 1u : 0u);
       sbmpc_cooperative_multi<NOB>(need && sub == 0, in, nsh - 1, P.sbmpc_nsamp, P.sbmpc_dt, pb, cb);
       pb = env_lane_d<LPE, 0>(pb, env_lane0);
       cb = env_lane_d<LPE, 0>(cb, env_lane0);
@@ -3841,6 +3850,13 @@ int shipsim_diag_lane_faults(uint32_t* out32) {
   if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(diag::g_lane_diag), 32 * sizeof(uint32_t)) != hipSuccess) return SHIPSIM_EHIP;
   const uint32_t zero[32] = {};
   if (hipMemcpyToSymbol(HIP_SYMBOL(diag::g_lane_diag), zero, sizeof(zero)) != hipSuccess) return SHIPSIM_EHIP;
+  return SHIPSIM_OK;
+#elif defined(SHIPSIM_SB_STATS)
+  if (hipDeviceSynchronize() != hipSuccess) return SHIPSIM_EHIP;
+  if (hipMemcpyFromSymbol(out32 + 16, HIP_SYMBOL(diag::g_sb_stats), 8 * sizeof(uint64_t)) != hipSuccess)
+    return SHIPSIM_EHIP;
+  const uint64_t zero[8] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(diag::g_sb_stats), zero, sizeof(zero)) != hipSuccess) return SHIPSIM_EHIP;
   return SHIPSIM_OK;
 #else
   return SHIPSIM_EINVAL;  // not a diagnostics build

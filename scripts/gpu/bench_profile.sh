@@ -5,7 +5,7 @@
 . "$(dirname "$0")/common.sh"
 TAG=${1:-bench}; PMC=${2:-}
 export TMPDIR=/tmp
-B="$R/bench.py --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream"
+B="$R/bench.py --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream --no-c4 --no-c5"
 if [ -n "$PMC" ]; then
   cd /tmp
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_$TAG" -o run -- python3 $B \

@@ -9,10 +9,10 @@ for i in $(seq 1 "$REPS"); do
   for n in tree "$@"; do
     f="$O/eabn_${TAG}_${n}_$i.json"
     if [ "$n" = tree ]; then
-      timeout -k 10 300 python bench.py --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream $ARGS > "$f" 2> "$f.err"
+      timeout -k 10 300 python bench.py --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream --no-c4 --no-c5 $ARGS > "$f" 2> "$f.err"
     else
       SHIPSIM_LIB=$R/ast_sac_amd/lib/abl/$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --sac-steps 0 --no-c2 \
-        --no-policy-stream $ARGS > "$f" 2> "$f.err"
+        --no-policy-stream --no-c4 --no-c5 $ARGS > "$f" 2> "$f.err"
     fi
     hard $? "$n"
     line="$line $n $(v "$f") M |"

@@ -39,7 +39,7 @@ tail -c 700 "$O/c4_loop_$TAG.json"; echo
 # the bench line's PMC inputs (HBM traffic, FP64 VALU), when the call has the time left for three short passes
 if [ "$SECONDS" -lt 780 ]; then
   echo "== pmc"; date +%T
-  B="$R/bench.py --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream"
+  B="$R/bench.py --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream --no-c4 --no-c5"
   cd /tmp
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_$TAG" -o run -- python3 $B \
     > "$O/pmc_fetch_$TAG.log" 2>&1; hard $? pmc_fetch

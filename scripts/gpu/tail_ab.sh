@@ -4,7 +4,7 @@
 . "$(dirname "$0")/common.sh"
 TAG=${1:-tail}; REPS=${2:-2}
 v() { python -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);print(round(d['value']/1e6,1),'M', round(d['ms_per_step'],2),'ms')"; }
-B="--collav sbmpc --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream"
+B="--collav sbmpc --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream --no-c4 --no-c5"
 for i in $(seq 1 "$REPS"); do
   timeout -k 10 200 python bench.py $B > "$O/tab_${TAG}_tail_$i.log" 2>&1; hard $? tail
   timeout -k 10 200 python bench.py $B --tail-ticks 0 > "$O/tab_${TAG}_notail_$i.log" 2>&1; hard $? notail

@@ -6,7 +6,7 @@ TAG=$1; REPS=$2; shift 2
 SQ=0; if [ "${1:-}" = sq ]; then SQ=1; shift; fi
 export TMPDIR=/tmp
 v() { python -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);print(round(d['value']/1e6,1),'M',round(d['roofline']['kernel_ms_timed'],3),'ms')"; }
-B="--collav sbmpc --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream"
+B="--collav sbmpc --no-cpu-baseline --sac-steps 0 --no-c2 --no-policy-stream --no-c4 --no-c5"
 for i in $(seq 1 "$REPS"); do
   line="rep $i:"
   for n in "$@"; do

@@ -18,14 +18,18 @@ DIAG = os.path.join(ROOT, "ast_sac_amd", "lib", "diag", "libsacfused_timing.so")
 KSTAMP, NST = 8192, 8
 
 
-def build():
+def diag_path(variant=None):
+    return DIAG if not variant else DIAG.replace(".so", f"_{variant}.so")
+
+
+def build(variant=None, flags=()):
     sys.path.insert(0, ROOT)
     from __graft_entry__ import HIPCC, HIPFLAGS, SAC_SRC
     from ast_sac_amd.build_hash import LIB_FLAGS
     os.makedirs(os.path.dirname(DIAG), exist_ok=True)
     subprocess.check_call([HIPCC] + HIPFLAGS + LIB_FLAGS["sacfused"] + ["-mllvm", "-amdgpu-sched-strategy=max-ilp"] + ["-DSACF_PHASE_TIMING", '-DSACF_SRC_HASH="diag"']
-                          + SAC_SRC + ["-o", DIAG])
-    print("built", DIAG)
+                          + list(flags) + SAC_SRC + ["-o", diag_path(variant)])
+    print("built", diag_path(variant))
 
 
 def kinds(kernel, nblocks, bt, cb, n_mfma, n_valu):
@@ -51,10 +55,12 @@ def main():
     p.add_argument("--hidden", type=int, default=256)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--out", default=None)
+    p.add_argument("--variant", default=None, help="diagnostics build name suffix (libsacfused_timing_<v>.so)")
+    p.add_argument("--flags", default="", help="--build: extra hipcc flags, e.g. -DSACF_WT=0")
     a = p.parse_args()
     if a.build:
-        return build()
-    os.environ["SACFUSED_LIB"] = DIAG
+        return build(a.variant, a.flags.split())
+    os.environ["SACFUSED_LIB"] = diag_path(a.variant)
     sys.path.insert(0, ROOT)
     import torch
     import bench

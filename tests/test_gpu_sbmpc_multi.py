@@ -15,6 +15,14 @@ from ast_sac_amd import shipsim_abi as abi
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
 def _requests_from_fixture(g, K):
     ins, outs = g[f"k{K}_in"], g[f"k{K}_out"]
     reqs, refs = [], []
