@@ -232,14 +232,22 @@ __device__ inline void block_sum(float (&v)[N], float (*red)[32], float* out) {
 #define SACF_WT 7
 #endif
 enum { WT_ACT = 1, WT_OPT = 2, WT_EPI = 4 };
+// the two masks the step kernels are instantiated with (the launch picks by batch: wt_mask_for)
+constexpr int kWtLarge = WT_ACT | WT_OPT | WT_EPI, kWtSmall = WT_OPT | WT_EPI;
+// (wt: the launch's mask — a template argument of every kernel that stores, so the test folds at compile time: a
+// run-time test per store cost 2 µs per grad step)
+template <int KIND>
+__device__ __forceinline__ bool wt_on(int wt) {
+  return (SACF_WT & KIND) != 0 && (wt & KIND) != 0;
+}
 template <int KIND, class T>
 __device__ __forceinline__ void pub(int wt, T* p, T v) {
-  if ((SACF_WT & KIND) != 0 && (wt & KIND) != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;  // (wt: the launch's mask, uniform)
+  if (wt_on<KIND>(wt)) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
 }
 template <int KIND>
 __device__ __forceinline__ void pub4(int wt, float* p, float x, float y, float z, float w) {
-  if ((SACF_WT & KIND) != 0 && (wt & KIND) != 0) {
+  if (wt_on<KIND>(wt)) {
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     const f32x4 v = {x, y, z, w};
     // (the compiler's hazard recognizer does not see an asm store: a store of more than 8 bytes needs a wait state
@@ -587,7 +595,7 @@ __device__ __forceinline__ void tile_of(int& bx, int& by) {
 // ---------------------------------------------------------------------------------------------
 // actor forward (gaussian_policy.py:105-118 up to the heads, mlp.py:86-99): h1 = relu(W1 x + b1) on the VALU,
 // h2 = relu(h1 W2ᵀ + b2) on MFMA, the mean / log_std head parts of this column block in the epilogue
-template <int H>
+template <int H, int WTM>
 __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, float* lds) {
   using KS = KSlice<H>;
   constexpr int CS = KS::CS, CB = KS::CB;
@@ -625,7 +633,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   if (by == 0 && w == 0 && h == 0) {  // the gathered batch for the later passes
     float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
 #pragma unroll
-    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(a.wt, xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(WTM, xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     if (!nrow) {
       float v[5];
       batch_aux(a, item, idx, e0, e1, v);
@@ -634,9 +642,9 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
       // R_LOGPN, P2 writes later in the step)
       static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11,
                     "record layout");
-      pub<WT_ACT>(a.wt, rc + R_EPS, v[AUX_E0]);
-      pub<WT_ACT>(a.wt, rc + R_EPSN, v[AUX_E1]);
-      pub4<WT_ACT>(a.wt, rc + R_REW, v[AUX_REW], v[AUX_TERM], v[AUX_ACT], 0.0f);
+      pub<WT_ACT>(WTM, rc + R_EPS, v[AUX_E0]);
+      pub<WT_ACT>(WTM, rc + R_EPSN, v[AUX_E1]);
+      pub4<WT_ACT>(WTM, rc + R_REW, v[AUX_REW], v[AUX_TERM], v[AUX_ACT], 0.0f);
     }
   }
   (void)B;
@@ -649,27 +657,27 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
     if (c) load_b<CS>(bv, a.T, H, k0, c0 + rl);
     float av[CS];
     first_layer<H, CS>(lw1, lx + rl * (kXLd + 1), O, k0, av);
-    if (!nrow) store_slice<H, CS>(a.wt, a.s.h1, r0, by, av, k0);
+    if (!nrow) store_slice<H, CS>(WTM, a.s.h1, r0, by, av, k0);
     mfma_n<CS>(acc, av, bv);
   }
   SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
-    if (r < Bp) pub<WT_EPI>(a.wt, a.s.h2 + (int64_t)r * H + col, y);
+    if (r < Bp) pub<WT_EPI>(WTM, a.s.h2 + (int64_t)r * H + col, y);
     const uint64_t pos = __ballot(y > 0.0f);  // (rows of the two half waves: the low / high 32 bits)
-    if (r < Bp && cc == 0) pub<WT_ACT>(a.wt, a.s.h2m + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
+    if (r < Bp && cc == 0) pub<WT_ACT>(WTM, a.s.h2m + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
     const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
     if (cc == 0) {
-      pub<WT_ACT>(a.wt, a.s.hpart + (int64_t)r * 2 * CB + by, pm);
-      pub<WT_ACT>(a.wt, a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
+      pub<WT_ACT>(WTM, a.s.hpart + (int64_t)r * 2 * CB + by, pm);
+      pub<WT_ACT>(WTM, a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
     }
   });
 }
 
 // critic forward on the (obs, a) data rows of one critic (mlp.py:127-136 ConcatMlp): the row's observation and
 // replayed action straight from the batch source (the same Philox draw as the actor tile's gather)
-template <int H>
+template <int H, int WTM>
 __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, int by, float* lds) {
   using KS = KSlice<H>;
   constexpr int CS = KS::CS, CB = KS::CB;
@@ -704,7 +712,7 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
       for (int m = 0; m < kXLd; ++m) q[m] = m == O ? act : xin[m];
       float* qd = a.s.qx + (int64_t)item * kXLd;
 #pragma unroll
-      for (int k = 0; k < kXLd / 4; ++k) pub4<WT_ACT>(a.wt, qd + 4 * k, q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+      for (int k = 0; k < kXLd / 4; ++k) pub4<WT_ACT>(WTM, qd + 4 * k, q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
     }
   }
   __syncthreads();
@@ -716,21 +724,21 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
     if (c) load_b<CS>(bv, WT, H, k0, c0 + rl);
     float av[CS], pre[CS];
     first_layer_pre<H, CS>(lw1, lx + rl * (kXLd + 1), O + 1, k0, pre, av);
-    store_slice<H, CS>(a.wt, a.s.g1[net], r0, by, av, k0);
-    store_slice<H, CS>(a.wt, a.s.pre[net], r0, by, pre, k0);
+    store_slice<H, CS>(WTM, a.s.g1[net], r0, by, av, k0);
+    store_slice<H, CS>(WTM, a.s.pre[net], r0, by, pre, k0);
     mfma_n<CS>(acc, av, bv);
   }
   if (rt == 0 && by == 0)  // fc0's action column, contiguous, for P2
-    for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(a.wt, a.s.w1a + net * H + k, lw1[O * H + k]);
+    for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(WTM, a.s.w1a + net * H + k, lw1[O * H + k]);
   SAC_STAMP(0, 2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr, col = c0 + cc;
     const float y = relu(v + b2c);
-    pub<WT_EPI>(a.wt, a.s.g2[net] + (int64_t)r * H + col, y);
+    pub<WT_EPI>(WTM, a.s.g2[net] + (int64_t)r * H + col, y);
     const uint64_t pos = __ballot(y > 0.0f);
-    if (cc == 0) pub<WT_ACT>(a.wt, a.s.g2m[net] + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
+    if (cc == 0) pub<WT_ACT>(WTM, a.s.g2m[net] + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
     const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
-    if (cc == 0) pub<WT_ACT>(a.wt, a.s.part + ((int64_t)r * PS_N + PS_Q1D + net) * CB + by, pq);
+    if (cc == 0) pub<WT_ACT>(WTM, a.s.part + ((int64_t)r * PS_N + PS_Q1D + net) * CB + by, pq);
   });
 }
 
@@ -738,7 +746,7 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
 // by·32 .. by·32 + 31: the block stages those 32 rows of W1 (and b1) in LDS with coalesced loads, then thread t takes
 // row t / 8 and four columns, the fmaf chain from the bias in input order as first_layer; row tile 0 also writes
 // fc0's action column of those columns
-template <int H>
+template <int H, int WTM>
 __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int rt, int by, float* lds) {
   const Layout& L = a.L;
   const int O = L.O, nin = O + 1;
@@ -764,20 +772,20 @@ __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int 
   for (int m = 0; m < kXLd; ++m)  // (unrolled, the run-time bound a select)
 #pragma unroll
     for (int j = 0; j < 4; ++j) pre[j] = m < O ? fmaf(w1[(cq + j) * (kXLd + 1) + m], x[m], pre[j]) : pre[j];
-  pub4<WT_ACT>(a.wt, a.s.pre[2 + net] + (int64_t)item * H + c0 + cq, pre[0], pre[1], pre[2], pre[3]);
-  if (rt == 0 && tid < kTile2) pub<WT_ACT>(a.wt, a.s.w1a + (2 + net) * H + c0 + tid, w1[tid * (kXLd + 1) + O]);
+  pub4<WT_ACT>(WTM, a.s.pre[2 + net] + (int64_t)item * H + c0 + cq, pre[0], pre[1], pre[2], pre[3]);
+  if (rt == 0 && tid < kTile2) pub<WT_ACT>(WTM, a.s.w1a + (2 + net) * H + c0 + tid, w1[tid * (kXLd + 1) + O]);
 }
 
-template <int H>
+template <int H, int WT>
 __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
   __shared__ float lds[FwdLds<H>::kFloats];
   SAC_STAMP(0, 0);
   int bx, by;
   tile_of<H>(bx, by);
   const int bt = a.L.Bp / kTile2;
-  if (bx < 2 * bt) p1_actor_tile<H>(a, bx, by, lds);
-  else if (bx < 4 * bt) p1_data_tile<H>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
-  else p1_target_pre_tile<H>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by, lds);
+  if (bx < 2 * bt) p1_actor_tile<H, WT>(a, bx, by, lds);
+  else if (bx < 4 * bt) p1_data_tile<H, WT>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
+  else p1_target_pre_tile<H, WT>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by, lds);
   SAC_STAMP(0, 3);
 }
 
@@ -803,7 +811,7 @@ struct RowHeadIn {
 // Q(obs, ã) of critic `net` and its tangent along the action: with t1 = [g1 > 0] ⊙ W1[:, a] (fc0's action
 // column), v = t1 W2ᵀ and ∂Q/∂ã = Σ_cols w3 ⊙ [g2 > 0] ⊙ v (forward mode: one more MFMA chain on the same W2ᵀ
 // operand). Also target rows (kTarget: T1 / T2 on (next_obs, ã'), no tangent).
-template <int H, bool kTarget>
+template <int H, bool kTarget, int WTM>
 __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, int by, float* lds) {
   using KS = KSlice<H>;
   constexpr int CS = KS::CS, CB = KS::CB;
@@ -836,10 +844,10 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   if (w == 0 && h == 0 && net == 0 && by == 0) {
     float* rc = a.s.rec + (int64_t)item * kRec;
     if (kTarget) {
-      pub<WT_ACT>(a.wt, rc + R_LOGPN, hd[HD_LOGP]);
+      pub<WT_ACT>(WTM, rc + R_LOGPN, hd[HD_LOGP]);
     } else {
 #pragma unroll
-      for (int q = 0; q < 6; ++q) pub<WT_ACT>(a.wt, rc + q, hd[q]);
+      for (int q = 0; q < 6; ++q) pub<WT_ACT>(WTM, rc + q, hd[q]);
     }
   }
   (void)O;
@@ -869,7 +877,7 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   if constexpr (kTarget) {
     splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
       const float pq = halfwave_sum(relu(v + b2c) * w3);
-      if (cc == 0) pub<WT_ACT>(a.wt, a.s.part + ((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by, pq);
+      if (cc == 0) pub<WT_ACT>(WTM, a.s.part + ((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by, pq);
     });
   } else {  // Q and its tangent reduced behind one barrier
     splitk_finish2(acc, act, lds, lds + FwdLds<H>::kSplit, [&](int, int rr, int cc, float v, float t) {
@@ -878,8 +886,8 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
       const float pd = halfwave_sum(y > 0.0f ? w3 * t : 0.0f);  // this column block's part of ∂Q/∂ã
       if (cc == 0) {
         float* pr = a.s.part + (int64_t)(r0 + rr) * PS_N * CB + by;
-        pub<WT_ACT>(a.wt, pr + (PS_Q1A + net) * CB, pq);
-        pub<WT_ACT>(a.wt, pr + (PS_D1 + net) * CB, pd);
+        pub<WT_ACT>(WTM, pr + (PS_Q1A + net) * CB, pq);
+        pub<WT_ACT>(WTM, pr + (PS_D1 + net) * CB, pd);
       }
     });
   }
@@ -900,7 +908,7 @@ __host__ __device__ constexpr int mask_words(int H) {
 // Σ_c W2[c][j] · hw[c] · [x2[r][c] > 0], with (x1, x2, hw) = (h1, h2, wm) and (h1, h2, ws) for the actor
 // (kActor: two chains on the same W2 operand) or (g1, g2, w3) of a critic on its data rows. The B operand is
 // W2 in its own (out, in) row-major layout: B[k = c][n = j] = W2[c][j].
-template <int H, bool kActor>
+template <int H, bool kActor, int WTM>
 __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, int by, float* lds) {
   using KS = KSlice<H>;
   constexpr int CS = KS::CS, N2 = KS::N2;
@@ -956,28 +964,28 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   if constexpr (kActor) {  // U_m and U_s behind one barrier
     splitk_finish2(acc, acc2, lds, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v, float v2) {
       const int64_t o = (int64_t)(r0 + rr) * H + j0 + cc;
-      pub<WT_EPI>(a.wt, o1 + o, m1[q] > 0.0f ? v : 0.0f);
-      pub<WT_EPI>(a.wt, a.s.us + o, m1[q] > 0.0f ? v2 : 0.0f);
+      pub<WT_EPI>(WTM, o1 + o, m1[q] > 0.0f ? v : 0.0f);
+      pub<WT_EPI>(WTM, a.s.us + o, m1[q] > 0.0f ? v2 : 0.0f);
     });
   } else {
     splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
-      pub<WT_EPI>(a.wt, o1 + (int64_t)(r0 + rr) * H + j0 + cc, m1[q] > 0.0f ? v : 0.0f);
+      pub<WT_EPI>(WTM, o1 + (int64_t)(r0 + rr) * H + j0 + cc, m1[q] > 0.0f ? v : 0.0f);
     });
   }
 }
 
-template <int H>
+template <int H, int WT>
 __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   __shared__ float lds[FwdLds<H>::kFloats];
   SAC_STAMP(1, 0);
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
       const int64_t t = *a.step + 1;
-      pub<WT_ACT>(a.wt, a.step, t);
+      pub<WT_ACT>(WT, a.step, t);
       const AdamStep st = adam_step(a.hp, t);
-      pub<WT_ACT>(a.wt, a.stats + 5, st.step_pi);
-      pub<WT_ACT>(a.wt, a.stats + 6, st.step_q);
-      pub<WT_ACT>(a.wt, a.stats + 7, st.bc2_sqrt);
+      pub<WT_ACT>(WT, a.stats + 5, st.step_pi);
+      pub<WT_ACT>(WT, a.stats + 6, st.step_q);
+      pub<WT_ACT>(WT, a.stats + 7, st.bc2_sqrt);
     }
     // the parameters P3 reads (it updates them in place), before this step's update
     const Layout& L = a.L;
@@ -985,22 +993,22 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
     float* sn = a.s.snap;
     if (threadIdx.x < 5) {
       const int i = threadIdx.x;
-      pub<WT_ACT>(a.wt, sn + i, i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3]);
+      pub<WT_ACT>(WT, sn + i, i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3]);
     }
     for (int j = threadIdx.x; j < L.H; j += kThreads) {
-      pub<WT_ACT>(a.wt, sn + SN_HEAD + j, P[L.p_wm + j]);
-      pub<WT_ACT>(a.wt, sn + SN_HEAD + L.H + j, P[L.p_ws + j]);
-      pub<WT_ACT>(a.wt, sn + SN_HEAD + 2 * L.H + j, P[L.q_base[0] + L.c_w3 + j]);
-      pub<WT_ACT>(a.wt, sn + SN_HEAD + 3 * L.H + j, P[L.q_base[1] + L.c_w3 + j]);
+      pub<WT_ACT>(WT, sn + SN_HEAD + j, P[L.p_wm + j]);
+      pub<WT_ACT>(WT, sn + SN_HEAD + L.H + j, P[L.p_ws + j]);
+      pub<WT_ACT>(WT, sn + SN_HEAD + 2 * L.H + j, P[L.q_base[0] + L.c_w3 + j]);
+      pub<WT_ACT>(WT, sn + SN_HEAD + 3 * L.H + j, P[L.q_base[1] + L.c_w3 + j]);
     }
   }
   int bx, by;
   tile_of<H>(bx, by);
   const int bt = a.L.Bp / kTile2;
-  if (bx < 2 * bt) p2_critic_tile<H, false>(a, bx / bt, bx % bt, by, lds);
-  else if (bx < 3 * bt) p2_factor_tile<H, true>(a, 0, bx - 2 * bt, by, lds);
-  else if (bx < 5 * bt) p2_critic_tile<H, true>(a, (bx - 3 * bt) / bt, (bx - 3 * bt) % bt, by, lds);
-  else p2_factor_tile<H, false>(a, (bx - 5 * bt) / bt, (bx - 5 * bt) % bt, by, lds);
+  if (bx < 2 * bt) p2_critic_tile<H, false, WT>(a, bx / bt, bx % bt, by, lds);
+  else if (bx < 3 * bt) p2_factor_tile<H, true, WT>(a, 0, bx - 2 * bt, by, lds);
+  else if (bx < 5 * bt) p2_critic_tile<H, true, WT>(a, (bx - 3 * bt) / bt, (bx - 3 * bt) % bt, by, lds);
+  else p2_factor_tile<H, false, WT>(a, (bx - 5 * bt) / bt, (bx - 5 * bt) % bt, by, lds);
   SAC_STAMP(1, 3);
 }
 
@@ -1114,19 +1122,19 @@ __device__ __forceinline__ AdamElem adam_ld(const ApplyArgs& a, int64_t e, bool 
   x.t = q ? a.targets[e - a.L.q_base[0]] : 0.0f;
   return x;
 }
-__device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, int64_t e, AdamElem& x, bool q) {
+__device__ __forceinline__ void adam_st(const ApplyArgs& a, const AdamStep& st, int64_t e, AdamElem& x, bool q, int wt) {
   const float g = x.g * a.hp.inv_world;
   const float m = x.m + (1.0f - a.hp.beta1) * (g - x.m);              // exp_avg.lerp_(grad, 1 - beta1)
   const float v = x.v * a.hp.beta2 + (1.0f - a.hp.beta2) * (g * g);   // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
   const float denom = sqrtf(v) / st.bc2_sqrt + a.hp.eps;
   const float p = x.p + (-(q ? st.step_q : st.step_pi)) * (m / denom);
-  pub<WT_OPT>(a.wt, a.m + e, m);
-  pub<WT_OPT>(a.wt, a.v + e, v);
-  pub<WT_OPT>(a.wt, a.params + e, p);
+  pub<WT_OPT>(wt, a.m + e, m);
+  pub<WT_OPT>(wt, a.v + e, v);
+  pub<WT_OPT>(wt, a.params + e, p);
   x.p = p;
   if (q) {
     x.t = x.t * (1.0f - a.hp.tau) + p * a.hp.tau;
-    pub<WT_OPT>(a.wt, a.targets + (e - a.L.q_base[0]), x.t);
+    pub<WT_OPT>(wt, a.targets + (e - a.L.q_base[0]), x.t);
   }
 }
 
@@ -1194,8 +1202,8 @@ __device__ __forceinline__ void mfma_tile_of(int bx, int& mat, int& j0, int& k0)
   k0 = (t % CB) * kTile2;
 }
 
-template <int H>
-__device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
+template <int H, int WT>
+__device__ __forceinline__ void p3_mfma_tile_wt(const WArgs& a, int bx, WLds& S) {
   constexpr int CB = H / kTile2;
   const MArgs& m = a.m;
   const AdamStep sst = adam_step_of(m);
@@ -1295,10 +1303,10 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
   const int64_t out_off = a.w2_off[mat];
   splitk_finish(acc, S.u.mm.split, [&](int q, int rr, int cc, float v) {
     const int64_t e = out_off + (int64_t)(j0 + rr) * H + k0 + cc;
-    pub<WT_OPT>(a.ap.wt, a.grads + e, v);
+    pub<WT_OPT>(WT, a.grads + e, v);
     if (a.fuse) {
       xe[q].g = v;
-      adam_st(a.ap, sst, e, xe[q], mat > 0);
+      adam_st(a.ap, sst, e, xe[q], mat > 0, WT);
       tt[0][cc][rr] = xe[q].p;
       tt[1][cc][rr] = xe[q].t;
     }
@@ -1309,8 +1317,8 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
     const int tc = tid % kTile2, tr = tid / kTile2;
     for (int cc = tr; cc < kTile2; cc += kThreads / kTile2) {
       const int64_t o = (int64_t)(k0 + cc) * H + j0 + tc;
-      pub<WT_OPT>(a.ap.wt, a.ap.T + (size_t)mat * HH + o, tt[0][cc][tc]);
-      if (mat > 0) pub<WT_OPT>(a.ap.wt, a.ap.T + (size_t)(2 + mat) * HH + o, tt[1][cc][tc]);
+      pub<WT_OPT>(WT, a.ap.T + (size_t)mat * HH + o, tt[0][cc][tc]);
+      if (mat > 0) pub<WT_OPT>(WT, a.ap.T + (size_t)(2 + mat) * HH + o, tt[1][cc][tc]);
     }
   }
   }
@@ -1322,8 +1330,8 @@ __device__ __forceinline__ void p3_mfma_tile(const WArgs& a, int bx, WLds& S) {
 // weight(s) (Σ dmean·h2, Σ dls·h2 / Σ dq·g2), with
 //   actor  dh1 = dmean U_m + dls U_s, dh2 = [h2 > 0] (wm dmean + ws dls);  critic  dg1 = dq U_q, dg2 = [g2 > 0] w3 dq
 constexpr int kValuUnits = 16, kValuStreams = kThreads / kValuUnits;
-template <int H>
-__device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
+template <int H, int WT>
+__device__ __forceinline__ void p3_valu_block_wt(const WArgs& a, int vb, WLds& S) {
   constexpr int CB = H / kTile2, NB = H / kValuUnits;
   static_assert(H % kValuUnits == 0, "units per VALU block");
   const MArgs& m = a.m;
@@ -1438,18 +1446,18 @@ __device__ __forceinline__ void p3_valu_block(const WArgs& a, int vb, WLds& S) {
 #pragma unroll
     for (int st = 1; st < kValuStreams; ++st) g += vr[st][i][u];
     const int64_t e = el_off(k);
-    pub<WT_OPT>(a.ap.wt, a.grads + e, g);
+    pub<WT_OPT>(WT, a.grads + e, g);
     if (a.fuse) {
       xe[q].g = g;
-      adam_st(a.ap, sst, e, xe[q], !actor);
+      adam_st(a.ap, sst, e, xe[q], !actor, WT);
     }
   }
 }
 
 // scalar block: per-row losses and diagnostics, the loss means, the bias gradients of the scalar heads
 // (Σ dmean, Σ dls, Σ dq1, Σ dq2), d(log α) (sac.py:174-180) and α
-template <int H>
-__device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
+template <int H, int WT>
+__device__ __forceinline__ void p3_scalar_block_wt(const WArgs& a, WLds& S) {
   constexpr int CB = H / kTile2;
   const MArgs& m = a.m;
   const AdamStep sst = adam_step_of(m);
@@ -1504,15 +1512,16 @@ __device__ __forceinline__ void p3_scalar_block(const WArgs& a, WLds& S) {
   }
   if (tid >= 5) return;
   const float g = tid == 0 ? (m.hp.auto_ent ? sum[4] * invB : 0.0f) : sum[4 + tid];
-  pub<WT_OPT>(a.ap.wt, a.grads + off, g);
+  pub<WT_OPT>(WT, a.grads + off, g);
   if (a.fuse && (tid > 0 || m.hp.auto_ent)) {
     xs.g = g;
-    adam_st(a.ap, sst, off, xs, tid >= 3);
+    adam_st(a.ap, sst, off, xs, tid >= 3, WT);
   }
 }
 
 // chain STAGE_NEXT: the next step's batch (P2 has advanced the step counter, so batch_item draws what the next
 // P1 would): item sb·256 + thread — its replay row, both observation rows, act / rew / term and its two normals
+template <int WT>
 __device__ __forceinline__ void p3_stage_block(const WArgs& a, int sb) {
   const MArgs& m = a.m;
   const int item = sb * kThreads + (int)threadIdx.x;
@@ -1527,12 +1536,12 @@ __device__ __forceinline__ void p3_stage_block(const WArgs& a, int sb) {
   float* dn = m.s.sxn + (int64_t)item * kXLd;
 #pragma unroll
   for (int q = 0; q < kXLd / 4; ++q) {
-    pub4<WT_ACT>(m.wt, dx + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-    pub4<WT_ACT>(m.wt, dn + 4 * q, xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
+    pub4<WT_ACT>(WT, dx + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    pub4<WT_ACT>(WT, dn + 4 * q, xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
   }
   float* q = m.s.saux + (int64_t)item * kAux;
-  pub4<WT_ACT>(m.wt, q, act, rew, term, e0);
-  pub<WT_ACT>(m.wt, q + AUX_E1, e1);
+  pub4<WT_ACT>(WT, q, act, rew, term, e0);
+  pub<WT_ACT>(WT, q + AUX_E1, e1);
 }
 
 // the kernel's WArgs read through the kernarg segment pointer, laundered: a field is a scalar load where a block
@@ -1544,21 +1553,22 @@ __device__ __forceinline__ const WArgs& wargs() {
   return *(const WArgs*)q;
 }
 
-template <int H>
+template <int H, int WT>
 __global__ __launch_bounds__(256) void sac_wgrad_kernel(WArgs a_arg) {
   (void)a_arg;  // read through wargs()
   __shared__ WLds S;
   const WArgs& a = wargs();
   SAC_STAMP(2, 0);
   const int bx = (int)blockIdx.x;
-  if (bx < a.n_mfma) p3_mfma_tile<H>(a, bx, S);
-  else if (bx < a.n_mfma + a.n_valu) p3_valu_block<H>(a, bx - a.n_mfma, S);
-  else if (bx == a.n_mfma + a.n_valu) p3_scalar_block<H>(a, S);
-  else p3_stage_block(a, bx - a.n_mfma - a.n_valu - 1);
+  if (bx < a.n_mfma) p3_mfma_tile_wt<H, WT>(a, bx, S);
+  else if (bx < a.n_mfma + a.n_valu) p3_valu_block_wt<H, WT>(a, bx - a.n_mfma, S);
+  else if (bx == a.n_mfma + a.n_valu) p3_scalar_block_wt<H, WT>(a, S);
+  else p3_stage_block<WT>(a, bx - a.n_mfma - a.n_valu - 1);
   SAC_STAMP(2, 3);
 }
 
 // world_size > 1 / split_update: the update from the (all-reduced) flat gradient
+template <int WT>
 __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
   __shared__ float tile[2][kTile2][kTile2 + 1];
   const AdamStep st{a.stats[5], a.stats[6], a.stats[7]};
@@ -1579,7 +1589,7 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int rr = tr + u * 8;
-      adam_st(a, st, w2[mat] + (int64_t)(r0 + rr) * H + c0 + tc, x[u], mat > 0);
+      adam_st(a, st, w2[mat] + (int64_t)(r0 + rr) * H + c0 + tc, x[u], mat > 0, WT);
       tile[0][tc][rr] = x[u].p;
       tile[1][tc][rr] = x[u].t;
     }
@@ -1587,10 +1597,10 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
     for (int cc = tr; cc < kTile2; cc += kThreads / kTile2) {
       const int64_t o = (int64_t)(c0 + cc) * H + r0 + tc;  // T[col][row]
       if (mat == 0) {
-        pub<WT_OPT>(a.wt, a.T + o, tile[0][cc][tc]);
+        pub<WT_OPT>(WT, a.T + o, tile[0][cc][tc]);
       } else {
-        pub<WT_OPT>(a.wt, a.T + (size_t)mat * HH + o, tile[0][cc][tc]);
-        pub<WT_OPT>(a.wt, a.T + (size_t)(2 + mat) * HH + o, tile[1][cc][tc]);
+        pub<WT_OPT>(WT, a.T + (size_t)mat * HH + o, tile[0][cc][tc]);
+        pub<WT_OPT>(WT, a.T + (size_t)(2 + mat) * HH + o, tile[1][cc][tc]);
       }
     }
     return;
@@ -1605,7 +1615,7 @@ __global__ __launch_bounds__(kThreads) void sac_apply_kernel(ApplyArgs a) {
   if (e == 0 && !a.hp.auto_ent) return;
   const bool q = e >= L.q_base[0];
   AdamElem x = adam_ld(a, e, q);
-  adam_st(a, st, e, x, q);
+  adam_st(a, st, e, x, q, WT);
 }
 
 __global__ void sac_transpose_kernel(const float* params, const float* targets, float* T, Layout L) {
@@ -1731,9 +1741,16 @@ __global__ __launch_bounds__(256) void sac_act_head_kernel(ActArgs a) {
 template <int H>
 void launch_step(const MArgs& m, const WArgs& w, hipStream_t st) {
   const unsigned bt = (unsigned)(m.L.Bp / kTile2), cb = H / kTile2;
-  hipLaunchKernelGGL(sac_fwd_kernel<H>, dim3(6 * bt * cb), dim3(256), 0, st, m);
-  hipLaunchKernelGGL(sac_mid_kernel<H>, dim3(7 * bt * cb), dim3(256), 0, st, m);
-  hipLaunchKernelGGL(sac_wgrad_kernel<H>, dim3((unsigned)(w.n_mfma + w.n_valu + 1 + w.n_stage)), dim3(256), 0, st, w);
+  const dim3 g1(6 * bt * cb), g2(7 * bt * cb), g3((unsigned)(w.n_mfma + w.n_valu + 1 + w.n_stage));
+  if (m.wt == kWtLarge) {
+    hipLaunchKernelGGL((sac_fwd_kernel<H, kWtLarge>), g1, dim3(256), 0, st, m);
+    hipLaunchKernelGGL((sac_mid_kernel<H, kWtLarge>), g2, dim3(256), 0, st, m);
+    hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtLarge>), g3, dim3(256), 0, st, w);
+  } else {
+    hipLaunchKernelGGL((sac_fwd_kernel<H, kWtSmall>), g1, dim3(256), 0, st, m);
+    hipLaunchKernelGGL((sac_mid_kernel<H, kWtSmall>), g2, dim3(256), 0, st, m);
+    hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtSmall>), g3, dim3(256), 0, st, w);
+  }
 }
 
 template <int H>
@@ -2032,7 +2049,7 @@ int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const fl
 
 // the write-through mask of a step's launches (see pub): everything from 128 padded rows up, below that not the row
 // inputs / parts / records (WT_ACT), whose write-through costs more there than the write-back it saves
-static int wt_mask_for(const Layout& L) { return L.Bp >= 128 ? (WT_ACT | WT_OPT | WT_EPI) : (WT_OPT | WT_EPI); }
+static int wt_mask_for(const Layout& L) { return L.Bp >= 128 ? kWtLarge : kWtSmall; }
 
 static ApplyArgs apply_args(const sacf_handle* h) {
   ApplyArgs a;
@@ -2128,8 +2145,9 @@ int sacf_apply(sacf_handle* h) {
   const int64_t HH = (int64_t)h->L.H * h->L.H;
   const int64_t rest = h->L.n_params - 3 * HH;
   SDev g(h->device);
-  hipLaunchKernelGGL(sac_apply_kernel, dim3((unsigned)(a.n_tile_blocks + (rest + kThreads - 1) / kThreads)),
-                     dim3(kThreads), 0, h->stream, a);
+  const dim3 grid((unsigned)(a.n_tile_blocks + (rest + kThreads - 1) / kThreads));
+  if (a.wt == kWtLarge) hipLaunchKernelGGL(sac_apply_kernel<kWtLarge>, grid, dim3(kThreads), 0, h->stream, a);
+  else hipLaunchKernelGGL(sac_apply_kernel<kWtSmall>, grid, dim3(kThreads), 0, h->stream, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? SACF_OK : sfail(h, SACF_EHIP, "sacf_apply: %s", hipGetErrorString(e));
 }
