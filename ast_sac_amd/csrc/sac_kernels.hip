@@ -614,6 +614,11 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   const int64_t idx = batch_row(a, item, nrow, x, e0, e1);
   SAC_STAMP_ON(0, 4, idx);
   SAC_STAMP_ON(0, 5, x[0]);
+  // column block 0 also hands the gathered batch on (x rows, act / rew / term / normals): its loads issued here, the
+  // stores after the barrier (before it they held every wave of the block for one more dependent load round trip)
+  const bool keeper = by == 0 && w == 0 && h == 0;
+  float aux[5];
+  if (keeper && !nrow) batch_aux(a, item, idx, e0, e1, aux);
   // then W1 (needed before the barrier), then the B operand and epilogue weights (needed after it): the LDS
   // stores below wait for W1 only
   W1Stage<H> w1s;
@@ -630,26 +635,24 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = x[m];  // (zero past O: no per-m mask kept live)
   }
-  if (by == 0 && w == 0 && h == 0) {  // the gathered batch for the later passes
+  (void)B;
+  __syncthreads();
+  SAC_STAMP(0, 1);
+  if (keeper) {  // the gathered batch for the later passes
     float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
 #pragma unroll
     for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(WTM, xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     if (!nrow) {
-      float v[5];
-      batch_aux(a, item, idx, e0, e1, v);
       float* rc = a.s.rec + (int64_t)item * kRec;
       // (R_EPS .. R_ACT are record words 6 .. 10: two words and one 16-byte store of words 8 .. 11, whose last word,
       // R_LOGPN, P2 writes later in the step)
       static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11,
                     "record layout");
-      pub<WT_ACT>(WTM, rc + R_EPS, v[AUX_E0]);
-      pub<WT_ACT>(WTM, rc + R_EPSN, v[AUX_E1]);
-      pub4<WT_ACT>(WTM, rc + R_REW, v[AUX_REW], v[AUX_TERM], v[AUX_ACT], 0.0f);
+      pub<WT_ACT>(WTM, rc + R_EPS, aux[AUX_E0]);
+      pub<WT_ACT>(WTM, rc + R_EPSN, aux[AUX_E1]);
+      pub4<WT_ACT>(WTM, rc + R_REW, aux[AUX_REW], aux[AUX_TERM], aux[AUX_ACT], 0.0f);
     }
   }
-  (void)B;
-  __syncthreads();
-  SAC_STAMP(0, 1);
   f32x16 acc = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -790,8 +793,8 @@ __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// P2 (sac_mid_kernel): row tiles [Q1, Q2 on (obs, ã) (2Bt) | actor factors (Bt) | T1, T2 on (next_obs, ã')
-// (2Bt) | Q1, Q2 data-row factors (2Bt)] x CB; the two-chain kinds first (dispatched first)
+// P2 (sac_mid_kernel): row tiles [Q1, Q2 on (obs, ã) (2Bt) | T1, T2 on (next_obs, ã') (2Bt) | Q1, Q2 data-row factors
+// (2Bt) | actor factors (Bt)] x CB, then one block for the step counter and P3's snapshot
 // ---------------------------------------------------------------------------------------------
 // the actor head of a row from its column-block parts (summed in block order) and its TanhNormal sample
 template <int CB>
@@ -978,7 +981,16 @@ template <int H, int WT>
 __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   __shared__ float lds[FwdLds<H>::kFloats];
   SAC_STAMP(1, 0);
-  if (blockIdx.x == 0) {
+  // Block order (block i and block i + 256 share a CU): the critic tiles (heavy prologue: the pre-activation rows and
+  // the W2ᵀ slice) take the first block of every CU, the backward-factor tiles (a mask word per row) the second, the
+  // one-chain critic factors beside the two-chain Q / tangent tiles and the two-chain actor factors beside one-chain
+  // target tiles. (With the T2 target tiles in second slots their prologue waited 2.5 µs behind the first block's
+  // loads, and two-chain tiles sharing a CU stretched each other's products: per-block stamps profiles/round6/r6i_*,
+  // r6j_*.) One extra block, the last, advances the step and snapshots what P3 reads: in front of a tile that serial
+  // work (a dependent load, the double-precision bias corrections, 4·H stores) held the tile 3 µs, behind one it
+  // ended the launch.
+  const int bt = a.L.Bp / kTile2;
+  if (blockIdx.x == gridDim.x - 1) {
     if (threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
       const int64_t t = *a.step + 1;
       pub<WT_ACT>(WT, a.step, t);
@@ -1001,14 +1013,14 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
       pub<WT_ACT>(WT, sn + SN_HEAD + 2 * L.H + j, P[L.q_base[0] + L.c_w3 + j]);
       pub<WT_ACT>(WT, sn + SN_HEAD + 3 * L.H + j, P[L.q_base[1] + L.c_w3 + j]);
     }
+    return;
   }
   int bx, by;
   tile_of<H>(bx, by);
-  const int bt = a.L.Bp / kTile2;
   if (bx < 2 * bt) p2_critic_tile<H, false, WT>(a, bx / bt, bx % bt, by, lds);
-  else if (bx < 3 * bt) p2_factor_tile<H, true, WT>(a, 0, bx - 2 * bt, by, lds);
-  else if (bx < 5 * bt) p2_critic_tile<H, true, WT>(a, (bx - 3 * bt) / bt, (bx - 3 * bt) % bt, by, lds);
-  else p2_factor_tile<H, false, WT>(a, (bx - 5 * bt) / bt, (bx - 5 * bt) % bt, by, lds);
+  else if (bx < 4 * bt) p2_critic_tile<H, true, WT>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
+  else if (bx < 6 * bt) p2_factor_tile<H, false, WT>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by, lds);
+  else p2_factor_tile<H, true, WT>(a, 0, bx - 6 * bt, by, lds);
   SAC_STAMP(1, 3);
 }
 
@@ -1741,14 +1753,14 @@ __global__ __launch_bounds__(256) void sac_act_head_kernel(ActArgs a) {
 template <int H>
 void launch_step(const MArgs& m, const WArgs& w, hipStream_t st) {
   const unsigned bt = (unsigned)(m.L.Bp / kTile2), cb = H / kTile2;
-  const dim3 g1(6 * bt * cb), g2(7 * bt * cb), g3((unsigned)(w.n_mfma + w.n_valu + 1 + w.n_stage));
+  const dim3 g1(6 * bt * cb), g2p(7 * bt * cb + 1), g3((unsigned)(w.n_mfma + w.n_valu + 1 + w.n_stage));
   if (m.wt == kWtLarge) {
     hipLaunchKernelGGL((sac_fwd_kernel<H, kWtLarge>), g1, dim3(256), 0, st, m);
-    hipLaunchKernelGGL((sac_mid_kernel<H, kWtLarge>), g2, dim3(256), 0, st, m);
+    hipLaunchKernelGGL((sac_mid_kernel<H, kWtLarge>), g2p, dim3(256), 0, st, m);
     hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtLarge>), g3, dim3(256), 0, st, w);
   } else {
     hipLaunchKernelGGL((sac_fwd_kernel<H, kWtSmall>), g1, dim3(256), 0, st, m);
-    hipLaunchKernelGGL((sac_mid_kernel<H, kWtSmall>), g2, dim3(256), 0, st, m);
+    hipLaunchKernelGGL((sac_mid_kernel<H, kWtSmall>), g2p, dim3(256), 0, st, m);
     hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtSmall>), g3, dim3(256), 0, st, w);
   }
 }

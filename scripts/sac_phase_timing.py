@@ -43,8 +43,8 @@ def kinds(kernel, nblocks, bt, cb, n_mfma, n_valu):
         if kernel == 0:
             out.append("actor_fwd" if bx < 2 * bt else "critic_data_fwd" if bx < 4 * bt else "target_pre")
         else:
-            out.append("critic_tangent" if bx < 2 * bt else "actor_factors" if bx < 3 * bt else
-                       "targets" if bx < 5 * bt else "critic_factors")
+            out.append("critic_tangent" if bx < 2 * bt else "targets" if bx < 4 * bt else
+                       "critic_factors" if bx < 6 * bt else "actor_factors" if bx < 7 * bt else "step_snapshot")
     return out
 
 
@@ -75,7 +75,7 @@ def main():
     st = np.frombuffer(buf, dtype=np.uint64).reshape(3, KSTAMP, NST).astype(np.float64)
     bp = (a.batch + 31) // 32 * 32
     bt, cb = bp // 32, a.hidden // 32
-    grids = [6 * bt * cb, 7 * bt * cb, 3 * cb * cb + 3 * (a.hidden // 16) + 1]
+    grids = [6 * bt * cb, 7 * bt * cb + 1, 3 * cb * cb + 3 * (a.hidden // 16) + 1]
     names = ["fwd (P1)", "mid (P2)", "wgrad (P3)"]
     res = {"step_us": r["ms_per_grad_step"] * 1e3, "batch": a.batch, "hidden": a.hidden, "kernels": {}}
     for k in range(3):
@@ -101,10 +101,15 @@ def main():
                     per[kind][f"p{q}_since_entry_med"] = float(np.median(m[:, q] - m[:, 0]))
                     per[kind][f"p{q}_since_entry_max"] = float((m[:, q] - m[:, 0]).max())
         res["kernels"][names[k]] = {"span_us": float(rel[:, 3].max()), "kinds": per}
+        # per block (relative to the kernel's first entry, µs): entry, operands ready, products done, exit, p4
+        res.setdefault("blocks", {})[names[k]] = {
+            "kind": ks, "entry": [round(float(x), 2) for x in rel[:, 0]], "ready": [round(float(x), 2) for x in rel[:, 1]],
+            "products": [round(float(x), 2) for x in rel[:, 2]], "exit": [round(float(x), 2) for x in rel[:, 3]],
+            "p4": [round(float(x), 2) if st[k, i, 4] > 0 else None for i, x in enumerate(rel[:, 4])]}
     gaps = [(st[k + 1, :grids[k + 1], 0].min() - st[k, :grids[k], 3].max()) / 100.0 for k in range(2)]
     res["gaps_us"] = {"fwd_exit_to_mid_entry": gaps[0], "mid_exit_to_wgrad_entry": gaps[1]}
     txt = json.dumps(res, indent=1)
-    print(txt)
+    print(json.dumps({k: v for k, v in res.items() if k != "blocks"}, indent=1))
     if a.out:
         with open(a.out, "w") as f:
             f.write(txt + "\n")
