@@ -615,7 +615,8 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   SAC_STAMP_ON(0, 4, idx);
   SAC_STAMP_ON(0, 5, x[0]);
   // column block 0 also hands the gathered batch on (x rows, act / rew / term / normals): its loads issued here, the
-  // stores after the barrier (before it they held every wave of the block for one more dependent load round trip)
+  // stores at the end of the tile (before the barrier they held every wave of the block for one more dependent load
+  // round trip)
   const bool keeper = by == 0 && w == 0 && h == 0;
   float aux[5];
   if (keeper && !nrow) batch_aux(a, item, idx, e0, e1, aux);
@@ -638,21 +639,6 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   (void)B;
   __syncthreads();
   SAC_STAMP(0, 1);
-  if (keeper) {  // the gathered batch for the later passes
-    float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
-#pragma unroll
-    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(WTM, xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-    if (!nrow) {
-      float* rc = a.s.rec + (int64_t)item * kRec;
-      // (R_EPS .. R_ACT are record words 6 .. 10: two words and one 16-byte store of words 8 .. 11, whose last word,
-      // R_LOGPN, P2 writes later in the step)
-      static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11,
-                    "record layout");
-      pub<WT_ACT>(WTM, rc + R_EPS, aux[AUX_E0]);
-      pub<WT_ACT>(WTM, rc + R_EPSN, aux[AUX_E1]);
-      pub4<WT_ACT>(WTM, rc + R_REW, aux[AUX_REW], aux[AUX_TERM], aux[AUX_ACT], 0.0f);
-    }
-  }
   f32x16 acc = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -676,6 +662,23 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
       pub<WT_ACT>(WTM, a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
     }
   });
+  // the gathered batch for the later passes, last: wave 0 would otherwise wait for these write-through stores at its
+  // next vmcnt wait (the compiler counts loads only), before its MFMA chain
+  if (keeper) {
+    float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
+#pragma unroll
+    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(WTM, xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    if (!nrow) {
+      float* rc = a.s.rec + (int64_t)item * kRec;
+      // (R_EPS .. R_ACT are record words 6 .. 10: two words and one 16-byte store of words 8 .. 11, whose last word,
+      // R_LOGPN, P2 writes later in the step)
+      static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11,
+                    "record layout");
+      pub<WT_ACT>(WTM, rc + R_EPS, aux[AUX_E0]);
+      pub<WT_ACT>(WTM, rc + R_EPSN, aux[AUX_E1]);
+      pub4<WT_ACT>(WTM, rc + R_REW, aux[AUX_REW], aux[AUX_TERM], aux[AUX_ACT], 0.0f);
+    }
+  }
 }
 
 // critic forward on the (obs, a) data rows of one critic (mlp.py:127-136 ConcatMlp): the row's observation and
@@ -1179,7 +1182,8 @@ struct WLds {
     } mm;
     float vred[kThreads / 16][kValuAcc][16];  // VALU blocks: [row stream][accumulator][unit]
   } u;
-  float s0[kRowChunk], s1[kRowChunk];
+  alignas(16) float s0[kRowChunk];
+  alignas(16) float s1[kRowChunk];
   float xs[kRowChunk][kXLd + 1];
   float red[4][32];
   float sum[32];
@@ -1294,12 +1298,19 @@ __device__ __forceinline__ void p3_mfma_tile_wt(const WArgs& a, int bx, WLds& S)
     SAC_STAMP(2, 1);
     // (every LDS read unconditional — rl0 + i < 256 for every chunk shape — and the actor / critic choice a select
     // of values: a guard or branch per read compiles into a wait per read)
+    // (rl0 is a multiple of 4 for every chunk shape — rows per wave a multiple of 8 — so the row scalars are read four at
+    // a time: 16 LDS reads per array instead of 32)
     float av[kMaxN2];
 #pragma unroll
-    for (int i = 0; i < kMaxN2; ++i) {
-      const float s0v = S.s0[rl0 + i], s1v = S.s1[rl0 + i];
-      const float d = actor ? c1 * s0v + c2 * s1v : c1 * s0v;
-      av[i] = ((yv[i] >> rl) & 1u) ? d : 0.0f;
+    for (int i4 = 0; i4 < kMaxN2; i4 += 4) {
+      const float4 s0q = *reinterpret_cast<const float4*>(&S.s0[rl0 + i4]);
+      const float4 s1q = *reinterpret_cast<const float4*>(&S.s1[rl0 + i4]);
+      const float s0a[4] = {s0q.x, s0q.y, s0q.z, s0q.w}, s1a[4] = {s1q.x, s1q.y, s1q.z, s1q.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float d = actor ? c1 * s0a[u] + c2 * s1a[u] : c1 * s0a[u];
+        av[i4 + u] = ((yv[i4 + u] >> rl) & 1u) ? d : 0.0f;
+      }
     }
     if (n2 == kMaxN2) mfma_n<kMaxN2>(acc, av, xv);  // (full chunks: one straight chain)
     else mfma_chain(acc, av, xv, n2);
@@ -1325,13 +1336,14 @@ __device__ __forceinline__ void p3_mfma_tile_wt(const WArgs& a, int bx, WLds& S)
   });
   if (a.fuse) {  // W2ᵀ (and the target's) for the next step's forward passes: T[col][row]
     __syncthreads();
+    // (thread t: T row k0 + t / 8, the four columns j0 + 4 (t mod 8) ..: one 16-byte store per copy)
     const int64_t HH = (int64_t)H * H;
-    const int tc = tid % kTile2, tr = tid / kTile2;
-    for (int cc = tr; cc < kTile2; cc += kThreads / kTile2) {
-      const int64_t o = (int64_t)(k0 + cc) * H + j0 + tc;
-      pub<WT_OPT>(WT, a.ap.T + (size_t)mat * HH + o, tt[0][cc][tc]);
-      if (mat > 0) pub<WT_OPT>(WT, a.ap.T + (size_t)(2 + mat) * HH + o, tt[1][cc][tc]);
-    }
+    const int cc = tid >> 3, j4 = (tid & 7) * 4;
+    const int64_t o = (int64_t)(k0 + cc) * H + j0 + j4;
+    pub4<WT_OPT>(WT, a.ap.T + (size_t)mat * HH + o, tt[0][cc][j4], tt[0][cc][j4 + 1], tt[0][cc][j4 + 2], tt[0][cc][j4 + 3]);
+    if (mat > 0)
+      pub4<WT_OPT>(WT, a.ap.T + (size_t)(2 + mat) * HH + o, tt[1][cc][j4], tt[1][cc][j4 + 1], tt[1][cc][j4 + 2],
+                   tt[1][cc][j4 + 3]);
   }
   }
 }

@@ -4,7 +4,7 @@ TAG=${1:-r6j}
 timeout -k 10 600 python -u -m pytest tests/test_sac.py -m gpu -x -q -p no:cacheprovider --timeout 300 \
   --timeout-method thread > "$O/pytest_$TAG.txt" 2>&1
 rc=$?; tail -2 "$O/pytest_$TAG.txt"; soft_pytest $rc pytest
-TESTS=0 bash scripts/gpu/sac_abn.sh ${TAG}s 3 r6f || exit $?
+TESTS=0 bash scripts/gpu/sac_abn.sh ${TAG}s 3 ${BASE:-r6f} || exit $?
 timeout -k 10 200 python scripts/sac_phase_timing.py --variant cur --batch 256 --steps 300 --out "$O/sac_phases_${TAG}_b256.json" \
   > "$O/sac_phases_${TAG}_b256.log" 2>&1; hard $? phases
 python -c "
