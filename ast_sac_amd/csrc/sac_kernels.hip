@@ -372,6 +372,41 @@ __device__ __forceinline__ void splitk_finish2(const f32x16& acc0, const f32x16&
     epi(q, (g & 3) + 8 * (g >> 2) + 4 * (lane >> 5), lane & 31, v0, v1);
   }
 }
+// A 32 x 32 epilogue tile staged in LDS (stage[row · kStageLd + col], written by splitk_finish's epilogue: one value
+// per lane and output register, a word store each) out to dst[row · ld + col] as 16-byte stores: thread t writes row
+// t / 8, columns 4 (t mod 8) .. 4 (t mod 8) + 3 (dst 16-byte aligned, ld a multiple of 4)
+constexpr int kStageLd = kTile2 + 4;
+template <int WTM>
+__device__ __forceinline__ void tile_out(const float* stage, float* dst, int ld) {
+  __syncthreads();
+  const int row = (int)threadIdx.x >> 3, c4 = ((int)threadIdx.x & 7) * 4;
+  const float4 v = *reinterpret_cast<const float4*>(stage + row * kStageLd + c4);
+  pub4<WT_EPI>(WTM, dst + (int64_t)row * ld + c4, v.x, v.y, v.z, v.w);
+}
+
+// the row of output register q (0..3) of this lane in splitk_finish's order (defined below)
+__device__ __forceinline__ int finish_row(int q);
+
+// The same for up to two tiles whose values the epilogue kept in registers (v[q] at row finish_row(q), column lane & 31):
+// staged into the split-K regions once their last reads are done (one more barrier), then out as 16-byte stores
+template <int WTM, int NT>
+__device__ __forceinline__ void tiles_out(const float (&v)[NT][4], float* const (&stage)[NT], float* const (&dst)[NT],
+                                          int ld) {
+  __syncthreads();  // (every wave's reads of the split regions are done)
+  const int col = (int)threadIdx.x & 31;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) stage[t][finish_row(q) * kStageLd + col] = v[t][q];
+  __syncthreads();
+  const int row = (int)threadIdx.x >> 3, c4 = ((int)threadIdx.x & 7) * 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float4 x = *reinterpret_cast<const float4*>(stage[t] + row * kStageLd + c4);
+    pub4<WT_EPI>(WTM, dst[t] + (int64_t)row * ld + c4, x.x, x.y, x.z, x.w);
+  }
+}
+
 // the row of output register q (0..3) of this lane in splitk_finish's order
 __device__ __forceinline__ int finish_row(int q) {
   const int g = 4 * (threadIdx.x >> 6) + q;
@@ -607,7 +642,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   const int kb = w * (H / 4) + h * KS::N2;
   // the batch gather first: its chain (step / size -> Philox -> replay row) is the longest of the prologue
   const int row = r0 + rl;
-  const bool nrow = row >= Bp;
+  const bool nrow = row >= Bp, nrow_tile = r0 >= Bp;  // (next_obs rows: a whole row tile)
   const int item = nrow ? row - Bp : row;
   float e0, e1;
   float x[kXLd];
@@ -650,10 +685,11 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
     mfma_n<CS>(acc, av, bv);
   }
   SAC_STAMP(0, 2);
+  float* stage = lds + FwdLds<H>::kSplit;  // (the second split region: free in P1)
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
-    const int r = r0 + rr, col = c0 + cc;
+    const int r = r0 + rr;
     const float y = relu(v + b2c);
-    if (r < Bp) pub<WT_EPI>(WTM, a.s.h2 + (int64_t)r * H + col, y);
+    stage[rr * kStageLd + cc] = y;
     const uint64_t pos = __ballot(y > 0.0f);  // (rows of the two half waves: the low / high 32 bits)
     if (r < Bp && cc == 0) pub<WT_ACT>(WTM, a.s.h2m + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
     const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
@@ -662,6 +698,7 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
       pub<WT_ACT>(WTM, a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
     }
   });
+  if (!nrow_tile) tile_out<WTM>(stage, a.s.h2 + (int64_t)r0 * H + c0, H);
   // the gathered batch for the later passes, last: wave 0 would otherwise wait for these write-through stores at its
   // next vmcnt wait (the compiler counts loads only), before its MFMA chain
   if (keeper) {
@@ -737,15 +774,17 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   if (rt == 0 && by == 0)  // fc0's action column, contiguous, for P2
     for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(WTM, a.s.w1a + net * H + k, lw1[O * H + k]);
   SAC_STAMP(0, 2);
+  float* stage = lds + FwdLds<H>::kSplit;  // (the second split region: free in P1)
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
-    const int r = r0 + rr, col = c0 + cc;
+    const int r = r0 + rr;
     const float y = relu(v + b2c);
-    pub<WT_EPI>(WTM, a.s.g2[net] + (int64_t)r * H + col, y);
+    stage[rr * kStageLd + cc] = y;
     const uint64_t pos = __ballot(y > 0.0f);
     if (cc == 0) pub<WT_ACT>(WTM, a.s.g2m[net] + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
     const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
     if (cc == 0) pub<WT_ACT>(WTM, a.s.part + ((int64_t)r * PS_N + PS_Q1D + net) * CB + by, pq);
   });
+  tile_out<WTM>(stage, a.s.g2[net] + (int64_t)r0 * H + c0, H);
 }
 
 // target critic `net`'s fc0 pre-activation (without the action term) on the next_obs rows of row tile rt, columns
@@ -967,16 +1006,22 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   }
   SAC_STAMP(1, 2);
   float* o1 = kActor ? a.s.um : a.s.uq[net];
+  // (the factors out through LDS as 16-byte stores: tiles_out)
   if constexpr (kActor) {  // U_m and U_s behind one barrier
-    splitk_finish2(acc, acc2, lds, lds + FwdLds<H>::kSplit, [&](int q, int rr, int cc, float v, float v2) {
-      const int64_t o = (int64_t)(r0 + rr) * H + j0 + cc;
-      pub<WT_EPI>(WTM, o1 + o, m1[q] > 0.0f ? v : 0.0f);
-      pub<WT_EPI>(WTM, a.s.us + o, m1[q] > 0.0f ? v2 : 0.0f);
+    float v[2][4];
+    splitk_finish2(acc, acc2, lds, lds + FwdLds<H>::kSplit, [&](int q, int, int, float x, float x2) {
+      v[0][q] = m1[q] > 0.0f ? x : 0.0f;
+      v[1][q] = m1[q] > 0.0f ? x2 : 0.0f;
     });
+    float* const st[2] = {lds, lds + FwdLds<H>::kSplit};
+    float* const dst[2] = {o1 + (int64_t)r0 * H + j0, a.s.us + (int64_t)r0 * H + j0};
+    tiles_out<WTM, 2>(v, st, dst, H);
   } else {
-    splitk_finish(acc, lds, [&](int q, int rr, int cc, float v) {
-      pub<WT_EPI>(WTM, o1 + (int64_t)(r0 + rr) * H + j0 + cc, m1[q] > 0.0f ? v : 0.0f);
-    });
+    float v[1][4];
+    splitk_finish(acc, lds, [&](int q, int, int, float x) { v[0][q] = m1[q] > 0.0f ? x : 0.0f; });
+    float* const st[1] = {lds};
+    float* const dst[1] = {o1 + (int64_t)r0 * H + j0};
+    tiles_out<WTM, 1>(v, st, dst, H);
   }
 }
 
