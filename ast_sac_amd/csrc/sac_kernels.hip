@@ -628,6 +628,32 @@ __device__ __forceinline__ void tile_of(int& bx, int& by) {
 // ---------------------------------------------------------------------------------------------
 // P1 (sac_fwd_kernel): row tiles [obs (Bp/32) | next_obs (Bp/32) | Q1 data (Bp/32) | Q2 data (Bp/32)] x CB
 // ---------------------------------------------------------------------------------------------
+// the gathered batch for the later passes of the step — the obs and next_obs rows, act / rew / term and the two
+// normals — of batch item `item` (its replay row idx and normals as batch_item drew them, its next_obs row xn), by one
+// lane per item of the T1 fc0 tiles of column block 0 (short tiles: in the actor tiles this hand-on set P1's span)
+template <int WTM>
+__device__ __forceinline__ void hand_on_batch(const MArgs& a, int item, int64_t idx, float e0, float e1,
+                                              const float (&xn)[kXLd]) {
+  float xo[kXLd], aux[5];
+  if (a.chain & SACF_CHAIN_FROM_STAGED) load_run<kXLd>(a.s.sx + (int64_t)item * kXLd, xo);
+  else load_obs_row(a.obs, idx, a.L.O, xo);
+  batch_aux(a, item, idx, e0, e1, aux);
+  float* xd = a.s.x + (int64_t)item * kXLd;
+  float* xnd = a.s.xn + (int64_t)item * kXLd;
+#pragma unroll
+  for (int q = 0; q < kXLd / 4; ++q) {
+    pub4<WT_ACT>(WTM, xd + 4 * q, xo[4 * q], xo[4 * q + 1], xo[4 * q + 2], xo[4 * q + 3]);
+    pub4<WT_ACT>(WTM, xnd + 4 * q, xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
+  }
+  float* rc = a.s.rec + (int64_t)item * kRec;
+  // (R_EPS .. R_ACT are record words 6 .. 10: two words and one 16-byte store of words 8 .. 11, whose last word,
+  // R_LOGPN, P2 writes later in the step)
+  static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11, "record layout");
+  pub<WT_ACT>(WTM, rc + R_EPS, aux[AUX_E0]);
+  pub<WT_ACT>(WTM, rc + R_EPSN, aux[AUX_E1]);
+  pub4<WT_ACT>(WTM, rc + R_REW, aux[AUX_REW], aux[AUX_TERM], aux[AUX_ACT], 0.0f);
+}
+
 // actor forward (gaussian_policy.py:105-118 up to the heads, mlp.py:86-99): h1 = relu(W1 x + b1) on the VALU,
 // h2 = relu(h1 W2ᵀ + b2) on MFMA, the mean / log_std head parts of this column block in the epilogue
 template <int H, int WTM>
@@ -649,12 +675,6 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   const int64_t idx = batch_row(a, item, nrow, x, e0, e1);
   SAC_STAMP_ON(0, 4, idx);
   SAC_STAMP_ON(0, 5, x[0]);
-  // column block 0 also hands the gathered batch on (x rows, act / rew / term / normals): its loads issued here, the
-  // stores at the end of the tile (before the barrier they held every wave of the block for one more dependent load
-  // round trip)
-  const bool keeper = by == 0 && w == 0 && h == 0;
-  float aux[5];
-  if (keeper && !nrow) batch_aux(a, item, idx, e0, e1, aux);
   // then W1 (needed before the barrier), then the B operand and epilogue weights (needed after it): the LDS
   // stores below wait for W1 only
   W1Stage<H> w1s;
@@ -699,23 +719,6 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
     }
   });
   if (!nrow_tile) tile_out<WTM>(stage, a.s.h2 + (int64_t)r0 * H + c0, H);
-  // the gathered batch for the later passes, last: wave 0 would otherwise wait for these write-through stores at its
-  // next vmcnt wait (the compiler counts loads only), before its MFMA chain
-  if (keeper) {
-    float* xd = (nrow ? a.s.xn : a.s.x) + (int64_t)item * kXLd;
-#pragma unroll
-    for (int q = 0; q < kXLd / 4; ++q) pub4<WT_ACT>(WTM, xd + 4 * q, x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-    if (!nrow) {
-      float* rc = a.s.rec + (int64_t)item * kRec;
-      // (R_EPS .. R_ACT are record words 6 .. 10: two words and one 16-byte store of words 8 .. 11, whose last word,
-      // R_LOGPN, P2 writes later in the step)
-      static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11,
-                    "record layout");
-      pub<WT_ACT>(WTM, rc + R_EPS, aux[AUX_E0]);
-      pub<WT_ACT>(WTM, rc + R_EPSN, aux[AUX_E1]);
-      pub4<WT_ACT>(WTM, rc + R_REW, aux[AUX_REW], aux[AUX_TERM], aux[AUX_ACT], 0.0f);
-    }
-  }
 }
 
 // critic forward on the (obs, a) data rows of one critic (mlp.py:127-136 ConcatMlp): the row's observation and
@@ -800,7 +803,8 @@ __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int 
   const int item = rt * kTile2 + row;
   float e0, e1;
   float x[kXLd];
-  (void)batch_row(a, item, true, x, e0, e1);
+  const int64_t idx = batch_row(a, item, true, x, e0, e1);
+  if (net == 0 && by == 0 && (tid & 7) == 0) hand_on_batch<WTM>(a, item, idx, e0, e1, x);
   float* w1 = lds;                   // [32][kXLd + 1]: W1 rows c0 .. c0 + 31
   float* b1 = lds + kTile2 * (kXLd + 1);
   const float* src = C + L.c_w1 + (int64_t)c0 * nin;  // the 32 rows are contiguous: 32·nin floats
@@ -836,7 +840,7 @@ __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // P2 (sac_mid_kernel): row tiles [Q1, Q2 on (obs, ã) (2Bt) | T1, T2 on (next_obs, ã') (2Bt) | Q1, Q2 data-row factors
-// (2Bt) | actor factors (Bt)] x CB, then one block for the step counter and P3's snapshot
+// (2Bt) | actor factors U_m (Bt) | U_s (Bt)] x CB, then one block for the step counter and P3's snapshot
 // ---------------------------------------------------------------------------------------------
 // the actor head of a row from its column-block parts (summed in block order) and its TanhNormal sample
 template <int CB>
@@ -950,13 +954,16 @@ __host__ __device__ constexpr int mask_words(int H) {
 }
 
 // backward factors (the backward pass of layer 2 for a unit head gradient): out[r][j] = [x1[r][j] > 0] ·
-// Σ_c W2[c][j] · hw[c] · [x2[r][c] > 0], with (x1, x2, hw) = (h1, h2, wm) and (h1, h2, ws) for the actor
-// (kActor: two chains on the same W2 operand) or (g1, g2, w3) of a critic on its data rows. The B operand is
-// W2 in its own (out, in) row-major layout: B[k = c][n = j] = W2[c][j].
-template <int H, bool kActor, int WTM>
+// Σ_c W2[c][j] · hw[c] · [x2[r][c] > 0], with (x1, x2, hw) = (h1, h2, wm) → U_m (FK 1) and (h1, h2, ws) → U_s (FK 2)
+// for the actor, or (g1, g2, w3) → U_q of a critic on its data rows (FK 0). The B operand is W2 in its own (out, in)
+// row-major layout: B[k = c][n = j] = W2[c][j]. One MFMA chain per tile (U_m and U_s are separate tiles: a two-chain tile
+// beside another tile on its CU set P2's span).
+enum { FK_CRITIC = 0, FK_UM = 1, FK_US = 2 };
+template <int H, int FK, int WTM>
 __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, int by, float* lds) {
   using KS = KSlice<H>;
   constexpr int CS = KS::CS, N2 = KS::N2;
+  constexpr bool kActor = FK != FK_CRITIC;
   const Layout& L = a.L;
   const float* P = a.params;
   const float* C = P + L.q_base[net];
@@ -966,8 +973,7 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   const float* X1 = kActor ? a.s.h1 : a.s.g1[net];
   const uint32_t* X2M = kActor ? a.s.h2m : a.s.g2m[net];
   const float* W2 = kActor ? P + L.p_w2 : C + L.c_w2;
-  const float* HW1 = kActor ? P + L.p_wm : C + L.c_w3;
-  const float* HW2 = P + L.p_ws;
+  const float* HW = FK == FK_UM ? P + L.p_wm : FK == FK_US ? P + L.p_ws : C + L.c_w3;
   // [x2 > 0] of this lane's K slice (row r0 + rl, columns kb .. kb + N2 - 1): the mask words covering it, and the
   // head weights of those columns
   constexpr int CB = KS::CB, NW = mask_words(H);
@@ -983,46 +989,27 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   float m1[4];  // [x1 > 0] of the four outputs this lane finishes
 #pragma unroll
   for (int q = 0; q < 4; ++q) m1[q] = X1[(int64_t)(r0 + finish_row(q)) * H + j0 + rl];
-  float hw1[N2], hw2[kActor ? N2 : 1];  // (parameter offsets are not 16-byte aligned: element loads)
+  float hw[N2];  // (parameter offsets are not 16-byte aligned: element loads)
 #pragma unroll
-  for (int i = 0; i < N2; ++i) hw1[i] = HW1[kb + i];
-  if constexpr (kActor)
-#pragma unroll
-    for (int i = 0; i < N2; ++i) hw2[i] = HW2[kb + i];
+  for (int i = 0; i < N2; ++i) hw[i] = HW[kb + i];
   SAC_STAMP(1, 1);
-  f32x16 acc = zero16(), acc2 = zero16();
+  f32x16 acc = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
     if (c) load_b<CS>(bv, W2, H, kb + c * CS, j0 + rl);
     float av[CS];
 #pragma unroll
-    for (int i = 0; i < CS; ++i) av[i] = pos2(c * CS + i) ? hw1[c * CS + i] : 0.0f;
+    for (int i = 0; i < CS; ++i) av[i] = pos2(c * CS + i) ? hw[c * CS + i] : 0.0f;
     mfma_n<CS>(acc, av, bv);
-    if constexpr (kActor) {
-#pragma unroll
-      for (int i = 0; i < CS; ++i) av[i] = pos2(c * CS + i) ? hw2[c * CS + i] : 0.0f;
-      mfma_n<CS>(acc2, av, bv);
-    }
   }
   SAC_STAMP(1, 2);
-  float* o1 = kActor ? a.s.um : a.s.uq[net];
-  // (the factors out through LDS as 16-byte stores: tiles_out)
-  if constexpr (kActor) {  // U_m and U_s behind one barrier
-    float v[2][4];
-    splitk_finish2(acc, acc2, lds, lds + FwdLds<H>::kSplit, [&](int q, int, int, float x, float x2) {
-      v[0][q] = m1[q] > 0.0f ? x : 0.0f;
-      v[1][q] = m1[q] > 0.0f ? x2 : 0.0f;
-    });
-    float* const st[2] = {lds, lds + FwdLds<H>::kSplit};
-    float* const dst[2] = {o1 + (int64_t)r0 * H + j0, a.s.us + (int64_t)r0 * H + j0};
-    tiles_out<WTM, 2>(v, st, dst, H);
-  } else {
-    float v[1][4];
-    splitk_finish(acc, lds, [&](int q, int, int, float x) { v[0][q] = m1[q] > 0.0f ? x : 0.0f; });
-    float* const st[1] = {lds};
-    float* const dst[1] = {o1 + (int64_t)r0 * H + j0};
-    tiles_out<WTM, 1>(v, st, dst, H);
-  }
+  float* o1 = FK == FK_UM ? a.s.um : FK == FK_US ? a.s.us : a.s.uq[net];
+  // (out through LDS as 16-byte stores: tiles_out)
+  float v[1][4];
+  splitk_finish(acc, lds, [&](int q, int, int, float x) { v[0][q] = m1[q] > 0.0f ? x : 0.0f; });
+  float* const st[1] = {lds};
+  float* const dst[1] = {o1 + (int64_t)r0 * H + j0};
+  tiles_out<WTM, 1>(v, st, dst, H);
 }
 
 template <int H, int WT>
@@ -1031,44 +1018,44 @@ __global__ __launch_bounds__(256) void sac_mid_kernel(MArgs a) {
   SAC_STAMP(1, 0);
   // Block order (block i and block i + 256 share a CU): the critic tiles (heavy prologue: the pre-activation rows and
   // the W2ᵀ slice) take the first block of every CU, the backward-factor tiles (a mask word per row) the second, the
-  // one-chain critic factors beside the two-chain Q / tangent tiles and the two-chain actor factors beside one-chain
-  // target tiles. (With the T2 target tiles in second slots their prologue waited 2.5 µs behind the first block's
-  // loads, and two-chain tiles sharing a CU stretched each other's products: per-block stamps profiles/round6/r6i_*,
-  // r6j_*.) One extra block, the last, advances the step and snapshots what P3 reads: in front of a tile that serial
-  // work (a dependent load, the double-precision bias corrections, 4·H stores) held the tile 3 µs, behind one it
-  // ended the launch.
+  // one-chain critic factors beside the two-chain Q / tangent tiles and the U_m / U_s tiles beside the target tiles.
+  // (With the T2 target tiles in second slots their prologue waited 2.5 µs behind the first block's loads, and
+  // two-chain tiles sharing a CU stretched each other's products: per-block stamps profiles/round6/r6i_*, r6j_*.)
+  // The target tiles, the first to end, also advance the step and snapshot what P3 reads, after their tile: in front
+  // of a tile that serial work (a dependent load, the double-precision bias corrections, 4·H stores) held the tile
+  // 3 µs, and as an extra block past the 2 × 256 slots it waited for a slot and ended the launch 1.6 µs late.
   const int bt = a.L.Bp / kTile2;
-  if (blockIdx.x == gridDim.x - 1) {
-    if (threadIdx.x == 0) {  // step t and Adam's bias corrections (P1 read the old value)
-      const int64_t t = *a.step + 1;
+  int bx, by;
+  tile_of<H>(bx, by);
+  if (bx < 2 * bt) p2_critic_tile<H, false, WT>(a, bx / bt, bx % bt, by, lds);
+  else if (bx < 4 * bt) {
+    constexpr int CB = H / kTile2;
+    const int nt = 2 * bt * CB, part = (int)blockIdx.x - nt, tid = threadIdx.x;
+    const Layout& L = a.L;
+    const float* P = a.params;
+    // the parameters P3 reads (it updates them in place), before this step's update: element e of [5 scalars | 4·H]
+    const int e = part * kThreads + tid;
+    float sv = 0.0f;
+    if (e < 5) sv = e == 0 ? P[0] : e < 3 ? P[L.q_base[e - 1] + L.c_b3] : a.targets[(int64_t)(e - 3) * L.q_size + L.c_b3];
+    else if (e < 5 + 4 * H) {
+      const int k = e - 5, m = k / H, j = k % H;
+      sv = P[(m == 0 ? L.p_wm : m == 1 ? L.p_ws : L.q_base[m - 2] + L.c_w3) + j];
+    }
+    const bool stepper = part == nt - 1 && tid == 0;
+    const int64_t t = stepper ? *a.step + 1 : 0;  // P1 read the old value
+    p2_critic_tile<H, true, WT>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
+    if (e < 5) pub<WT_ACT>(WT, a.s.snap + e, sv);
+    else if (e < 5 + 4 * H) pub<WT_ACT>(WT, a.s.snap + SN_HEAD + (e - 5), sv);
+    if (stepper) {  // step t and Adam's bias corrections
       pub<WT_ACT>(WT, a.step, t);
       const AdamStep st = adam_step(a.hp, t);
       pub<WT_ACT>(WT, a.stats + 5, st.step_pi);
       pub<WT_ACT>(WT, a.stats + 6, st.step_q);
       pub<WT_ACT>(WT, a.stats + 7, st.bc2_sqrt);
     }
-    // the parameters P3 reads (it updates them in place), before this step's update
-    const Layout& L = a.L;
-    const float* P = a.params;
-    float* sn = a.s.snap;
-    if (threadIdx.x < 5) {
-      const int i = threadIdx.x;
-      pub<WT_ACT>(WT, sn + i, i == 0 ? P[0] : i < 3 ? P[L.q_base[i - 1] + L.c_b3] : a.targets[(int64_t)(i - 3) * L.q_size + L.c_b3]);
-    }
-    for (int j = threadIdx.x; j < L.H; j += kThreads) {
-      pub<WT_ACT>(WT, sn + SN_HEAD + j, P[L.p_wm + j]);
-      pub<WT_ACT>(WT, sn + SN_HEAD + L.H + j, P[L.p_ws + j]);
-      pub<WT_ACT>(WT, sn + SN_HEAD + 2 * L.H + j, P[L.q_base[0] + L.c_w3 + j]);
-      pub<WT_ACT>(WT, sn + SN_HEAD + 3 * L.H + j, P[L.q_base[1] + L.c_w3 + j]);
-    }
-    return;
-  }
-  int bx, by;
-  tile_of<H>(bx, by);
-  if (bx < 2 * bt) p2_critic_tile<H, false, WT>(a, bx / bt, bx % bt, by, lds);
-  else if (bx < 4 * bt) p2_critic_tile<H, true, WT>(a, (bx - 2 * bt) / bt, (bx - 2 * bt) % bt, by, lds);
-  else if (bx < 6 * bt) p2_factor_tile<H, false, WT>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by, lds);
-  else p2_factor_tile<H, true, WT>(a, 0, bx - 6 * bt, by, lds);
+  } else if (bx < 6 * bt) p2_factor_tile<H, FK_CRITIC, WT>(a, (bx - 4 * bt) / bt, (bx - 4 * bt) % bt, by, lds);
+  else if (bx < 7 * bt) p2_factor_tile<H, FK_UM, WT>(a, 0, bx - 6 * bt, by, lds);
+  else p2_factor_tile<H, FK_US, WT>(a, 0, bx - 7 * bt, by, lds);
   SAC_STAMP(1, 3);
 }
 
@@ -1810,7 +1797,7 @@ __global__ __launch_bounds__(256) void sac_act_head_kernel(ActArgs a) {
 template <int H>
 void launch_step(const MArgs& m, const WArgs& w, hipStream_t st) {
   const unsigned bt = (unsigned)(m.L.Bp / kTile2), cb = H / kTile2;
-  const dim3 g1(6 * bt * cb), g2p(7 * bt * cb + 1), g3((unsigned)(w.n_mfma + w.n_valu + 1 + w.n_stage));
+  const dim3 g1(6 * bt * cb), g2p(8 * bt * cb), g3((unsigned)(w.n_mfma + w.n_valu + 1 + w.n_stage));
   if (m.wt == kWtLarge) {
     hipLaunchKernelGGL((sac_fwd_kernel<H, kWtLarge>), g1, dim3(256), 0, st, m);
     hipLaunchKernelGGL((sac_mid_kernel<H, kWtLarge>), g2p, dim3(256), 0, st, m);

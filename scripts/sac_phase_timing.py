@@ -44,7 +44,7 @@ def kinds(kernel, nblocks, bt, cb, n_mfma, n_valu):
             out.append("actor_fwd" if bx < 2 * bt else "critic_data_fwd" if bx < 4 * bt else "target_pre")
         else:
             out.append("critic_tangent" if bx < 2 * bt else "targets" if bx < 4 * bt else
-                       "critic_factors" if bx < 6 * bt else "actor_factors" if bx < 7 * bt else "step_snapshot")
+                       "critic_factors" if bx < 6 * bt else "actor_factors")
     return out
 
 
@@ -75,7 +75,7 @@ def main():
     st = np.frombuffer(buf, dtype=np.uint64).reshape(3, KSTAMP, NST).astype(np.float64)
     bp = (a.batch + 31) // 32 * 32
     bt, cb = bp // 32, a.hidden // 32
-    grids = [6 * bt * cb, 7 * bt * cb + 1, 3 * cb * cb + 3 * (a.hidden // 16) + 1]
+    grids = [6 * bt * cb, 8 * bt * cb, 3 * cb * cb + 3 * (a.hidden // 16) + 1]
     names = ["fwd (P1)", "mid (P2)", "wgrad (P3)"]
     res = {"step_us": r["ms_per_grad_step"] * 1e3, "batch": a.batch, "hidden": a.hidden, "kernels": {}}
     for k in range(3):
