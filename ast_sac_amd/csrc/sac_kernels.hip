@@ -505,14 +505,37 @@ __device__ __forceinline__ void first_layer_pre(const float* lw1t, const float* 
   for (int i = 0; i < CS; ++i) av[i] = relu(fmaf(lw1t[(nin - 1) * H + k0 + i], xl, pre[i]));
 }
 
-// this lane's first-layer chunk (row lane & 31, columns k0 .. k0 + CS) straight to its row of the matrix by the
-// block that owns column block k0 / 32 (every block computes the same values): float4 stores
-template <int H, int CS>
-__device__ __forceinline__ void store_slice(int wt, float* base, int r0, int by, const float (&av)[CS], int k0) {
+// this lane's first-layer chunk (row lane & 31, columns k0 .. k0 + CS) out to its row of the matrix by the block that
+// owns column block k0 / 32 (every block computes the same values). A chunk of exactly one column block (CS = 32: H =
+// 256, 512) goes through the half wave's own 32 x 32 tile in LDS (st) and out as whole 128-byte row segments, four
+// rows per store instruction, still inside the product loop; other chunks straight from registers as 16-byte
+// pieces. (Each 16-byte store instruction of the direct form wrote 32 rows' pieces: P1 0.85 µs longer at B = 256 than
+// without these stores; staged to the block's end they moved the cost into the launch boundary, profiles/round6/r6s_*.)
+template <int H, int CS, int WTM>
+__device__ __forceinline__ void slice_out(float* st, float* base, int r0, int by, const float (&av)[CS], int k0) {
   if (k0 / kTile2 != by) return;
-  float* d = base + (int64_t)(r0 + (threadIdx.x & 31)) * H + k0;
+  const int rl = (int)threadIdx.x & 31;
+  if constexpr (CS == kTile2 && (WTM & WT_ACT) != 0) {  // (plain stores, below 128 rows: direct, 0.1 µs less at B = 64)
+    float* d = st + rl * kStageLd;
 #pragma unroll
-  for (int q = 0; q < CS / 4; ++q) pub4<WT_ACT>(wt, d + 4 * q, av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+    for (int q = 0; q < CS / 4; ++q)
+      *reinterpret_cast<float4*>(d + 4 * q) = make_float4(av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+    // (the lanes reading back are the writing half wave's own: in-order LDS, a compiler barrier only)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int lr = rl >> 3, c4 = (rl & 7) * 4;
+    float* g = base + (int64_t)r0 * H + k0 + c4;
+#pragma unroll
+    for (int j = 0; j < kTile2 / 4; ++j) {
+      const int row = 4 * j + lr;
+      const float4 v = *reinterpret_cast<const float4*>(st + row * kStageLd + c4);
+      pub4<WT_ACT>(WTM, g + (int64_t)row * H, v.x, v.y, v.z, v.w);
+    }
+  } else {
+    float* d = base + (int64_t)(r0 + rl) * H + k0;
+#pragma unroll
+    for (int q = 0; q < CS / 4; ++q) pub4<WT_ACT>(WTM, d + 4 * q, av[4 * q], av[4 * q + 1], av[4 * q + 2], av[4 * q + 3]);
+  }
 }
 
 // a batch row's O inputs, zero past O, branch-free: a clamped index and a compare against O held in a VGPR, so
@@ -549,6 +572,7 @@ struct FwdLds {
   static constexpr int kFloats = 2 * kSplit + kW1 + kX;
   static constexpr int kW1Off = 2 * kSplit;
   static constexpr int kXOff = 2 * kSplit + kW1;
+  static_assert(3 * kTile2 * kStageLd <= kSplit, "P1's staged tiles share the second split region");
 };
 
 // TanhNormal.rsample_and_logprob (distributions.py:346-392) of one row's head
@@ -694,6 +718,8 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
   (void)B;
   __syncthreads();
   SAC_STAMP(0, 1);
+  float* stage = lds + FwdLds<H>::kSplit;  // (the second split region: free in P1) h2 | h1 tiles
+  float* st_h1 = stage + kTile2 * kStageLd;
   f32x16 acc = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -701,11 +727,10 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
     if (c) load_b<CS>(bv, a.T, H, k0, c0 + rl);
     float av[CS];
     first_layer<H, CS>(lw1, lx + rl * (kXLd + 1), O, k0, av);
-    if (!nrow) store_slice<H, CS>(WTM, a.s.h1, r0, by, av, k0);
+    if (!nrow) slice_out<H, CS, WTM>(st_h1, a.s.h1, r0, by, av, k0);
     mfma_n<CS>(acc, av, bv);
   }
   SAC_STAMP(0, 2);
-  float* stage = lds + FwdLds<H>::kSplit;  // (the second split region: free in P1)
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr;
     const float y = relu(v + b2c);
@@ -763,6 +788,9 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   }
   __syncthreads();
   SAC_STAMP(0, 1);
+  float* stage = lds + FwdLds<H>::kSplit;  // (the second split region: free in P1) g2 | g1 | pre tiles
+  float* st_g1 = stage + kTile2 * kStageLd;
+  float* st_pre = st_g1 + kTile2 * kStageLd;
   f32x16 acc = zero16();
 #pragma unroll
   for (int c = 0; c < KS::NCH; ++c) {
@@ -770,14 +798,13 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
     if (c) load_b<CS>(bv, WT, H, k0, c0 + rl);
     float av[CS], pre[CS];
     first_layer_pre<H, CS>(lw1, lx + rl * (kXLd + 1), O + 1, k0, pre, av);
-    store_slice<H, CS>(WTM, a.s.g1[net], r0, by, av, k0);
-    store_slice<H, CS>(WTM, a.s.pre[net], r0, by, pre, k0);
+    slice_out<H, CS, WTM>(st_g1, a.s.g1[net], r0, by, av, k0);
+    slice_out<H, CS, WTM>(st_pre, a.s.pre[net], r0, by, pre, k0);
     mfma_n<CS>(acc, av, bv);
   }
   if (rt == 0 && by == 0)  // fc0's action column, contiguous, for P2
     for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(WTM, a.s.w1a + net * H + k, lw1[O * H + k]);
   SAC_STAMP(0, 2);
-  float* stage = lds + FwdLds<H>::kSplit;  // (the second split region: free in P1)
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
     const int r = r0 + rr;
     const float y = relu(v + b2c);
