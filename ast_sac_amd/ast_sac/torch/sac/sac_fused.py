@@ -290,7 +290,9 @@ class FusedSACTrainer(TorchTrainer):
         Philox counter of the batch draw, Adam's bias corrections), so the steps are the same as one graph each.
         The steps form a chain (sacf_grads_chain): each but the last stages the next step's batch in its
         weight-gradient pass, and each but the first starts from that staged batch (nothing writes the replay
-        ring inside the graph, so it is the batch its own gather would draw)."""
+        ring inside the graph, so it is the batch its own gather would draw). With the update in the same launch,
+        each but the last leaves the flat gradient unwritten (nothing reads it in between: p.grad after the run is
+        the last step's gradient, as with one graph per step)."""
         self._hip_step_prepare(replay_buffer)
         key = (id(replay_buffer), self.GRAPH_STEPS)
         if getattr(self, "_mgraph", None) is None or self._mgraph[0] != key:
@@ -303,8 +305,9 @@ class FusedSACTrainer(TorchTrainer):
             with torch.cuda.graph(g):
                 sf.set_stream()
                 for k in range(self.GRAPH_STEPS):
-                    chain = ((sfb.CHAIN_FROM_STAGED if k > 0 else 0) |
-                             (sfb.CHAIN_STAGE_NEXT if k < self.GRAPH_STEPS - 1 else 0))
+                    last = k == self.GRAPH_STEPS - 1
+                    chain = ((sfb.CHAIN_FROM_STAGED if k > 0 else 0) | (0 if last else sfb.CHAIN_STAGE_NEXT) |
+                             (0 if last or self.split else sfb.CHAIN_NO_GRADS))
                     self._hip_launch(replay_buffer, "a" if self.split else "ab", chain)
                     if self.split:
                         torch.distributed.all_reduce(self.flat_grad, group=self.pg)

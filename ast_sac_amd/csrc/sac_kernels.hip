@@ -232,6 +232,9 @@ __device__ inline void block_sum(float (&v)[N], float (*red)[32], float* out) {
 #define SACF_WT 7
 #endif
 enum { WT_ACT = 1, WT_OPT = 2, WT_EPI = 4 };
+// (not a store class: set in the weight-gradient kernel's mask, its launch does not write the flat gradient —
+// SACF_CHAIN_NO_GRADS with the update fused; a compile-time choice: a run-time test around the stores cost 0.5 µs)
+constexpr int WT_NOG = 8;
 // the two masks the step kernels are instantiated with (the launch picks by batch: wt_mask_for)
 constexpr int kWtLarge = WT_ACT | WT_OPT | WT_EPI, kWtSmall = WT_OPT | WT_EPI;
 // (wt: the launch's mask — a template argument of every kernel that stores, so the test folds at compile time: a
@@ -1219,6 +1222,8 @@ struct WArgs {
   MArgs m;
   float* grads;
   int fuse;   // single process: each block also applies Adam / soft update / W2ᵀ to the elements it finished
+  int pub_grads;  // write the flat gradient (always without fuse; chain SACF_CHAIN_NO_GRADS clears it): the host's
+                  // choice of kernel (WT_NOG)
   int n_mfma, n_valu;
   int n_stage;  // chain STAGE_NEXT: blocks staging the next step's batch (after the scalar block), else 0
   ApplyArgs ap;
@@ -1385,7 +1390,7 @@ __device__ __forceinline__ void p3_mfma_tile_wt(const WArgs& a, int bx, WLds& S)
   const int64_t out_off = a.w2_off[mat];
   splitk_finish(acc, S.u.mm.split, [&](int q, int rr, int cc, float v) {
     const int64_t e = out_off + (int64_t)(j0 + rr) * H + k0 + cc;
-    pub<WT_OPT>(WT, a.grads + e, v);
+    if constexpr ((WT & WT_NOG) == 0) pub<WT_OPT>(WT, a.grads + e, v);
     if (a.fuse) {
       xe[q].g = v;
       adam_st(a.ap, sst, e, xe[q], mat > 0, WT);
@@ -1529,7 +1534,7 @@ __device__ __forceinline__ void p3_valu_block_wt(const WArgs& a, int vb, WLds& S
 #pragma unroll
     for (int st = 1; st < kValuStreams; ++st) g += vr[st][i][u];
     const int64_t e = el_off(k);
-    pub<WT_OPT>(WT, a.grads + e, g);
+    if constexpr ((WT & WT_NOG) == 0) pub<WT_OPT>(WT, a.grads + e, g);
     if (a.fuse) {
       xe[q].g = g;
       adam_st(a.ap, sst, e, xe[q], !actor, WT);
@@ -1595,7 +1600,7 @@ __device__ __forceinline__ void p3_scalar_block_wt(const WArgs& a, WLds& S) {
   }
   if (tid >= 5) return;
   const float g = tid == 0 ? (m.hp.auto_ent ? sum[4] * invB : 0.0f) : sum[4 + tid];
-  pub<WT_OPT>(WT, a.grads + off, g);
+  if constexpr ((WT & WT_NOG) == 0) pub<WT_OPT>(WT, a.grads + off, g);
   if (a.fuse && (tid > 0 || m.hp.auto_ent)) {
     xs.g = g;
     adam_st(a.ap, sst, off, xs, tid >= 3, WT);
@@ -1828,11 +1833,13 @@ void launch_step(const MArgs& m, const WArgs& w, hipStream_t st) {
   if (m.wt == kWtLarge) {
     hipLaunchKernelGGL((sac_fwd_kernel<H, kWtLarge>), g1, dim3(256), 0, st, m);
     hipLaunchKernelGGL((sac_mid_kernel<H, kWtLarge>), g2p, dim3(256), 0, st, m);
-    hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtLarge>), g3, dim3(256), 0, st, w);
+    if (w.pub_grads) hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtLarge>), g3, dim3(256), 0, st, w);
+    else hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtLarge | WT_NOG>), g3, dim3(256), 0, st, w);
   } else {
     hipLaunchKernelGGL((sac_fwd_kernel<H, kWtSmall>), g1, dim3(256), 0, st, m);
     hipLaunchKernelGGL((sac_mid_kernel<H, kWtSmall>), g2p, dim3(256), 0, st, m);
-    hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtSmall>), g3, dim3(256), 0, st, w);
+    if (w.pub_grads) hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtSmall>), g3, dim3(256), 0, st, w);
+    else hipLaunchKernelGGL((sac_wgrad_kernel<H, kWtSmall | WT_NOG>), g3, dim3(256), 0, st, w);
   }
 }
 
@@ -2183,6 +2190,7 @@ static int grads_impl(sacf_handle* h, const float* obs, const float* act, const 
   w.m = a;
   w.grads = h->grads;
   w.fuse = h->cfg.world_size == 1 && !h->cfg.split_update;  // no all-reduce in between: apply in the same kernel
+  w.pub_grads = !(w.fuse && (chain & SACF_CHAIN_NO_GRADS));
   w.ap = apply_args(h);
   const int CB = h->L.H / kTile2;
   w.n_mfma = 3 * CB * CB;
@@ -2211,9 +2219,10 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
 
 int sacf_grads_chain(sacf_handle* h, const float* eps, int32_t flags) {
   if (!h) return SACF_EINVAL;
-  if (flags & ~(SACF_CHAIN_STAGE_NEXT | SACF_CHAIN_FROM_STAGED)) return sfail(h, SACF_EINVAL, "sacf_grads_chain: flags");
+  if (flags & ~(SACF_CHAIN_STAGE_NEXT | SACF_CHAIN_FROM_STAGED | SACF_CHAIN_NO_GRADS))
+    return sfail(h, SACF_EINVAL, "sacf_grads_chain: flags");
   // a staged batch carries the normals of the call that staged it, so a chained step cannot take the caller's eps
-  if (flags && eps)
+  if ((flags & (SACF_CHAIN_STAGE_NEXT | SACF_CHAIN_FROM_STAGED)) && eps)
     return sfail(h, SACF_EINVAL, "sacf_grads_chain: STAGE_NEXT / FROM_STAGED need eps == NULL (in-kernel normals)");
   if (!h->r_obs) return sfail(h, SACF_ESTATE, "sacf_grads_chain: no replay bound");
   if ((flags & SACF_CHAIN_FROM_STAGED) && !h->staged)

@@ -9,8 +9,8 @@ import torch  # noqa: F401  (HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACFUSED_LIB") or os.path.join(_HERE, "lib", "libsacfused.so")
-ABI_VERSION = 3
-CHAIN_STAGE_NEXT, CHAIN_FROM_STAGED = 1, 2  # sacf_grads_chain flags
+ABI_VERSION = 4
+CHAIN_STAGE_NEXT, CHAIN_FROM_STAGED, CHAIN_NO_GRADS = 1, 2, 4  # sacf_grads_chain flags
 EXPORTED_SYMBOLS = ("sacf_abi_version", "sacf_build_info", "sacf_create", "sacf_destroy", "sacf_last_error", "sacf_set_stream",
                     "sacf_param_count", "sacf_target_count", "sacf_stats_count", "sacf_bind", "sacf_sync_params",
                     "sacf_set_replay", "sacf_grads", "sacf_grads_chain", "sacf_apply", "sacf_policy_reserve", "sacf_policy_act",
@@ -133,7 +133,8 @@ class SacFused:
 
     def grads_chain(self, flags, eps=None):
         """A replay-sampled step of a chain (sacf_grads_chain): CHAIN_STAGE_NEXT stages the next step's batch,
-        CHAIN_FROM_STAGED starts from the batch the previous call staged (no replay change in between)."""
+        CHAIN_FROM_STAGED starts from the batch the previous call staged (no replay change in between),
+        CHAIN_NO_GRADS leaves the gradient buffer unwritten when the update is applied in the same call."""
         self._check(self.L.sacf_grads_chain(self.h, _p(eps), int(flags)), "sacf_grads_chain")
 
     def apply(self):

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SACF_ABI_VERSION 3 /* 3: sacf_grads_chain (steps in a chain stage the next batch); 2: three-pass step */
+#define SACF_ABI_VERSION 4 /* 4: SACF_CHAIN_NO_GRADS; 3: sacf_grads_chain (steps in a chain stage the next batch); 2: three-pass step */
 #define SACF_OK 0
 #define SACF_EINVAL -1
 #define SACF_EHIP -2
@@ -110,11 +110,17 @@ int sacf_grads(sacf_handle* h, const float* obs, const float* act, const float* 
  *                           it (the same rows and normals: results are bitwise those of sacf_grads). Only right
  *                           after a call with SACF_CHAIN_STAGE_NEXT on this handle (SACF_ESTATE otherwise), and
  *                           the caller guarantees the replay ring and its size did not change in between.
- * A replay ring must be bound (sacf_set_replay). With either flag eps must be NULL (the normals then come from the
+ * A replay ring must be bound (sacf_set_replay). With either staging flag eps must be NULL (the normals then come from the
  * in-kernel Philox stream, and a staged batch carries the ones of the call that staged it): SACF_EINVAL otherwise.
+ *   SACF_CHAIN_NO_GRADS     with the update applied in the same call (world_size == 1, no split_update): the step
+ *                           does not write `grads` (it keeps its previous contents; the update, the parameters,
+ *                           targets and Adam state are bitwise those of the step without the flag). The trainer's
+ *                           multi-step graph sets it on every step but its last, whose gradient stays inspectable.
+ *                           Ignored when the update is a separate sacf_apply (which reads `grads`).
  * flags == 0 is sacf_grads(h, NULL x 5, eps). */
 #define SACF_CHAIN_STAGE_NEXT 1
 #define SACF_CHAIN_FROM_STAGED 2
+#define SACF_CHAIN_NO_GRADS 4
 int sacf_grads_chain(sacf_handle* h, const float* eps, int32_t flags);
 /* Adam + soft target update from `grads` (divided by world_size); a no-op when sacf_grads applied it. */
 int sacf_apply(sacf_handle* h);

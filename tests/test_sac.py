@@ -278,8 +278,9 @@ def test_hip_sac_graph_replay_equals_eager_launches():
 @pytest.mark.parametrize("H,B", [(256, 256), (64, 96)])
 def test_hip_sac_multi_step_graph_equals_single_step_graphs(H, B):
     """train_from_buffer's runs of GRAPH_STEPS steps in one captured graph give bitwise the parameters, targets,
-    Adam state, step counter and statistics of one graph replay per step (21 steps: the first alone for the
-    epoch statistics, two 8-step replays, four single steps)."""
+    Adam state, step counter, statistics and last gradient of one graph replay per step (21 steps: the first alone
+    for the epoch statistics, two 8-step replays, four single steps; the multi-step graph's steps but its last leave
+    the gradient unwritten)."""
     from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
     rb = DeviceReplayBuffer(5000, 8, 1, "cuda")
     b, _ = _rand_batch(3000, "cuda", seed=5)
@@ -294,8 +295,35 @@ def test_hip_sac_multi_step_graph_equals_single_step_graphs(H, B):
         torch.cuda.synchronize()
         assert (getattr(tr, "_mgraph", None) is not None) == multi
         assert int(tr._step_t.item()) == 21 and tr._n_train_steps_total == 21
-        res.append(torch.cat([tr.flat_param, tr.flat_target, tr._adam_m, tr._adam_v, tr._stats_t]).cpu())
+        res.append(torch.cat([tr.flat_param, tr.flat_target, tr._adam_m, tr._adam_v, tr._stats_t,
+                              tr.flat_grad]).cpu())
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,B", [(256, 256), (96, 64)])
+def test_hip_sac_chain_no_grads(H, B):
+    """SACF_CHAIN_NO_GRADS: a fused chained step leaves the gradient buffer as it was, and its update (parameters,
+    targets, Adam state, statistics) is bitwise the same step's without the flag."""
+    from ast_sac_amd import sacfused
+    from ast_sac_amd.ast_sac.data_management.replay_buffer import DeviceReplayBuffer
+    rb = DeviceReplayBuffer(4000, 8, 1, "cuda")
+    b, _ = _rand_batch(3000, "cuda", seed=8)
+    rb.add_batch(b["observations"], b["actions"], b["rewards"], b["next_observations"], b["terminals"])
+    res, grads = [], []
+    for flag in (0, sacfused.CHAIN_NO_GRADS):
+        tr = _trainer("hip", H, B, "cuda", use_graph=False, seed=5)
+        tr.train_from_buffer(rb, 1)  # binds the replay ring
+        sf = tr._sf
+        sf.grads_chain(sacfused.CHAIN_STAGE_NEXT)
+        tr.flat_grad.fill_(7.0)
+        sf.grads_chain(sacfused.CHAIN_FROM_STAGED | sacfused.CHAIN_STAGE_NEXT | flag)
+        sf.grads_chain(sacfused.CHAIN_FROM_STAGED | flag)
+        torch.cuda.synchronize()
+        res.append(torch.cat([tr.flat_param, tr.flat_target, tr._adam_m, tr._adam_v, tr._stats_t]).cpu())
+        grads.append(tr.flat_grad.cpu())
+    assert torch.equal(res[0], res[1])
+    assert bool((grads[1] == 7.0).all()) and not bool((grads[0] == 7.0).all())
 
 
 @pytest.mark.gpu
