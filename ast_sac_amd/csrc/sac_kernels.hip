@@ -83,9 +83,17 @@ struct Hyper {
   float inv_world;
 };
 
-// per-row parts (one per 32-column block, in block order) of the head dot products, [Bp][set][CB]: a row's
-// sets are contiguous, so a reader's set offsets are compile-time constants off one row address
+// per-row parts (one per 32-column block, in block order) of the head dot products, in the row-tile word layout
+// (rw_at below: [Bp / 32][set][CB][32])
 enum { PS_Q1D, PS_Q2D, PS_T1, PS_T2, PS_Q1A, PS_Q2A, PS_D1, PS_D2, PS_N };
+// The row-tile word layout of the per-row words (parts, head parts, activation masks): the words of one 32-row tile
+// for one (set, column block) are contiguous, so the block that produced them writes them as runs (row_words_out)
+// and a reader whose lanes hold consecutive rows reads them coalesced. (Row-major [row][set][CB], every epilogue
+// store of these words was 4 bytes into a different row: P1 / P2 took 0.3 / 0.4 µs longer at B = 256 than
+// without them, profiles/round6/r6y_*.)
+__host__ __device__ __forceinline__ int64_t rw_at(int r, int set, int nsets, int CB, int by) {
+  return ((((int64_t)(r >> 5) * nsets + set) * CB + by) << 5) + (r & 31);
+}
 // the per-row record [Bp][kRec]: the obs row's actor head (HD_*: mean, ls_raw, std, z, a, logp), its two
 // reparameterisation normals, the replayed reward / terminal / action and log π(ã'|s') of the next_obs row
 enum { HD_MEAN, HD_LSRAW, HD_STD, HD_Z, HD_A, HD_LOGP, R_EPS, R_EPSN, R_REW, R_TERM, R_ACT, R_LOGPN };
@@ -100,15 +108,16 @@ struct Scr {
   float *um, *us;            // actor backward factors
   float *uq[2];              // critic backward factors (data rows)
   float *rec;                // [Bp][kRec] per-row record (HD_* / R_*)
-  float *hpart;              // [2Bp][2][CB] actor head parts (mean | log_std) of the obs and next_obs rows
+  float *hpart;              // actor head parts (mean | log_std) of the obs and next_obs rows, 2Bp rows (rw_at, 2 sets)
   // fc0 of a critic up to (not including) its action term — b1 + Σ_{m < O} W1[:, m] x_m, the fmaf chain in input
   // order — on the obs rows (Q1, Q2: from P1's data tiles) and the next_obs rows (T1, T2: P1's target tiles), and
   // fc0's action column W1[:, O] of Q1, Q2, T1, T2 [4][H]: P2's critic tiles on (obs, ã) / (next_obs, ã') add the
   // action term themselves (the same chain, so the same bits as fc0 on the whole row)
   float *pre[4];             // [Bp][H] each: Q1, Q2 (obs rows), T1, T2 (next_obs rows)
   float *w1a;                // [4][H]
-  float *part;               // [Bp][PS_N][CB]
-  // [h2 > 0] and [g2 > 0] of Q1 / Q2 as bit masks, [Bp][CB] words (bit c of word (r, b): column 32b + c of row r):
+  float *part;               // Bp rows (rw_at, PS_N sets)
+  // [h2 > 0] and [g2 > 0] of Q1 / Q2 as bit masks, Bp x CB words (rw_at, 1 set; bit c of word (r, b): column 32b + c
+  // of row r):
   // the backward factors (P2) and the MFMA weight-gradient tiles (P3) use the layer-2 activations only through this
   // mask, so they read 1 bit per element instead of the float
   uint32_t *h2m, *g2m[2];
@@ -387,6 +396,20 @@ __device__ __forceinline__ void tile_out(const float* stage, float* dst, int ld)
   pub4<WT_EPI>(WTM, dst + (int64_t)row * ld + c4, v.x, v.y, v.z, v.w);
 }
 
+// per-row words of a 32-row tile that splitk_finish's epilogue left in LDS (rwl[set · 32 + row], by its cc == 0
+// lanes) out to the row-tile layout, dst[set] the run of the tile's 32 rows: wave w writes rows 8w .. 8w + 7, the
+// rows splitk_finish gives it, so the LDS round trip stays inside the wave (no block barrier)
+template <int WTM, int NS, class T>
+__device__ __forceinline__ void row_words_out(const T* rwl, T* const (&dst)[NS]) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  if (lane < 8 * NS) {
+    const int st = lane >> 3, row = 8 * w + (lane & 7);
+    pub<WT_ACT>(WTM, dst[st] + row, rwl[st * 32 + row]);
+  }
+}
+
 // the row of output register q (0..3) of this lane in splitk_finish's order (defined below)
 __device__ __forceinline__ int finish_row(int q);
 
@@ -575,7 +598,7 @@ struct FwdLds {
   static constexpr int kFloats = 2 * kSplit + kW1 + kX;
   static constexpr int kW1Off = 2 * kSplit;
   static constexpr int kXOff = 2 * kSplit + kW1;
-  static_assert(3 * kTile2 * kStageLd <= kSplit, "P1's staged tiles share the second split region");
+  static_assert(3 * kTile2 * kStageLd + 3 * 32 <= kSplit, "P1's staged tiles and row words share the second split region");
 };
 
 // TanhNormal.rsample_and_logprob (distributions.py:346-392) of one row's head
@@ -734,18 +757,28 @@ __device__ __forceinline__ void p1_actor_tile(const MArgs& a, int rt, int by, fl
     mfma_n<CS>(acc, av, bv);
   }
   SAC_STAMP(0, 2);
+  float* rwl = st_h1 + kTile2 * kStageLd;  // row words: head parts (mean | log_std) [2][32], mask words [32]
+  uint32_t* rwm = reinterpret_cast<uint32_t*>(rwl + 2 * kTile2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
-    const int r = r0 + rr;
     const float y = relu(v + b2c);
     stage[rr * kStageLd + cc] = y;
     const uint64_t pos = __ballot(y > 0.0f);  // (rows of the two half waves: the low / high 32 bits)
-    if (r < Bp && cc == 0) pub<WT_ACT>(WTM, a.s.h2m + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
     const float pm = halfwave_sum(y * wm), ps = halfwave_sum(y * ws);
     if (cc == 0) {
-      pub<WT_ACT>(WTM, a.s.hpart + (int64_t)r * 2 * CB + by, pm);
-      pub<WT_ACT>(WTM, a.s.hpart + (int64_t)r * 2 * CB + CB + by, ps);
+      rwm[rr] = (uint32_t)(lane < 32 ? pos : pos >> 32);
+      rwl[rr] = pm;
+      rwl[kTile2 + rr] = ps;
     }
   });
+  {
+    float* const dp[2] = {a.s.hpart + rw_at(r0, 0, 2, CB, by), a.s.hpart + rw_at(r0, 1, 2, CB, by)};
+    row_words_out<WTM, 2>(rwl, dp);
+    if (!nrow_tile) {
+      uint32_t* const dm[1] = {a.s.h2m + rw_at(r0, 0, 1, CB, by)};
+      row_words_out<WTM, 1>(rwm, dm);
+    }
+  }
+  (void)Bp;
   if (!nrow_tile) tile_out<WTM>(stage, a.s.h2 + (int64_t)r0 * H + c0, H);
 }
 
@@ -808,15 +841,24 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
   if (rt == 0 && by == 0)  // fc0's action column, contiguous, for P2
     for (int k = threadIdx.x; k < H; k += kThreads) pub<WT_ACT>(WTM, a.s.w1a + net * H + k, lw1[O * H + k]);
   SAC_STAMP(0, 2);
+  float* rwl = st_pre + kTile2 * kStageLd;  // row words: parts [32], mask words [32]
+  uint32_t* rwm = reinterpret_cast<uint32_t*>(rwl + kTile2);
   splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
-    const int r = r0 + rr;
     const float y = relu(v + b2c);
     stage[rr * kStageLd + cc] = y;
     const uint64_t pos = __ballot(y > 0.0f);
-    if (cc == 0) pub<WT_ACT>(WTM, a.s.g2m[net] + (int64_t)r * CB + by, (uint32_t)(lane < 32 ? pos : pos >> 32));
-    const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r
-    if (cc == 0) pub<WT_ACT>(WTM, a.s.part + ((int64_t)r * PS_N + PS_Q1D + net) * CB + by, pq);
+    const float pq = halfwave_sum(y * w3);  // this column block's part of g2 · w3 for row r0 + rr
+    if (cc == 0) {
+      rwm[rr] = (uint32_t)(lane < 32 ? pos : pos >> 32);
+      rwl[rr] = pq;
+    }
   });
+  {
+    float* const dp[1] = {a.s.part + rw_at(r0, PS_Q1D + net, PS_N, CB, by)};
+    row_words_out<WTM, 1>(rwl, dp);
+    uint32_t* const dm[1] = {a.s.g2m[net] + rw_at(r0, 0, 1, CB, by)};
+    row_words_out<WTM, 1>(rwm, dm);
+  }
   tile_out<WTM>(stage, a.s.g2[net] + (int64_t)r0 * H + c0, H);
 }
 
@@ -877,8 +919,11 @@ template <int CB>
 struct RowHeadIn {
   float pm[CB], pl[CB], bm, bs;
   __device__ __forceinline__ void load(const MArgs& a, int hrow) {
-    load_run<CB>(a.s.hpart + (int64_t)hrow * 2 * CB, pm);
-    load_run<CB>(a.s.hpart + (int64_t)hrow * 2 * CB + CB, pl);
+#pragma unroll
+    for (int b = 0; b < CB; ++b) {
+      pm[b] = a.s.hpart[rw_at(hrow, 0, 2, CB, b)];
+      pl[b] = a.s.hpart[rw_at(hrow, 1, 2, CB, b)];
+    }
     bm = a.params[a.L.p_bm];
     bs = a.params[a.L.p_bs];
   }
@@ -953,22 +998,27 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
     }
   }
   SAC_STAMP(1, 2);
+  float* rwl = lds + FwdLds<H>::kW1Off;  // row words (the W1 region: unused in P2)
   if constexpr (kTarget) {
     splitk_finish(acc, lds, [&](int, int rr, int cc, float v) {
       const float pq = halfwave_sum(relu(v + b2c) * w3);
-      if (cc == 0) pub<WT_ACT>(WTM, a.s.part + ((int64_t)(r0 + rr) * PS_N + PS_T1 + net) * CB + by, pq);
+      if (cc == 0) rwl[rr] = pq;
     });
+    float* const dp[1] = {a.s.part + rw_at(r0, PS_T1 + net, PS_N, CB, by)};
+    row_words_out<WTM, 1>(rwl, dp);
   } else {  // Q and its tangent reduced behind one barrier
     splitk_finish2(acc, act, lds, lds + FwdLds<H>::kSplit, [&](int, int rr, int cc, float v, float t) {
       const float y = relu(v + b2c);
       const float pq = halfwave_sum(y * w3);
       const float pd = halfwave_sum(y > 0.0f ? w3 * t : 0.0f);  // this column block's part of ∂Q/∂ã
       if (cc == 0) {
-        float* pr = a.s.part + (int64_t)(r0 + rr) * PS_N * CB + by;
-        pub<WT_ACT>(WTM, pr + (PS_Q1A + net) * CB, pq);
-        pub<WT_ACT>(WTM, pr + (PS_D1 + net) * CB, pd);
+        rwl[rr] = pq;
+        rwl[kTile2 + rr] = pd;
       }
     });
+    float* const dp[2] = {a.s.part + rw_at(r0, PS_Q1A + net, PS_N, CB, by),
+                          a.s.part + rw_at(r0, PS_D1 + net, PS_N, CB, by)};
+    row_words_out<WTM, 2>(rwl, dp);
   }
 }
 
@@ -1009,7 +1059,7 @@ __device__ __forceinline__ void p2_factor_tile(const MArgs& a, int net, int rt, 
   constexpr int CB = KS::CB, NW = mask_words(H);
   uint32_t mw[NW];
 #pragma unroll
-  for (int q = 0; q < NW; ++q) mw[q] = X2M[(int64_t)(r0 + rl) * CB + min(kb / 32 + q, CB - 1)];
+  for (int q = 0; q < NW; ++q) mw[q] = X2M[rw_at(r0 + rl, 0, 1, CB, min(kb / 32 + q, CB - 1))];
   auto pos2 = [&](int i) __attribute__((always_inline)) {  // bit kb + i (compile-time i)
     const int b = (kb & 31) + i;
     return ((mw[b >> 5] >> (b & 31)) & 1u) != 0u;
@@ -1100,7 +1150,9 @@ template <int CB>
 struct RowIn {
   float p[4 * CB], rc[kRec];
   __device__ __forceinline__ void load(const MArgs& a, int r, bool actor) {
-    load_run<4 * CB>(a.s.part + ((int64_t)r * PS_N + (actor ? PS_Q1A : PS_Q1D)) * CB, p);
+    const float* pp = a.s.part + rw_at(r, actor ? PS_Q1A : PS_Q1D, PS_N, CB, 0);  // (set k, block b: + (k·CB + b)·32)
+#pragma unroll
+    for (int i = 0; i < 4 * CB; ++i) p[i] = pp[(int64_t)i << 5];
     load_run<kRec>(a.s.rec + (int64_t)r * kRec, rc);
   }
   // Σ of set k's column-block parts in block order (a left fold: every reader gets the same bits)
@@ -1320,11 +1372,17 @@ __device__ __forceinline__ void p3_mfma_tile_wt(const WArgs& a, int bx, WLds& S)
     const int rb = rc + rl0, jw = j0 >> 5;
     auto load_chunk = [&](auto n_tag) __attribute__((always_inline)) {
       constexpr int N = decltype(n_tag)::value;
+      // (N rows from rb, a multiple of N: inside one 32-row tile, so their mask words are one 16-byte aligned run)
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      typedef const u32x4 __attribute__((address_space(1))) * gu4;
+      const gu4 yq = reinterpret_cast<gu4>(Y + ((((int64_t)(rb >> 5) * CB + jw) << 5) + (rb & 31)));
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-        yv[i] = Y[(int64_t)(rb + i) * CB + jw];
-        xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
+      for (int i4 = 0; i4 < N / 4; ++i4) {
+        const u32x4 u = yq[i4];
+        yv[4 * i4] = u[0]; yv[4 * i4 + 1] = u[1]; yv[4 * i4 + 2] = u[2]; yv[4 * i4 + 3] = u[3];
       }
+#pragma unroll
+      for (int i = 0; i < N; ++i) xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
     };
     if (n2 == 32) load_chunk(std::integral_constant<int, 32>{});
     else if (n2 == 16) load_chunk(std::integral_constant<int, 16>{});
@@ -1336,7 +1394,7 @@ __device__ __forceinline__ void p3_mfma_tile_wt(const WArgs& a, int bx, WLds& S)
         yv[i] = 0u;
         xv[i] = 0.0f;
         if (i >= n2) continue;  // (continue, not break: the constant trip count keeps the loop unrolled)
-        yv[i] = Y[(int64_t)(rb + i) * CB + jw];
+        yv[i] = Y[rw_at(rb + i, 0, 1, CB, jw)];
         xv[i] = X[(int64_t)(rb + i) * H + k0 + rl];
       }
     }
