@@ -94,20 +94,23 @@ enum { PS_Q1D, PS_Q2D, PS_T1, PS_T2, PS_Q1A, PS_Q2A, PS_D1, PS_D2, PS_N };
 __host__ __device__ __forceinline__ int64_t rw_at(int r, int set, int nsets, int CB, int by) {
   return ((((int64_t)(r >> 5) * nsets + set) * CB + by) << 5) + (r & 31);
 }
-// the per-row record [Bp][kRec]: the obs row's actor head (HD_*: mean, ls_raw, std, z, a, logp), its two
-// reparameterisation normals, the replayed reward / terminal / action and log π(ã'|s') of the next_obs row
+// the per-row record, kRec words per row in the row-tile layout (rec_at below): the obs row's actor head (HD_*: mean,
+// ls_raw, std, z, a, logp), its two reparameterisation normals, the replayed reward / terminal / action and
+// log π(ã'|s') of the next_obs row
 enum { HD_MEAN, HD_LSRAW, HD_STD, HD_Z, HD_A, HD_LOGP, R_EPS, R_EPSN, R_REW, R_TERM, R_ACT, R_LOGPN };
 constexpr int kRec = 16;
+// word f of row r's record
+__host__ __device__ __forceinline__ int64_t rec_at(int r, int f) { return rw_at(r, f, kRec, 1, 0); }
 
 // library-owned activations, all [Bp][...] (row pitch H unless stated)
 struct Scr {
-  float *x, *xn;             // gathered obs / next_obs rows [Bp][kXLd]
+  float *x;                  // gathered obs rows [Bp][kXLd]
   float *qx;                 // critic data rows (obs | a) [Bp][kXLd]
   float *h1, *h2;            // actor on the obs rows
   float *g1[2], *g2[2];      // Q1 / Q2 on the (obs, a) rows
   float *um, *us;            // actor backward factors
   float *uq[2];              // critic backward factors (data rows)
-  float *rec;                // [Bp][kRec] per-row record (HD_* / R_*)
+  float *rec;                // per-row record (HD_* / R_*), Bp rows (rec_at)
   float *hpart;              // actor head parts (mean | log_std) of the obs and next_obs rows, 2Bp rows (rw_at, 2 sets)
   // fc0 of a critic up to (not including) its action term — b1 + Σ_{m < O} W1[:, m] x_m, the fmaf chain in input
   // order — on the obs rows (Q1, Q2: from P1's data tiles) and the next_obs rows (T1, T2: P1's target tiles), and
@@ -678,31 +681,54 @@ __device__ __forceinline__ void tile_of(int& bx, int& by) {
 // ---------------------------------------------------------------------------------------------
 // P1 (sac_fwd_kernel): row tiles [obs (Bp/32) | next_obs (Bp/32) | Q1 data (Bp/32) | Q2 data (Bp/32)] x CB
 // ---------------------------------------------------------------------------------------------
-// the gathered batch for the later passes of the step — the obs and next_obs rows, act / rew / term and the two
-// normals — of batch item `item` (its replay row idx and normals as batch_item drew them, its next_obs row xn), by one
-// lane per item of the T1 fc0 tiles of column block 0 (short tiles: in the actor tiles this hand-on set P1's span)
-template <int WTM>
-__device__ __forceinline__ void hand_on_batch(const MArgs& a, int item, int64_t idx, float e0, float e1,
-                                              const float (&xn)[kXLd]) {
-  float xo[kXLd], aux[5];
-  if (a.chain & SACF_CHAIN_FROM_STAGED) load_run<kXLd>(a.s.sx + (int64_t)item * kXLd, xo);
-  else load_obs_row(a.obs, idx, a.L.O, xo);
-  batch_aux(a, item, idx, e0, e1, aux);
-  float* xd = a.s.x + (int64_t)item * kXLd;
-  float* xnd = a.s.xn + (int64_t)item * kXLd;
+// the gathered batch for the later passes of the step — the obs row, act / rew / term and the two normals — of
+// batch item `item` (its replay row idx and normals as batch_item drew them) by the eight threads of its row in the
+// T1 fc0 tiles of column block 0 (short tiles: in the actor tiles this hand-on set P1's span): thread j < 4 a quarter
+// of the obs row (16 bytes; a row tile's rows are one contiguous run), j = 4 .. 7 the record words (each a run of the
+// row tile's rows in the record's layout). load() at the tile's start, store() at its end: stored at once, the
+// loads' wait held the tile's own operand loads back (the T1 tiles of column block 0 ended P1 1 µs late,
+// profiles/round6/r6z_*)
+struct HandOn {
+  float v[4];
+  __device__ __forceinline__ void load(const MArgs& a, int item, int64_t idx, float e0, float e1, int j) {
+    const bool staged = (a.chain & SACF_CHAIN_FROM_STAGED) != 0;
+    if (j < 4) {
+      if (staged) {
+        const float4 u = *reinterpret_cast<const float4*>(a.s.sx + (int64_t)item * kXLd + 4 * j);
+        v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+      } else {
+        const int O = a.L.O;
 #pragma unroll
-  for (int q = 0; q < kXLd / 4; ++q) {
-    pub4<WT_ACT>(WTM, xd + 4 * q, xo[4 * q], xo[4 * q + 1], xo[4 * q + 2], xo[4 * q + 3]);
-    pub4<WT_ACT>(WTM, xnd + 4 * q, xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
+        for (int k = 0; k < 4; ++k) {
+          const int c = 4 * j + k;
+          const float x = a.obs[idx * O + min(c, O - 1)];
+          v[k] = c < O ? x : 0.0f;
+        }
+      }
+      return;
+    }
+    const float* sa = a.s.saux + (int64_t)item * kAux;
+    if (j == 4) v[0] = staged ? sa[AUX_E0] : e0;
+    else if (j == 5) v[0] = staged ? sa[AUX_E1] : e1;
+    else if (j == 6) v[0] = staged ? sa[AUX_REW] : a.rew[idx];
+    else {
+      v[0] = staged ? sa[AUX_TERM] : a.term[idx];
+      v[1] = staged ? sa[AUX_ACT] : a.act[idx];
+    }
   }
-  float* rc = a.s.rec + (int64_t)item * kRec;
-  // (R_EPS .. R_ACT are record words 6 .. 10: two words and one 16-byte store of words 8 .. 11, whose last word,
-  // R_LOGPN, P2 writes later in the step)
-  static_assert(R_EPS == 6 && R_EPSN == 7 && R_REW == 8 && R_TERM == 9 && R_ACT == 10 && R_LOGPN == 11, "record layout");
-  pub<WT_ACT>(WTM, rc + R_EPS, aux[AUX_E0]);
-  pub<WT_ACT>(WTM, rc + R_EPSN, aux[AUX_E1]);
-  pub4<WT_ACT>(WTM, rc + R_REW, aux[AUX_REW], aux[AUX_TERM], aux[AUX_ACT], 0.0f);
-}
+  template <int WTM>
+  __device__ __forceinline__ void store(const MArgs& a, int item, int j) const {
+    float* rc = a.s.rec;
+    if (j < 4) pub4<WT_ACT>(WTM, a.s.x + (int64_t)item * kXLd + 4 * j, v[0], v[1], v[2], v[3]);
+    else if (j == 4) pub<WT_ACT>(WTM, rc + rec_at(item, R_EPS), v[0]);
+    else if (j == 5) pub<WT_ACT>(WTM, rc + rec_at(item, R_EPSN), v[0]);
+    else if (j == 6) pub<WT_ACT>(WTM, rc + rec_at(item, R_REW), v[0]);
+    else {
+      pub<WT_ACT>(WTM, rc + rec_at(item, R_TERM), v[0]);
+      pub<WT_ACT>(WTM, rc + rec_at(item, R_ACT), v[1]);
+    }
+  }
+};
 
 // actor forward (gaussian_policy.py:105-118 up to the heads, mlp.py:86-99): h1 = relu(W1 x + b1) on the VALU,
 // h2 = relu(h1 W2ᵀ + b2) on MFMA, the mean / log_std head parts of this column block in the epilogue
@@ -813,16 +839,13 @@ __device__ __forceinline__ void p1_data_tile(const MArgs& a, int net, int rt, in
 #pragma unroll
     for (int m = 0; m < kXLd; ++m) lx[rl * (kXLd + 1) + m] = xin[m];  // (zero past O; the action goes at O)
     lx[rl * (kXLd + 1) + O] = act;
-    if (net == 0 && by == 0) {
-      float q[kXLd];
-#pragma unroll
-      for (int m = 0; m < kXLd; ++m) q[m] = m == O ? act : xin[m];
-      float* qd = a.s.qx + (int64_t)item * kXLd;
-#pragma unroll
-      for (int k = 0; k < kXLd / 4; ++k) pub4<WT_ACT>(WTM, qd + 4 * k, q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
-    }
   }
   __syncthreads();
+  if (net == 0 && by == 0 && threadIdx.x < kTile2 * 4) {  // the (obs | a) rows for P3: 16 bytes per thread, one run
+    const int row = (int)threadIdx.x >> 2, q4 = ((int)threadIdx.x & 3) * 4;
+    const float* l = lx + row * (kXLd + 1) + q4;
+    pub4<WT_ACT>(WTM, a.s.qx + (int64_t)(r0 + row) * kXLd + q4, l[0], l[1], l[2], l[3]);
+  }
   SAC_STAMP(0, 1);
   float* stage = lds + FwdLds<H>::kSplit;  // (the second split region: free in P1) g2 | g1 | pre tiles
   float* st_g1 = stage + kTile2 * kStageLd;
@@ -876,7 +899,9 @@ __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int 
   float e0, e1;
   float x[kXLd];
   const int64_t idx = batch_row(a, item, true, x, e0, e1);
-  if (net == 0 && by == 0 && (tid & 7) == 0) hand_on_batch<WTM>(a, item, idx, e0, e1, x);
+  const bool hand_on = net == 0 && by == 0;
+  HandOn ho;
+  if (hand_on) ho.load(a, item, idx, e0, e1, tid & 7);
   float* w1 = lds;                   // [32][kXLd + 1]: W1 rows c0 .. c0 + 31
   float* b1 = lds + kTile2 * (kXLd + 1);
   const float* src = C + L.c_w1 + (int64_t)c0 * nin;  // the 32 rows are contiguous: 32·nin floats
@@ -895,6 +920,7 @@ __device__ __forceinline__ void p1_target_pre_tile(const MArgs& a, int net, int 
     for (int j = 0; j < 4; ++j) pre[j] = m < O ? fmaf(w1[(cq + j) * (kXLd + 1) + m], x[m], pre[j]) : pre[j];
   pub4<WT_ACT>(WTM, a.s.pre[2 + net] + (int64_t)item * H + c0 + cq, pre[0], pre[1], pre[2], pre[3]);
   if (rt == 0 && tid < kTile2) pub<WT_ACT>(WTM, a.s.w1a + (2 + net) * H + c0 + tid, w1[tid * (kXLd + 1) + O]);
+  if (hand_on) ho.store<WTM>(a, item, tid & 7);
 }
 
 template <int H, int WT>
@@ -952,7 +978,7 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   // prologue's longest chain), the pre-activation and action column of this lane's K slice, the B operand
   RowHeadIn<CB> rh;
   rh.load(a, (kTarget ? Bp : 0) + item);
-  const float ev = a.s.rec[(int64_t)item * kRec + (kTarget ? R_EPSN : R_EPS)];
+  const float ev = a.s.rec[rec_at(item, kTarget ? R_EPSN : R_EPS)];
   const float* PRE = a.s.pre[(kTarget ? 2 : 0) + net] + (int64_t)item * H;
   const float* W1A = a.s.w1a + ((kTarget ? 2 : 0) + net) * H;
   float pre[CS], wa[CS];
@@ -966,12 +992,12 @@ __device__ __forceinline__ void p2_critic_tile(const MArgs& a, int net, int rt, 
   rh.head(ev, hd);
   SAC_STAMP_ON(1, 4, hd[HD_A]);
   if (w == 0 && h == 0 && net == 0 && by == 0) {
-    float* rc = a.s.rec + (int64_t)item * kRec;
+    float* rc = a.s.rec;
     if (kTarget) {
-      pub<WT_ACT>(WTM, rc + R_LOGPN, hd[HD_LOGP]);
+      pub<WT_ACT>(WTM, rc + rec_at(item, R_LOGPN), hd[HD_LOGP]);
     } else {
 #pragma unroll
-      for (int q = 0; q < 6; ++q) pub<WT_ACT>(WTM, rc + q, hd[q]);
+      for (int q = 0; q < 6; ++q) pub<WT_ACT>(WTM, rc + rec_at(item, q), hd[q]);
     }
   }
   (void)O;
@@ -1153,7 +1179,9 @@ struct RowIn {
     const float* pp = a.s.part + rw_at(r, actor ? PS_Q1A : PS_Q1D, PS_N, CB, 0);  // (set k, block b: + (k·CB + b)·32)
 #pragma unroll
     for (int i = 0; i < 4 * CB; ++i) p[i] = pp[(int64_t)i << 5];
-    load_run<kRec>(a.s.rec + (int64_t)r * kRec, rc);
+    const float* rp = a.s.rec + rec_at(r, 0);  // (word f: + f·32)
+#pragma unroll
+    for (int f = 0; f < kRec; ++f) rc[f] = rp[f << 5];
   }
   // Σ of set k's column-block parts in block order (a left fold: every reader gets the same bits)
   __device__ __forceinline__ float sum(int k) const {
@@ -2084,8 +2112,8 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
 
   SDev g(device);
   const int64_t Bp = L.Bp, BH = Bp * H, CB = H / kTile2;
-  // rows 3·16, activations 10·H, the row record, parts (2 + 8)·CB, the snapshot
-  const int64_t n_scr = Bp * 3 * kXLd + 14 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H + 4 * H +
+  // rows 2·16, activations 10·H, the row record, parts (2 + 8)·CB, the snapshot
+  const int64_t n_scr = Bp * 2 * kXLd + 14 * BH + Bp * kRec + 2 * Bp * 2 * CB + PS_N * Bp * CB + SN_HEAD + 4 * H + 4 * H +
                         Bp * (2 * kXLd + kAux) + 3 * Bp * CB;
   hipError_t e = hipMalloc(&h->scratch, sizeof(float) * n_scr);
   if (e != hipSuccess) {
@@ -2096,7 +2124,6 @@ int sacf_create(const sacf_config* cfg, int device, void* stream, sacf_handle** 
   float* s = h->scratch;
   Scr& sc = h->s;
   sc.x = s; s += Bp * kXLd;
-  sc.xn = s; s += Bp * kXLd;
   sc.qx = s; s += Bp * kXLd;
   sc.h1 = s; s += BH;
   sc.h2 = s; s += BH;
