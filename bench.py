@@ -74,8 +74,8 @@ def parse():
     p.add_argument("--no-c2", action="store_true", help="skip the configs[1] single-ship secondary line")
     p.add_argument("--no-policy-stream", action="store_true",
                    help="skip the secondary line of the same envs with the policy in the loop (shipsim_run_policy)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round5", "r5zp_pmc_traffic.json"))
-    p.add_argument("--pmc-fp64-json", default=os.path.join(ROOT, "profiles", "round5", "r5zp_pmc_fp64.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "round6", "r6fin_pmc_traffic.json"))
+    p.add_argument("--pmc-fp64-json", default=os.path.join(ROOT, "profiles", "round6", "r6fin_pmc_fp64.json"))
     p.add_argument("--sac-steps", type=int, default=300, help="timed SAC grad steps (0 = skip the SAC line)")
     p.add_argument("--sac-global-batch", type=int, default=256,
                    help="SAC batch summed over all ranks (runner: 256); each rank samples global / N rows "

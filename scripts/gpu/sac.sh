@@ -20,7 +20,7 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
 f=$(find "$O/prof_sac_$TAG" -name "*kernel_stats.csv" | head -1); cut -d, -f1-4,7 "$f" | head -12
 cd "$R"
 for b in 256 64; do  # per-block phase stamps of a diagnostics build (scripts/sac_phase_timing.py --build, here)
-  timeout -k 10 200 python scripts/sac_phase_timing.py --batch $b --out "$O/sac_phases_${TAG}_b$b.json" \
+  timeout -k 10 200 python scripts/sac_phase_timing.py --variant cur --batch $b --out "$O/sac_phases_${TAG}_b$b.json" \
     > "$O/sac_phases_${TAG}_b$b.log" 2>&1; hard $? sac_phases_$b
 done
 cd /tmp

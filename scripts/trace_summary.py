@@ -8,9 +8,10 @@ import os
 import re
 import sys
 
-# the decision-stream (CHAIN 1, shipsim_run_table) instantiations the headline times; the bench's secondary
-# policy-stream line (CHAIN 2) runs the same kernel template with the policy in the loop
-TABLE = re.compile(r"ast_step_kernel<[^>]*,\s*1,\s*\d+>")
+# the decision-stream (CHAIN 1, shipsim_run_table) instantiation of two-ship envs (SLOTS 2) the headline times; the
+# bench's secondary lines run other instantiations: the policy stream (CHAIN 2), the C4 shard (LPE 8) and the C5
+# multi-obstacle legs (SLOTS 4 / 8)
+TABLE = re.compile(r"ast_step_kernel<true,\s*\d+,\s*16,\s*false,\s*1,\s*2>")
 
 d, bench_log, out = sys.argv[1:4]
 rows = []
@@ -28,5 +29,11 @@ res = dict(command="rocprofv3 --kernel-trace --stats -- python3 bench.py (defaul
            mean_ms_timed_last=sum(ms[-b["steps"]:]) / max(1, len(ms[-b["steps"]:])),
            bench_kernel_ms_all_launches=b["roofline"].get("kernel_ms_all_launches"),
            bench_kernel_ms_timed=b["roofline"].get("kernel_ms_timed"))
+for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):  # rocprof's own per-kernel means
+    for r in csv.DictReader(open(f)):
+        if TABLE.search(r["Name"]):
+            res["stats_kernel"] = r["Name"]
+            res["stats_calls"] = int(r["Calls"])
+            res["stats_mean_ms"] = float(r["AverageNs"]) / 1e6
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
