@@ -938,7 +938,7 @@ __global__ __launch_bounds__(256) void sac_fwd_kernel(MArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // P2 (sac_mid_kernel): row tiles [Q1, Q2 on (obs, ã) (2Bt) | T1, T2 on (next_obs, ã') (2Bt) | Q1, Q2 data-row factors
-// (2Bt) | actor factors U_m (Bt) | U_s (Bt)] x CB, then one block for the step counter and P3's snapshot
+// (2Bt) | actor factors U_m (Bt) | U_s (Bt)] x CB; the target tiles also advance the step counter and snapshot for P3
 // ---------------------------------------------------------------------------------------------
 // the actor head of a row from its column-block parts (summed in block order) and its TanhNormal sample
 template <int CB>
