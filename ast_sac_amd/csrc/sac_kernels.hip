@@ -544,7 +544,7 @@ template <int H, int CS, int WTM>
 __device__ __forceinline__ void slice_out(float* st, float* base, int r0, int by, const float (&av)[CS], int k0) {
   if (k0 / kTile2 != by) return;
   const int rl = (int)threadIdx.x & 31;
-  if constexpr (CS == kTile2 && (WTM & WT_ACT) != 0) {  // (plain stores, below 128 rows: direct, 0.1 µs less at B = 64)
+  if constexpr (CS == kTile2 && (WTM & WT_ACT) != 0) {  // (plain stores, the small-batch mask: direct)
     float* d = st + rl * kStageLd;
 #pragma unroll
     for (int q = 0; q < CS / 4; ++q)
@@ -2222,9 +2222,14 @@ int sacf_set_replay(sacf_handle* h, const float* obs, const float* act, const fl
   return SACF_OK;
 }
 
-// the write-through mask of a step's launches (see pub): everything from 128 padded rows up, below that not the row
-// inputs / parts / records (WT_ACT), whose write-through costs more there than the write-back it saves
-static int wt_mask_for(const Layout& L) { return L.Bp >= 128 ? kWtLarge : kWtSmall; }
+// the write-through mask of a step's launches (see pub): everything from SACF_WT_ROWS padded rows up, below that not
+// the row inputs / parts / records (WT_ACT). The threshold was 128 while those were 4- and 16-byte pieces of many
+// rows; written as whole runs their write-through pays at every batch (0.3 µs less at B = 64 than plain stores,
+// profiles/round6/r6wt_sac_ab.txt), so it is 32 now: every batch (the knob stays for A/B builds)
+#ifndef SACF_WT_ROWS
+#define SACF_WT_ROWS 32
+#endif
+static int wt_mask_for(const Layout& L) { return L.Bp >= SACF_WT_ROWS ? kWtLarge : kWtSmall; }
 
 static ApplyArgs apply_args(const sacf_handle* h) {
   ApplyArgs a;
