@@ -1484,8 +1484,10 @@ __device__ __forceinline__ void p3_mfma_tile_wt(const WArgs& a, int bx, WLds& S)
       tt[1][cc][rr] = xe[q].t;
     }
   });
+  SAC_STAMP_ON(2, 6, xe[3].p);
   if (a.fuse) {  // W2ᵀ (and the target's) for the next step's forward passes: T[col][row]
     __syncthreads();
+    SAC_STAMP(2, 7);
     // (thread t: T row k0 + t / 8, the four columns j0 + 4 (t mod 8) ..: one 16-byte store per copy)
     const int64_t HH = (int64_t)H * H;
     const int cc = tid >> 3, j4 = (tid & 7) * 4;
