@@ -2,6 +2,7 @@
 # A whole libshipsim (both objects, the product's flags) from the kernel sources of another git revision, with this
 # tree's include/ (the C ABI header), for env timing A/Bs through SHIPSIM_LIB (scripts/gpu/env_abn.sh).
 #   bash scripts/build_shipsim_at.sh NAME [GITREF=HEAD]  ->  ast_sac_amd/lib/abl/NAME.so
+# EXTRA="flags" adds hipcc flags to every object; STRATEGY=name replaces the machine scheduler strategy.
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; REF=${2:-HEAD}
@@ -15,7 +16,8 @@ BASE="$(cd "$R" && python3 -c 'from ast_sac_amd.build_hash import HIPFLAGS; prin
 OBJS=()
 i=0
 while IFS= read -r SET; do
-  /opt/rocm/bin/hipcc $BASE $SET -I"$D" -I"$R/include" -DSHIPSIM_SRC_HASH="\"variant-$NAME\"" -c "$D/shipsim_kernels.hip" \
+  if [ -n "${STRATEGY:-}" ]; then SET=${SET//amdgpu-sched-strategy=max-ilp/amdgpu-sched-strategy=$STRATEGY}; fi
+  /opt/rocm/bin/hipcc $BASE $SET ${EXTRA:-} -I"$D" -I"$R/include" -DSHIPSIM_SRC_HASH="\"variant-$NAME\"" -c "$D/shipsim_kernels.hip" \
     -o "$OUT.$i.o" &
   OBJS+=("$OUT.$i.o")
   i=$((i + 1))
